@@ -1,0 +1,369 @@
+"""gpuseqalign_amd -- MI355X-native NW-LG engine (drop-in for GpuSeqAlign's align path).
+
+Python host side over the C ABI of ``libgsa.so`` (include/gsa.h).  The compute path is the
+hand-written gfx950 HIP kernel in ``csrc/nw_strip.hip``; there is no CPU fallback: if the
+library is missing or no GPU is visible, GPU entry points raise.
+
+Mirrors the reference's registry (src/nw_algorithm.cpp:48-69): an ``NwAlgorithm`` is an
+{align, trace, hash} triple; the plain family pairs with Trace1/Hash1, the sparse (mlsp)
+family with Trace2/Hash2.
+"""
+from __future__ import annotations
+
+import ctypes
+import dataclasses
+import os
+import subprocess
+from typing import Callable, Dict, Optional, Tuple
+
+import numpy as np
+
+__all__ = [
+    "NwStat", "NwError", "lib", "build_library", "Engine", "AlignResult", "SparseResult",
+    "NwAlgorithm", "get_nw_algorithm_map", "hash_full", "trace_full", "trace_sparse", "hash_sparse",
+    "sparse_align_cost", "sparse_tile_by",
+]
+
+_PKG = os.path.dirname(os.path.abspath(__file__))
+_SO = os.environ.get("GSA_LIB") or os.path.join(_PKG, "libgsa.so")  # GSA_LIB: diagnostic builds only
+_LIB = None
+
+
+class NwStat:
+    """NwStat (src/run_types.hpp:12-24)."""
+    success = 0
+    helpMenuRequested = 1
+    errorCudaGeneral = 2
+    errorMemoryAllocation = 3
+    errorMemoryTransfer = 4
+    errorKernelFailure = 5
+    errorIoStream = 6
+    errorInvalidFormat = 7
+    errorInvalidValue = 8
+    errorInvalidResult = 9
+    names = {0: "success", 1: "helpMenuRequested", 2: "errorCudaGeneral", 3: "errorMemoryAllocation",
+             4: "errorMemoryTransfer", 5: "errorKernelFailure", 6: "errorIoStream", 7: "errorInvalidFormat",
+             8: "errorInvalidValue", 9: "errorInvalidResult"}
+
+
+class NwError(RuntimeError):
+    def __init__(self, stat: int, where: str, hip_error: int = 0):
+        self.stat = stat
+        self.hip_error = hip_error
+        super().__init__(f"{where}: {NwStat.names.get(stat, stat)} (hipError {hip_error})")
+
+
+def build_library(force: bool = False) -> str:
+    """Compile libgsa.so in-tree (hipcc --offload-arch=gfx950)."""
+    csrc = os.path.join(_PKG, "csrc")
+    if force or not os.path.exists(_SO):
+        subprocess.check_call(["make", "-s", "-C", csrc, "-j4"])
+    return _SO
+
+
+class _Laps(ctypes.Structure):
+    _fields_ = [("alloc", ctypes.c_float), ("cpy_dev", ctypes.c_float), ("init_hdr", ctypes.c_float),
+                ("calc", ctypes.c_float), ("cpy_host", ctypes.c_float), ("calc_kernel_ms", ctypes.c_float)]
+
+    def as_dict(self):
+        return {"align.alloc": self.alloc, "align.cpy_dev": self.cpy_dev, "align.init_hdr": self.init_hdr,
+                "align.calc": self.calc, "align.cpy_host": self.cpy_host, "calc_kernel_ms": self.calc_kernel_ms}
+
+
+class SparseGeom(ctypes.Structure):
+    _fields_ = [("tileBx", ctypes.c_int32), ("tileBy", ctypes.c_int32), ("tileHdrMatRows", ctypes.c_int32),
+                ("tileHdrMatCols", ctypes.c_int32), ("tileHrowLen", ctypes.c_int32), ("tileHcolLen", ctypes.c_int32),
+                ("hrowElems", ctypes.c_int64), ("hcolElems", ctypes.c_int64)]
+
+
+_i32p = ctypes.POINTER(ctypes.c_int32)
+_vp = ctypes.c_void_p
+_i32 = ctypes.c_int32
+_i64 = ctypes.c_int64
+
+# symbol -> (restype, argtypes); every function declared in include/gsa.h
+SIGNATURES = {
+    "gsa_ctx_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(_vp)]),
+    "gsa_ctx_destroy": (None, [_vp]),
+    "gsa_last_hip_error": (ctypes.c_int, [_vp]),
+    "gsa_device_cu_count": (ctypes.c_int, [_vp]),
+    "gsa_version": (ctypes.c_char_p, []),
+    "gsa_sparse_tile_by": (_i32, []),
+    "gsa_sparse_geometry": (ctypes.c_int, [_i32, _i32, _i32, ctypes.POINTER(SparseGeom)]),
+    "gsa_fill_full_dev": (ctypes.c_int, [_vp, _vp, _i32, _vp, _i32, _vp, _i32, _i32, _vp, _vp]),
+    "gsa_fill_sparse_dev": (ctypes.c_int, [_vp, _vp, _i32, _vp, _i32, _vp, _i32, _i32, _i32, _vp, _vp, _vp]),
+    "gsa_sync": (ctypes.c_int, [_vp, _vp]),
+    "gsa_align_full": (ctypes.c_int, [_vp, _i32p, _i32, _i32p, _i32, _i32p, _i32, _i32, _i32p, _i32p,
+                                      ctypes.POINTER(_Laps)]),
+    "gsa_align_sparse": (ctypes.c_int, [_vp, _i32p, _i32, _i32p, _i32, _i32p, _i32, _i32, _i32, _i32p, _i32p,
+                                        ctypes.POINTER(SparseGeom), _i32p, ctypes.POINTER(_Laps)]),
+    "gsa_hash_full": (ctypes.c_uint32, [_i32p, _i32, _i32]),
+    "gsa_trace_full": (ctypes.c_int, [_i32p, _i32p, _i32, _i32p, _i32, ctypes.c_char_p, _i64,
+                                      ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_uint32)]),
+    "gsa_trace_sparse": (ctypes.c_int, [_i32p, _i32p, ctypes.POINTER(SparseGeom), _i32p, _i32, _i32p, _i32, _i32p,
+                                        _i32, _i32, ctypes.c_char_p, _i64, ctypes.POINTER(ctypes.c_int64),
+                                        ctypes.POINTER(ctypes.c_uint32), _i32p]),
+    "gsa_hash_sparse": (ctypes.c_uint32, [_i32p, _i32p, ctypes.POINTER(SparseGeom), _i32p, _i32, _i32p, _i32, _i32p,
+                                          _i32, _i32]),
+    "gsa_sparse_align_cost": (_i32, [_i32p, _i32p, ctypes.POINTER(SparseGeom), _i32p, _i32, _i32p, _i32, _i32p,
+                                     _i32, _i32]),
+}
+
+
+def lib():
+    """Load libgsa.so.  Raises if it has not been built: there is no fallback path."""
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(_SO):
+            raise ImportError(f"{_SO} missing: run __graft_entry__.build() (hipcc --offload-arch=gfx950)")
+        L = ctypes.CDLL(_SO)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _LIB = L
+    return _LIB
+
+
+def _p(a: np.ndarray):
+    assert a.dtype == np.int32 and a.flags["C_CONTIGUOUS"], (a.dtype, a.flags)
+    return a.ctypes.data_as(_i32p)
+
+
+def _c32(a) -> np.ndarray:
+    return np.ascontiguousarray(a, dtype=np.int32)
+
+
+def sparse_tile_by() -> int:
+    return int(lib().gsa_sparse_tile_by())
+
+
+def sparse_geometry(adjrows: int, adjcols: int, tileBx: int) -> SparseGeom:
+    g = SparseGeom()
+    st = lib().gsa_sparse_geometry(adjrows, adjcols, tileBx, ctypes.byref(g))
+    if st != NwStat.success:
+        raise NwError(st, "gsa_sparse_geometry")
+    return g
+
+
+@dataclasses.dataclass
+class AlignResult:
+    score: np.ndarray  # (adjrows, adjcols) int32
+    align_cost: int
+    laps: dict
+
+
+@dataclasses.dataclass
+class SparseResult:
+    hrow: np.ndarray
+    hcol: np.ndarray
+    geom: SparseGeom
+    align_cost: int
+    laps: dict
+
+    @property
+    def trows(self):
+        return self.geom.tileHdrMatRows
+
+    @property
+    def tcols(self):
+        return self.geom.tileHdrMatCols
+
+
+class Engine:
+    """One device context (initNwInput equivalent, src/benchmark.cpp:175-223)."""
+
+    def __init__(self, device: int = 0):
+        self.device = device
+        h = _vp()
+        st = lib().gsa_ctx_create(device, ctypes.byref(h))
+        if st != NwStat.success:
+            raise NwError(st, f"gsa_ctx_create(device={device})")
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().gsa_ctx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    @property
+    def cu_count(self) -> int:
+        return int(lib().gsa_device_cu_count(self._h))
+
+    def _check(self, st, where):
+        if st != NwStat.success:
+            raise NwError(st, where, int(lib().gsa_last_hip_error(self._h)))
+
+    # -- NwAlignFn equivalents (host buffers) -------------------------------------------
+    def align_full(self, seqY, seqX, subst, gapo: int) -> AlignResult:
+        """Full int32 score matrix (the gpu3..gpu6 family's nw.score)."""
+        seqY, seqX, subst = _c32(seqY), _c32(seqX), _c32(subst)
+        substsz = int(round(np.sqrt(subst.size)))
+        score = np.empty((len(seqY), len(seqX)), dtype=np.int32)
+        cost = ctypes.c_int32(0)
+        laps = _Laps()
+        st = lib().gsa_align_full(self._h, _p(seqY), len(seqY), _p(seqX), len(seqX), _p(subst), substsz, gapo,
+                                  _p(score), ctypes.byref(cost), ctypes.byref(laps))
+        self._check(st, "gsa_align_full")
+        return AlignResult(score, int(cost.value), laps.as_dict())
+
+    def align_sparse(self, seqY, seqX, subst, gapo: int, tileBx: int = 256) -> SparseResult:
+        """Tile-header (mlsp) representation (the gpu7..gpu9 family's tileHrowMat/tileHcolMat)."""
+        seqY, seqX, subst = _c32(seqY), _c32(seqX), _c32(subst)
+        substsz = int(round(np.sqrt(subst.size)))
+        geom = sparse_geometry(len(seqY), len(seqX), tileBx)
+        hrow = np.empty(geom.hrowElems, dtype=np.int32)
+        hcol = np.empty(geom.hcolElems, dtype=np.int32)
+        cost = ctypes.c_int32(0)
+        laps = _Laps()
+        st = lib().gsa_align_sparse(self._h, _p(seqY), len(seqY), _p(seqX), len(seqX), _p(subst), substsz, gapo,
+                                    tileBx, _p(hrow), _p(hcol), ctypes.byref(geom), ctypes.byref(cost),
+                                    ctypes.byref(laps))
+        self._check(st, "gsa_align_sparse")
+        return SparseResult(hrow, hcol, geom, int(cost.value), laps.as_dict())
+
+    # -- hot path on device-resident buffers (torch tensors or raw pointers) -------------
+    def fill_full_dev(self, seqY_ptr: int, adjrows: int, seqX_ptr: int, adjcols: int, subst_ptr: int, substsz: int,
+                      gapo: int, score_ptr: int, stream: Optional[int] = None):
+        st = lib().gsa_fill_full_dev(self._h, seqY_ptr, adjrows, seqX_ptr, adjcols, subst_ptr, substsz, gapo,
+                                     score_ptr, stream)
+        self._check(st, "gsa_fill_full_dev")
+
+    def fill_sparse_dev(self, seqY_ptr: int, adjrows: int, seqX_ptr: int, adjcols: int, subst_ptr: int,
+                        substsz: int, gapo: int, tileBx: int, hrow_ptr: int, hcol_ptr: int,
+                        stream: Optional[int] = None):
+        st = lib().gsa_fill_sparse_dev(self._h, seqY_ptr, adjrows, seqX_ptr, adjcols, subst_ptr, substsz, gapo,
+                                       tileBx, hrow_ptr, hcol_ptr, stream)
+        self._check(st, "gsa_fill_sparse_dev")
+
+    def sync(self, stream: Optional[int] = None):
+        self._check(lib().gsa_sync(self._h, stream), "gsa_sync")
+
+
+# ---- host consumers (the reference's L4) ----------------------------------------------
+
+def hash_full(score: np.ndarray) -> int:
+    """NwHash1_Plain (src/nwtrace1_plain.cpp:133-154)."""
+    score = _c32(score)
+    return int(lib().gsa_hash_full(_p(score), score.shape[0], score.shape[1]))
+
+
+def trace_full(score: np.ndarray, seqY, seqX) -> Tuple[int, str]:
+    """NwTrace1_Plain (src/nwtrace1_plain.cpp:6-131) -> (trace_hash, edit_trace)."""
+    score, seqY, seqX = _c32(score), _c32(seqY), _c32(seqX)
+    cap = 8 * (len(seqY) + len(seqX)) + 64
+    buf = ctypes.create_string_buffer(cap)
+    n = ctypes.c_int64(0)
+    h = ctypes.c_uint32(0)
+    st = lib().gsa_trace_full(_p(score), _p(seqY), len(seqY), _p(seqX), len(seqX), buf, cap, ctypes.byref(n),
+                              ctypes.byref(h))
+    if st != NwStat.success:
+        raise NwError(st, "gsa_trace_full")
+    return int(h.value), buf.raw[:n.value].decode()
+
+
+def trace_sparse(res: SparseResult, seqY, seqX, subst, gapo: int) -> Tuple[int, str, int]:
+    """NwTrace2_Sparse (src/nwtrace2_sparse.cpp:102-257) -> (trace_hash, edit_trace, align_cost)."""
+    seqY, seqX, subst = _c32(seqY), _c32(seqX), _c32(subst)
+    substsz = int(round(np.sqrt(subst.size)))
+    cap = 8 * (len(seqY) + len(seqX)) + 64
+    buf = ctypes.create_string_buffer(cap)
+    n = ctypes.c_int64(0)
+    h = ctypes.c_uint32(0)
+    cost = ctypes.c_int32(0)
+    st = lib().gsa_trace_sparse(_p(_c32(res.hrow)), _p(_c32(res.hcol)), ctypes.byref(res.geom), _p(seqY), len(seqY),
+                                _p(seqX), len(seqX), _p(subst), substsz, gapo, buf, cap, ctypes.byref(n),
+                                ctypes.byref(h), ctypes.byref(cost))
+    if st != NwStat.success:
+        raise NwError(st, "gsa_trace_sparse")
+    return int(h.value), buf.raw[:n.value].decode(), int(cost.value)
+
+
+def hash_sparse(res: SparseResult, seqY, seqX, subst, gapo: int) -> int:
+    """NwHash2_Sparse (src/nwtrace2_sparse.cpp:263-340)."""
+    seqY, seqX, subst = _c32(seqY), _c32(seqX), _c32(subst)
+    substsz = int(round(np.sqrt(subst.size)))
+    return int(lib().gsa_hash_sparse(_p(_c32(res.hrow)), _p(_c32(res.hcol)), ctypes.byref(res.geom), _p(seqY),
+                                     len(seqY), _p(seqX), len(seqX), _p(subst), substsz, gapo))
+
+
+def sparse_align_cost(res: SparseResult, seqY, seqX, subst, gapo: int) -> int:
+    seqY, seqX, subst = _c32(seqY), _c32(seqX), _c32(subst)
+    substsz = int(round(np.sqrt(subst.size)))
+    return int(lib().gsa_sparse_align_cost(_p(_c32(res.hrow)), _p(_c32(res.hcol)), ctypes.byref(res.geom),
+                                           _p(seqY), len(seqY), _p(seqX), len(seqX), _p(subst), substsz, gapo))
+
+
+# ---- the registry (src/nw_algorithm.hpp:8-42) --------------------------------------------
+
+@dataclasses.dataclass
+class NwResult:
+    """The fields of NwAlgResult the driver verifies (src/benchmark.cpp:120-147)."""
+    align_cost: int = 0
+    score_hash: int = 0
+    trace_hash: int = 0
+    edit_trace: str = ""
+    laps: dict = dataclasses.field(default_factory=dict)
+    payload: object = None
+
+
+@dataclasses.dataclass
+class NwAlgorithm:
+    name: str
+    align: Callable
+    trace: Callable
+    hash: Callable
+    params: Dict[str, list] = dataclasses.field(default_factory=dict)
+
+
+def _align_plain(engine: Engine, seqY, seqX, subst, gapo, **_):
+    r = engine.align_full(seqY, seqX, subst, gapo)
+    return NwResult(align_cost=r.align_cost, laps=r.laps, payload=r)
+
+
+def _align_mlsp(engine: Engine, seqY, seqX, subst, gapo, tileBx=256, **_):
+    r = engine.align_sparse(seqY, seqX, subst, gapo, tileBx=tileBx)
+    return NwResult(align_cost=r.align_cost, laps=r.laps, payload=r)
+
+
+def _trace1(res: NwResult, seqY, seqX, subst, gapo):
+    res.trace_hash, res.edit_trace = trace_full(res.payload.score, seqY, seqX)
+
+
+def _hash1(res: NwResult, seqY, seqX, subst, gapo):
+    res.score_hash = hash_full(res.payload.score)
+
+
+def _trace2(res: NwResult, seqY, seqX, subst, gapo):
+    res.trace_hash, res.edit_trace, _ = trace_sparse(res.payload, seqY, seqX, subst, gapo)
+
+
+def _hash2(res: NwResult, seqY, seqX, subst, gapo):
+    res.score_hash = hash_sparse(res.payload, seqY, seqX, subst, gapo)
+
+
+def get_nw_algorithm_map() -> Dict[str, NwAlgorithm]:
+    """getNwAlgorithmMap (src/nw_algorithm.cpp:48-69) for this engine.
+
+    The reference's GPU family names resolve to the MI355X strip-wavefront kernels: the
+    full-matrix names (gpu3..gpu6) to the plain fill with Trace1/Hash1, the mlsp names
+    (gpu7..gpu9) to the tile-header fill with Trace2/Hash2."""
+    plain = ["NwAlign_Amd_Strip_Full", "NwAlign_Gpu3_Ml_DiagDiag", "NwAlign_Gpu4_Ml_DiagDiag2Pass",
+             "NwAlign_Gpu5_Coop_DiagDiag", "NwAlign_Gpu6_Coop_DiagDiag2Pass"]
+    mlsp = ["NwAlign_Amd_Strip_Mlsp", "NwAlign_Gpu7_Mlsp_DiagDiag", "NwAlign_Gpu8_Mlsp_DiagDiag",
+            "NwAlign_Gpu9_Mlsp_DiagDiagDiag"]
+    m = {n: NwAlgorithm(n, _align_plain, _trace1, _hash1) for n in plain}
+    m.update({n: NwAlgorithm(n, _align_mlsp, _trace2, _hash2, {"tileBx": [256]}) for n in mlsp})
+    return m

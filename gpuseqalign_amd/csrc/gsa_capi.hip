@@ -1,0 +1,355 @@
+// gsa_capi.hip -- extern "C" boundary of libgsa.so (declared in include/gsa.h).
+//
+// Device-resident entry points enqueue the strip-wavefront fill (nw_strip.hip); host-buffer
+// entry points reproduce what the reference's align functions do around their kernels
+// (allocate, copy in, fill, copy out, Stopwatch laps):
+//   NwAlign_Gpu3_Ml_DiagDiag        nwalign_gpu3_ml_diagdiag.cu:288-596     -> gsa_align_full
+//   NwAlign_Gpu9_Mlsp_DiagDiagDiag  nwalign_gpu9_mlsp_diagdiagdiag.cu:368-722 -> gsa_align_sparse
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <new>
+
+#include "../../include/gsa.h"
+#include "nw_strip.h"
+
+struct gsa_ctx
+{
+    int device = 0;
+    int cu_count = 0;
+    hipStream_t stream = nullptr;
+    unsigned* ctl = nullptr;  // [0] ticket, [1] error flags (16 B, zeroed per launch)
+    unsigned long long* gran = nullptr;
+    size_t gran_elems = 0;
+    unsigned epoch = 0;
+    int last_hip_error = 0;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    unsigned long long* dbg = nullptr;  // stamp buffer of diagnostic builds
+    // scratch buffers for the host-buffer entry points (grow-only, like DeviceArray::init)
+    void* dbuf[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+    size_t dcap[5] = {0, 0, 0, 0, 0};
+};
+
+namespace {
+
+using Clock = std::chrono::steady_clock;
+
+inline float ms_since(Clock::time_point& t)
+{
+    auto now = Clock::now();
+    float ms = std::chrono::duration<float, std::milli>(now - t).count();
+    t = now;
+    return ms;
+}
+
+inline int fail(gsa_ctx* ctx, hipError_t e, int stat)
+{
+    ctx->last_hip_error = (int)e;
+    return stat;
+}
+
+int ensure_dev(gsa_ctx* ctx, int slot, size_t bytes)
+{
+    if (ctx->dcap[slot] >= bytes && ctx->dbuf[slot]) return GSA_SUCCESS;
+    if (ctx->dbuf[slot]) (void)hipFree(ctx->dbuf[slot]);
+    ctx->dbuf[slot] = nullptr;
+    ctx->dcap[slot] = 0;
+    hipError_t e = hipMalloc(&ctx->dbuf[slot], std::max<size_t>(bytes, 256));
+    if (e != hipSuccess) return fail(ctx, e, GSA_ERROR_MEMORY_ALLOCATION);
+    ctx->dcap[slot] = std::max<size_t>(bytes, 256);
+    return GSA_SUCCESS;
+}
+
+int ensure_gran(gsa_ctx* ctx, size_t elems)
+{
+    if (ctx->gran_elems >= elems && ctx->gran) return GSA_SUCCESS;
+    if (ctx->gran) (void)hipFree(ctx->gran);
+    ctx->gran = nullptr;
+    ctx->gran_elems = 0;
+    hipError_t e = hipMalloc(&ctx->gran, elems * sizeof(unsigned long long));
+    if (e != hipSuccess) return fail(ctx, e, GSA_ERROR_MEMORY_ALLOCATION);
+    // tags must never match a live epoch by accident: clear once per allocation
+    e = hipMemset(ctx->gran, 0, elems * sizeof(unsigned long long));
+    if (e != hipSuccess) return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
+    ctx->gran_elems = elems;
+    return GSA_SUCCESS;
+}
+
+int check_inputs(int32_t adjrows, int32_t adjcols, int32_t substsz)
+{
+    if (adjrows < 1 || adjcols < 1) return GSA_ERROR_INVALID_VALUE;
+    if (substsz < 1 || substsz > 32) return GSA_ERROR_INVALID_VALUE;  // LDS profile holds <= 32 letters
+    return GSA_SUCCESS;
+}
+
+// NULL is the HIP null stream, as everywhere in HIP; the host-buffer entry points use the
+// context's own stream explicitly.
+hipStream_t pick_stream(gsa_ctx*, void* stream) { return (hipStream_t)stream; }
+
+int enqueue_fill(gsa_ctx* ctx, int mode, const int32_t* seqY, int32_t adjrows, const int32_t* seqX, int32_t adjcols,
+                 const int32_t* subst, int32_t substsz, int32_t gapo, int32_t* score, int32_t tileBx, int32_t* hrow,
+                 int32_t* hcol, hipStream_t st)
+{
+    gsa::StripArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.seqY = seqY;
+    a.seqX = seqX;
+    a.subst = subst;
+    a.substsz = substsz;
+    a.g = gapo;
+    a.R = adjrows - 1;
+    a.C = adjcols - 1;
+    if (mode == gsa::kModeFull)
+    {
+        a.score = score;
+        a.ld = adjcols;
+        a.Cp = a.C;
+        a.nTickets = (a.R + gsa::kStripRows - 1) / gsa::kStripRows;
+    }
+    else
+    {
+        gsa_sparse_geom geom;
+        int s = gsa_sparse_geometry(adjrows, adjcols, tileBx, &geom);
+        if (s != GSA_SUCCESS) return s;
+        a.hrow = hrow;
+        a.hcol = hcol;
+        a.trows = geom.tileHdrMatRows;
+        a.tcols = geom.tileHdrMatCols;
+        a.tBx = geom.tileBx;
+        a.tBy = geom.tileBy;
+        a.Cp = a.tcols * a.tBx;
+        a.nTickets = a.trows;
+    }
+    hipError_t e = hipSetDevice(ctx->device);
+    if (e != hipSuccess) return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
+    // headers (row 0 / column 0, or the header row of tile row 0)
+    e = gsa::launch_headers(a, mode, st);
+    if (e != hipSuccess) return fail(ctx, e, GSA_ERROR_KERNEL_FAILURE);
+    if (a.nTickets == 0 || (mode == gsa::kModeFull && a.C == 0)) return GSA_SUCCESS;
+
+    a.granStride = (long long)a.Cp + 1;
+    int s = ensure_gran(ctx, (size_t)a.nTickets * (size_t)a.granStride);
+    if (s != GSA_SUCCESS) return s;
+    a.gran = ctx->gran;
+    a.ticket = ctx->ctl;
+    a.err = ctx->ctl + 1;
+    a.dbg = ctx->dbg;
+    a.epoch = ++ctx->epoch;
+    if (a.epoch == 0) a.epoch = ++ctx->epoch;  // 0 is the cleared-tag value
+    e = hipMemsetAsync(ctx->ctl, 0, 16, st);
+    if (e != hipSuccess) return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
+    const int grid = std::max(1, std::min(a.nTickets, ctx->cu_count));
+    e = gsa::launch_strip_fill(a, mode, grid, st);
+    if (e != hipSuccess) return fail(ctx, e, GSA_ERROR_KERNEL_FAILURE);
+    return GSA_SUCCESS;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* gsa_version(void) { return "gpuseqalign_amd 0.1 (gfx950 strip-wavefront)"; }
+
+int32_t gsa_sparse_tile_by(void) { return gsa::kStripRows; }
+
+int gsa_ctx_create(int device, gsa_ctx** out)
+{
+    if (!out) return GSA_ERROR_INVALID_VALUE;
+    *out = nullptr;
+    gsa_ctx* ctx = new (std::nothrow) gsa_ctx();
+    if (!ctx) return GSA_ERROR_MEMORY_ALLOCATION;
+    ctx->device = device;
+    hipError_t e = hipSetDevice(device);
+    if (e == hipSuccess) e = hipDeviceGetAttribute(&ctx->cu_count, hipDeviceAttributeMultiprocessorCount, device);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipMalloc(&ctx->ctl, 256);
+    if (e == hipSuccess) e = hipMemset(ctx->ctl, 0, 256);
+    if (e == hipSuccess) e = hipEventCreate(&ctx->ev0);
+    if (e == hipSuccess) e = hipEventCreate(&ctx->ev1);
+#if defined(GSA_STAMP) && GSA_STAMP
+    if (e == hipSuccess) e = hipMalloc(&ctx->dbg, 16 * 256 * 4 * sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipMemset(ctx->dbg, 0, 16 * 256 * 4 * sizeof(unsigned long long));
+#endif
+    if (e != hipSuccess)
+    {
+        int code = (int)e;
+        gsa_ctx_destroy(ctx);
+        (void)code;
+        return GSA_ERROR_CUDA_GENERAL;
+    }
+    *out = ctx;
+    return GSA_SUCCESS;
+}
+
+void gsa_ctx_destroy(gsa_ctx* ctx)
+{
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    for (int k = 0; k < 5; k++)
+        if (ctx->dbuf[k]) (void)hipFree(ctx->dbuf[k]);
+    if (ctx->gran) (void)hipFree(ctx->gran);
+    if (ctx->dbg) (void)hipFree(ctx->dbg);
+    if (ctx->ctl) (void)hipFree(ctx->ctl);
+    if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
+    if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+int gsa_last_hip_error(const gsa_ctx* ctx) { return ctx ? ctx->last_hip_error : 0; }
+
+#if defined(GSA_STAMP) && GSA_STAMP
+// diagnostic builds only: copy the stamp buffer out
+int gsa_debug_stamps(gsa_ctx* ctx, unsigned long long* out, int n)
+{
+    if (!ctx || !ctx->dbg) return GSA_ERROR_INVALID_VALUE;
+    hipError_t e = hipMemcpy(out, ctx->dbg, (size_t)n * sizeof(unsigned long long), hipMemcpyDeviceToHost);
+    return e == hipSuccess ? GSA_SUCCESS : GSA_ERROR_MEMORY_TRANSFER;
+}
+#endif
+
+int gsa_device_cu_count(const gsa_ctx* ctx) { return ctx ? ctx->cu_count : 0; }
+
+int gsa_sparse_geometry(int32_t adjrows, int32_t adjcols, int32_t tileBx, gsa_sparse_geom* geom)
+{
+    if (!geom || adjrows < 1 || adjcols < 1) return GSA_ERROR_INVALID_VALUE;
+    if (tileBx < 64 || tileBx % 16 != 0) return GSA_ERROR_INVALID_VALUE;
+    const int64_t tBy = gsa::kStripRows;
+    // padded dims as nwalign_gpu9_mlsp_diagdiagdiag.cu:416-431 (empty sequences -> one tile)
+    int64_t trows = ((int64_t)adjrows - 1 + tBy - 1) / tBy;
+    int64_t tcols = ((int64_t)adjcols - 1 + tileBx - 1) / tileBx;
+    trows = std::max<int64_t>(trows, 1);
+    tcols = std::max<int64_t>(tcols, 1);
+    geom->tileBx = tileBx;
+    geom->tileBy = (int32_t)tBy;
+    geom->tileHdrMatRows = (int32_t)trows;
+    geom->tileHdrMatCols = (int32_t)tcols;
+    geom->tileHrowLen = tileBx + 1;
+    geom->tileHcolLen = (int32_t)tBy + 1;
+    geom->hrowElems = trows * tcols * (tileBx + 1);
+    geom->hcolElems = trows * tcols * (tBy + 1);
+    return GSA_SUCCESS;
+}
+
+int gsa_fill_full_dev(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, const int32_t* seqX, int32_t adjcols,
+                      const int32_t* subst, int32_t substsz, int32_t gapo, int32_t* score, void* stream)
+{
+    if (!ctx || !score) return GSA_ERROR_INVALID_VALUE;
+    int s = check_inputs(adjrows, adjcols, substsz);
+    if (s != GSA_SUCCESS) return s;
+    return enqueue_fill(ctx, gsa::kModeFull, seqY, adjrows, seqX, adjcols, subst, substsz, gapo, score, 0, nullptr,
+                        nullptr, pick_stream(ctx, stream));
+}
+
+int gsa_fill_sparse_dev(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, const int32_t* seqX, int32_t adjcols,
+                        const int32_t* subst, int32_t substsz, int32_t gapo, int32_t tileBx, int32_t* hrow,
+                        int32_t* hcol, void* stream)
+{
+    if (!ctx || !hrow || !hcol) return GSA_ERROR_INVALID_VALUE;
+    int s = check_inputs(adjrows, adjcols, substsz);
+    if (s != GSA_SUCCESS) return s;
+    return enqueue_fill(ctx, gsa::kModeSparse, seqY, adjrows, seqX, adjcols, subst, substsz, gapo, nullptr, tileBx,
+                        hrow, hcol, pick_stream(ctx, stream));
+}
+
+int gsa_sync(gsa_ctx* ctx, void* stream)
+{
+    if (!ctx) return GSA_ERROR_INVALID_VALUE;
+    hipError_t e = hipStreamSynchronize(pick_stream(ctx, stream));
+    if (e != hipSuccess) return fail(ctx, e, GSA_ERROR_KERNEL_FAILURE);
+    unsigned flags[2] = {0, 0};
+    e = hipMemcpy(flags, ctx->ctl, sizeof(flags), hipMemcpyDeviceToHost);
+    if (e != hipSuccess) return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
+    if (flags[1] != 0) return GSA_ERROR_KERNEL_FAILURE;  // a hand-off spin gave up
+    return GSA_SUCCESS;
+}
+
+int gsa_align_full(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, const int32_t* seqX, int32_t adjcols,
+                   const int32_t* subst, int32_t substsz, int32_t gapo, int32_t* score_out, int32_t* align_cost,
+                   gsa_laps* laps)
+{
+    if (!ctx || !seqY || !seqX || !subst || !score_out) return GSA_ERROR_INVALID_VALUE;
+    int s = check_inputs(adjrows, adjcols, substsz);
+    if (s != GSA_SUCCESS) return s;
+    gsa_laps L {};
+    auto t = Clock::now();
+    const size_t cells = (size_t)adjrows * (size_t)adjcols;
+    if ((s = ensure_dev(ctx, 0, (size_t)adjrows * 4)) || (s = ensure_dev(ctx, 1, (size_t)adjcols * 4)) ||
+        (s = ensure_dev(ctx, 2, (size_t)substsz * substsz * 4)) || (s = ensure_dev(ctx, 3, cells * 4)))
+        return s;
+    L.alloc = ms_since(t);
+    hipError_t e;
+    if ((e = hipMemcpyAsync(ctx->dbuf[0], seqY, (size_t)adjrows * 4, hipMemcpyHostToDevice, ctx->stream)) ||
+        (e = hipMemcpyAsync(ctx->dbuf[1], seqX, (size_t)adjcols * 4, hipMemcpyHostToDevice, ctx->stream)) ||
+        (e = hipMemcpyAsync(ctx->dbuf[2], subst, (size_t)substsz * substsz * 4, hipMemcpyHostToDevice, ctx->stream)) ||
+        (e = hipStreamSynchronize(ctx->stream)))
+        return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
+    L.cpy_dev = ms_since(t);
+    L.init_hdr = 0.f;  // headers are written by the fill launch itself
+    (void)hipEventRecord(ctx->ev0, ctx->stream);
+    s = gsa_fill_full_dev(ctx, (const int32_t*)ctx->dbuf[0], adjrows, (const int32_t*)ctx->dbuf[1], adjcols,
+                          (const int32_t*)ctx->dbuf[2], substsz, gapo, (int32_t*)ctx->dbuf[3], ctx->stream);
+    if (s != GSA_SUCCESS) return s;
+    (void)hipEventRecord(ctx->ev1, ctx->stream);
+    if ((s = gsa_sync(ctx, ctx->stream)) != GSA_SUCCESS) return s;
+    L.calc = ms_since(t);
+    (void)hipEventElapsedTime(&L.calc_kernel_ms, ctx->ev0, ctx->ev1);
+    if ((e = hipMemcpy(score_out, ctx->dbuf[3], cells * 4, hipMemcpyDeviceToHost)))
+        return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
+    L.cpy_host = ms_since(t);
+    if (align_cost) *align_cost = score_out[cells - 1];
+    if (laps) *laps = L;
+    return GSA_SUCCESS;
+}
+
+int gsa_align_sparse(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, const int32_t* seqX, int32_t adjcols,
+                     const int32_t* subst, int32_t substsz, int32_t gapo, int32_t tileBx, int32_t* hrow_out,
+                     int32_t* hcol_out, gsa_sparse_geom* geom_out, int32_t* align_cost, gsa_laps* laps)
+{
+    if (!ctx || !seqY || !seqX || !subst || !hrow_out || !hcol_out) return GSA_ERROR_INVALID_VALUE;
+    int s = check_inputs(adjrows, adjcols, substsz);
+    if (s != GSA_SUCCESS) return s;
+    gsa_sparse_geom geom;
+    if ((s = gsa_sparse_geometry(adjrows, adjcols, tileBx, &geom)) != GSA_SUCCESS) return s;
+    gsa_laps L {};
+    auto t = Clock::now();
+    if ((s = ensure_dev(ctx, 0, (size_t)adjrows * 4)) || (s = ensure_dev(ctx, 1, (size_t)adjcols * 4)) ||
+        (s = ensure_dev(ctx, 2, (size_t)substsz * substsz * 4)) || (s = ensure_dev(ctx, 3, (size_t)geom.hrowElems * 4)) ||
+        (s = ensure_dev(ctx, 4, (size_t)geom.hcolElems * 4)))
+        return s;
+    L.alloc = ms_since(t);
+    hipError_t e;
+    if ((e = hipMemcpyAsync(ctx->dbuf[0], seqY, (size_t)adjrows * 4, hipMemcpyHostToDevice, ctx->stream)) ||
+        (e = hipMemcpyAsync(ctx->dbuf[1], seqX, (size_t)adjcols * 4, hipMemcpyHostToDevice, ctx->stream)) ||
+        (e = hipMemcpyAsync(ctx->dbuf[2], subst, (size_t)substsz * substsz * 4, hipMemcpyHostToDevice, ctx->stream)) ||
+        (e = hipStreamSynchronize(ctx->stream)))
+        return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
+    L.cpy_dev = ms_since(t);
+    (void)hipEventRecord(ctx->ev0, ctx->stream);
+    s = gsa_fill_sparse_dev(ctx, (const int32_t*)ctx->dbuf[0], adjrows, (const int32_t*)ctx->dbuf[1], adjcols,
+                            (const int32_t*)ctx->dbuf[2], substsz, gapo, tileBx, (int32_t*)ctx->dbuf[3],
+                            (int32_t*)ctx->dbuf[4], ctx->stream);
+    if (s != GSA_SUCCESS) return s;
+    (void)hipEventRecord(ctx->ev1, ctx->stream);
+    if ((s = gsa_sync(ctx, ctx->stream)) != GSA_SUCCESS) return s;
+    L.calc = ms_since(t);
+    (void)hipEventElapsedTime(&L.calc_kernel_ms, ctx->ev0, ctx->ev1);
+    if ((e = hipMemcpy(hrow_out, ctx->dbuf[3], (size_t)geom.hrowElems * 4, hipMemcpyDeviceToHost)) ||
+        (e = hipMemcpy(hcol_out, ctx->dbuf[4], (size_t)geom.hcolElems * 4, hipMemcpyDeviceToHost)))
+        return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
+    L.cpy_host = ms_since(t);
+    // align_cost from the last tile, as the reference does after its copy-back (:713-716);
+    // the reference adds this to the align.calc lap.
+    int32_t cost = gsa_sparse_align_cost(hrow_out, hcol_out, &geom, seqY, adjrows, seqX, adjcols, subst, substsz, gapo);
+    L.calc += ms_since(t);
+    if (align_cost) *align_cost = cost;
+    if (geom_out) *geom_out = geom;
+    if (laps) *laps = L;
+    return GSA_SUCCESS;
+}
+
+}  // extern "C"

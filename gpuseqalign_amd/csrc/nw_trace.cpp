@@ -1,0 +1,255 @@
+// nw_trace.cpp -- host-side consumers of a fill (the reference's L4, CPU in the reference too):
+// score hash, traceback and edit-trace hash for both output representations.
+//
+//   NwHash1_Plain  / NwTrace1_Plain   (src/nwtrace1_plain.cpp:6-154)
+//   NwHash2_Sparse / NwTrace2_Sparse  (src/nwtrace2_sparse.cpp:8-340)
+//
+// Tie-break, RLE edit-string format and djb2-xor hashing follow the reference exactly;
+// indices are 64-bit.
+#include <algorithm>
+#include <climits>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/gsa.h"
+
+namespace {
+
+inline uint32_t djb2x(uint32_t h, uint32_t v) { return ((h << 5) + h) ^ v; }
+
+inline int32_t max3(int32_t a, int32_t b, int32_t c) { return std::max(std::max(a, b), c); }
+
+// Run-length builder: push (prev_edit, reversed count) when the letter changes, reverse at
+// the end (src/nwtrace1_plain.cpp:81-106).
+class EditTrace
+{
+public:
+    void push(char edit)
+    {
+        if (edit != prev_ && prev_ != '\0')
+        {
+            std::string cnt = std::to_string(same_);
+            std::reverse(cnt.begin(), cnt.end());
+            s_.push_back(prev_);
+            s_.append(cnt);
+            same_ = 1;
+        }
+        else if (edit == prev_)
+            same_++;
+        prev_ = edit;
+    }
+    uint32_t finish()
+    {
+        std::reverse(s_.begin(), s_.end());
+        uint32_t h = 5381;
+        for (char c : s_) h = djb2x(h, (uint32_t)(int32_t)c);
+        return h;
+    }
+    const std::string& str() const { return s_; }
+
+private:
+    std::string s_;
+    int64_t same_ = 1;
+    char prev_ = '\0';
+};
+
+int emit(const EditTrace& t, char* edit, int64_t cap, int64_t* edit_len)
+{
+    const std::string& s = t.str();
+    if ((int64_t)s.size() > cap) return GSA_ERROR_MEMORY_ALLOCATION;
+    std::memcpy(edit, s.data(), s.size());
+    if ((int64_t)s.size() < cap) edit[s.size()] = '\0';
+    *edit_len = (int64_t)s.size();
+    return GSA_SUCCESS;
+}
+
+struct SparseView
+{
+    const int32_t *hrow, *hcol, *seqY, *seqX, *subst;
+    int64_t adjrows, adjcols, rows, cols, hrowLen, hcolLen;
+    int32_t substsz, g;
+};
+
+struct TileIJ
+{
+    int64_t iTile, jTile, iTileElem, jTileElem;
+};
+
+// NwTrace2_GetTileAndElemIJ (src/nwtrace2_sparse.cpp:8-38), with its saturation.
+TileIJ tile_of(const SparseView& v, int64_t i, int64_t j)
+{
+    TileIJ co {i / (v.hcolLen - 1), j / (v.hrowLen - 1), i % (v.hcolLen - 1), j % (v.hrowLen - 1)};
+    if (co.iTile == v.rows) { co.iTile -= 1; co.iTileElem += v.hcolLen - 1; }
+    if (co.jTile == v.cols) { co.jTile -= 1; co.jTileElem += v.hrowLen - 1; }
+    return co;
+}
+
+// NwTrace2_AlignTile (src/nwtrace2_sparse.cpp:40-96).
+void align_tile(const SparseView& v, std::vector<int32_t>& tile, const TileIJ& co)
+{
+    const int64_t W = v.hrowLen, H = v.hcolLen, k = v.cols * co.iTile + co.jTile;
+    std::copy(v.hrow + k * W, v.hrow + k * W + W, tile.begin());
+    for (int64_t i = 0; i < H; i++) tile[i * W] = v.hcol[k * H + i];
+    const int64_t ibeg = co.iTile * (H - 1), jbeg = co.jTile * (W - 1);
+    const int64_t iend = std::min(H, co.iTileElem + 1), jend = std::min(W, co.jTileElem + 1);
+    for (int64_t i = 1; i < iend; i++)
+    {
+        const bool rowOut = ibeg + i >= v.adjrows;
+        const int32_t* srow = rowOut ? nullptr : v.subst + (int64_t)v.seqY[ibeg + i] * v.substsz;
+        for (int64_t j = 1; j < jend; j++)
+        {
+            if (rowOut || jbeg + j >= v.adjcols) { tile[i * W + j] = 0; continue; }
+            tile[i * W + j] = max3(tile[(i - 1) * W + j - 1] + srow[v.seqX[jbeg + j]], tile[(i - 1) * W + j] + v.g,
+                                   tile[i * W + j - 1] + v.g);
+        }
+    }
+}
+
+SparseView make_view(const int32_t* hrow, const int32_t* hcol, const gsa_sparse_geom* geom, const int32_t* seqY,
+                     int32_t adjrows, const int32_t* seqX, int32_t adjcols, const int32_t* subst, int32_t substsz,
+                     int32_t g)
+{
+    return SparseView {hrow, hcol, seqY, seqX, subst, adjrows, adjcols, geom->tileHdrMatRows, geom->tileHdrMatCols,
+                       geom->tileHrowLen, geom->tileHcolLen, substsz, g};
+}
+
+}  // namespace
+
+extern "C" {
+
+uint32_t gsa_hash_full(const int32_t* score, int32_t adjrows, int32_t adjcols)
+{
+    uint32_t h = 5381;
+    const int64_t n = (int64_t)adjrows * adjcols;
+    for (int64_t k = 0; k < n; k++) h = djb2x(h, (uint32_t)score[k]);
+    return h;
+}
+
+int gsa_trace_full(const int32_t* score, const int32_t* seqY, int32_t adjrows, const int32_t* seqX, int32_t adjcols,
+                   char* edit, int64_t cap, int64_t* edit_len, uint32_t* trace_hash)
+{
+    const int64_t W = adjcols;
+    auto at = [&](int64_t i, int64_t j) { return score[i * W + j]; };
+    EditTrace t;
+    int64_t i = adjrows - 1, j = adjcols - 1;
+    for (;;)
+    {
+        int64_t best = INT64_MIN;
+        int di = 0, dj = 0;
+        char e = '\0';
+        if (i > 0 && j > 0) { best = at(i - 1, j - 1); di = dj = -1; e = (seqX[j] == seqY[i]) ? '=' : 'X'; }
+        if (i > 0 && best < at(i - 1, j)) { best = at(i - 1, j); di = -1; dj = 0; e = 'I'; }
+        if (j > 0 && best < at(i, j - 1)) { best = at(i, j - 1); di = 0; dj = -1; e = 'D'; }
+        i += di;
+        j += dj;
+        t.push(e);
+        if (di == 0 && dj == 0) break;
+    }
+    *trace_hash = t.finish();
+    return emit(t, edit, cap, edit_len);
+}
+
+int32_t gsa_sparse_align_cost(const int32_t* hrow, const int32_t* hcol, const gsa_sparse_geom* geom,
+                              const int32_t* seqY, int32_t adjrows, const int32_t* seqX, int32_t adjcols,
+                              const int32_t* subst, int32_t substsz, int32_t g)
+{
+    SparseView v = make_view(hrow, hcol, geom, seqY, adjrows, seqX, adjcols, subst, substsz, g);
+    std::vector<int32_t> tile((size_t)(v.hrowLen * v.hcolLen), 0);
+    TileIJ co = tile_of(v, adjrows - 1, adjcols - 1);
+    align_tile(v, tile, co);
+    return tile[co.iTileElem * v.hrowLen + co.jTileElem];
+}
+
+int gsa_trace_sparse(const int32_t* hrow, const int32_t* hcol, const gsa_sparse_geom* geom, const int32_t* seqY,
+                     int32_t adjrows, const int32_t* seqX, int32_t adjcols, const int32_t* subst, int32_t substsz,
+                     int32_t g, char* edit, int64_t cap, int64_t* edit_len, uint32_t* trace_hash, int32_t* align_cost)
+{
+    SparseView v = make_view(hrow, hcol, geom, seqY, adjrows, seqX, adjcols, subst, substsz, g);
+    const int64_t W = v.hrowLen;
+    std::vector<int32_t> tile((size_t)(v.hrowLen * v.hcolLen), 0);
+    int64_t i = adjrows - 1, j = adjcols - 1;
+    TileIJ co = tile_of(v, i, j);
+    align_tile(v, tile, co);
+    if (align_cost) *align_cost = tile[co.iTileElem * W + co.jTileElem];
+    EditTrace t;
+    for (;;)
+    {
+        auto at = [&](int64_t a, int64_t b) { return tile[a * W + b]; };
+        int64_t best = INT64_MIN;
+        int di = 0, dj = 0;
+        char e = '\0';
+        if (co.iTileElem > 0 && co.jTileElem > 0)
+        {
+            best = at(co.iTileElem - 1, co.jTileElem - 1);
+            di = dj = -1;
+            e = (seqX[j] == seqY[i]) ? '=' : 'X';
+        }
+        if (co.iTileElem > 0 && best < at(co.iTileElem - 1, co.jTileElem))
+        {
+            best = at(co.iTileElem - 1, co.jTileElem);
+            di = -1; dj = 0; e = 'I';
+        }
+        if (co.jTileElem > 0 && best < at(co.iTileElem, co.jTileElem - 1))
+        {
+            best = at(co.iTileElem, co.jTileElem - 1);
+            di = 0; dj = -1; e = 'D';
+        }
+        i += di;
+        j += dj;
+        co.iTileElem += di;
+        co.jTileElem += dj;
+        // step into the up / left / up-left tile when we reach a header (src/nwtrace2_sparse.cpp:195-214)
+        const int64_t diT = -(int64_t)(co.iTileElem == 0 && co.iTile > 0);
+        const int64_t djT = -(int64_t)(co.jTileElem == 0 && co.jTile > 0);
+        if (diT != 0 || djT != 0)
+        {
+            co.iTile += diT;
+            co.jTile += djT;
+            if (co.iTileElem == 0 && di != 0) co.iTileElem = v.hcolLen - 1;
+            if (co.jTileElem == 0 && dj != 0) co.jTileElem = v.hrowLen - 1;
+            align_tile(v, tile, co);
+        }
+        t.push(e);
+        if (di == 0 && dj == 0) break;
+    }
+    *trace_hash = t.finish();
+    return emit(t, edit, cap, edit_len);
+}
+
+uint32_t gsa_hash_sparse(const int32_t* hrow, const int32_t* hcol, const gsa_sparse_geom* geom, const int32_t* seqY,
+                         int32_t adjrows, const int32_t* seqX, int32_t adjcols, const int32_t* subst, int32_t substsz,
+                         int32_t g)
+{
+    // As in the reference, the tile coordinates are taken for the constant (adjrows-1, adjcols-1)
+    // (src/nwtrace2_sparse.cpp:293), so the header branches below fire only for degenerate
+    // geometries and the hash is a row-streaming recompute of the whole matrix.
+    SparseView v = make_view(hrow, hcol, geom, seqY, adjrows, seqX, adjcols, subst, substsz, g);
+    std::vector<int32_t> curr((size_t)adjcols, 0), prev((size_t)adjcols, 0);
+    const TileIJ co = tile_of(v, adjrows - 1, adjcols - 1);
+    uint32_t h = 5381;
+    for (int64_t i = 0; i < adjrows; i++)
+    {
+        const int32_t* srow = subst + (int64_t)seqY[i] * substsz;
+        for (int64_t j = 0; j < adjcols; j++)
+        {
+            int32_t e = 0;
+            if (co.iTileElem == 0 && i != adjrows - 1)
+                e = hrow[(v.cols * co.iTile + co.jTile) * v.hrowLen + co.jTileElem];
+            else if (co.jTileElem == 0 && j != adjcols - 1)
+                e = hcol[(v.cols * co.iTile + co.jTile) * v.hcolLen + co.iTileElem];
+            else if (i > 0 && j > 0)
+                e = max3(prev[j - 1] + srow[seqX[j]], prev[j] + g, curr[j - 1] + g);
+            else if (i > 0)
+                e = prev[j] + g;
+            else if (j > 0)
+                e = curr[j - 1] + g;
+            curr[j] = e;
+            h = djb2x(h, (uint32_t)e);
+        }
+        std::swap(curr, prev);
+    }
+    return h;
+}
+
+}  // extern "C"

@@ -1,0 +1,127 @@
+/*
+ * gsa.h -- C ABI of the MI355X NW-LG engine (libgsa.so).
+ *
+ * This is the drop-in boundary for the reference's align slot
+ *     using NwAlignFn = NwStat (*)(const NwAlgParams&, NwAlgInput&, NwAlgResult&);
+ * (markods/GpuSeqAlign src/nw_algorithm.hpp:11, registered in src/nw_algorithm.cpp:48-66)
+ * and for the consumers the registry pairs with it (NwTrace1_Plain / NwHash1_Plain,
+ * NwTrace2_Sparse / NwHash2_Sparse, src/nw_fns.hpp:22-39).  Plain pointers and sizes only.
+ *
+ * Conventions (identical to NwAlgInput, src/run_types.hpp:70-110):
+ *  - seqY / seqX are int32 letter indices WITH the dummy header element 0
+ *    (src/file_formats.cpp:43-47); adjrows = |seqY|+1, adjcols = |seqX|+1.
+ *  - subst is substsz*substsz int32, row = seqY letter, column = seqX letter
+ *    (src/nwalign_cpu1_st_row.cpp:6).
+ *  - gapo is the linear gap cost (reference default -11, src/cmd_parser.cpp:298).
+ *  - full score matrix: adjrows*adjcols int32 row-major, unpadded (nw.score).
+ *  - sparse (mlsp) matrices: tileHrowMat[trows*tcols*(1+tileBx)] and
+ *    tileHcolMat[trows*tcols*(1+tileBy)], tile-major row-major k = tcols*iTile + jTile
+ *    (nwalign_gpu9_mlsp_diagdiagdiag.cu:15-63, :147-171, :319-358).
+ *  - every int-returning function returns an NwStat code (src/run_types.hpp:12-24); the
+ *    raw hipError_t of the failing runtime call is kept in the context
+ *    (gsa_last_hip_error), like NwAlgResult::cudaStat.
+ */
+#ifndef GSA_H
+#define GSA_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* NwStat (src/run_types.hpp:12-24), same numbering. */
+enum gsa_stat
+{
+    GSA_SUCCESS = 0,
+    GSA_HELP_MENU_REQUESTED = 1,
+    GSA_ERROR_CUDA_GENERAL = 2, /* errorCudaGeneral: HIP runtime failure */
+    GSA_ERROR_MEMORY_ALLOCATION = 3,
+    GSA_ERROR_MEMORY_TRANSFER = 4,
+    GSA_ERROR_KERNEL_FAILURE = 5,
+    GSA_ERROR_IO_STREAM = 6,
+    GSA_ERROR_INVALID_FORMAT = 7,
+    GSA_ERROR_INVALID_VALUE = 8,
+    GSA_ERROR_INVALID_RESULT = 9
+};
+
+typedef struct gsa_ctx gsa_ctx;
+
+/* Sparse geometry produced by a fill (NwAlgInput tileHdrMatRows/Cols, tileHrowLen/HcolLen,
+ * src/run_types.hpp:97-100; set at nwalign_gpu9_mlsp_diagdiagdiag.cu:696-699). */
+typedef struct gsa_sparse_geom
+{
+    int32_t tileBx, tileBy;
+    int32_t tileHdrMatRows, tileHdrMatCols; /* trows, tcols */
+    int32_t tileHrowLen, tileHcolLen;       /* 1+tileBx, 1+tileBy */
+    int64_t hrowElems, hcolElems;           /* trows*tcols*(1+tileBx), trows*tcols*(1+tileBy) */
+} gsa_sparse_geom;
+
+/* Stopwatch laps of NwAlgResult::sw_align, in ms (src/stopwatch.cpp:43-50; names at
+ * src/file_formats.cpp:505-519).  calc_kernel_ms is the hipEvent time of the fill kernels. */
+typedef struct gsa_laps
+{
+    float alloc, cpy_dev, init_hdr, calc, cpy_host;
+    float calc_kernel_ms;
+} gsa_laps;
+
+/* ---- context --------------------------------------------------------------------- */
+/* One context per device and host thread (the reference's initNwInput, src/benchmark.cpp:175-223). */
+int gsa_ctx_create(int device, gsa_ctx** out);
+void gsa_ctx_destroy(gsa_ctx* ctx);
+int gsa_last_hip_error(const gsa_ctx* ctx);
+int gsa_device_cu_count(const gsa_ctx* ctx);
+const char* gsa_version(void);
+
+/* Tile height of the sparse representation this build produces (63 * strips per workgroup). */
+int32_t gsa_sparse_tile_by(void);
+/* Geometry for (adjrows, adjcols, tileBx); tileBx must be a multiple of 16 and >= 64. */
+int gsa_sparse_geometry(int32_t adjrows, int32_t adjcols, int32_t tileBx, gsa_sparse_geom* geom);
+
+/* ---- hot path, device-resident buffers (inputs already in HBM) --------------------- */
+/* Enqueue the fill on `stream` (a hipStream_t; NULL = the HIP null stream); asynchronous.  Call
+ * gsa_sync() before reading outputs: it also reports hand-off time-outs. */
+int gsa_fill_full_dev(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, const int32_t* seqX, int32_t adjcols,
+                      const int32_t* subst, int32_t substsz, int32_t gapo, int32_t* score, void* stream);
+int gsa_fill_sparse_dev(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, const int32_t* seqX, int32_t adjcols,
+                        const int32_t* subst, int32_t substsz, int32_t gapo, int32_t tileBx, int32_t* tileHrowMat,
+                        int32_t* tileHcolMat, void* stream);
+int gsa_sync(gsa_ctx* ctx, void* stream);
+
+/* ---- NwAlignFn equivalents, host buffers (alloc + H2D + fill + D2H, laps as the
+ * reference's NwAlign_Gpu3_Ml_DiagDiag / NwAlign_Gpu9_Mlsp_DiagDiagDiag) -------------- */
+int gsa_align_full(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, const int32_t* seqX, int32_t adjcols,
+                   const int32_t* subst, int32_t substsz, int32_t gapo, int32_t* score_out, int32_t* align_cost,
+                   gsa_laps* laps);
+int gsa_align_sparse(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, const int32_t* seqX, int32_t adjcols,
+                     const int32_t* subst, int32_t substsz, int32_t gapo, int32_t tileBx, int32_t* tileHrowMat_out,
+                     int32_t* tileHcolMat_out, gsa_sparse_geom* geom, int32_t* align_cost, gsa_laps* laps);
+
+/* ---- consumers (host), the reference's L4 ----------------------------------------- */
+/* NwHash1_Plain (src/nwtrace1_plain.cpp:133-154). */
+uint32_t gsa_hash_full(const int32_t* score, int32_t adjrows, int32_t adjcols);
+/* NwTrace1_Plain (src/nwtrace1_plain.cpp:6-131); edit string NUL-terminated if room.
+ * Returns GSA_ERROR_MEMORY_ALLOCATION if `cap` is too small. */
+int gsa_trace_full(const int32_t* score, const int32_t* seqY, int32_t adjrows, const int32_t* seqX,
+                   int32_t adjcols, char* edit, int64_t cap, int64_t* edit_len, uint32_t* trace_hash);
+/* NwTrace2_Sparse (src/nwtrace2_sparse.cpp:102-257) + the align_cost recompute of the mlsp
+ * align functions (nwalign_gpu9_mlsp_diagdiagdiag.cu:713-716). */
+int gsa_trace_sparse(const int32_t* tileHrowMat, const int32_t* tileHcolMat, const gsa_sparse_geom* geom,
+                     const int32_t* seqY, int32_t adjrows, const int32_t* seqX, int32_t adjcols,
+                     const int32_t* subst, int32_t substsz, int32_t gapo, char* edit, int64_t cap,
+                     int64_t* edit_len, uint32_t* trace_hash, int32_t* align_cost);
+/* NwHash2_Sparse (src/nwtrace2_sparse.cpp:263-340). */
+uint32_t gsa_hash_sparse(const int32_t* tileHrowMat, const int32_t* tileHcolMat, const gsa_sparse_geom* geom,
+                         const int32_t* seqY, int32_t adjrows, const int32_t* seqX, int32_t adjcols,
+                         const int32_t* subst, int32_t substsz, int32_t gapo);
+/* align_cost of a sparse result: NwTrace2_GetTileAndElemIJ + NwTrace2_AlignTile of the last
+ * tile (nwalign_gpu9_mlsp_diagdiagdiag.cu:713-716). */
+int32_t gsa_sparse_align_cost(const int32_t* tileHrowMat, const int32_t* tileHcolMat, const gsa_sparse_geom* geom,
+                              const int32_t* seqY, int32_t adjrows, const int32_t* seqX, int32_t adjcols,
+                              const int32_t* subst, int32_t substsz, int32_t gapo);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GSA_H */

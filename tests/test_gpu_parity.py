@@ -1,0 +1,149 @@
+"""GPU parity: the HIP strip-wavefront fill (through the C ABI, libgsa.so) against the oracle.
+
+Bar: bit-exact (integer DP).  Plain family: the whole (R+1)x(C+1) matrix equals
+cpu1-st-row's; mlsp family: the whole tileHrowMat/tileHcolMat buffers equal what the
+reference's gpu7-9 kernels leave for the same tile geometry (oracle.sparse_headers).  The
+reference's own known answers (align_cost, score_hash, trace_hash) are checked end to end.
+"""
+import numpy as np
+import pytest
+
+import gpuseqalign_amd as gsa
+import oracle
+from tests._data import random_pair, related_pair
+
+pytestmark = pytest.mark.gpu
+
+
+def _hex(v):
+    return "%08x" % v
+
+
+@pytest.mark.parametrize("idx", range(6))
+def test_known_answers_plain(engine, golden, idx):
+    case = golden.known["cases"][idx]
+    Y, X = golden.pair(case["pair"])
+    r = engine.align_full(Y, X, golden.blosum62, golden.known["gapo"])
+    assert r.align_cost == case["align_cost"]
+    assert _hex(gsa.hash_full(r.score)) == case["score_hash"]
+    th, edit = gsa.trace_full(r.score, Y, X)
+    assert _hex(th) == case["trace_hash"]
+    if "edit_trace" in case:
+        assert edit == case["edit_trace"]
+
+
+@pytest.mark.parametrize("idx", range(6))
+def test_known_answers_mlsp(engine, golden, idx):
+    case = golden.known["cases"][idx]
+    Y, X = golden.pair(case["pair"])
+    r = engine.align_sparse(Y, X, golden.blosum62, golden.known["gapo"], tileBx=256)
+    assert r.align_cost == case["align_cost"]
+    th, edit, cost = gsa.trace_sparse(r, Y, X, golden.blosum62, -11)
+    assert _hex(th) == case["trace_hash"] and cost == case["align_cost"]
+    if len(Y) * len(X) < 3e7:
+        hr, hc, tr, tc, _ = oracle.sparse_headers(Y, X, golden.blosum62, -11, r.geom.tileBy, 256)
+        assert np.array_equal(r.hrow, hr) and np.array_equal(r.hcol, hc)
+
+
+def test_pair_debug_plain(engine, golden):
+    """All 173 pairs of resrc/pair_debug.txt (lengths 1..728, tile-edge cases)."""
+    for p, Y, X in golden.pairs("pair_debug.txt"):
+        r = engine.align_full(Y, X, golden.blosum62, -11)
+        S, cost = oracle.fill_full(Y, X, golden.blosum62, -11)
+        assert r.align_cost == cost, p
+        assert np.array_equal(r.score, S), p
+
+
+def test_pair_debug_mlsp(engine, golden):
+    tBy = gsa.sparse_tile_by()
+    for p, Y, X in golden.pairs("pair_debug.txt")[::3]:
+        r = engine.align_sparse(Y, X, golden.blosum62, -11, tileBx=64)
+        hr, hc, tr, tc, cost = oracle.sparse_headers(Y, X, golden.blosum62, -11, tBy, 64)
+        assert r.align_cost == cost, p
+        assert np.array_equal(r.hrow, hr), p
+        assert np.array_equal(r.hcol, hc), p
+
+
+EDGES = [1, 2, 62, 63, 64, 65, 126, 127, 252, 253, 255, 256, 257, 505, 1000]
+
+
+@pytest.mark.parametrize("R", EDGES)
+def test_plain_edge_shapes(engine, golden, R):
+    for C in (1, 15, 16, 17, 63, 64, 200, 777):
+        Y, X = random_pair(R, C, 1000 * R + C)
+        r = engine.align_full(Y, X, golden.blosum62, -11)
+        S, cost = oracle.fill_full(Y, X, golden.blosum62, -11)
+        assert np.array_equal(r.score, S), (R, C)
+
+
+@pytest.mark.parametrize("tBx", [64, 80, 256, 512])
+@pytest.mark.parametrize("R,C", [(1, 1), (63, 64), (252, 256), (253, 257), (700, 300), (300, 1500), (1100, 1029)])
+def test_mlsp_shapes(engine, golden, tBx, R, C):
+    Y, X = random_pair(R, C, 7 * R + C + tBx)
+    r = engine.align_sparse(Y, X, golden.blosum62, -11, tileBx=tBx)
+    hr, hc, tr, tc, cost = oracle.sparse_headers(Y, X, golden.blosum62, -11, gsa.sparse_tile_by(), tBx)
+    assert (r.trows, r.tcols) == (tr, tc)
+    assert np.array_equal(r.hrow, hr)
+    assert np.array_equal(r.hcol, hc)
+    assert r.align_cost == cost
+
+
+@pytest.mark.parametrize("name,gapo", [("blosum45", -11), ("blosum80", -1), ("blosum90", -30), ("blosum50", 3)])
+def test_other_substitution_and_gaps(engine, golden, name, gapo):
+    sub = golden.subst_data.matrix(name)
+    Y, X = random_pair(777, 901, 31, alphabet=25)
+    r = engine.align_full(Y, X, sub, gapo)
+    S, cost = oracle.fill_full(Y, X, sub, gapo)
+    assert np.array_equal(r.score, S)
+    rs = engine.align_sparse(Y, X, sub, gapo, tileBx=128)
+    hr, hc, _, _, _ = oracle.sparse_headers(Y, X, sub, gapo, gsa.sparse_tile_by(), 128)
+    assert np.array_equal(rs.hrow, hr) and np.array_equal(rs.hcol, hc)
+
+
+def test_relaunch_is_deterministic(engine, golden):
+    """Back-to-back launches reuse the hand-off buffer under a new epoch tag."""
+    Y, X = related_pair(3000, 11)
+    a = engine.align_full(Y, X, golden.blosum62, -11).score.copy()
+    Y2, X2 = random_pair(1200, 2600, 3)
+    engine.align_full(Y2, X2, golden.blosum62, -11)
+    b = engine.align_full(Y, X, golden.blosum62, -11).score
+    assert np.array_equal(a, b)
+    S, _ = oracle.fill_full(Y, X, golden.blosum62, -11)
+    assert np.array_equal(a, S)
+
+
+def test_device_api_on_torch_stream(engine, golden):
+    import torch
+    Y, X = random_pair(2000, 2500, 77)
+    dev = torch.device("cuda:0")
+    tY = torch.from_numpy(Y).to(dev)
+    tX = torch.from_numpy(X).to(dev)
+    tS = torch.from_numpy(golden.blosum62).to(dev)
+    out = torch.full((len(Y), len(X)), -7, dtype=torch.int32, device=dev)
+    s = torch.cuda.current_stream()
+    engine.fill_full_dev(tY.data_ptr(), len(Y), tX.data_ptr(), len(X), tS.data_ptr(), 25, -11, out.data_ptr(),
+                         s.cuda_stream)
+    engine.sync(s.cuda_stream)
+    S, _ = oracle.fill_full(Y, X, golden.blosum62, -11)
+    assert np.array_equal(out.cpu().numpy(), S)
+
+
+def test_10k_config_plain_and_mlsp(engine, golden):
+    """Config 2 pair (len12124[:10000] x len15390[:10000]) both representations."""
+    Y, X = golden.pair("len12124[:10000] len15390[:10000]")
+    r = engine.align_full(Y, X, golden.blosum62, -11)
+    S, cost = oracle.fill_full(Y, X, golden.blosum62, -11)
+    assert np.array_equal(r.score, S)
+    rs = engine.align_sparse(Y, X, golden.blosum62, -11, tileBx=256)
+    hr, hc, _, _, c2 = oracle.sparse_headers(Y, X, golden.blosum62, -11, gsa.sparse_tile_by(), 256)
+    assert np.array_equal(rs.hrow, hr) and np.array_equal(rs.hcol, hc) and rs.align_cost == cost == c2
+
+
+def test_mlsp_40k_related(engine, golden):
+    """Beyond a tile-row count of 150: every header buffer word against the streaming oracle."""
+    Y, X = related_pair(40000, 101)
+    rs = engine.align_sparse(Y, X, golden.blosum62, -11, tileBx=512)
+    hr, hc, _, _, cost = oracle.sparse_headers(Y, X, golden.blosum62, -11, gsa.sparse_tile_by(), 512)
+    assert np.array_equal(rs.hrow, hr)
+    assert np.array_equal(rs.hcol, hc)
+    assert rs.align_cost == cost
