@@ -28,7 +28,7 @@ n = 16 * 256 * 4
 buf = (ctypes.c_uint64 * n)()
 assert L.gsa_debug_stamps(eng._h, buf, n) == 0
 st = np.frombuffer(buf, dtype=np.uint64).reshape(16, 256, 4).astype(np.int64)
-for w in range(6):
+for w in range(10):
     s = st[w]
     if s[:, 0].max() == 0:
         continue
