@@ -151,7 +151,7 @@ def main():
                        "parallelism": f"pair-sharded x{world}"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": PEAK_HBM_GBPS, "unit": "GB/s",
                          "frac": round(achieved / PEAK_HBM_GBPS, 4), "traffic": traffic,
-                         "kernel": "gsa::nw_strip_kernel<4,16,0>", "kernel_ms": round(kern_ms, 4),
+                         "kernel": "gsa::nw_strip_kernel<1,0> (full)", "kernel_ms": round(kern_ms, 4),
                          "algorithmic_bytes_per_launch": bytes_per_launch},
             "align_costs": costs[:8],
         }

@@ -10,6 +10,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 
@@ -85,6 +86,18 @@ int check_inputs(int32_t adjrows, int32_t adjcols, int32_t substsz)
     return GSA_SUCCESS;
 }
 
+// Strip waves per workgroup of full fills: 1 spreads the scattered-row stores of the full
+// matrix over the most CUs; GSA_FULL_NS (1, 2 or 4) overrides it for experiments.
+int full_ns()
+{
+    static int ns = [] {
+        const char* e = std::getenv("GSA_FULL_NS");
+        int v = e ? std::atoi(e) : gsa::kFullNSDefault;
+        return (v == 1 || v == 2 || v == 4) ? v : gsa::kFullNSDefault;
+    }();
+    return ns;
+}
+
 // NULL is the HIP null stream, as everywhere in HIP; the host-buffer entry points use the
 // context's own stream explicitly.
 hipStream_t pick_stream(gsa_ctx*, void* stream) { return (hipStream_t)stream; }
@@ -107,7 +120,8 @@ int enqueue_fill(gsa_ctx* ctx, int mode, const int32_t* seqY, int32_t adjrows, c
         a.score = score;
         a.ld = adjcols;
         a.Cp = a.C;
-        a.nTickets = (a.R + gsa::kStripRows - 1) / gsa::kStripRows;
+        a.ns = full_ns();
+        a.nTickets = (a.R + gsa::kWaveRows * a.ns - 1) / (gsa::kWaveRows * a.ns);
     }
     else
     {
@@ -121,6 +135,7 @@ int enqueue_fill(gsa_ctx* ctx, int mode, const int32_t* seqY, int32_t adjrows, c
         a.tBx = geom.tileBx;
         a.tBy = geom.tileBy;
         a.Cp = a.tcols * a.tBx;
+        a.ns = gsa::kSparseNS;
         a.nTickets = a.trows;
     }
     hipError_t e = hipSetDevice(ctx->device);
@@ -153,7 +168,7 @@ extern "C" {
 
 const char* gsa_version(void) { return "gpuseqalign_amd 0.1 (gfx950 strip-wavefront)"; }
 
-int32_t gsa_sparse_tile_by(void) { return gsa::kStripRows; }
+int32_t gsa_sparse_tile_by(void) { return gsa::kSparseTileBy; }
 
 int gsa_ctx_create(int device, gsa_ctx** out)
 {
@@ -218,7 +233,7 @@ int gsa_sparse_geometry(int32_t adjrows, int32_t adjcols, int32_t tileBx, gsa_sp
 {
     if (!geom || adjrows < 1 || adjcols < 1) return GSA_ERROR_INVALID_VALUE;
     if (tileBx < 64 || tileBx % 16 != 0) return GSA_ERROR_INVALID_VALUE;
-    const int64_t tBy = gsa::kStripRows;
+    const int64_t tBy = gsa::kSparseTileBy;
     // padded dims as nwalign_gpu9_mlsp_diagdiagdiag.cu:416-431 (empty sequences -> one tile)
     int64_t trows = ((int64_t)adjrows - 1 + tBy - 1) / tBy;
     int64_t tcols = ((int64_t)adjcols - 1 + tileBx - 1) / tileBx;

@@ -8,9 +8,10 @@ namespace gsa {
 
 constexpr int kModeFull = 0;
 constexpr int kModeSparse = 1;
-constexpr int kStripNS = 4;   // strips (waves) per workgroup -> tile height 63*NS
-constexpr int kStripBLK = 16; // wavefront steps between workgroup barriers
-constexpr int kStripRows = 63 * kStripNS;
+constexpr int kWaveRows = 256;                          // rows per strip (one wave, 4 rows per lane)
+constexpr int kSparseNS = 4;                            // strip waves per workgroup, sparse fills
+constexpr int kSparseTileBy = kWaveRows * kSparseNS;    // = tile height of the mlsp matrices
+constexpr int kFullNSDefault = 1;                       // strip waves per workgroup, full fills
 
 struct StripArgs
 {
@@ -23,6 +24,7 @@ struct StripArgs
     int C;  // adjcols-1
     int Cp; // last column computed (sparse: tcols*tBx, full: C)
     int nTickets;
+    int ns;  // strip waves per workgroup (super-strip = ns*kWaveRows rows)
     // FULL
     int* score;
     long long ld;  // = adjcols

@@ -1,406 +1,605 @@
 // nw_strip.hip -- NW-LG score-matrix fill for gfx950 (MI355X), hand-written wave64 HIP.
 //
-// Replaces the reference's tiled anti-diagonal fill family (gpu3..gpu9,
-// e.g. nwalign_gpu9_mlsp_diagdiagdiag.cu:69-360 Kernel B and its per-diagonal launch
-// loop :616-660) with ONE persistent launch that sweeps horizontal strips:
+// Replaces the reference's tiled anti-diagonal fill family (gpu3..gpu9, e.g.
+// nwalign_gpu9_mlsp_diagdiagdiag.cu:69-360 Kernel B and its per-diagonal launch loop
+// :616-660) with ONE persistent launch that sweeps horizontal strips.
 //
-//  * A wave owns a strip of 63 matrix rows.  Lane l>=1 is row (r0-1+l); lane 0 is a
-//    HALO lane that replays the row just above the strip.  At local step t lane l
-//    works on column (t-l), so one wave instruction advances one anti-diagonal.
-//  * The recurrence (nwalign_cpu1_st_row.cpp:4-10) runs in the shifted space
-//        H'[i][j] = H[i][j] - (i+j)*g
-//    where it becomes  H'[i][j] = max3(H'[i-1][j-1] + s(i,j) - 2g, H'[i-1][j], H'[i][j-1]):
-//    three VALU ops per cell (v_add_u32_dpp, v_max3 / v_max_dpp); the up/diag neighbours
-//    arrive from lane l-1 through DPP wave_shr:1.  H' is >= 0 and non-decreasing along
-//    rows and columns, which is what lets the halo lane replay the row above through
-//    the same instruction stream (its diag input is 0 and its S input is the value).
-//  * s(i,j)-2g comes from a per-wave LDS profile P[x][lane] (conflict-free: bank = lane);
-//    column letters come from a per-workgroup LDS ring of x*256 byte offsets.
-//  * A workgroup holds NS strips (a "super-strip" of 63*NS rows = one tile row of the
-//    sparse format).  Waves run in lock-step blocks of BLK steps separated by s_barrier;
-//    wave w lags wave w-1 by DELTA blocks and reads wave w-1's last row straight from
-//    its LDS staging ring (the staging ring holds every computed cell for a few blocks).
-//  * Super-strips are handed out by an atomic ticket (so the launch cannot deadlock
-//    whatever the residency); super-strip k's wave 0 consumes super-strip k-1's last
-//    row from HBM through 8-byte {epoch, value} granules (sc1 stores / sc1 loads,
-//    MI355X_MICROARCH.md "R2" form) -- no flags, no fences.
+// Recurrence (nwalign_cpu1_st_row.cpp:4-10) in the shifted space H' = H - (i+j)*g:
+//     H'[i][j] = max3(H'[i-1][j-1] + s(i,j) - 2g, H'[i-1][j], H'[i][j-1])
+// H' is >= 0 and non-decreasing along rows and columns; one cell = one v_add + one v_max3.
+//
+// Strip = one wave = 256 rows.  Lane l owns the 4 consecutive rows r0+4l .. r0+4l+3 and at
+// step t works on column c = t - l for all four of them (skewed across lanes, not within a
+// lane), so one step is
+//     up  = DPP wave_shr:1 (row D of lane l-1) [+ halo for lane 0]      v_add_u32_dpp
+//     A   = max3(diagA + sA, up, A)                                      v_add_sdwa + v_max3
+//     B   = max3(A_prev + sB, A, B) ... D                                 (x3)
+// = 9 VALU for 4 cells, chain of 5 dependent ops.  The four s(i,j)-2g values of a lane
+// come from ONE ds_read_b64 of a per-wave LDS profile P[x][lane] = 4 x int16 (bank =
+// lane, conflict-free); the column letters come as one ds_read_b128 per 4 steps from 4
+// pre-shifted copies of a per-workgroup letter ring.
+//
+// Hand-off between strips (no barriers): every 4 steps each lane writes its 4 row-D values
+// with one unconditional ds_write_b128 into a 128-slot "diagonal" ring at slot (group -
+// lane); lane 63's values there survive 65 groups before later writes of lower lanes land
+// on them.  The next strip's lane 0 reads 5 slots per 16-step block and injects the row
+// above through the DPP add.  Producer/consumer order is kept with LDS progress words
+// (LDS ops of one wave execute in order, so a progress word written after the data is
+// never seen before the data).
+//
+// Workgroup = NS strip waves + 1 loader wave (letters, the previous super-strip's last row
+// from HBM through 8-byte {epoch, value} granules, and the draining of the last strip's
+// row to HBM).  Super-strips are handed out by an atomic ticket, so the launch cannot
+// deadlock whatever the residency.  Every wait is bounded in wall time (error word set).
 //
 // Outputs (MODE):
 //  * FULL   : the whole (R+1) x (C+1) int32 matrix, row-major, unpadded
 //             (what NwAlign_Gpu3..6 return in nw.score after their 2-D crop).
-//  * SPARSE : tileHrowMat / tileHcolMat exactly as gpu7/8/9 leave them, for tile
-//             height tBy = 63*NS and a tile width tBx (multiple of 16, >= 64);
-//             padded cells use letter 0 as the reference does
-//             (nwalign_gpu9_mlsp_diagdiagdiag.cu:469-478).
+//  * SPARSE : tileHrowMat / tileHcolMat exactly as gpu7/8/9 leave them, for tile height
+//             tBy = 256*NS and a tile width tBx (multiple of 16, >= 64); padded cells use
+//             letter 0 as the reference does (nwalign_gpu9_mlsp_diagdiagdiag.cu:469-478).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
+#include <algorithm>
+#include <type_traits>
 
 #include "nw_strip.h"
 
 namespace gsa {
 
-constexpr int kRowsPerWave = 63;  // lane 0 is the halo
-constexpr int kSR = 96;           // staging ring depth (steps); multiple of 32 and of BLK
-constexpr int kSlot = 65;         // dwords per staging slot (64 lanes + 1 pad: conflict-free column reads)
-constexpr int kXR = 1024;         // column-letter ring (entries), plus a BLK mirror
-constexpr int kHN = 128;          // inter-workgroup halo ring (entries, power of 2)
-constexpr int kRN = 128;          // halo-ramp entries per wave (>= kSR, kHN)
-constexpr int kNegS = -(1 << 29); // "minus infinity" profile row for columns <= 0
+constexpr int kK = 4;               // rows per lane
+static_assert(kWaveRows == 64 * kK, "rows per strip");
+constexpr int kBLK = 16;            // wavefront steps per block
+constexpr int kXR = 1024;           // letter ring (columns), per pre-shifted copy
+// Copy m starts at m*kXCopy + kXSkew(m): with these bank offsets the 16 lanes of every
+// ds_read_b128 lane group read 16 disjoint 4-bank slots (lane l reads copy (-l)&3).
+constexpr int kXCopy = kXR * 4 + 256;
+__host__ __device__ constexpr uint32_t xcopy_base(int m) { return (uint32_t)m * kXCopy + (m == 0 ? 0 : m == 1 ? 208 : m == 2 ? 144 : 80); }
+constexpr int kRing = 128;          // hand-off ring slots (16 B) per strip boundary
+constexpr int kBig = 0x3fffffff;    // "everything published"
+constexpr uint64_t kSpinLimit = 20000000ull;  // 0.2 s of s_memrealtime (100 MHz) without progress
+
 
 extern __shared__ __attribute__((aligned(16))) char smem[];
 
+typedef int int2v __attribute__((ext_vector_type(2)));
+typedef int int4v __attribute__((ext_vector_type(4)));
+typedef int int4a __attribute__((ext_vector_type(4), aligned(4)));
+
 __device__ __forceinline__ int lds_ld(uint32_t a) { return *(const int*)(smem + a); }
 __device__ __forceinline__ void lds_st(uint32_t a, int v) { *(int*)(smem + a) = v; }
+__device__ __forceinline__ int2v lds_ld2(uint32_t a) { return *(const int2v*)(smem + a); }
+__device__ __forceinline__ int4v lds_ld4(uint32_t a) { return *(const int4v*)(smem + a); }
+__device__ __forceinline__ void lds_st4(uint32_t a, int4v v) { *(int4v*)(smem + a) = v; }
+// progress words: relaxed workgroup-scope atomics (no waits; a volatile access would make the
+// compiler drain every outstanding global store around it)
+__device__ __forceinline__ int flag_ld(uint32_t a)
+{
+    int* p = (int*)__builtin_assume_aligned(smem + a, 4);
+    return __builtin_amdgcn_readfirstlane(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+}
+__device__ __forceinline__ void flag_st(uint32_t a, int v)
+{
+    asm volatile("" ::: "memory");  // data writes are issued before the word (LDS executes in order)
+    int* p = (int*)__builtin_assume_aligned(smem + a, 4);
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void cbar() { asm volatile("" ::: "memory"); }
 
 // lane l <- lane l-1, lane 0 <- 0 (DPP wave_shr:1, bound_ctrl zero)
 __device__ __forceinline__ int shr1z(int v) { return __builtin_amdgcn_update_dpp(0, v, 0x138, 0xF, 0xF, true); }
 
-struct Lds {
-    uint32_t st, prof, rmp, xo, hrg, misc, psz;
+struct Lds
+{
+    uint32_t xo, ring, zero, flags, prof, psz;
 };
+
+// flags: prog[i] @ 4i (ring i holds the row above strip i; valid for columns < prog[i]),
+//        cons[i] @ 32+4i (ring i's reader no longer needs columns < cons[i]),
+//        xo_cols @ 64 (letter ring valid for columns < xo_cols), ticket @ 68.
+constexpr uint32_t kFProg = 0, kFCons = 32, kFXo = 64, kFTicket = 68;
 
 template <int NS>
 __device__ __forceinline__ Lds lds_layout(int substsz)
 {
+    static_assert(NS >= 1 && NS <= 7, "flag layout");
     Lds L;
-    L.psz = (uint32_t)(substsz + 1) * 256u;
-    L.st = 0;
-    L.prof = L.st + NS * kSR * kSlot * 4;
-    L.rmp = L.prof + NS * L.psz;
-    L.xo = L.rmp + NS * kRN * 4;
-    L.hrg = L.xo + (kXR + 64) * 4;
-    L.misc = L.hrg + kHN * 4;
+    L.psz = (uint32_t)(substsz + 1) * 512u;  // P[x][lane] = 4 x int16; row substsz = NEG
+    L.xo = 0;
+    L.ring = L.xo + 4 * kXCopy;
+    L.zero = L.ring + (NS + 1) * kRing * 16;
+    L.flags = L.zero + 16;
+    L.prof = L.flags + 128;
     return L;
 }
 
 size_t strip_lds_bytes(int ns, int substsz)
 {
-    size_t psz = (size_t)(substsz + 1) * 256u;
-    return (size_t)ns * kSR * kSlot * 4 + ns * psz + (size_t)ns * kRN * 4 + (kXR + 64) * 4 + kHN * 4 + 16;
+    return (size_t)4 * kXCopy + (size_t)(ns + 1) * kRing * 16 + 16 + 128 + (size_t)ns * (substsz + 1) * 512;
 }
 
-// Poll one {epoch, value} granule written by the previous super-strip.  Bounded by wall
-// time (s_memrealtime, 100 MHz): on time-out the error word is set and every later poll of
-// the launch returns at once, so a broken hand-off ends the kernel instead of hanging it.
-__device__ __forceinline__ int poll_granule(const StripArgs& a, const unsigned long long* gp)
+__device__ __forceinline__ bool err_set(const StripArgs& a)
 {
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    for (;;)
-    {
-        unsigned long long q = __hip_atomic_load(gp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if ((uint32_t)(q >> 32) == a.epoch) return (int)(uint32_t)q;
-        if (__hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return 0;
-        if (__builtin_amdgcn_s_memrealtime() - t0 > 20000000ull)  // 0.2 s
-        {
-            atomicOr(a.err, 1u);
-            return 0;
-        }
-        __builtin_amdgcn_s_sleep(1);
-    }
+    return __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
 }
 
-__device__ __forceinline__ void xo_store(const Lds& L, int c, int v)
-{
-    int k = c & (kXR - 1);
-    lds_st(L.xo + 4 * k, v);
-    if (k < 64) lds_st(L.xo + 4 * (kXR + k), v);  // mirror so a block never wraps
-}
-
-// One block of BLK wavefront steps: the whole hot loop.  S values of this block are
-// already in registers (s); the next block's letter offsets and S values are fetched
-// while this block computes (LAG steps between a letter read and its S read), so no
-// LDS latency is exposed on the critical chain.
-template <int BLK>
-__device__ __forceinline__ void sweep_block(int& c0, int& c1, int (&s)[BLK], uint32_t xo_next, uint32_t laneoff,
-                                            uint32_t st_base)
-{
-    constexpr int LAG = 4;
-    int xn[BLK];
-    int sn[BLK];
-#pragma unroll
-    for (int u = 0; u < BLK + LAG; ++u)
-    {
-        if (u < BLK) xn[u] = lds_ld(xo_next + 4 * u);
-        if (u >= LAG) sn[u - LAG] = lds_ld((uint32_t)xn[u - LAG] + laneoff);
-        if (u < BLK)
-        {
-            int d = shr1z(c1) + s[u];      // H'[i-1][j-1] + s - 2g
-            int e = max(d, c0);            // vs H'[i][j-1]
-            int cn = max(shr1z(c0), e);    // vs H'[i-1][j]
-            lds_st(st_base + 4 * kSlot * u, cn);
-            c1 = c0;
-            c0 = cn;
-        }
-    }
-#pragma unroll
-    for (int u = 0; u < BLK; ++u) s[u] = sn[u];
-}
-
-template <int BLK>
-__device__ __forceinline__ void load_block(int (&s)[BLK], uint32_t xo_cur, uint32_t laneoff)
-{
-    int x[BLK];
-#pragma unroll
-    for (int u = 0; u < BLK; ++u) x[u] = lds_ld(xo_cur + 4 * u);
-#pragma unroll
-    for (int u = 0; u < BLK; ++u) s[u] = lds_ld((uint32_t)x[u] + laneoff);
-}
-
-typedef int int4a __attribute__((ext_vector_type(4), aligned(4)));
-
-// letter byte-offset for column c given its loaded letter x
+// letter byte-offset into the profile for column c given its loaded letter x
 __device__ __forceinline__ int x_offset(const StripArgs& a, int c, int x)
 {
-    if (c <= 0 || c > a.Cp) return a.substsz * 256;  // NEG row
+    if (c <= 0 || c > a.Cp) return a.substsz * 512;  // NEG row
     if (c > a.C) return 0;                            // padding letter 0
-    return ((unsigned)x < (unsigned)a.substsz ? x : 0) * 256;
+    return ((unsigned)x < (unsigned)a.substsz ? x : 0) * 512;
 }
 
 __device__ __forceinline__ int load_letter(const StripArgs& a, int c) { return (c >= 1 && c <= a.C) ? a.seqX[c] : 0; }
 
-// Raw workgroup barrier: waits for this wave's LDS traffic only (global stores stay in
-// flight); the "memory" clobber keeps the compiler from moving memory ops across it.
+// ring slot / element of the lane-63 value of column c (written at step c+63, group (c+63)/4)
+__device__ __forceinline__ uint32_t ring_elem(int c)
+{
+    const int gi = (c + 63) >> 2;
+    return 16u * (uint32_t)((gi - 63) & (kRing - 1)) + 4u * (uint32_t)((c + 63) & 3);
+}
+
 #ifndef GSA_STAMP
 #define GSA_STAMP 0
 #endif
-// Diagnostic stamps (separate build, never in the shipped library): s_memtime at fixed points
-// of the first 256 blocks of ticket 0, lane 0 of each wave.
-__device__ __forceinline__ void stamp(const StripArgs& a, int tk, int w, int G, int k, int lane)
+// Timing-experiment knobs (separate builds only; any set bit makes results WRONG):
+// 1 no halo loads, 2 no progress words / waits, 4 no sparse captures, 8 no hand-off writes
+#ifndef GSA_KNOB
+#define GSA_KNOB 0
+#endif
+// Diagnostic stamps (separate build, never in the shipped library): s_memtime at the start
+// of each of the first 256 blocks of ticket 0, lane 0 of each strip wave.
+__device__ __forceinline__ void stamp(const StripArgs& a, int tk, int w, int b, int k, int lane)
 {
     if constexpr (GSA_STAMP)
     {
-        if (tk == 0 && G < 256 && lane == 0 && a.dbg)
+        if (tk == 0 && b < 256 && lane == 0 && a.dbg)
         {
             unsigned long long t;
             asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-            a.dbg[((size_t)w * 256 + G) * 4 + k] = t;
+            a.dbg[((size_t)w * 256 + b) * 4 + k] = t;
         }
     }
 }
 
-__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+// Per-ticket timeline (stamp builds): s_memtime of strip wave 0 at [0] profile built, [1] first
+// block ready, [2] last block done, and of the loader at [3] first granule chunk fed.
+__device__ __forceinline__ void tstamp(const StripArgs& a, int tk, int j, int lane)
+{
+    if constexpr (GSA_STAMP)
+    {
+        if (tk < 2048 && lane == 0 && a.dbg)
+        {
+            unsigned long long t;
+            asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+            a.dbg[8192 + (size_t)tk * 4 + j] = t;
+        }
+    }
+}
 
-// Workgroup = NS compute waves (one 63-row strip each) + 1 loader wave (wave NS) that owns
-// every global load of the sweep: column letters and the previous super-strip's last row,
-// fetched in 64-column chunks several blocks ahead.  The two roles run separate loops with
-// the same barrier count, so the compute loop carries no pending loads (no vmcnt waits).
-template <int NS, int BLK, int MODE>
+// ------------------------------------------------------------------------------------
+// strip wave
+// ------------------------------------------------------------------------------------
+// Software pipeline (one wave, LDS reads execute in order and a single wave gets a fraction
+// of the LDS rate, so every read is issued a whole block before its use):
+//   block b computes with  S[b%2]  (issued during block b-1)  and  hv[b%2]  (halo, ditto);
+//   during block b it issues  S[(b+1)%2] from letters L[(b+1)%2]  (read during block b-1),
+//   letters L[b%2] for block b+2  and  hv[(b+1)%2].
+template <int NS, int MODE>
+__device__ __forceinline__ void strip_wave(const StripArgs& a, const Lds& L, int tk, int w, int lane)
+{
+    constexpr int TR = kWaveRows * NS;  // rows per super-strip
+    const int g = a.g;
+    const int Cp = a.Cp;
+    const int r0 = tk * TR + kWaveRows * w + 1;  // first row of the strip
+    const uint32_t F = L.flags;
+    if (MODE == kModeFull && r0 > a.R)
+    {
+        // nothing to store below the matrix: pass the (never read) hand-off through
+        flag_st(F + kFProg + 4 * (w + 1), kBig);
+        flag_st(F + kFCons + 4 * w, kBig);
+        return;
+    }
+
+    // ---- profile P[x][lane] = 4 x int16 (s(row_k, x) - 2g), row substsz = NEG ----------
+    const uint32_t my_prof = L.prof + (uint32_t)w * L.psz;
+    {
+        const int* srow[kK];
+#pragma unroll
+        for (int k = 0; k < kK; ++k)
+        {
+            const int r = r0 + kK * lane + k;
+            int y = (r <= a.R) ? a.seqY[r] : 0;
+            y = ((unsigned)y < (unsigned)a.substsz) ? y : 0;
+            srow[k] = a.subst + y * a.substsz;
+        }
+        bool bad = false;
+        for (int x = 0; x < a.substsz; ++x)
+        {
+            int v[kK];
+#pragma unroll
+            for (int k = 0; k < kK; ++k)
+            {
+                v[k] = srow[k][x] - 2 * g;
+                bad |= (v[k] < -32767) || (v[k] > 32767);
+            }
+            int2v p;
+            p.x = (v[0] & 0xffff) | (v[1] << 16);
+            p.y = (v[2] & 0xffff) | (v[3] << 16);
+            *(int2v*)(smem + my_prof + 512 * x + 8 * lane) = p;
+        }
+        *(int2v*)(smem + my_prof + 512 * a.substsz + 8 * lane) = int2v {(int)0x80008000u, (int)0x80008000u};
+        if (bad) atomicOr(a.err, 2u);
+    }
+
+    const int NB = (Cp + 64 + kBLK - 1) / kBLK;  // blocks: lane 63 reaches column Cp
+    const uint32_t laneoff = my_prof + 8u * lane;
+    const int xm = (-lane) & 3;
+    const uint32_t xo_base = L.xo + xcopy_base(xm);
+    const int lanepos = (-lane - xm) >> 2;  // in 16-byte units
+    auto xo_addr = [&](int t0) { return xo_base + 16u * (uint32_t)(((t0 >> 2) + lanepos) & (kXR / 4 - 1)); };
+    const uint32_t ring_in = L.ring + (uint32_t)w * (kRing * 16);
+    const uint32_t ring_out = L.ring + (uint32_t)(w + 1) * (kRing * 16);
+    const uint32_t fin = F + kFProg + 4 * w, fcout = F + kFCons + 4 * (w + 1);
+
+    // halo window of block b: lane-63 slots of the row above for groups 4b+15 .. 4b+19
+    // (steps 16b+60 .. 16b+79 = columns 16b-3 .. 16b+16); lanes >= 1 read zeros.
+    auto hv_load = [&](int b, int (&hv)[kBLK]) {
+        int4v win[5];
+#pragma unroll
+        for (int j = 0; j < 5; ++j)
+            win[j] = lds_ld4(lane == 0 ? ring_in + 16u * (uint32_t)((4 * b - 48 + j) & (kRing - 1)) : L.zero);
+#pragma unroll
+        for (int u = 0; u < kBLK; ++u) hv[u] = win[(u + 3) >> 2][(u + 3) & 3];
+        if constexpr (GSA_KNOB & 1)
+            for (int u = 0; u < kBLK; ++u) hv[u] = 0;
+    };
+    auto letters_load = [&](int b, int4v (&lx)[4]) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) lx[q] = lds_ld4(xo_addr(16 * b + 4 * q));
+    };
+    auto raw_ld = [&](uint32_t ad) {
+        return __hip_atomic_load((int*)__builtin_assume_aligned(smem + ad, 4), __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_WORKGROUP);
+    };
+
+    // block b may start once: the row above is valid up to the halo of block b+1, ring_out
+    // has room for block b, and (strip 0) the letters of block b+2 are published
+    auto ready = [&](int pin, int pco, int pxo, int b) {
+        if constexpr ((GSA_KNOB & 2) != 0) return true;
+        bool ok = pin >= min(16 * b + 32, Cp + 1) && pco >= 16 * b - 307;
+        if (w == 0) ok = ok && pxo >= min(16 * b + 48, Cp + 1);
+        return ok;
+    };
+    // bounded spin until ready(b); false on time-out / error
+    auto wait_ready = [&](int& pin, int& pco, int& pxo, int b) {
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        while (!ready(pin, pco, pxo, b))
+        {
+            __builtin_amdgcn_s_sleep(1);
+            if (__builtin_amdgcn_s_memrealtime() - t0 > kSpinLimit || err_set(a))
+            {
+                atomicOr(a.err, 1u);
+                return false;
+            }
+            pin = flag_ld(fin);
+            pco = flag_ld(fcout);
+            if (w == 0) pxo = flag_ld(F + kFXo);
+        }
+        return true;
+    };
+
+    // ---- prologue: halo of block 0, letters of blocks 0 and 1, S of block 0 ----
+    if (w == 0) tstamp(a, tk, 0, lane);
+    int pin = flag_ld(fin), pco = flag_ld(fcout), pxo = (w == 0) ? flag_ld(F + kFXo) : 0;
+    if (!wait_ready(pin, pco, pxo, -1)) return;
+    if (w == 0) tstamp(a, tk, 1, lane);
+    cbar();
+    int hvA[kBLK], hvB[kBLK];
+    int4v lxA[4], lxB[4];
+    int2v sA[kBLK], sB[kBLK];
+    hv_load(0, hvA);
+    letters_load(0, lxA);
+    letters_load(1, lxB);
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) sA[4 * q + u] = lds_ld2((uint32_t)lxA[q][u] + laneoff);
+
+    int A = 0, B = 0, Cc = 0, D = 0, dA = 0;
+    // full mode: per-lane part of (i+j)*g and row pointers
+    const int vb = (r0 + 3 * lane) * g;
+    const bool wave_rows_ok = r0 + kWaveRows - 1 <= a.R;  // every row of the strip is stored
+    bool rowok[kK];
+    int* rowp[kK];
+#pragma unroll
+    for (int k = 0; k < kK; ++k)
+    {
+        const int r = r0 + kK * lane + k;
+        rowok[k] = (MODE == kModeFull) && r <= a.R;
+        rowp[k] = (MODE == kModeFull) ? a.score + (size_t)(rowok[k] ? r : 0) * (size_t)a.ld : nullptr;
+    }
+    int cap[kK] = {0, 0, 0, 0};
+    int kg[7];  // (k+u)*g, scalar
+#pragma unroll
+    for (int i = 0; i < 7; ++i) kg[i] = __builtin_amdgcn_readfirstlane(i * g);
+    int rpin = pin, rpco = pco, rpxo = pxo;  // progress words as loaded (VGPR), checked a block later
+
+    // compute block b with (scur, hvcur); issue snext from lnext (letters of b+1), letters of
+    // b+2 into lfree, and hvnext
+    auto block = [&](int b, int2v (&scur)[kBLK], int2v (&snext)[kBLK], int4v (&lnext)[4], int4v (&lfree)[4],
+                     int (&hvcur)[kBLK], int (&hvnext)[kBLK], auto capT) {
+        constexpr bool CAP = decltype(capT)::value;
+        const int cb = CAP ? ((16 * b) / a.tBx) * a.tBx : 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+        {
+            const int t0 = 16 * b + 4 * q;
+            lfree[q] = lds_ld4(xo_addr(t0 + 32));
+#pragma unroll
+            for (int u = 0; u < 4; ++u) snext[4 * q + u] = lds_ld2((uint32_t)lnext[q][u] + laneoff);
+            int Xa[4], Xb[4], Xc[4], Xd[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+            {
+                const int2v sv = scur[4 * q + u];
+                const int up = shr1z(D) + hvcur[4 * q + u];
+                const int na = max(max(dA + (int)(short)sv.x, up), A);
+                const int nb = max(max(A + (sv.x >> 16), na), B);
+                const int nc = max(max(B + (int)(short)sv.y, nb), Cc);
+                const int nd = max(max(Cc + (sv.y >> 16), nc), D);
+                dA = up;
+                A = na;
+                B = nb;
+                Cc = nc;
+                D = nd;
+                Xa[u] = na;
+                Xb[u] = nb;
+                Xc[u] = nc;
+                Xd[u] = nd;
+                if constexpr (CAP)
+                {
+                    const bool hit = (t0 + u - lane) == cb;
+                    cap[0] = hit ? na : cap[0];
+                    cap[1] = hit ? nb : cap[1];
+                    cap[2] = hit ? nc : cap[2];
+                    cap[3] = hit ? nd : cap[3];
+                }
+            }
+            // hand-off: row D of 4 steps, slot (group - lane)
+            if constexpr (!(GSA_KNOB & 8))
+                lds_st4(ring_out + 16u * (uint32_t)(((t0 >> 2) - lane) & (kRing - 1)), int4v {Xd[0], Xd[1], Xd[2], Xd[3]});
+            if constexpr (MODE == kModeFull)
+            {
+                const int c0 = t0 - lane;
+                const int sb = vb + __builtin_amdgcn_readfirstlane(t0 * g);  // + (k+u)*g
+                const int* X[kK] = {Xa, Xb, Xc, Xd};
+                if (t0 - 63 >= 1 && t0 + 3 <= a.C)
+                {
+                    // interior columns (wave-uniform): four 16-byte row stores; rows below the
+                    // matrix (last strip only) masked per row
+#pragma unroll
+                    for (int k = 0; k < kK; ++k)
+                        if (wave_rows_ok || rowok[k])
+                            *(int4a*)(rowp[k] + c0) = int4a {X[k][0] + sb + kg[k], X[k][1] + sb + kg[k + 1],
+                                                             X[k][2] + sb + kg[k + 2], X[k][3] + sb + kg[k + 3]};
+                }
+                else if (c0 + 3 >= 1 && c0 <= a.C)
+                {
+#pragma unroll
+                    for (int k = 0; k < kK; ++k)
+#pragma unroll
+                        for (int u = 0; u < 4; ++u)
+                            if (rowok[k] && c0 + u >= 1 && c0 + u <= a.C) rowp[k][c0 + u] = X[k][u] + sb + kg[k + u];
+                }
+            }
+            if (q == 0)
+            {
+                // halo of the next block (its progress was checked before this block)
+                hv_load(b + 1, hvnext);
+                flag_st(F + kFCons + 4 * w, 16 * (b + 1) - 3);
+                rpin = raw_ld(fin);
+                rpco = raw_ld(fcout);
+                if (w == 0) rpxo = raw_ld(F + kFXo);
+            }
+        }
+        if constexpr (CAP)
+        {
+            if (16 * b + 15 == cb + 63)
+            {
+                // header column of tile (tk, cb/tBx): entries 256w+4l+1 .. +4 (rows r0+4l+k)
+                const int jT = cb / a.tBx;
+                const int rr = r0 + kK * lane;
+                int4a v = int4a {cap[0] + (rr + cb) * g, cap[1] + (rr + 1 + cb) * g, cap[2] + (rr + 2 + cb) * g,
+                                 cap[3] + (rr + 3 + cb) * g};
+                *(int4a*)(a.hcol + ((size_t)tk * a.tcols + jT) * (size_t)(a.tBy + 1) + kWaveRows * w + kK * lane + 1) = v;
+            }
+        }
+        flag_st(F + kFProg + 4 * (w + 1), b + 1 == NB ? kBig : 16 * (b + 1) - 63);
+    };
+
+    auto run_block = [&](int b, int2v (&scur)[kBLK], int2v (&snext)[kBLK], int4v (&lnext)[4], int4v (&lfree)[4],
+                         int (&hvcur)[kBLK], int (&hvnext)[kBLK]) {
+        stamp(a, tk, w, b, 0, lane);
+        pin = __builtin_amdgcn_readfirstlane(rpin);
+        pco = __builtin_amdgcn_readfirstlane(rpco);
+        pxo = (w == 0) ? __builtin_amdgcn_readfirstlane(rpxo) : 0;
+        if (!ready(pin, pco, pxo, b))
+        {
+            if (!wait_ready(pin, pco, pxo, b)) return false;
+        }
+        cbar();
+        stamp(a, tk, w, b, 1, lane);
+        bool capblk = false;
+        if constexpr (MODE == kModeSparse)
+        {
+            const int jT = (16 * b) / a.tBx;
+            capblk = !(GSA_KNOB & 4) && jT >= 1 && jT < a.tcols && 16 * b - jT * a.tBx < 64;
+        }
+        if (capblk)
+            block(b, scur, snext, lnext, lfree, hvcur, hvnext, std::integral_constant<bool, true>());
+        else
+            block(b, scur, snext, lnext, lfree, hvcur, hvnext, std::integral_constant<bool, false>());
+        stamp(a, tk, w, b, 3, lane);
+        return true;
+    };
+
+    for (int b = 0; b < NB; b += 2)
+    {
+        if (!run_block(b, sA, sB, lxB, lxA, hvA, hvB)) return;
+        if (b + 1 < NB && !run_block(b + 1, sB, sA, lxA, lxB, hvB, hvA)) return;
+    }
+    if (w == NS - 1) tstamp(a, tk, 2, lane);
+    flag_st(F + kFCons + 4 * w, kBig);
+}
+
+// ------------------------------------------------------------------------------------
+// loader wave: letters in, the previous super-strip's last row in, our last row out
+// ------------------------------------------------------------------------------------
+template <int NS, int MODE>
+__device__ __forceinline__ void loader_wave(const StripArgs& a, const Lds& L, int tk, int lane)
+{
+    const int Cp = a.Cp;
+    const int nCh = (Cp + 1 + 63) / 64;  // 64-column chunks covering columns 0..Cp
+    const uint32_t F = L.flags;
+    const uint32_t ring0 = L.ring;
+    const bool feed = tk > 0;
+    const unsigned long long* gprev = a.gran + (size_t)(feed ? tk - 1 : 0) * a.granStride;
+    unsigned long long* gout = a.gran + (size_t)tk * a.granStride;
+    const bool pub = tk + 1 < a.nTickets;
+    constexpr int TR = kWaveRows * NS;
+    const int hrowg = (tk + 1) * TR;  // global row of our last row
+    // strips below the matrix (full mode, last super-strip) pass BIG through: the last
+    // strip that computes is the one whose progress bounds the letter ring
+    const int nAct = (MODE == kModeFull) ? min(NS, (a.R - tk * TR + kWaveRows - 1) / kWaveRows) : NS;
+    const uint32_t ringN = L.ring + (uint32_t)nAct * (kRing * 16);
+    int kx = 0;                       // next letter chunk (64 columns)
+    int hnext = feed ? 0 : Cp + 1;    // next column of the row above to feed into ring 0
+    int dnext = 0;                    // next column of our last row to drain
+    int xl = load_letter(a, lane);
+    uint64_t last = __builtin_amdgcn_s_memrealtime();
+    while (kx < nCh || hnext <= Cp || dnext <= Cp)
+    {
+        bool moved = false;
+        const int pl = flag_ld(F + kFProg + 4 * nAct);
+        const int cs0 = flag_ld(F + kFCons + 0);
+        // (1) letters of chunk kx, once the last strip no longer reads the columns they replace
+        if (kx < nCh && 64 * kx <= pl + 960)
+        {
+            const int c = 64 * kx + lane;
+            const int off = x_offset(a, c, xl);
+#pragma unroll
+            for (int m = 0; m < 4; ++m) lds_st(L.xo + xcopy_base(m) + 4u * (uint32_t)((c - m) & (kXR - 1)), off);
+            ++kx;
+            xl = load_letter(a, 64 * kx + lane);
+            flag_st(F + kFXo, kx == nCh ? kBig : 64 * kx);
+            moved = true;
+        }
+        // (2) the row above strip 0: the prefix of granules already published by the previous
+        //     super-strip -> ring 0 (ring 0 holds 512 columns: stay within 448 of strip 0)
+        if (hnext <= Cp && cs0 >= hnext + 63 - 511)
+        {
+            const int c = hnext + lane;
+            const bool in = c <= Cp;
+            unsigned long long q = in ? __hip_atomic_load(gprev + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+            const bool good = in && (uint32_t)(q >> 32) == a.epoch;
+            const uint64_t badm = __ballot(!good);
+            const int n = badm ? __builtin_ctzll(badm) : 64;  // granules arrive in column order
+            if (n > 0)
+            {
+                if (lane < n) lds_st(ring0 + ring_elem(c), (int)(uint32_t)q);
+                if (hnext == 0) tstamp(a, tk, 3, lane);
+                hnext += n;
+                flag_st(F + kFProg + 0, hnext > Cp ? kBig : hnext);
+                moved = true;
+            }
+        }
+        // (3) drain whatever prefix of our last row is complete: granules for the next
+        //     super-strip, sparse hrow
+        const int avail = min(pl, Cp + 1);
+        if (dnext < avail)
+        {
+            const int c = dnext + lane;
+            if (c < avail)
+            {
+                const int v = lds_ld(ringN + ring_elem(c));
+                if (pub)
+                    __hip_atomic_store(gout + c, ((unsigned long long)a.epoch << 32) | (uint32_t)v, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+                if constexpr (MODE == kModeSparse)
+                {
+                    if (tk + 1 < a.trows)
+                    {
+                        const int hv = v + (hrowg + c) * a.g;
+                        const int jT = c / a.tBx, jj = c - jT * a.tBx;
+                        const size_t rowbase = (size_t)(tk + 1) * a.tcols;
+                        if (jT < a.tcols) a.hrow[(rowbase + jT) * (size_t)(a.tBx + 1) + jj] = hv;
+                        if (jj == 0 && jT > 0) a.hrow[(rowbase + jT - 1) * (size_t)(a.tBx + 1) + a.tBx] = hv;
+                        if (jj == 0 && jT > 0 && jT < a.tcols) a.hcol[(rowbase + jT) * (size_t)(a.tBy + 1)] = hv;
+                    }
+                }
+            }
+            dnext = min(dnext + 64, avail);
+            flag_st(F + kFCons + 4 * NS, dnext > Cp ? kBig : dnext);
+            moved = true;
+        }
+        const uint64_t now = __builtin_amdgcn_s_memrealtime();
+        if (moved)
+            last = now;
+        else
+        {
+            if (now - last > kSpinLimit || err_set(a))
+            {
+                atomicOr(a.err, 1u);
+                return;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+}
+
+template <int NS, int MODE>
 __global__ void __launch_bounds__(64 * (NS + 1)) nw_strip_kernel(StripArgs a)
 {
-    // block lag between waves: wave w's halo lane prefetches (one block ahead) wave w-1's
-    // row-63 cells up to 2*BLK-1+63 steps past its own block start.
-    constexpr int DELTA = 2 + (kRowsPerWave + BLK - 1) / BLK;
-    constexpr int CPB = 64 / BLK;  // blocks per 64-column chunk
-    static_assert(kSR % BLK == 0 && kSR % 32 == 0 && 64 % BLK == 0, "ring geometry");
-    const int w = threadIdx.x >> 6;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
-    const bool loader = (w == NS);
     const Lds L = lds_layout<NS>(a.substsz);
-    const int g = a.g;
-    const int NB = (a.Cp + 64 + BLK - 1) / BLK + 1;  // local blocks per strip
-    const int NG = NB + DELTA * (NS - 1);           // global blocks per super-strip
-    const uint32_t my_st = L.st + (uint32_t)w * kSR * kSlot * 4;
-    const uint32_t my_prof = L.prof + (uint32_t)w * L.psz;
-    const uint32_t my_rmp = L.rmp + (uint32_t)w * kRN * 4;
-    const int rn = (w == 0) ? kHN : kSR;  // period of this wave's halo ramp
-
-    // Static halo-address ramps: lane 0 of wave w reads, at local step t, the value of the
-    // row above at column t.  Wave 0: the inter-workgroup ring; wave w>0: lane 63 of wave
-    // w-1's staging slot for its step t+63.
-    if (!loader)
-        for (int k = lane; k < rn; k += 64)
-        {
-            uint32_t v = (w == 0) ? L.hrg + 4u * (uint32_t)k
-                                  : L.st + (uint32_t)(w - 1) * kSR * kSlot * 4 + 4u * kSlot * (uint32_t)((k + 63) % kSR) +
-                                        4u * 63;
-            lds_st(my_rmp + 4 * k, (int)v);
-        }
-
+    const uint32_t F = L.flags;
     for (;;)
     {
         __syncthreads();
-        if (threadIdx.x == 0) lds_st(L.misc, (int)atomicAdd(a.ticket, 1u));
+        if (threadIdx.x == 0) lds_st(F + kFTicket, (err_set(a) ? (int)a.nTickets : (int)atomicAdd(a.ticket, 1u)));
         __syncthreads();
-        const int tk = lds_ld(L.misc);
+        const int tk = __builtin_amdgcn_readfirstlane(lds_ld(F + kFTicket));
         if (tk >= a.nTickets) break;
-
-        const int rbase = tk * kRowsPerWave * NS;     // halo row of wave 0
-        const int r0 = rbase + kRowsPerWave * w + 1;  // first real row of wave w
-        const int row = r0 - 1 + lane;                // this lane's row
-
-        for (int k = threadIdx.x; k < kXR + 64; k += 64 * (NS + 1)) lds_st(L.xo + 4 * k, a.substsz * 256);
-        if (!loader)
+        // per-super-strip state: letter ring = NEG, ring 0 = row 0 (H' = 0), progress words
+        for (int k = threadIdx.x; k < kXCopy; k += 64 * (NS + 1)) lds_st(L.xo + 4 * k, a.substsz * 512);
+        for (int k = threadIdx.x; k < kRing * 4; k += 64 * (NS + 1)) lds_st(L.ring + 4 * k, 0);
+        if (threadIdx.x < 4) lds_st(L.zero + 4 * threadIdx.x, 0);
+        if (threadIdx.x < 8)
         {
-            int y = (lane == 0) ? 0 : (row <= a.R ? a.seqY[row] : 0);
-            y = ((unsigned)y < (unsigned)a.substsz) ? y : 0;
-            const int* srow = a.subst + y * a.substsz;
-            for (int x = 0; x < a.substsz; ++x) lds_st(my_prof + 256 * x + 4 * lane, lane == 0 ? 0 : srow[x] - 2 * g);
-            lds_st(my_prof + 256 * a.substsz + 4 * lane, kNegS);
+            // nothing valid yet: -64 < every column a lane can touch (lane 63 starts at -63)
+            lds_st(F + kFProg + 4 * threadIdx.x, (threadIdx.x == 0 && tk == 0) ? kBig : -64);
+            lds_st(F + kFCons + 4 * threadIdx.x, 0);
         }
+        if (threadIdx.x == 0) lds_st(F + kFXo, 0);
         __syncthreads();
-
-        if (loader)
-        {
-            // ================= loader wave =================
-            const unsigned long long* gprev = a.gran + (size_t)(tk > 0 ? tk - 1 : 0) * a.granStride;
-            const bool hand = tk > 0;
-            auto gload = [&](int c) -> unsigned long long {
-                return (hand && c <= a.Cp) ? __hip_atomic_load(gprev + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                           : 0ull;
-            };
-            auto publish = [&](int c, int x, unsigned long long q) {
-                xo_store(L, c, x_offset(a, c, x));
-                int v = 0;
-                if (hand && c <= a.Cp) v = ((uint32_t)(q >> 32) == a.epoch) ? (int)(uint32_t)q : poll_granule(a, gprev + c);
-                lds_st(L.hrg + 4 * (c & (kHN - 1)), v);
-            };
-            // chunk 0 now; letters of chunks 1..3 and granules of chunks 1..2 in flight
-            publish(lane, load_letter(a, lane), gload(lane));
-            int xa = load_letter(a, 64 + lane), xb = load_letter(a, 128 + lane), xc = load_letter(a, 192 + lane);
-            unsigned long long qa = gload(64 + lane), qb = gload(128 + lane);
-            lds_barrier();
-            for (int G = 0; G < NG; ++G)
-            {
-                stamp(a, tk, w, G, 0, lane);
-                if (G % CPB == 0)
-                {
-                    // chunk n+1 (needed from block 4n+3's prefetch on); fetch chunk n+4 / n+3
-                    const int n = G / CPB;
-                    publish(64 * (n + 1) + lane, xa, qa);
-                    xa = xb;
-                    xb = xc;
-                    xc = load_letter(a, 64 * (n + 4) + lane);
-                    qa = qb;
-                    qb = gload(64 * (n + 3) + lane);
-                }
-                stamp(a, tk, w, G, 2, lane);
-                lds_barrier();
-            }
-        }
+        if (w == NS)
+            loader_wave<NS, MODE>(a, L, tk, lane);
         else
         {
-            // ================= compute waves =================
-            lds_barrier();
-            int c0 = 0, c1 = 0;
-            int sv[BLK];
-            const uint32_t laneoff = (lane == 0) ? 0u : my_prof + 4u * lane;
-            const int hgl = (rbase + kRowsPerWave * NS);  // global row of the super-strip's last row
-            for (int G = 0; G < NG; ++G)
-            {
-                stamp(a, tk, w, G, 0, lane);
-                const int b = G - DELTA * w;
-                if (b >= 0 && b < NB)
-                {
-                    const int t0 = BLK * b;
-                    const uint32_t st_base = my_st + 4u * kSlot * (uint32_t)(t0 % kSR) + 4u * lane;
-                    if (b == 0)
-                    {
-                        const uint32_t xo_cur = (lane == 0) ? my_rmp : L.xo + 4u * (uint32_t)((-lane) & (kXR - 1));
-                        load_block<BLK>(sv, xo_cur, laneoff);
-                    }
-                    const int t1 = t0 + BLK;
-                    const uint32_t xo_next = (lane == 0) ? my_rmp + 4u * (uint32_t)(t1 % rn)
-                                                         : L.xo + 4u * (uint32_t)((t1 - lane) & (kXR - 1));
-                    sweep_block<BLK>(c0, c1, sv, xo_next, laneoff, st_base);
-                    stamp(a, tk, w, G, 1, lane);
-
-                    if constexpr (MODE == kModeFull)
-                    {
-                        // write out columns [c0s, c0s+BLK) of the 63 rows: complete once step
-                        // c0s+BLK-1+63 ran.  Lanes hold 4 consecutive columns of one row
-                        // (16-byte stores, 4-byte aligned rows).
-                        static_assert(BLK == 16, "write-out mapping assumes 16-column blocks");
-                        constexpr int LAGB = (kRowsPerWave + BLK) / BLK;
-                        const int c0s = BLK * (b - LAGB);
-                        if (c0s + BLK > 0 && c0s <= a.C)
-                        {
-                            const int j0 = c0s + 4 * (lane & 3);
-                            // staging slot of (row l, column j0+k) is (j0+k+l) mod kSR; l = 16p + (lane>>2) + 1
-                            int sl0 = (j0 + (lane >> 2) + 1) % kSR;
-#pragma unroll
-                            for (int p = 0; p < 4; ++p)
-                            {
-                                const int l = 16 * p + (lane >> 2) + 1;
-                                const int rr = r0 - 1 + l;
-                                if (l < 64 && rr <= a.R && j0 + 3 >= 1 && j0 <= a.C)
-                                {
-                                    int v[4];
-#pragma unroll
-                                    for (int k = 0; k < 4; ++k)
-                                    {
-                                        int sl = sl0 + k;
-                                        sl = (sl >= kSR) ? sl - kSR : sl;
-                                        v[k] = lds_ld(my_st + 4u * (kSlot * (uint32_t)sl + (uint32_t)l)) + (rr + j0 + k) * g;
-                                    }
-                                    int* dst = a.score + (size_t)rr * (size_t)a.ld + j0;
-                                    if (j0 >= 1 && j0 + 3 <= a.C)
-                                        *(int4a*)dst = int4a {v[0], v[1], v[2], v[3]};
-                                    else
-                                    {
-#pragma unroll
-                                        for (int k = 0; k < 4; ++k)
-                                            if (j0 + k >= 1 && j0 + k <= a.C) dst[k] = v[k];
-                                    }
-                                }
-                                sl0 += 16;
-                                sl0 = (sl0 >= kSR) ? sl0 - kSR : sl0;
-                            }
-                        }
-                    }
-                    else
-                    {
-                        // Sparse: header column of tile (tk, jT) at column cb = jT*tBx is
-                        // complete after step cb+63.
-                        const int lo = t0 - 63, hi = t0 + BLK - 1 - 63;  // cb in [lo, hi]
-                        const int cb = (lo <= 0) ? 0 : ((lo + a.tBx - 1) / a.tBx) * a.tBx;
-                        if (cb <= hi && cb <= a.Cp - a.tBx && cb >= lo)
-                        {
-                            const int jT = cb / a.tBx;
-                            if (w == 0 || lane >= 1)
-                            {
-                                int v = lds_ld(my_st + 4u * (kSlot * (uint32_t)((cb + lane) % kSR) + (uint32_t)lane));
-                                a.hcol[((size_t)tk * a.tcols + jT) * (size_t)(a.tBy + 1) + kRowsPerWave * w + lane] =
-                                    v + (row + cb) * g;
-                            }
-                        }
-                    }
-
-                    if (w == NS - 1 && lane < BLK)
-                    {
-                        // last row of the super-strip for steps [t0, t0+BLK): column t0+lane-63
-                        const int c = t0 + lane - 63;
-                        if (c >= 0 && c <= a.Cp)
-                        {
-                            int v = lds_ld(my_st + 4u * (kSlot * (uint32_t)((t0 + lane) % kSR) + 63u));
-                            if (tk + 1 < a.nTickets)
-                            {
-                                unsigned long long q = ((unsigned long long)a.epoch << 32) | (uint32_t)v;
-                                __hip_atomic_store(a.gran + (size_t)tk * a.granStride + c, q, __ATOMIC_RELAXED,
-                                                   __HIP_MEMORY_SCOPE_AGENT);
-                            }
-                            if constexpr (MODE == kModeSparse)
-                            {
-                                if (tk + 1 < a.trows)
-                                {
-                                    const int hv = v + (hgl + c) * g;
-                                    const int jT = c / a.tBx, jj = c - jT * a.tBx;
-                                    const size_t rowbase = (size_t)(tk + 1) * a.tcols;
-                                    if (jT < a.tcols) a.hrow[(rowbase + jT) * (size_t)(a.tBx + 1) + jj] = hv;
-                                    if (jj == 0 && jT > 0) a.hrow[(rowbase + jT - 1) * (size_t)(a.tBx + 1) + a.tBx] = hv;
-                                }
-                            }
-                        }
-                    }
-                }
-                stamp(a, tk, w, G, 2, lane);
-                lds_barrier();
-            }
+            __builtin_amdgcn_s_setprio(3);
+            strip_wave<NS, MODE>(a, L, tk, w, lane);
+            __builtin_amdgcn_s_setprio(0);
         }
     }
 }
 
-// Headers: row 0 / column 0 of the full matrix, or header row of tile row 0 (Kernel A of
-// nwalign_gpu9_mlsp_diagdiagdiag.cu:15-63; column 0 comes out of the strip kernel).
+// Headers: row 0 / column 0 of the full matrix; for the sparse matrices the header row of
+// tile row 0 (Kernel A of nwalign_gpu9_mlsp_diagdiagdiag.cu:15-63), the header column of
+// tile column 0 and entry 0 of tile row 0's header columns (all plain multiples of g).
 __global__ void nw_headers_kernel(StripArgs a, int mode)
 {
     const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -411,20 +610,27 @@ __global__ void nw_headers_kernel(StripArgs a, int mode)
     }
     else
     {
-        const int64_t n = (int64_t)a.tcols * (a.tBx + 1);
-        if (tid < n)
+        const int64_t nrow = (int64_t)a.tcols * (a.tBx + 1);
+        const int64_t ncol = (int64_t)a.trows * (a.tBy + 1);
+        if (tid < nrow)
         {
             const int jT = (int)(tid / (a.tBx + 1)), jj = (int)(tid % (a.tBx + 1));
             a.hrow[tid] = (jT * a.tBx + jj) * a.g;
+            if (jj == 0) a.hcol[(size_t)jT * (size_t)(a.tBy + 1)] = jT * a.tBx * a.g;
+        }
+        if (tid < ncol)
+        {
+            const int iT = (int)(tid / (a.tBy + 1)), e = (int)(tid % (a.tBy + 1));
+            a.hcol[((size_t)iT * a.tcols) * (size_t)(a.tBy + 1) + e] = (iT * a.tBy + e) * a.g;
         }
     }
 }
 
-template <int NS, int BLK, int MODE>
+template <int NS, int MODE>
 static hipError_t launch_strip(const StripArgs& a, int grid, hipStream_t stream)
 {
     const size_t lds = strip_lds_bytes(NS, a.substsz);
-    auto kern = nw_strip_kernel<NS, BLK, MODE>;
+    auto kern = nw_strip_kernel<NS, MODE>;
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * (NS + 1)), lds, stream, a);
@@ -433,7 +639,8 @@ static hipError_t launch_strip(const StripArgs& a, int grid, hipStream_t stream)
 
 hipError_t launch_headers(const StripArgs& a, int mode, hipStream_t stream)
 {
-    int64_t n = (mode == kModeFull) ? (int64_t)(a.R > a.C ? a.R : a.C) + 1 : (int64_t)a.tcols * (a.tBx + 1);
+    int64_t n = (mode == kModeFull) ? (int64_t)(a.R > a.C ? a.R : a.C) + 1
+                                    : std::max<int64_t>((int64_t)a.tcols * (a.tBx + 1), (int64_t)a.trows * (a.tBy + 1));
     int blocks = (int)((n + 255) / 256);
     hipLaunchKernelGGL(nw_headers_kernel, dim3(blocks), dim3(256), 0, stream, a, mode);
     return hipGetLastError();
@@ -441,8 +648,10 @@ hipError_t launch_headers(const StripArgs& a, int mode, hipStream_t stream)
 
 hipError_t launch_strip_fill(const StripArgs& a, int mode, int grid, hipStream_t stream)
 {
-    if (mode == kModeFull) return launch_strip<kStripNS, kStripBLK, kModeFull>(a, grid, stream);
-    return launch_strip<kStripNS, kStripBLK, kModeSparse>(a, grid, stream);
+    if (mode == kModeSparse) return launch_strip<kSparseNS, kModeSparse>(a, grid, stream);
+    if (a.ns == 2) return launch_strip<2, kModeFull>(a, grid, stream);
+    if (a.ns == 4) return launch_strip<4, kModeFull>(a, grid, stream);
+    return launch_strip<1, kModeFull>(a, grid, stream);
 }
 
 }  // namespace gsa

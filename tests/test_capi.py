@@ -30,8 +30,8 @@ def test_library_exports_header():
 
 def test_geometry():
     g = gsa.sparse_geometry(10001, 10001, 256)
-    assert g.tileBy == gsa.sparse_tile_by() == 252
-    assert g.tileHdrMatRows == -(-10000 // 252) and g.tileHdrMatCols == -(-10000 // 256)
+    assert g.tileBy == gsa.sparse_tile_by() == 1024
+    assert g.tileHdrMatRows == -(-10000 // 1024) and g.tileHdrMatCols == -(-10000 // 256)
     assert g.hrowElems == g.tileHdrMatRows * g.tileHdrMatCols * 257
     e = gsa.sparse_geometry(1, 1, 64)  # empty sequences -> one tile (gpu9 host :419-426)
     assert (e.tileHdrMatRows, e.tileHdrMatCols) == (1, 1)

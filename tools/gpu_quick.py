@@ -15,7 +15,7 @@ def main():
     G = Golden()
     eng = gsa.Engine(0)
     print("cu_count", eng.cu_count, flush=True)
-    shapes = [(1, 1), (5, 7), (63, 64), (64, 64), (200, 300), (252, 252), (253, 300), (600, 1000), (2000, 1500)]
+    shapes = [(1, 1), (5, 7), (63, 64), (64, 64), (200, 300), (256, 256), (257, 300), (600, 1000), (1023, 500), (1025, 1029), (2000, 1500), (3100, 2222)]
     bad = 0
     for R, C in shapes:
         Y, X = random_pair(R, C, R * 31 + C)

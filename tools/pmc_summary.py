@@ -1,0 +1,15 @@
+"""Summarise tools/pmc_probe.sh output: per-counter value of the LAST nw_strip dispatch."""
+import csv, collections, glob, json, sys
+out = {}
+for f in sorted(glob.glob(sys.argv[1] + "/p*/run_counter_collection.csv")):
+    agg = collections.defaultdict(float)
+    for r in csv.DictReader(open(f)):
+        if "nw_strip" in r["Kernel_Name"]:
+            agg[(int(r["Dispatch_Id"]), r["Counter_Name"])] += float(r["Counter_Value"])
+    if not agg:
+        continue
+    last = max(d for d, _ in agg)
+    for (d, c), v in agg.items():
+        if d == last:
+            out[c] = v
+print(json.dumps(out, indent=1))

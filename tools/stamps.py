@@ -9,7 +9,7 @@ import gpuseqalign_amd as gsa
 from tests._data import Golden, random_pair
 
 ap = argparse.ArgumentParser()
-ap.add_argument("--R", type=int, default=252)
+ap.add_argument("--R", type=int, default=256)
 ap.add_argument("--C", type=int, default=20000)
 ap.add_argument("--mode", default="sparse")
 a = ap.parse_args()
@@ -28,16 +28,16 @@ n = 16 * 256 * 4
 buf = (ctypes.c_uint64 * n)()
 assert L.gsa_debug_stamps(eng._h, buf, n) == 0
 st = np.frombuffer(buf, dtype=np.uint64).reshape(16, 256, 4).astype(np.int64)
-for w in range(10):
+for w in range(8):
     s = st[w]
     if s[:, 0].max() == 0:
         continue
-    valid = (s[:, 0] > 0) & (s[:, 2] > 0)
-    idx = np.where(valid)[0]
-    idx = idx[(idx > 40) & (idx < 250)]
+    idx = np.where((s[:, 0] > 0) & (s[:, 3] > 0))[0]
+    idx = idx[(idx > 20) & (idx < 250)]
+    if len(idx) < 3:
+        continue
     blk = np.diff(s[idx, 0])
-    sweep = (s[idx, 1] - s[idx, 0]) if s[idx, 1].max() > 0 else np.zeros(len(idx))
-    post = (s[idx, 2] - s[idx, 1]) if s[idx, 1].max() > 0 else (s[idx, 2] - s[idx, 0])
-    wait = s[idx[:-1] + 1, 0] - s[idx[:-1], 2]
-    print(f"wave {w}: block {np.median(blk):.0f} cyc, sweep {np.median(sweep):.0f}, post {np.median(post):.0f}, barrier wait {np.median(wait):.0f}  (n={len(idx)})")
-    print("   sample block lengths", blk[:12].tolist())
+    wait, flags, comp = s[idx, 1] - s[idx, 0], s[idx, 2] - s[idx, 1], s[idx, 3] - s[idx, 2]
+    print(f"wave {w}: block {np.median(blk):.0f} cyc = wait {np.median(wait):.0f} + halo/flags {np.median(flags):.0f}"
+          f" + compute {np.median(comp):.0f} (+ tail {np.median(blk) - np.median(wait+flags+comp):.0f})  n={len(idx)}")
+    print("   blocks", blk[:10].tolist(), " wait", wait[:10].tolist())
