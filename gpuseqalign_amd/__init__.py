@@ -19,7 +19,7 @@ from typing import Callable, Dict, Optional, Tuple
 import numpy as np
 
 __all__ = [
-    "NwStat", "NwError", "lib", "build_library", "Engine", "AlignResult", "SparseResult",
+    "NwStat", "NwError", "lib", "build_library", "Engine", "AlignResult", "SparseResult", "PairDev",
     "NwAlgorithm", "get_nw_algorithm_map", "hash_full", "trace_full", "trace_sparse", "hash_sparse",
     "sparse_align_cost", "sparse_tile_by",
 ]
@@ -76,6 +76,13 @@ class SparseGeom(ctypes.Structure):
                 ("hrowElems", ctypes.c_int64), ("hcolElems", ctypes.c_int64)]
 
 
+class PairDev(ctypes.Structure):
+    """gsa_pair_dev (include/gsa.h): device pointers of one pair of a batched fill."""
+    _fields_ = [("seqY", ctypes.c_void_p), ("adjrows", ctypes.c_int32), ("seqX", ctypes.c_void_p),
+                ("adjcols", ctypes.c_int32), ("score", ctypes.c_void_p), ("tileHrowMat", ctypes.c_void_p),
+                ("tileHcolMat", ctypes.c_void_p)]
+
+
 _i32p = ctypes.POINTER(ctypes.c_int32)
 _vp = ctypes.c_void_p
 _i32 = ctypes.c_int32
@@ -93,6 +100,8 @@ SIGNATURES = {
     "gsa_fill_full_dev": (ctypes.c_int, [_vp, _vp, _i32, _vp, _i32, _vp, _i32, _i32, _vp, _vp]),
     "gsa_fill_sparse_dev": (ctypes.c_int, [_vp, _vp, _i32, _vp, _i32, _vp, _i32, _i32, _i32, _vp, _vp, _vp]),
     "gsa_sync": (ctypes.c_int, [_vp, _vp]),
+    "gsa_fill_full_batch_dev": (ctypes.c_int, [_vp, _i32, ctypes.POINTER(PairDev), _vp, _i32, _i32, _vp]),
+    "gsa_fill_sparse_batch_dev": (ctypes.c_int, [_vp, _i32, ctypes.POINTER(PairDev), _vp, _i32, _i32, _i32, _vp]),
     "gsa_align_full": (ctypes.c_int, [_vp, _i32p, _i32, _i32p, _i32, _i32p, _i32, _i32, _i32p, _i32p,
                                       ctypes.POINTER(_Laps)]),
     "gsa_align_sparse": (ctypes.c_int, [_vp, _i32p, _i32, _i32p, _i32, _i32p, _i32, _i32, _i32, _i32p, _i32p,
@@ -118,6 +127,8 @@ def lib():
             raise ImportError(f"{_SO} missing: run __graft_entry__.build() (hipcc --offload-arch=gfx950)")
         L = ctypes.CDLL(_SO)
         for name, (res, args) in SIGNATURES.items():
+            if os.environ.get("GSA_LIB") and not hasattr(L, name):
+                continue  # diagnostic builds of older revisions may lack newer entry points
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
@@ -247,6 +258,23 @@ class Engine:
         st = lib().gsa_fill_sparse_dev(self._h, seqY_ptr, adjrows, seqX_ptr, adjcols, subst_ptr, substsz, gapo,
                                        tileBx, hrow_ptr, hcol_ptr, stream)
         self._check(st, "gsa_fill_sparse_dev")
+
+    def fill_batch_dev(self, pairs, subst_ptr: int, substsz: int, gapo: int, mode: str = "sparse",
+                       tileBx: int = 256, stream: Optional[int] = None):
+        """One persistent launch over many pairs.  `pairs`: sequence of (seqY_ptr, adjrows,
+        seqX_ptr, adjcols, out) with out = score_ptr (full) or (hrow_ptr, hcol_ptr) (sparse)."""
+        arr = (PairDev * len(pairs))()
+        for k, (yp, ar, xp, ac, out) in enumerate(pairs):
+            arr[k].seqY, arr[k].adjrows, arr[k].seqX, arr[k].adjcols = yp, ar, xp, ac
+            if mode == "sparse":
+                arr[k].tileHrowMat, arr[k].tileHcolMat = out
+            else:
+                arr[k].score = out
+        if mode == "sparse":
+            st = lib().gsa_fill_sparse_batch_dev(self._h, len(pairs), arr, subst_ptr, substsz, gapo, tileBx, stream)
+        else:
+            st = lib().gsa_fill_full_batch_dev(self._h, len(pairs), arr, subst_ptr, substsz, gapo, stream)
+        self._check(st, "gsa_fill_%s_batch_dev" % mode)
 
     def sync(self, stream: Optional[int] = None):
         self._check(lib().gsa_sync(self._h, stream), "gsa_sync")

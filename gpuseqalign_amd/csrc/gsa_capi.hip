@@ -13,6 +13,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <new>
+#include <vector>
 
 #include "../../include/gsa.h"
 #include "nw_strip.h"
@@ -32,6 +33,16 @@ struct gsa_ctx
     // scratch buffers for the host-buffer entry points (grow-only, like DeviceArray::init)
     void* dbuf[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
     size_t dcap[5] = {0, 0, 0, 0, 0};
+    // pair descriptors of the last launches: device copy + pinned host staging slots, each
+    // slot reused only after the event recorded behind its copy has completed
+    gsa::PairDesc* desc = nullptr;
+    size_t desc_cap = 0;
+    static constexpr int kStage = 4;
+    gsa::PairDesc* stage[kStage] = {nullptr, nullptr, nullptr, nullptr};
+    size_t stage_cap[kStage] = {0, 0, 0, 0};
+    hipEvent_t stage_ev[kStage] = {nullptr, nullptr, nullptr, nullptr};
+    bool stage_used[kStage] = {false, false, false, false};
+    int stage_next = 0;
 };
 
 namespace {
@@ -79,6 +90,19 @@ int ensure_gran(gsa_ctx* ctx, size_t elems)
     return GSA_SUCCESS;
 }
 
+int ensure_desc(gsa_ctx* ctx, size_t n)
+{
+    if (ctx->desc_cap >= n && ctx->desc) return GSA_SUCCESS;
+    if (ctx->desc) (void)hipFree(ctx->desc);
+    ctx->desc = nullptr;
+    ctx->desc_cap = 0;
+    const size_t cap = std::max<size_t>(n, 64);
+    hipError_t e = hipMalloc(&ctx->desc, cap * sizeof(gsa::PairDesc));
+    if (e != hipSuccess) return fail(ctx, e, GSA_ERROR_MEMORY_ALLOCATION);
+    ctx->desc_cap = cap;
+    return GSA_SUCCESS;
+}
+
 int check_inputs(int32_t adjrows, int32_t adjcols, int32_t substsz)
 {
     if (adjrows < 1 || adjcols < 1) return GSA_ERROR_INVALID_VALUE;
@@ -102,52 +126,101 @@ int full_ns()
 // context's own stream explicitly.
 hipStream_t pick_stream(gsa_ctx*, void* stream) { return (hipStream_t)stream; }
 
-int enqueue_fill(gsa_ctx* ctx, int mode, const int32_t* seqY, int32_t adjrows, const int32_t* seqX, int32_t adjcols,
-                 const int32_t* subst, int32_t substsz, int32_t gapo, int32_t* score, int32_t tileBx, int32_t* hrow,
-                 int32_t* hcol, hipStream_t st)
+// One batched launch: headers of every pair, then the persistent strip kernel over the
+// tickets of all pairs (pair-major).  `pairs` holds device pointers.
+int enqueue_batch(gsa_ctx* ctx, int mode, int npairs, const gsa_pair_dev* pairs, const int32_t* subst, int32_t substsz,
+                  int32_t gapo, int32_t tileBx, hipStream_t st)
 {
+    if (npairs < 1 || !pairs || !subst) return GSA_ERROR_INVALID_VALUE;
+    if (substsz < 1 || substsz > 32) return GSA_ERROR_INVALID_VALUE;  // LDS profile holds <= 32 letters
     gsa::StripArgs a;
     std::memset(&a, 0, sizeof(a));
-    a.seqY = seqY;
-    a.seqX = seqX;
     a.subst = subst;
     a.substsz = substsz;
     a.g = gapo;
-    a.R = adjrows - 1;
-    a.C = adjcols - 1;
-    if (mode == gsa::kModeFull)
+    a.ns = (mode == gsa::kModeFull) ? full_ns() : gsa::kSparseNS;
+    if (mode == gsa::kModeSparse)
     {
-        a.score = score;
-        a.ld = adjcols;
-        a.Cp = a.C;
-        a.ns = full_ns();
-        a.nTickets = (a.R + gsa::kWaveRows * a.ns - 1) / (gsa::kWaveRows * a.ns);
+        if (tileBx < 64 || tileBx % 16 != 0) return GSA_ERROR_INVALID_VALUE;
+        a.tBx = tileBx;
+        a.tBy = gsa::kSparseTileBy;
     }
-    else
+    std::vector<gsa::PairDesc> hd((size_t)npairs);
+    long long tickets = 0, gran = 0, maxWork = 1;
+    for (int p = 0; p < npairs; ++p)
     {
-        gsa_sparse_geom geom;
-        int s = gsa_sparse_geometry(adjrows, adjcols, tileBx, &geom);
-        if (s != GSA_SUCCESS) return s;
-        a.hrow = hrow;
-        a.hcol = hcol;
-        a.trows = geom.tileHdrMatRows;
-        a.tcols = geom.tileHdrMatCols;
-        a.tBx = geom.tileBx;
-        a.tBy = geom.tileBy;
-        a.Cp = a.tcols * a.tBx;
-        a.ns = gsa::kSparseNS;
-        a.nTickets = a.trows;
+        const gsa_pair_dev& in = pairs[p];
+        if (in.adjrows < 1 || in.adjcols < 1 || !in.seqY || !in.seqX) return GSA_ERROR_INVALID_VALUE;
+        gsa::PairDesc& d = hd[(size_t)p];
+        std::memset(&d, 0, sizeof(d));
+        d.seqY = in.seqY;
+        d.seqX = in.seqX;
+        d.R = in.adjrows - 1;
+        d.C = in.adjcols - 1;
+        if (mode == gsa::kModeFull)
+        {
+            if (!in.score) return GSA_ERROR_INVALID_VALUE;
+            d.score = in.score;
+            d.ld = in.adjcols;
+            d.Cp = d.C;
+            // an empty row or column leaves nothing but headers to compute
+            d.nTickets = (d.C == 0) ? 0 : (d.R + gsa::kWaveRows * a.ns - 1) / (gsa::kWaveRows * a.ns);
+            maxWork = std::max<long long>(maxWork, (long long)std::max(d.R, d.C) + 1);
+        }
+        else
+        {
+            if (!in.tileHrowMat || !in.tileHcolMat) return GSA_ERROR_INVALID_VALUE;
+            gsa_sparse_geom geom;
+            int s = gsa_sparse_geometry(in.adjrows, in.adjcols, tileBx, &geom);
+            if (s != GSA_SUCCESS) return s;
+            d.hrow = in.tileHrowMat;
+            d.hcol = in.tileHcolMat;
+            d.trows = geom.tileHdrMatRows;
+            d.tcols = geom.tileHdrMatCols;
+            d.Cp = d.tcols * tileBx;
+            d.nTickets = d.trows;
+            maxWork = std::max<long long>(maxWork, std::max((long long)d.tcols * (tileBx + 1),
+                                                            (long long)d.trows * (gsa::kSparseTileBy + 1)));
+        }
+        d.ticketBase = (int)tickets;
+        d.granOff = gran;
+        tickets += d.nTickets;
+        gran += (long long)d.nTickets * ((long long)d.Cp + 1);
+        if (tickets > (1ll << 30)) return GSA_ERROR_INVALID_VALUE;
     }
     hipError_t e = hipSetDevice(ctx->device);
     if (e != hipSuccess) return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
-    // headers (row 0 / column 0, or the header row of tile row 0)
-    e = gsa::launch_headers(a, mode, st);
-    if (e != hipSuccess) return fail(ctx, e, GSA_ERROR_KERNEL_FAILURE);
-    if (a.nTickets == 0 || (mode == gsa::kModeFull && a.C == 0)) return GSA_SUCCESS;
-
-    a.granStride = (long long)a.Cp + 1;
-    int s = ensure_gran(ctx, (size_t)a.nTickets * (size_t)a.granStride);
+    int s = ensure_desc(ctx, (size_t)npairs);
     if (s != GSA_SUCCESS) return s;
+    // stage the descriptors in a pinned slot and copy them in stream order
+    const int slot = ctx->stage_next;
+    ctx->stage_next = (slot + 1) % gsa_ctx::kStage;
+    if (ctx->stage_used[slot] && (e = hipEventSynchronize(ctx->stage_ev[slot])) != hipSuccess)
+        return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
+    if (ctx->stage_cap[slot] < (size_t)npairs)
+    {
+        if (ctx->stage[slot]) (void)hipHostFree(ctx->stage[slot]);
+        ctx->stage[slot] = nullptr;
+        ctx->stage_cap[slot] = 0;
+        if ((e = hipHostMalloc((void**)&ctx->stage[slot], (size_t)npairs * sizeof(gsa::PairDesc))) != hipSuccess)
+            return fail(ctx, e, GSA_ERROR_MEMORY_ALLOCATION);
+        ctx->stage_cap[slot] = (size_t)npairs;
+    }
+    std::memcpy(ctx->stage[slot], hd.data(), (size_t)npairs * sizeof(gsa::PairDesc));
+    e = hipMemcpyAsync(ctx->desc, ctx->stage[slot], (size_t)npairs * sizeof(gsa::PairDesc), hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) e = hipEventRecord(ctx->stage_ev[slot], st);
+    if (e != hipSuccess) return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
+    ctx->stage_used[slot] = true;
+
+    a.pairs = ctx->desc;
+    a.nPairs = npairs;
+    a.nTicketsTotal = (int)tickets;
+    e = gsa::launch_headers(a, mode, maxWork, st);
+    if (e != hipSuccess) return fail(ctx, e, GSA_ERROR_KERNEL_FAILURE);
+    if (tickets == 0) return GSA_SUCCESS;
+
+    // granule stride (Cp+1) and base are per pair: the kernel takes them from the descriptor
+    if ((s = ensure_gran(ctx, (size_t)gran)) != GSA_SUCCESS) return s;
     a.gran = ctx->gran;
     a.ticket = ctx->ctl;
     a.err = ctx->ctl + 1;
@@ -156,10 +229,19 @@ int enqueue_fill(gsa_ctx* ctx, int mode, const int32_t* seqY, int32_t adjrows, c
     if (a.epoch == 0) a.epoch = ++ctx->epoch;  // 0 is the cleared-tag value
     e = hipMemsetAsync(ctx->ctl, 0, 16, st);
     if (e != hipSuccess) return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
-    const int grid = std::max(1, std::min(a.nTickets, ctx->cu_count));
+    // one pair: one workgroup per CU (its tickets are a chain); a batch: all resident slots
+    const int grid = (npairs == 1) ? std::max(1, std::min((int)tickets, ctx->cu_count)) : 0;
     e = gsa::launch_strip_fill(a, mode, grid, st);
     if (e != hipSuccess) return fail(ctx, e, GSA_ERROR_KERNEL_FAILURE);
     return GSA_SUCCESS;
+}
+
+int enqueue_fill(gsa_ctx* ctx, int mode, const int32_t* seqY, int32_t adjrows, const int32_t* seqX, int32_t adjcols,
+                 const int32_t* subst, int32_t substsz, int32_t gapo, int32_t* score, int32_t tileBx, int32_t* hrow,
+                 int32_t* hcol, hipStream_t st)
+{
+    gsa_pair_dev p {seqY, adjrows, seqX, adjcols, score, hrow, hcol};
+    return enqueue_batch(ctx, mode, 1, &p, subst, substsz, gapo, tileBx, st);
 }
 
 }  // namespace
@@ -184,6 +266,8 @@ int gsa_ctx_create(int device, gsa_ctx** out)
     if (e == hipSuccess) e = hipMemset(ctx->ctl, 0, 256);
     if (e == hipSuccess) e = hipEventCreate(&ctx->ev0);
     if (e == hipSuccess) e = hipEventCreate(&ctx->ev1);
+    for (int k = 0; k < gsa_ctx::kStage && e == hipSuccess; ++k)
+        e = hipEventCreateWithFlags(&ctx->stage_ev[k], hipEventDisableTiming);
 #if defined(GSA_STAMP) && GSA_STAMP
     if (e == hipSuccess) e = hipMalloc(&ctx->dbg, 16 * 256 * 4 * sizeof(unsigned long long));
     if (e == hipSuccess) e = hipMemset(ctx->dbg, 0, 16 * 256 * 4 * sizeof(unsigned long long));
@@ -207,6 +291,12 @@ void gsa_ctx_destroy(gsa_ctx* ctx)
     for (int k = 0; k < 5; k++)
         if (ctx->dbuf[k]) (void)hipFree(ctx->dbuf[k]);
     if (ctx->gran) (void)hipFree(ctx->gran);
+    if (ctx->desc) (void)hipFree(ctx->desc);
+    for (int k = 0; k < gsa_ctx::kStage; ++k)
+    {
+        if (ctx->stage[k]) (void)hipHostFree(ctx->stage[k]);
+        if (ctx->stage_ev[k]) (void)hipEventDestroy(ctx->stage_ev[k]);
+    }
     if (ctx->dbg) (void)hipFree(ctx->dbg);
     if (ctx->ctl) (void)hipFree(ctx->ctl);
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
@@ -269,6 +359,21 @@ int gsa_fill_sparse_dev(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, cons
     if (s != GSA_SUCCESS) return s;
     return enqueue_fill(ctx, gsa::kModeSparse, seqY, adjrows, seqX, adjcols, subst, substsz, gapo, nullptr, tileBx,
                         hrow, hcol, pick_stream(ctx, stream));
+}
+
+int gsa_fill_full_batch_dev(gsa_ctx* ctx, int32_t npairs, const gsa_pair_dev* pairs, const int32_t* subst,
+                            int32_t substsz, int32_t gapo, void* stream)
+{
+    if (!ctx) return GSA_ERROR_INVALID_VALUE;
+    return enqueue_batch(ctx, gsa::kModeFull, npairs, pairs, subst, substsz, gapo, 0, pick_stream(ctx, stream));
+}
+
+int gsa_fill_sparse_batch_dev(gsa_ctx* ctx, int32_t npairs, const gsa_pair_dev* pairs, const int32_t* subst,
+                              int32_t substsz, int32_t gapo, int32_t tileBx, void* stream)
+{
+    if (!ctx) return GSA_ERROR_INVALID_VALUE;
+    return enqueue_batch(ctx, gsa::kModeSparse, npairs, pairs, subst, substsz, gapo, tileBx,
+                         pick_stream(ctx, stream));
 }
 
 int gsa_sync(gsa_ctx* ctx, void* stream)

@@ -13,6 +13,21 @@ constexpr int kSparseNS = 4;                            // strip waves per workg
 constexpr int kSparseTileBy = kWaveRows * kSparseNS;    // = tile height of the mlsp matrices
 constexpr int kFullNSDefault = 1;                       // strip waves per workgroup, full fills
 
+// One pair of a batched fill (device-resident array; tickets of pair p are
+// [ticketBase, ticketBase + nTickets), pair-major, so every ticket depends only on lower ones).
+struct PairDesc
+{
+    const int* seqY;
+    const int* seqX;
+    int R, C, Cp, nTickets;
+    int ticketBase, trows, tcols, pad;
+    int* score;
+    long long ld;
+    int* hrow;
+    int* hcol;
+    long long granOff;  // first granule of this pair in the hand-off buffer
+};
+
 struct StripArgs
 {
     const int* seqY;  // adjrows ints, element 0 = header (unused)
@@ -39,10 +54,16 @@ struct StripArgs
     unsigned* err;
     unsigned epoch;
     unsigned long long* dbg;  // diagnostic builds only (GSA_STAMP): per-wave block time stamps
+    // batch: the per-pair fields above are loaded from pairs[] for every ticket
+    const PairDesc* pairs;
+    int nPairs;
+    int nTicketsTotal;
 };
 
 size_t strip_lds_bytes(int ns, int substsz);
-hipError_t launch_headers(const StripArgs& a, int mode, hipStream_t stream);
+// headers of every pair of the batch (grid.y = pair); maxWork = largest per-pair element count
+hipError_t launch_headers(const StripArgs& a, int mode, long long maxWork, hipStream_t stream);
+// grid <= 0: as many workgroups as can be co-resident (capped by the ticket count)
 hipError_t launch_strip_fill(const StripArgs& a, int mode, int grid, hipStream_t stream);
 
 }  // namespace gsa

@@ -87,6 +87,17 @@ __device__ __forceinline__ void flag_st(uint32_t a, int v)
 }
 __device__ __forceinline__ void cbar() { asm volatile("" ::: "memory"); }
 
+// Pointers read from the pair descriptors are global memory: every access goes through a
+// pointer of the global address space, or it would become a flat instruction (which also
+// counts against lgkmcnt and serialises against the LDS traffic of the hot loop).
+template <typename T>
+using gptr = __attribute__((address_space(1))) T*;
+template <typename T>
+__device__ __forceinline__ gptr<T> G(T* p)
+{
+    return (gptr<T>)p;
+}
+
 // lane l <- lane l-1, lane 0 <- 0 (DPP wave_shr:1, bound_ctrl zero)
 __device__ __forceinline__ int shr1z(int v) { return __builtin_amdgcn_update_dpp(0, v, 0x138, 0xF, 0xF, true); }
 
@@ -132,7 +143,7 @@ __device__ __forceinline__ int x_offset(const StripArgs& a, int c, int x)
     return ((unsigned)x < (unsigned)a.substsz ? x : 0) * 512;
 }
 
-__device__ __forceinline__ int load_letter(const StripArgs& a, int c) { return (c >= 1 && c <= a.C) ? a.seqX[c] : 0; }
+__device__ __forceinline__ int load_letter(const StripArgs& a, int c) { return (c >= 1 && c <= a.C) ? G(a.seqX)[c] : 0; }
 
 // ring slot / element of the lane-63 value of column c (written at step c+63, group (c+63)/4)
 __device__ __forceinline__ uint32_t ring_elem(int c)
@@ -203,17 +214,32 @@ __device__ __forceinline__ void strip_wave(const StripArgs& a, const Lds& L, int
         return;
     }
 
+    if constexpr (GSA_STAMP)
+    {
+        if (lane == 0 && a.dbg && tk < 4 && w < 4)
+        {
+            unsigned long long* o = a.dbg + 16200 + (tk * 4 + w) * 8;
+            o[0] = 0x5757ull;
+            o[1] = (unsigned long long)a.hcol;
+            o[2] = ((unsigned long long)(unsigned)a.R << 32) | (unsigned)a.C;
+            o[3] = ((unsigned long long)(unsigned)a.Cp << 32) | (unsigned)a.nTickets;
+            o[4] = ((unsigned long long)(unsigned)a.trows << 32) | (unsigned)a.tcols;
+            o[5] = ((unsigned long long)(unsigned)a.tBx << 32) | (unsigned)r0;
+            o[6] = (unsigned long long)a.seqY;
+            o[7] = (unsigned long long)a.gran;
+        }
+    }
     // ---- profile P[x][lane] = 4 x int16 (s(row_k, x) - 2g), row substsz = NEG ----------
     const uint32_t my_prof = L.prof + (uint32_t)w * L.psz;
     {
-        const int* srow[kK];
+        gptr<const int> srow[kK];
 #pragma unroll
         for (int k = 0; k < kK; ++k)
         {
             const int r = r0 + kK * lane + k;
-            int y = (r <= a.R) ? a.seqY[r] : 0;
+            int y = (r <= a.R) ? G(a.seqY)[r] : 0;
             y = ((unsigned)y < (unsigned)a.substsz) ? y : 0;
-            srow[k] = a.subst + y * a.substsz;
+            srow[k] = G(a.subst) + y * a.substsz;
         }
         bool bad = false;
         for (int x = 0; x < a.substsz; ++x)
@@ -313,13 +339,13 @@ __device__ __forceinline__ void strip_wave(const StripArgs& a, const Lds& L, int
     const int vb = (r0 + 3 * lane) * g;
     const bool wave_rows_ok = r0 + kWaveRows - 1 <= a.R;  // every row of the strip is stored
     bool rowok[kK];
-    int* rowp[kK];
+    gptr<int> rowp[kK];
 #pragma unroll
     for (int k = 0; k < kK; ++k)
     {
         const int r = r0 + kK * lane + k;
         rowok[k] = (MODE == kModeFull) && r <= a.R;
-        rowp[k] = (MODE == kModeFull) ? a.score + (size_t)(rowok[k] ? r : 0) * (size_t)a.ld : nullptr;
+        rowp[k] = G(a.score) + (MODE == kModeFull ? (size_t)(rowok[k] ? r : 0) * (size_t)a.ld : 0);
     }
     int cap[kK] = {0, 0, 0, 0};
     int kg[7];  // (k+u)*g, scalar
@@ -383,7 +409,7 @@ __device__ __forceinline__ void strip_wave(const StripArgs& a, const Lds& L, int
 #pragma unroll
                     for (int k = 0; k < kK; ++k)
                         if (wave_rows_ok || rowok[k])
-                            *(int4a*)(rowp[k] + c0) = int4a {X[k][0] + sb + kg[k], X[k][1] + sb + kg[k + 1],
+                            *(gptr<int4a>)(rowp[k] + c0) = int4a {X[k][0] + sb + kg[k], X[k][1] + sb + kg[k + 1],
                                                              X[k][2] + sb + kg[k + 2], X[k][3] + sb + kg[k + 3]};
                 }
                 else if (c0 + 3 >= 1 && c0 <= a.C)
@@ -414,7 +440,7 @@ __device__ __forceinline__ void strip_wave(const StripArgs& a, const Lds& L, int
                 const int rr = r0 + kK * lane;
                 int4a v = int4a {cap[0] + (rr + cb) * g, cap[1] + (rr + 1 + cb) * g, cap[2] + (rr + 2 + cb) * g,
                                  cap[3] + (rr + 3 + cb) * g};
-                *(int4a*)(a.hcol + ((size_t)tk * a.tcols + jT) * (size_t)(a.tBy + 1) + kWaveRows * w + kK * lane + 1) = v;
+                *(gptr<int4a>)(G(a.hcol) + ((size_t)tk * a.tcols + jT) * (size_t)(a.tBy + 1) + kWaveRows * w + kK * lane + 1) = v;
             }
         }
         flag_st(F + kFProg + 4 * (w + 1), b + 1 == NB ? kBig : 16 * (b + 1) - 63);
@@ -535,9 +561,9 @@ __device__ __forceinline__ void loader_wave(const StripArgs& a, const Lds& L, in
                         const int hv = v + (hrowg + c) * a.g;
                         const int jT = c / a.tBx, jj = c - jT * a.tBx;
                         const size_t rowbase = (size_t)(tk + 1) * a.tcols;
-                        if (jT < a.tcols) a.hrow[(rowbase + jT) * (size_t)(a.tBx + 1) + jj] = hv;
-                        if (jj == 0 && jT > 0) a.hrow[(rowbase + jT - 1) * (size_t)(a.tBx + 1) + a.tBx] = hv;
-                        if (jj == 0 && jT > 0 && jT < a.tcols) a.hcol[(rowbase + jT) * (size_t)(a.tBy + 1)] = hv;
+                        if (jT < a.tcols) G(a.hrow)[(rowbase + jT) * (size_t)(a.tBx + 1) + jj] = hv;
+                        if (jj == 0 && jT > 0) G(a.hrow)[(rowbase + jT - 1) * (size_t)(a.tBx + 1) + a.tBx] = hv;
+                        if (jj == 0 && jT > 0 && jT < a.tcols) G(a.hcol)[(rowbase + jT) * (size_t)(a.tBy + 1)] = hv;
                     }
                 }
             }
@@ -560,6 +586,24 @@ __device__ __forceinline__ void loader_wave(const StripArgs& a, const Lds& L, in
     }
 }
 
+// A pair descriptor into scalar registers: the loads go through the vector path (the compiler
+// cannot prove the descriptor array unclobbered after the ticket atomic), every word is then
+// made wave-uniform so nothing per-pair lives in VGPRs.
+__device__ __forceinline__ PairDesc load_desc(const PairDesc* p)
+{
+    static_assert(sizeof(PairDesc) % 4 == 0, "descriptor words");
+    constexpr int N = sizeof(PairDesc) / 4;
+    const int* w = (const int*)p;
+    union
+    {
+        int v[N];
+        PairDesc d;
+    } u;
+#pragma unroll
+    for (int k = 0; k < N; ++k) u.v[k] = __builtin_amdgcn_readfirstlane(G(w)[k]);
+    return u.d;
+}
+
 template <int NS, int MODE>
 __global__ void __launch_bounds__(64 * (NS + 1)) nw_strip_kernel(StripArgs a)
 {
@@ -570,12 +614,67 @@ __global__ void __launch_bounds__(64 * (NS + 1)) nw_strip_kernel(StripArgs a)
     for (;;)
     {
         __syncthreads();
-        if (threadIdx.x == 0) lds_st(F + kFTicket, (err_set(a) ? (int)a.nTickets : (int)atomicAdd(a.ticket, 1u)));
+        if (threadIdx.x == 0) lds_st(F + kFTicket, (err_set(a) ? a.nTicketsTotal : (int)atomicAdd(a.ticket, 1u)));
         __syncthreads();
-        const int tk = __builtin_amdgcn_readfirstlane(lds_ld(F + kFTicket));
-        if (tk >= a.nTickets) break;
+        const int tkg = __builtin_amdgcn_readfirstlane(lds_ld(F + kFTicket));
+        if constexpr (GSA_STAMP)
+        {
+            if (threadIdx.x == 0 && a.dbg && blockIdx.x < 8)
+            {
+                unsigned long long* o = a.dbg + 16100 + blockIdx.x * 8;
+                o[0] = 0xABCDull;
+                o[1] = (unsigned)tkg;
+                o[2] = (unsigned)a.nTicketsTotal;
+                o[3] = (unsigned long long)a.pairs;
+                o[4] = (unsigned)a.nPairs;
+                o[5] = __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                o[6] = (unsigned long long)a.ticket;
+            }
+        }
+        if (tkg >= a.nTicketsTotal) break;
+        // pair of this ticket: last descriptor with ticketBase <= tkg (binary search, uniform)
+        int lo = 0, hi = a.nPairs - 1;
+        while (lo < hi)
+        {
+            const int mid = (lo + hi + 1) >> 1;
+            if (__builtin_amdgcn_readfirstlane(a.pairs[mid].ticketBase) <= tkg)
+                lo = mid;
+            else
+                hi = mid - 1;
+        }
+        const PairDesc d = load_desc(a.pairs + lo);
+        StripArgs pa = a;
+        pa.seqY = d.seqY;
+        pa.seqX = d.seqX;
+        pa.R = d.R;
+        pa.C = d.C;
+        pa.Cp = d.Cp;
+        pa.nTickets = d.nTickets;
+        pa.score = d.score;
+        pa.ld = d.ld;
+        pa.hrow = d.hrow;
+        pa.hcol = d.hcol;
+        pa.trows = d.trows;
+        pa.tcols = d.tcols;
+        pa.gran = a.gran + d.granOff;
+        pa.granStride = (long long)d.Cp + 1;
+        const int tk = tkg - d.ticketBase;
+        if constexpr (GSA_STAMP)
+        {
+            // diagnostic builds: the per-pair arguments as this workgroup sees them
+            if (tkg < 64 && threadIdx.x == 0 && a.dbg)
+            {
+                unsigned long long* o = a.dbg + 16000 - 64 * 6 + tkg * 6;
+                o[0] = (unsigned long long)pa.hcol;
+                o[1] = (unsigned long long)pa.hrow;
+                o[2] = ((unsigned long long)(unsigned)pa.R << 32) | (unsigned)pa.C;
+                o[3] = ((unsigned long long)(unsigned)pa.Cp << 32) | (unsigned)pa.nTickets;
+                o[4] = ((unsigned long long)(unsigned)pa.trows << 32) | (unsigned)pa.tcols;
+                o[5] = ((unsigned long long)(unsigned)a.tBx << 32) | (unsigned)tk;
+            }
+        }
         // per-super-strip state: letter ring = NEG, ring 0 = row 0 (H' = 0), progress words
-        for (int k = threadIdx.x; k < kXCopy; k += 64 * (NS + 1)) lds_st(L.xo + 4 * k, a.substsz * 512);
+        for (int k = threadIdx.x; k < kXCopy; k += 64 * (NS + 1)) lds_st(L.xo + 4 * k, pa.substsz * 512);
         for (int k = threadIdx.x; k < kRing * 4; k += 64 * (NS + 1)) lds_st(L.ring + 4 * k, 0);
         if (threadIdx.x < 4) lds_st(L.zero + 4 * threadIdx.x, 0);
         if (threadIdx.x < 8)
@@ -587,11 +686,11 @@ __global__ void __launch_bounds__(64 * (NS + 1)) nw_strip_kernel(StripArgs a)
         if (threadIdx.x == 0) lds_st(F + kFXo, 0);
         __syncthreads();
         if (w == NS)
-            loader_wave<NS, MODE>(a, L, tk, lane);
+            loader_wave<NS, MODE>(pa, L, tk, lane);
         else
         {
             __builtin_amdgcn_s_setprio(3);
-            strip_wave<NS, MODE>(a, L, tk, w, lane);
+            strip_wave<NS, MODE>(pa, L, tk, w, lane);
             __builtin_amdgcn_s_setprio(0);
         }
     }
@@ -600,28 +699,33 @@ __global__ void __launch_bounds__(64 * (NS + 1)) nw_strip_kernel(StripArgs a)
 // Headers: row 0 / column 0 of the full matrix; for the sparse matrices the header row of
 // tile row 0 (Kernel A of nwalign_gpu9_mlsp_diagdiagdiag.cu:15-63), the header column of
 // tile column 0 and entry 0 of tile row 0's header columns (all plain multiples of g).
+// grid.y = pair of the batch.
 __global__ void nw_headers_kernel(StripArgs a, int mode)
 {
+    const PairDesc& d = a.pairs[blockIdx.y];
+    const gptr<int> score = G(d.score);
+    const gptr<int> hrow = G(d.hrow);
+    const gptr<int> hcol = G(d.hcol);
     const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (mode == kModeFull)
     {
-        if (tid <= a.C) a.score[tid] = (int)tid * a.g;
-        if (tid >= 1 && tid <= a.R) a.score[(size_t)tid * (size_t)a.ld] = (int)tid * a.g;
+        if (tid <= d.C) score[tid] = (int)tid * a.g;
+        if (tid >= 1 && tid <= d.R) score[(size_t)tid * (size_t)d.ld] = (int)tid * a.g;
     }
     else
     {
-        const int64_t nrow = (int64_t)a.tcols * (a.tBx + 1);
-        const int64_t ncol = (int64_t)a.trows * (a.tBy + 1);
+        const int64_t nrow = (int64_t)d.tcols * (a.tBx + 1);
+        const int64_t ncol = (int64_t)d.trows * (a.tBy + 1);
         if (tid < nrow)
         {
             const int jT = (int)(tid / (a.tBx + 1)), jj = (int)(tid % (a.tBx + 1));
-            a.hrow[tid] = (jT * a.tBx + jj) * a.g;
-            if (jj == 0) a.hcol[(size_t)jT * (size_t)(a.tBy + 1)] = jT * a.tBx * a.g;
+            hrow[tid] = (jT * a.tBx + jj) * a.g;
+            if (jj == 0) hcol[(size_t)jT * (size_t)(a.tBy + 1)] = jT * a.tBx * a.g;
         }
         if (tid < ncol)
         {
             const int iT = (int)(tid / (a.tBy + 1)), e = (int)(tid % (a.tBy + 1));
-            a.hcol[((size_t)iT * a.tcols) * (size_t)(a.tBy + 1) + e] = (iT * a.tBy + e) * a.g;
+            hcol[((size_t)iT * d.tcols) * (size_t)(a.tBy + 1) + e] = (iT * a.tBy + e) * a.g;
         }
     }
 }
@@ -633,16 +737,24 @@ static hipError_t launch_strip(const StripArgs& a, int grid, hipStream_t stream)
     auto kern = nw_strip_kernel<NS, MODE>;
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
+    if (grid <= 0)
+    {
+        // every workgroup that can be resident at once: a batch keeps them all busy
+        int per_cu = 0, dev = 0, cus = 0;
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)kern, 64 * (NS + 1), lds);
+        if (e == hipSuccess) e = hipGetDevice(&dev);
+        if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        if (e != hipSuccess) return e;
+        grid = std::max(1, std::min(a.nTicketsTotal, std::max(1, per_cu) * cus));
+    }
     hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * (NS + 1)), lds, stream, a);
     return hipGetLastError();
 }
 
-hipError_t launch_headers(const StripArgs& a, int mode, hipStream_t stream)
+hipError_t launch_headers(const StripArgs& a, int mode, long long maxWork, hipStream_t stream)
 {
-    int64_t n = (mode == kModeFull) ? (int64_t)(a.R > a.C ? a.R : a.C) + 1
-                                    : std::max<int64_t>((int64_t)a.tcols * (a.tBx + 1), (int64_t)a.trows * (a.tBy + 1));
-    int blocks = (int)((n + 255) / 256);
-    hipLaunchKernelGGL(nw_headers_kernel, dim3(blocks), dim3(256), 0, stream, a, mode);
+    int blocks = (int)((maxWork + 255) / 256);
+    hipLaunchKernelGGL(nw_headers_kernel, dim3(std::max(1, blocks), a.nPairs), dim3(256), 0, stream, a, mode);
     return hipGetLastError();
 }
 

@@ -1,0 +1,222 @@
+"""Pair sharding across GPUs (BASELINE configs[3]).
+
+Independent sequence pairs are the unit of work: one process per GPU (torch.distributed;
+backend "nccl" = RCCL over xGMI on the MI355X node, "gloo" in the CPU tests), pairs split by
+LPT (longest processing time first, weight R*C) so every rank derives the same partition with
+no exchange.  The collectives are only the ones the path needs:
+
+  * broadcast of the substitution table from rank 0 (the reference uploads it once per run,
+    src/benchmark.cpp:204-216),
+  * one all-reduce of a [n_pairs, 4] int64 table in which each rank fills only its own rows
+    (= a gather of the per-pair results to every rank),
+  * MAX all-reduce of the wall time of the timed region.
+
+No data moves between GPUs during the fills.  Inside a rank, one pair's fill occupies only
+~R/1024 (sparse) or ~R/256 (full) workgroups, so a rank's pairs go to the device as ONE
+persistent launch whose tickets span all of them (gsa_fill_*_batch_dev).
+"""
+from __future__ import annotations
+
+import dataclasses
+import heapq
+import os
+import time
+from typing import Callable, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+__all__ = ["lpt_partition", "synthetic_batch", "PairResult", "ShardReport", "shard_align", "gpu_batch_align"]
+
+
+def lpt_partition(weights: Sequence[int], n_parts: int) -> List[List[int]]:
+    """LPT: pairs in decreasing weight (ties by index) to the currently least-loaded part
+    (ties by part index).  Deterministic, so every rank computes the same split."""
+    if n_parts < 1:
+        raise ValueError("n_parts must be >= 1")
+    order = sorted(range(len(weights)), key=lambda i: (-int(weights[i]), i))
+    heap = [(0, p) for p in range(n_parts)]
+    parts: List[List[int]] = [[] for _ in range(n_parts)]
+    for i in order:
+        load, p = heapq.heappop(heap)
+        parts[p].append(i)
+        heapq.heappush(heap, (load + int(weights[i]), p))
+    return parts
+
+
+def synthetic_batch(n_pairs: int, lo: int, hi: int, seed0: int = 1000) -> List[Tuple[np.ndarray, np.ndarray]]:
+    """BASELINE configs[3]-shaped batch: pair k has lengths uniform in [lo, hi] drawn from
+    splitmix64(seed0+k); letters iid over the 20 standard amino acids (formats.synthetic_seq)."""
+    from . import formats as F
+    out = []
+    for k in range(n_pairs):
+        g = F.splitmix64(seed0 + k)
+        ry = lo + next(g) % (hi - lo + 1)
+        rx = lo + next(g) % (hi - lo + 1)
+        out.append((F.synthetic_seq(int(ry), 2 * (seed0 + k)), F.synthetic_seq(int(rx), 2 * (seed0 + k) + 1)))
+    return out
+
+
+@dataclasses.dataclass
+class PairResult:
+    index: int
+    align_cost: int
+    cells: int
+    rank: int
+
+
+@dataclasses.dataclass
+class ShardReport:
+    results: List[PairResult]  # ordered by pair index, gathered on every rank
+    elapsed_s: float           # max over ranks of the timed region
+    cells: int                 # R*C summed over all pairs
+    world: int
+
+    @property
+    def gcups(self) -> float:
+        return self.cells / self.elapsed_s / 1e9 if self.elapsed_s > 0 else 0.0
+
+
+AlignBatchFn = Callable[[List[int], List[Tuple[np.ndarray, np.ndarray]], np.ndarray, int], Tuple[List[int], float]]
+
+
+def shard_align(pairs: List[Tuple[np.ndarray, np.ndarray]], subst: Optional[np.ndarray], gapo: int,
+                align_batch: AlignBatchFn, group=None, device=None) -> ShardReport:
+    """Run `pairs` (seqY, seqX with header element; identical list on every rank) sharded over
+    the process group.  `subst` is needed on rank 0 only (broadcast to the others).
+    `align_batch(indices, pairs, subst, gapo) -> (align_costs, seconds)` runs one rank's share
+    and returns the time of its timed region; `device` is where collective tensors live
+    (a CUDA device for RCCL, None/CPU for gloo)."""
+    import torch
+    import torch.distributed as dist
+
+    dist_on = dist.is_available() and dist.is_initialized()
+    world = dist.get_world_size(group) if dist_on else 1
+    rank = dist.get_rank(group) if dist_on else 0
+    dev = torch.device(device) if device is not None else torch.device("cpu")
+
+    # substitution table from rank 0 (size first, so other ranks need not know it)
+    if dist_on:
+        n = torch.tensor([subst.size if rank == 0 else 0], dtype=torch.int64, device=dev)
+        dist.broadcast(n, src=0, group=group)
+        st = (torch.from_numpy(np.ascontiguousarray(subst, dtype=np.int32).ravel()).to(dev) if rank == 0
+              else torch.empty(int(n.item()), dtype=torch.int32, device=dev))
+        dist.broadcast(st, src=0, group=group)
+        subst = st.cpu().numpy()
+    subst = np.ascontiguousarray(subst, dtype=np.int32)
+
+    weights = [(len(y) - 1) * (len(x) - 1) for y, x in pairs]
+    mine = lpt_partition(weights, world)[rank]
+
+    if dist_on:
+        dist.barrier(group=group)
+    costs, secs = align_batch(mine, pairs, subst, gapo)
+    if len(costs) != len(mine):
+        raise RuntimeError("align_batch returned a wrong number of results")
+
+    table = torch.zeros((len(pairs), 4), dtype=torch.int64, device=dev)
+    for i, c in zip(mine, costs):
+        table[i, 0] = 1
+        table[i, 1] = int(c)
+        table[i, 2] = weights[i]
+        table[i, 3] = rank
+    t = torch.tensor([secs], dtype=torch.float64, device=dev)
+    if dist_on:
+        dist.all_reduce(table, op=dist.ReduceOp.SUM, group=group)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    tab = table.cpu().numpy()
+    if not np.all(tab[:, 0] == 1):
+        raise RuntimeError("some pairs were not aligned exactly once")
+    results = [PairResult(i, int(tab[i, 1]), int(tab[i, 2]), int(tab[i, 3])) for i in range(len(pairs))]
+    return ShardReport(results, float(t.item()), int(sum(weights)), world)
+
+
+def gpu_batch_align(device: int = 0, mode: str = "sparse", tileBx: int = 256, repeats: int = 1,
+                    out_budget_bytes: Optional[int] = None) -> AlignBatchFn:
+    """The GPU `align_batch` of one rank: inputs uploaded before the timed region, then the
+    rank's pairs in as few persistent launches as the output memory allows (one launch for
+    the whole share when it fits `out_budget_bytes`, default 60 % of free HBM): the launch's
+    ticket space spans all its pairs, so every CU stays busy.  align_cost: the last cell of
+    the full matrix, or the last tile's recompute from its headers for the sparse form (as
+    the reference's mlsp align functions, nwalign_gpu9_mlsp_diagdiagdiag.cu:713-716)."""
+    import torch
+    from . import Engine, sparse_geometry, sparse_align_cost, SparseResult
+
+    def run(indices, pairs, subst, gapo):
+        if not indices:
+            return [], 0.0
+        dev = torch.device("cuda", device)
+        substsz = int(round(np.sqrt(subst.size)))
+        eng = Engine(device)
+        stream = torch.cuda.Stream(device=dev)
+        ts = torch.from_numpy(subst).to(dev)
+        ins = [(torch.from_numpy(pairs[i][0]).to(dev), torch.from_numpy(pairs[i][1]).to(dev)) for i in indices]
+        geoms = [sparse_geometry(len(y), len(x), tileBx) if mode == "sparse" else None for y, x in ins]
+        sizes = [(g.hrowElems + g.hcolElems) if g is not None else len(y) * len(x) for (y, x), g in zip(ins, geoms)]
+        budget = out_budget_bytes
+        if budget is None:
+            free, _ = torch.cuda.mem_get_info(dev)
+            budget = int(0.6 * free)
+        # chunks of consecutive pairs whose outputs fit the budget; one flat buffer reused per chunk
+        chunks, cur, cur_sz = [], [], 0
+        for j, sz in enumerate(sizes):
+            if cur and (cur_sz + sz) * 4 > budget:
+                chunks.append(cur)
+                cur, cur_sz = [], 0
+            cur.append(j)
+            cur_sz += sz
+        chunks.append(cur)
+        flat = torch.empty(max(sum(sizes[j] for j in c) for c in chunks), dtype=torch.int32, device=dev)
+        keep = [torch.empty((g.tileHrowLen + g.tileHcolLen) if g is not None else 1, dtype=torch.int32, device=dev)
+                for g in geoms]
+        descs = []
+        for c in chunks:
+            off, d = 0, []
+            for j in c:
+                y, x = ins[j]
+                g = geoms[j]
+                if g is not None:
+                    hr = flat[off:off + g.hrowElems]
+                    hc = flat[off + g.hrowElems:off + g.hrowElems + g.hcolElems]
+                    d.append((y.data_ptr(), len(y), x.data_ptr(), len(x), (hr.data_ptr(), hc.data_ptr()), hr, hc))
+                else:
+                    sc = flat[off:off + sizes[j]]
+                    d.append((y.data_ptr(), len(y), x.data_ptr(), len(x), sc.data_ptr(), sc, None))
+                off += sizes[j]
+            descs.append(d)
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(max(1, repeats)):
+            for c, d in zip(chunks, descs):
+                eng.fill_batch_dev([e[:5] for e in d], ts.data_ptr(), substsz, gapo, mode=mode, tileBx=tileBx,
+                                   stream=stream.cuda_stream)
+                # result slices, in stream order behind the fill: last cell / last tile's headers
+                with torch.cuda.stream(stream):
+                    for j, e in zip(c, d):
+                        g = geoms[j]
+                        if g is None:
+                            keep[j].copy_(e[5][-1:])
+                        else:
+                            last = g.tileHdrMatRows * g.tileHdrMatCols - 1
+                            keep[j][:g.tileHrowLen].copy_(e[5][last * g.tileHrowLen:(last + 1) * g.tileHrowLen])
+                            keep[j][g.tileHrowLen:].copy_(e[6][last * g.tileHcolLen:(last + 1) * g.tileHcolLen])
+        eng.sync(stream.cuda_stream)
+        torch.cuda.synchronize(dev)
+        secs = (time.perf_counter() - t0) / max(1, repeats)
+        costs = []
+        for j, g in enumerate(geoms):
+            v = keep[j].cpu().numpy()
+            if g is None:
+                costs.append(int(v[0]))
+                continue
+            # only the last tile's header row / column are read by the recompute
+            hr = np.zeros(g.hrowElems, dtype=np.int32)
+            hc = np.zeros(g.hcolElems, dtype=np.int32)
+            last = g.tileHdrMatRows * g.tileHdrMatCols - 1
+            hr[last * g.tileHrowLen:(last + 1) * g.tileHrowLen] = v[:g.tileHrowLen]
+            hc[last * g.tileHcolLen:(last + 1) * g.tileHcolLen] = v[g.tileHrowLen:]
+            costs.append(sparse_align_cost(SparseResult(hr, hc, g, 0, {}), pairs[indices[j]][0], pairs[indices[j]][1],
+                                           subst, gapo))
+        eng.close()
+        return costs, secs
+
+    return run

@@ -88,6 +88,28 @@ int gsa_fill_sparse_dev(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, cons
                         int32_t* tileHcolMat, void* stream);
 int gsa_sync(gsa_ctx* ctx, void* stream);
 
+/* ---- batched fills: many independent pairs in ONE persistent launch ------------------- */
+/* Device pointers of one pair: score for full fills (adjrows*adjcols), the two header
+ * matrices for sparse fills (sizes from gsa_sparse_geometry). */
+typedef struct gsa_pair_dev
+{
+    const int32_t* seqY;
+    int32_t adjrows;
+    const int32_t* seqX;
+    int32_t adjcols;
+    int32_t* score;
+    int32_t* tileHrowMat;
+    int32_t* tileHcolMat;
+} gsa_pair_dev;
+/* `pairs` is a host array of `npairs` entries; results are identical to one fill per pair.
+ * The reference runs pairs one at a time through its benchmark loop (src/benchmark.cpp:
+ * 393-520); a batch replaces that loop for throughput runs (BASELINE configs[3]).
+ * Launches on one context must be ordered (same stream, or synchronised). */
+int gsa_fill_full_batch_dev(gsa_ctx* ctx, int32_t npairs, const gsa_pair_dev* pairs, const int32_t* subst,
+                            int32_t substsz, int32_t gapo, void* stream);
+int gsa_fill_sparse_batch_dev(gsa_ctx* ctx, int32_t npairs, const gsa_pair_dev* pairs, const int32_t* subst,
+                              int32_t substsz, int32_t gapo, int32_t tileBx, void* stream);
+
 /* ---- NwAlignFn equivalents, host buffers (alloc + H2D + fill + D2H, laps as the
  * reference's NwAlign_Gpu3_Ml_DiagDiag / NwAlign_Gpu9_Mlsp_DiagDiagDiag) -------------- */
 int gsa_align_full(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, const int32_t* seqX, int32_t adjcols,
