@@ -110,14 +110,14 @@ int check_inputs(int32_t adjrows, int32_t adjcols, int32_t substsz)
     return GSA_SUCCESS;
 }
 
-// Strip waves per workgroup of full fills: 1 spreads the scattered-row stores of the full
-// matrix over the most CUs; GSA_FULL_NS (1, 2 or 4) overrides it for experiments.
+// Strip waves per workgroup of full fills (1 or 2: each strip stages its output in 36 KB of
+// LDS); GSA_FULL_NS overrides the default for experiments.
 int full_ns()
 {
     static int ns = [] {
         const char* e = std::getenv("GSA_FULL_NS");
         int v = e ? std::atoi(e) : gsa::kFullNSDefault;
-        return (v == 1 || v == 2 || v == 4) ? v : gsa::kFullNSDefault;
+        return (v == 1 || v == 2) ? v : gsa::kFullNSDefault;
     }();
     return ns;
 }

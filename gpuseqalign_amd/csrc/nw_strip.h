@@ -60,7 +60,7 @@ struct StripArgs
     int nTicketsTotal;
 };
 
-size_t strip_lds_bytes(int ns, int substsz);
+size_t strip_lds_bytes(int ns, int substsz, int mode);
 // headers of every pair of the batch (grid.y = pair); maxWork = largest per-pair element count
 hipError_t launch_headers(const StripArgs& a, int mode, long long maxWork, hipStream_t stream);
 // grid <= 0: as many workgroups as can be co-resident (capped by the ticket count)

@@ -103,15 +103,25 @@ __device__ __forceinline__ int shr1z(int v) { return __builtin_amdgcn_update_dpp
 
 struct Lds
 {
-    uint32_t xo, ring, zero, flags, prof, psz;
+    uint32_t xo, ring, zero, flags, prof, psz, out;
 };
 
 // flags: prog[i] @ 4i (ring i holds the row above strip i; valid for columns < prog[i]),
 //        cons[i] @ 32+4i (ring i's reader no longer needs columns < cons[i]),
-//        xo_cols @ 64 (letter ring valid for columns < xo_cols), ticket @ 68.
-constexpr uint32_t kFProg = 0, kFCons = 32, kFXo = 64, kFTicket = 68;
+//        xo_cols @ 64 (letter ring valid for columns < xo_cols), ticket @ 68,
+//        sto[w][s] @ 80+16w+4s (full fills: blocks of strip w stored to HBM by store wave s).
+constexpr uint32_t kFProg = 0, kFCons = 32, kFXo = 64, kFTicket = 68, kFSto = 80;
+// Full fills: store waves per workgroup (<= 4; full fills use NS <= 2).  One wave sustains ~5.5 B/clk of 16-byte stores
+// whatever the pattern (tools/ubench/store_ubench.hip); a strip emits 1 KB per step.
+constexpr int kStoreWaves = 3;
 
-template <int NS>
+// Full fills: each strip stages its H' values in LDS, [row 0..255][step mod 32], and the
+// loader wave stores them row-contiguously.  144-byte rows: 32 slots
+// + 16 bytes of pad (16-byte aligned rows for ds_*_b128).
+constexpr uint32_t kOutRow = 32 * 4 + 16;
+constexpr uint32_t kOutStrip = kWaveRows * kOutRow;
+
+template <int NS, int MODE>
 __device__ __forceinline__ Lds lds_layout(int substsz)
 {
     static_assert(NS >= 1 && NS <= 7, "flag layout");
@@ -122,12 +132,14 @@ __device__ __forceinline__ Lds lds_layout(int substsz)
     L.zero = L.ring + (NS + 1) * kRing * 16;
     L.flags = L.zero + 16;
     L.prof = L.flags + 128;
+    L.out = L.prof + NS * L.psz;
     return L;
 }
 
-size_t strip_lds_bytes(int ns, int substsz)
+size_t strip_lds_bytes(int ns, int substsz, int mode)
 {
-    return (size_t)4 * kXCopy + (size_t)(ns + 1) * kRing * 16 + 16 + 128 + (size_t)ns * (substsz + 1) * 512;
+    return (size_t)4 * kXCopy + (size_t)(ns + 1) * kRing * 16 + 16 + 128 + (size_t)ns * (substsz + 1) * 512 +
+           (mode == kModeFull ? (size_t)ns * kOutStrip : 0);
 }
 
 __device__ __forceinline__ bool err_set(const StripArgs& a)
@@ -268,7 +280,8 @@ __device__ __forceinline__ void strip_wave(const StripArgs& a, const Lds& L, int
     auto xo_addr = [&](int t0) { return xo_base + 16u * (uint32_t)(((t0 >> 2) + lanepos) & (kXR / 4 - 1)); };
     const uint32_t ring_in = L.ring + (uint32_t)w * (kRing * 16);
     const uint32_t ring_out = L.ring + (uint32_t)(w + 1) * (kRing * 16);
-    const uint32_t fin = F + kFProg + 4 * w, fcout = F + kFCons + 4 * (w + 1);
+    const uint32_t fin = F + kFProg + 4 * w, fcout = F + kFCons + 4 * (w + 1), fsto = F + kFSto + 16 * w;
+    const uint32_t out_w = L.out + (uint32_t)w * kOutStrip + (uint32_t)lane * 4 * kOutRow;
 
     // halo window of block b: lane-63 slots of the row above for groups 4b+15 .. 4b+19
     // (steps 16b+60 .. 16b+79 = columns 16b-3 .. 16b+16); lanes >= 1 read zeros.
@@ -293,16 +306,18 @@ __device__ __forceinline__ void strip_wave(const StripArgs& a, const Lds& L, int
 
     // block b may start once: the row above is valid up to the halo of block b+1, ring_out
     // has room for block b, and (strip 0) the letters of block b+2 are published
-    auto ready = [&](int pin, int pco, int pxo, int b) {
+    // (full fills) and the loader has stored block b-2 whose staging slots block b reuses
+    auto ready = [&](int pin, int pco, int pxo, int psto, int b) {
         if constexpr ((GSA_KNOB & 2) != 0) return true;
         bool ok = pin >= min(16 * b + 32, Cp + 1) && pco >= 16 * b - 307;
         if (w == 0) ok = ok && pxo >= min(16 * b + 48, Cp + 1);
+        if constexpr (MODE == kModeFull) ok = ok && psto >= b - 1;
         return ok;
     };
     // bounded spin until ready(b); false on time-out / error
-    auto wait_ready = [&](int& pin, int& pco, int& pxo, int b) {
+    auto wait_ready = [&](int& pin, int& pco, int& pxo, int& psto, int b) {
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        while (!ready(pin, pco, pxo, b))
+        while (!ready(pin, pco, pxo, psto, b))
         {
             __builtin_amdgcn_s_sleep(1);
             if (__builtin_amdgcn_s_memrealtime() - t0 > kSpinLimit || err_set(a))
@@ -313,14 +328,20 @@ __device__ __forceinline__ void strip_wave(const StripArgs& a, const Lds& L, int
             pin = flag_ld(fin);
             pco = flag_ld(fcout);
             if (w == 0) pxo = flag_ld(F + kFXo);
+            if constexpr (MODE == kModeFull)
+            {
+                psto = flag_ld(fsto);
+#pragma unroll
+                for (int k = 1; k < kStoreWaves; ++k) psto = min(psto, flag_ld(fsto + 4 * k));
+            }
         }
         return true;
     };
 
     // ---- prologue: halo of block 0, letters of blocks 0 and 1, S of block 0 ----
     if (w == 0) tstamp(a, tk, 0, lane);
-    int pin = flag_ld(fin), pco = flag_ld(fcout), pxo = (w == 0) ? flag_ld(F + kFXo) : 0;
-    if (!wait_ready(pin, pco, pxo, -1)) return;
+    int pin = flag_ld(fin), pco = flag_ld(fcout), pxo = (w == 0) ? flag_ld(F + kFXo) : 0, psto = 0;
+    if (!wait_ready(pin, pco, pxo, psto, -1)) return;
     if (w == 0) tstamp(a, tk, 1, lane);
     cbar();
     int hvA[kBLK], hvB[kBLK];
@@ -335,23 +356,8 @@ __device__ __forceinline__ void strip_wave(const StripArgs& a, const Lds& L, int
         for (int u = 0; u < 4; ++u) sA[4 * q + u] = lds_ld2((uint32_t)lxA[q][u] + laneoff);
 
     int A = 0, B = 0, Cc = 0, D = 0, dA = 0;
-    // full mode: per-lane part of (i+j)*g and row pointers
-    const int vb = (r0 + 3 * lane) * g;
-    const bool wave_rows_ok = r0 + kWaveRows - 1 <= a.R;  // every row of the strip is stored
-    bool rowok[kK];
-    gptr<int> rowp[kK];
-#pragma unroll
-    for (int k = 0; k < kK; ++k)
-    {
-        const int r = r0 + kK * lane + k;
-        rowok[k] = (MODE == kModeFull) && r <= a.R;
-        rowp[k] = G(a.score) + (MODE == kModeFull ? (size_t)(rowok[k] ? r : 0) * (size_t)a.ld : 0);
-    }
     int cap[kK] = {0, 0, 0, 0};
-    int kg[7];  // (k+u)*g, scalar
-#pragma unroll
-    for (int i = 0; i < 7; ++i) kg[i] = __builtin_amdgcn_readfirstlane(i * g);
-    int rpin = pin, rpco = pco, rpxo = pxo;  // progress words as loaded (VGPR), checked a block later
+    int rpin = pin, rpco = pco, rpxo = pxo, rpsto = psto;  // progress words as loaded, checked a block later
 
     // compute block b with (scur, hvcur); issue snext from lnext (letters of b+1), letters of
     // b+2 into lfree, and hvnext
@@ -399,26 +405,13 @@ __device__ __forceinline__ void strip_wave(const StripArgs& a, const Lds& L, int
                 lds_st4(ring_out + 16u * (uint32_t)(((t0 >> 2) - lane) & (kRing - 1)), int4v {Xd[0], Xd[1], Xd[2], Xd[3]});
             if constexpr (MODE == kModeFull)
             {
-                const int c0 = t0 - lane;
-                const int sb = vb + __builtin_amdgcn_readfirstlane(t0 * g);  // + (k+u)*g
-                const int* X[kK] = {Xa, Xb, Xc, Xd};
-                if (t0 - 63 >= 1 && t0 + 3 <= a.C)
+                // stage H' of the 4 rows x 4 steps; the loader wave un-shifts and stores them
+#pragma unroll
+                for (int k = 0; k < kK; ++k)
                 {
-                    // interior columns (wave-uniform): four 16-byte row stores; rows below the
-                    // matrix (last strip only) masked per row
-#pragma unroll
-                    for (int k = 0; k < kK; ++k)
-                        if (wave_rows_ok || rowok[k])
-                            *(gptr<int4a>)(rowp[k] + c0) = int4a {X[k][0] + sb + kg[k], X[k][1] + sb + kg[k + 1],
-                                                             X[k][2] + sb + kg[k + 2], X[k][3] + sb + kg[k + 3]};
-                }
-                else if (c0 + 3 >= 1 && c0 <= a.C)
-                {
-#pragma unroll
-                    for (int k = 0; k < kK; ++k)
-#pragma unroll
-                        for (int u = 0; u < 4; ++u)
-                            if (rowok[k] && c0 + u >= 1 && c0 + u <= a.C) rowp[k][c0 + u] = X[k][u] + sb + kg[k + u];
+                    const int* X[kK] = {Xa, Xb, Xc, Xd};
+                    lds_st4(out_w + (uint32_t)k * kOutRow + (uint32_t)(t0 & 31) * 4,
+                            int4v {X[k][0], X[k][1], X[k][2], X[k][3]});
                 }
             }
             if (q == 0)
@@ -429,6 +422,12 @@ __device__ __forceinline__ void strip_wave(const StripArgs& a, const Lds& L, int
                 rpin = raw_ld(fin);
                 rpco = raw_ld(fcout);
                 if (w == 0) rpxo = raw_ld(F + kFXo);
+                if constexpr (MODE == kModeFull)
+                {
+                    rpsto = raw_ld(fsto);
+#pragma unroll
+                    for (int k = 1; k < kStoreWaves; ++k) rpsto = min(rpsto, raw_ld(fsto + 4 * k));
+                }
             }
         }
         if constexpr (CAP)
@@ -452,9 +451,10 @@ __device__ __forceinline__ void strip_wave(const StripArgs& a, const Lds& L, int
         pin = __builtin_amdgcn_readfirstlane(rpin);
         pco = __builtin_amdgcn_readfirstlane(rpco);
         pxo = (w == 0) ? __builtin_amdgcn_readfirstlane(rpxo) : 0;
-        if (!ready(pin, pco, pxo, b))
+        psto = (MODE == kModeFull) ? __builtin_amdgcn_readfirstlane(rpsto) : 0;
+        if (!ready(pin, pco, pxo, psto, b))
         {
-            if (!wait_ready(pin, pco, pxo, b)) return false;
+            if (!wait_ready(pin, pco, pxo, psto, b)) return false;
         }
         cbar();
         stamp(a, tk, w, b, 1, lane);
@@ -604,12 +604,94 @@ __device__ __forceinline__ PairDesc load_desc(const PairDesc* p)
     return u.d;
 }
 
+// ------------------------------------------------------------------------------------
+// store wave (full fills): the strips' staged H' blocks -> HBM, row-contiguous, un-shifted.
+// Its own wave because it issues no vector loads: a wave's vmcnt retires in order, so any
+// load behind these stores would wait for their write acknowledgements.
+// ------------------------------------------------------------------------------------
+template <int NS>
+__device__ __forceinline__ void store_wave(const StripArgs& a, const Lds& L, int tk, int sw, int lane)
+{
+    constexpr int TR = kWaveRows * NS;
+    const uint32_t F = L.flags;
+    const int NB = (a.Cp + 64 + kBLK - 1) / kBLK;  // blocks per strip (as strip_wave)
+    const int nAct = min(NS, (a.R - tk * TR + kWaveRows - 1) / kWaveRows);
+    const int q = lane & 3;
+    int sb[NS];  // next block to store, per strip
+#pragma unroll
+    for (int w = 0; w < NS; ++w) sb[w] = (w < nAct) ? 0 : NB;
+    auto left = [&]() {
+        bool any = false;
+#pragma unroll
+        for (int w = 0; w < NS; ++w) any |= sb[w] < NB;
+        return any;
+    };
+    uint64_t last = __builtin_amdgcn_s_memrealtime();
+    while (left())
+    {
+        bool moved = false;
+#pragma unroll
+        for (int w = 0; w < NS; ++w)
+        {
+            if (sb[w] >= NB) continue;
+            const int pw = flag_ld(F + kFProg + 4 * (w + 1));
+            const int done = (pw >= kBig) ? NB : (pw + 63) / 16;  // blocks completed by strip w
+            if (sb[w] >= done) continue;
+            cbar();
+            const int bs = sb[w];
+            const int r0w = tk * TR + kWaveRows * w + 1;
+            const uint32_t ob = L.out + (uint32_t)w * kOutStrip + (uint32_t)((16 * bs) & 31) * 4;
+#pragma unroll 4
+            for (int j = sw; j < 16; j += kStoreWaves)
+            {
+                const int rl = 16 * j + (lane >> 2);  // local row; its owner lane is rl/4
+                const int4v v = lds_ld4(ob + (uint32_t)rl * kOutRow + (uint32_t)q * 16);
+                const int r = r0w + rl;
+                const int c = 16 * bs + 4 * q - (rl >> 2);  // column of v.x (step 16bs+4q, lane rl/4)
+                if (r <= a.R && c + 3 >= 1 && c <= a.C)
+                {
+                    const int base = (r + c) * a.g;
+                    const gptr<int> dst = G(a.score) + (size_t)r * (size_t)a.ld + c;
+                    if (c >= 1 && c + 3 <= a.C)
+                        *(gptr<int4a>)dst =
+                            int4a {v.x + base, v.y + base + a.g, v.z + base + 2 * a.g, v.w + base + 3 * a.g};
+                    else
+                    {
+#pragma unroll
+                        for (int e = 0; e < 4; ++e)
+                            if (c + e >= 1 && c + e <= a.C) dst[e] = v[e] + base + e * a.g;
+                    }
+                }
+            }
+            sb[w] = bs + 1;
+            flag_st(F + kFSto + 16 * w + 4 * sw, sb[w]);  // after the block's LDS reads (in order)
+            moved = true;
+        }
+        const uint64_t now = __builtin_amdgcn_s_memrealtime();
+        if (moved)
+            last = now;
+        else
+        {
+            if (now - last > kSpinLimit || err_set(a))
+            {
+                atomicOr(a.err, 1u);
+                return;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+}
+
+// waves per workgroup: NS strips + loader (+ store waves for full fills)
 template <int NS, int MODE>
-__global__ void __launch_bounds__(64 * (NS + 1)) nw_strip_kernel(StripArgs a)
+constexpr int kWaves = NS + 1 + (MODE == kModeFull ? kStoreWaves : 0);
+
+template <int NS, int MODE>
+__global__ void __launch_bounds__(64 * (NS + 1 + (MODE == kModeFull ? kStoreWaves : 0))) nw_strip_kernel(StripArgs a)
 {
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
-    const Lds L = lds_layout<NS>(a.substsz);
+    const Lds L = lds_layout<NS, MODE>(a.substsz);
     const uint32_t F = L.flags;
     for (;;)
     {
@@ -674,18 +756,23 @@ __global__ void __launch_bounds__(64 * (NS + 1)) nw_strip_kernel(StripArgs a)
             }
         }
         // per-super-strip state: letter ring = NEG, ring 0 = row 0 (H' = 0), progress words
-        for (int k = threadIdx.x; k < kXCopy; k += 64 * (NS + 1)) lds_st(L.xo + 4 * k, pa.substsz * 512);
-        for (int k = threadIdx.x; k < kRing * 4; k += 64 * (NS + 1)) lds_st(L.ring + 4 * k, 0);
+        for (int k = threadIdx.x; k < kXCopy; k += 64 * kWaves<NS, MODE>) lds_st(L.xo + 4 * k, pa.substsz * 512);
+        for (int k = threadIdx.x; k < kRing * 4; k += 64 * kWaves<NS, MODE>) lds_st(L.ring + 4 * k, 0);
         if (threadIdx.x < 4) lds_st(L.zero + 4 * threadIdx.x, 0);
         if (threadIdx.x < 8)
         {
             // nothing valid yet: -64 < every column a lane can touch (lane 63 starts at -63)
             lds_st(F + kFProg + 4 * threadIdx.x, (threadIdx.x == 0 && tk == 0) ? kBig : -64);
             lds_st(F + kFCons + 4 * threadIdx.x, 0);
+            lds_st(F + kFSto + 4 * threadIdx.x, 0);  // sto[0..1][0..3]
         }
         if (threadIdx.x == 0) lds_st(F + kFXo, 0);
         __syncthreads();
-        if (w == NS)
+        if (w > NS)
+        {
+            if constexpr (MODE == kModeFull) store_wave<NS>(pa, L, tk, w - NS - 1, lane);
+        }
+        else if (w == NS)
             loader_wave<NS, MODE>(pa, L, tk, lane);
         else
         {
@@ -733,7 +820,7 @@ __global__ void nw_headers_kernel(StripArgs a, int mode)
 template <int NS, int MODE>
 static hipError_t launch_strip(const StripArgs& a, int grid, hipStream_t stream)
 {
-    const size_t lds = strip_lds_bytes(NS, a.substsz);
+    const size_t lds = strip_lds_bytes(NS, a.substsz, MODE);
     auto kern = nw_strip_kernel<NS, MODE>;
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
@@ -741,13 +828,13 @@ static hipError_t launch_strip(const StripArgs& a, int grid, hipStream_t stream)
     {
         // every workgroup that can be resident at once: a batch keeps them all busy
         int per_cu = 0, dev = 0, cus = 0;
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)kern, 64 * (NS + 1), lds);
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)kern, 64 * kWaves<NS, MODE>, lds);
         if (e == hipSuccess) e = hipGetDevice(&dev);
         if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
         if (e != hipSuccess) return e;
         grid = std::max(1, std::min(a.nTicketsTotal, std::max(1, per_cu) * cus));
     }
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * (NS + 1)), lds, stream, a);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * kWaves<NS, MODE>), lds, stream, a);
     return hipGetLastError();
 }
 
@@ -762,7 +849,6 @@ hipError_t launch_strip_fill(const StripArgs& a, int mode, int grid, hipStream_t
 {
     if (mode == kModeSparse) return launch_strip<kSparseNS, kModeSparse>(a, grid, stream);
     if (a.ns == 2) return launch_strip<2, kModeFull>(a, grid, stream);
-    if (a.ns == 4) return launch_strip<4, kModeFull>(a, grid, stream);
     return launch_strip<1, kModeFull>(a, grid, stream);
 }
 
