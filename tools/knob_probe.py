@@ -7,7 +7,7 @@ import sys, json; sys.path.insert(0, "%s")
 import gpuseqalign_amd as gsa
 from tools.gpu_perf import run
 eng = gsa.Engine(0)
-for R, C, mode, tbx in [(256, 20000, "sparse", 256), (256, 20000, "sparse", 4096), (256, 20000, "full", 256), (1024, 20000, "sparse", 256)]:
+for R, C, mode, tbx in [(256, 20000, "sparse", 256), (256, 20000, "sparse", 4096), (256, 20000, "full", 256), (10000, 10000, "full", 256)]:
     r = run(eng, R, C, mode, tbx, reps=3)
     steps = C + 64
     print(json.dumps({"lib": "%s", "R": R, "C": C, "mode": mode, "tBx": tbx, "ms": round(r["ms"], 4), "cyc_per_step@2.4GHz": round(r["ms"] * 2.4e6 / steps, 1)}))
