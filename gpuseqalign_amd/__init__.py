@@ -83,6 +83,14 @@ class PairDev(ctypes.Structure):
                 ("tileHcolMat", ctypes.c_void_p)]
 
 
+class CheckResult(ctypes.Structure):
+    """gsa_check_result (include/gsa.h): outcome of a device-side verification."""
+    _fields_ = [("checked", ctypes.c_int64), ("mismatches", ctypes.c_int64), ("first", ctypes.c_int64)]
+
+    def as_dict(self):
+        return {"checked": int(self.checked), "mismatches": int(self.mismatches), "first": int(self.first)}
+
+
 _i32p = ctypes.POINTER(ctypes.c_int32)
 _vp = ctypes.c_void_p
 _i32 = ctypes.c_int32
@@ -116,6 +124,13 @@ SIGNATURES = {
                                           _i32, _i32]),
     "gsa_sparse_align_cost": (_i32, [_i32p, _i32p, ctypes.POINTER(SparseGeom), _i32p, _i32, _i32p, _i32, _i32p,
                                      _i32, _i32]),
+    "gsa_check_sparse_dev": (ctypes.c_int, [_vp, _vp, _i32, _vp, _i32, _vp, _i32, _i32, ctypes.POINTER(SparseGeom),
+                                            _vp, _vp, ctypes.POINTER(CheckResult), _vp]),
+    "gsa_check_full_dev": (ctypes.c_int, [_vp, _vp, _i32, _vp, _i32, _vp, _i32, _i32, _vp,
+                                          ctypes.POINTER(CheckResult), _vp]),
+    "gsa_trace_sparse_dev": (ctypes.c_int, [_vp, _vp, _i32, _vp, _i32, _vp, _i32, _i32, ctypes.POINTER(SparseGeom),
+                                            _vp, _vp, ctypes.c_char_p, _i64, ctypes.POINTER(ctypes.c_int64),
+                                            ctypes.POINTER(ctypes.c_uint32), _i32p, _vp]),
 }
 
 
@@ -278,6 +293,43 @@ class Engine:
 
     def sync(self, stream: Optional[int] = None):
         self._check(lib().gsa_sync(self._h, stream), "gsa_sync")
+
+    # -- device-side verification ---------------------------------------
+    def check_sparse_dev(self, seqY_ptr: int, adjrows: int, seqX_ptr: int, adjcols: int, subst_ptr: int,
+                         substsz: int, gapo: int, geom: SparseGeom, hrow_ptr: int, hcol_ptr: int,
+                         stream: Optional[int] = None) -> dict:
+        """Every header value of a sparse fill against the recurrence (tile consistency);
+        synchronous.  Returns {"checked", "mismatches", "first"}."""
+        r = CheckResult()
+        st = lib().gsa_check_sparse_dev(self._h, seqY_ptr, adjrows, seqX_ptr, adjcols, subst_ptr, substsz, gapo,
+                                        ctypes.byref(geom), hrow_ptr, hcol_ptr, ctypes.byref(r), stream)
+        self._check(st, "gsa_check_sparse_dev")
+        return r.as_dict()
+
+    def trace_sparse_dev(self, seqY_ptr: int, adjrows: int, seqX_ptr: int, adjcols: int, subst_ptr: int,
+                         substsz: int, gapo: int, geom: SparseGeom, hrow_ptr: int, hcol_ptr: int,
+                         stream: Optional[int] = None) -> Tuple[int, str, int]:
+        """NwTrace2_Sparse on the device (headers stay in HBM): (trace_hash, edit string,
+        align_cost), identical to trace_sparse()."""
+        cap = 8 * (adjrows + adjcols) + 64  # run-length string: <= 2 chars per move, digits reversed
+        buf = ctypes.create_string_buffer(cap)
+        n = ctypes.c_int64(0)
+        h = ctypes.c_uint32(0)
+        cost = ctypes.c_int32(0)
+        st = lib().gsa_trace_sparse_dev(self._h, seqY_ptr, adjrows, seqX_ptr, adjcols, subst_ptr, substsz, gapo,
+                                        ctypes.byref(geom), hrow_ptr, hcol_ptr, buf, cap, ctypes.byref(n),
+                                        ctypes.byref(h), ctypes.byref(cost), stream)
+        self._check(st, "gsa_trace_sparse_dev")
+        return int(h.value), buf.raw[:n.value].decode(), int(cost.value)
+
+    def check_full_dev(self, seqY_ptr: int, adjrows: int, seqX_ptr: int, adjcols: int, subst_ptr: int,
+                       substsz: int, gapo: int, score_ptr: int, stream: Optional[int] = None) -> dict:
+        """Every cell of a full matrix against its stored neighbours; synchronous."""
+        r = CheckResult()
+        st = lib().gsa_check_full_dev(self._h, seqY_ptr, adjrows, seqX_ptr, adjcols, subst_ptr, substsz, gapo,
+                                      score_ptr, ctypes.byref(r), stream)
+        self._check(st, "gsa_check_full_dev")
+        return r.as_dict()
 
 
 # ---- host consumers (the reference's L4) ----------------------------------------------

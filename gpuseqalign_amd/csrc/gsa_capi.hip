@@ -16,7 +16,13 @@
 #include <vector>
 
 #include "../../include/gsa.h"
+#include "nw_check.h"
 #include "nw_strip.h"
+#include "nw_trace_dev.h"
+
+namespace gsa {
+int fold_moves(const unsigned char* moves, int64_t n, char* edit, int64_t cap, int64_t* edit_len, uint32_t* trace_hash);
+}
 
 struct gsa_ctx
 {
@@ -43,6 +49,13 @@ struct gsa_ctx
     hipEvent_t stage_ev[kStage] = {nullptr, nullptr, nullptr, nullptr};
     bool stage_used[kStage] = {false, false, false, false};
     int stage_next = 0;
+    unsigned long long* chk = nullptr;  // verification results (nw_check.hip)
+    // device traceback (nw_trace_dev.hip): move bytes, [moves, cost], global move codes
+    unsigned char* tmoves = nullptr;
+    size_t tmoves_cap = 0;
+    long long* tres = nullptr;
+    unsigned* tdirs = nullptr;
+    size_t tdirs_cap = 0;
 };
 
 namespace {
@@ -125,6 +138,28 @@ int full_ns()
 // NULL is the HIP null stream, as everywhere in HIP; the host-buffer entry points use the
 // context's own stream explicitly.
 hipStream_t pick_stream(gsa_ctx*, void* stream) { return (hipStream_t)stream; }
+
+// Verification launch (nw_check.hip): zero the result words, launch, read them back.
+int run_check(gsa_ctx* ctx, gsa::CheckArgs& a, bool sparse, hipStream_t st, gsa_check_result* out)
+{
+    hipError_t e = hipSetDevice(ctx->device);
+    if (e != hipSuccess) return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
+    if (!ctx->chk && (e = hipMalloc(&ctx->chk, 64)) != hipSuccess) return fail(ctx, e, GSA_ERROR_MEMORY_ALLOCATION);
+    const unsigned long long init[3] = {0ull, 0ull, ~0ull};
+    unsigned long long res[3];
+    if ((e = hipMemcpyAsync(ctx->chk, init, sizeof(init), hipMemcpyHostToDevice, st)) != hipSuccess)
+        return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
+    a.res = ctx->chk;
+    e = sparse ? gsa::launch_check_sparse(a, ctx->cu_count, st) : gsa::launch_check_full(a, st);
+    if (e != hipSuccess) return fail(ctx, e, GSA_ERROR_KERNEL_FAILURE);
+    if ((e = hipMemcpyAsync(res, ctx->chk, sizeof(res), hipMemcpyDeviceToHost, st)) != hipSuccess ||
+        (e = hipStreamSynchronize(st)) != hipSuccess)
+        return fail(ctx, e, GSA_ERROR_KERNEL_FAILURE);
+    out->checked = (int64_t)res[0];
+    out->mismatches = (int64_t)res[1];
+    out->first = res[1] ? (int64_t)res[2] : -1;
+    return GSA_SUCCESS;
+}
 
 // One batched launch: headers of every pair, then the persistent strip kernel over the
 // tickets of all pairs (pair-major).  `pairs` holds device pointers.
@@ -292,6 +327,10 @@ void gsa_ctx_destroy(gsa_ctx* ctx)
         if (ctx->dbuf[k]) (void)hipFree(ctx->dbuf[k]);
     if (ctx->gran) (void)hipFree(ctx->gran);
     if (ctx->desc) (void)hipFree(ctx->desc);
+    if (ctx->chk) (void)hipFree(ctx->chk);
+    if (ctx->tmoves) (void)hipFree(ctx->tmoves);
+    if (ctx->tres) (void)hipFree(ctx->tres);
+    if (ctx->tdirs) (void)hipFree(ctx->tdirs);
     for (int k = 0; k < gsa_ctx::kStage; ++k)
     {
         if (ctx->stage[k]) (void)hipHostFree(ctx->stage[k]);
@@ -470,6 +509,130 @@ int gsa_align_sparse(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, const i
     if (geom_out) *geom_out = geom;
     if (laps) *laps = L;
     return GSA_SUCCESS;
+}
+
+int gsa_check_sparse_dev(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, const int32_t* seqX, int32_t adjcols,
+                         const int32_t* subst, int32_t substsz, int32_t gapo, const gsa_sparse_geom* geom,
+                         const int32_t* hrow, const int32_t* hcol, gsa_check_result* out, void* stream)
+{
+    if (!ctx || !seqY || !seqX || !subst || !geom || !hrow || !hcol || !out) return GSA_ERROR_INVALID_VALUE;
+    int s = check_inputs(adjrows, adjcols, substsz);
+    if (s != GSA_SUCCESS) return s;
+    gsa_sparse_geom g;
+    if ((s = gsa_sparse_geometry(adjrows, adjcols, geom->tileBx, &g)) != GSA_SUCCESS) return s;
+    if (std::memcmp(&g, geom, sizeof(g)) != 0) return GSA_ERROR_INVALID_VALUE;  // not this pair's geometry
+    gsa::CheckArgs a {};
+    a.seqY = seqY;
+    a.seqX = seqX;
+    a.subst = subst;
+    a.substsz = substsz;
+    a.g = gapo;
+    a.adjrows = adjrows;
+    a.adjcols = adjcols;
+    a.tBx = g.tileBx;
+    a.tBy = g.tileBy;
+    a.trows = g.tileHdrMatRows;
+    a.tcols = g.tileHdrMatCols;
+    a.hrowElems = g.hrowElems;
+    a.hrow = hrow;
+    a.hcol = hcol;
+    return run_check(ctx, a, true, pick_stream(ctx, stream), out);
+}
+
+int gsa_check_full_dev(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, const int32_t* seqX, int32_t adjcols,
+                       const int32_t* subst, int32_t substsz, int32_t gapo, const int32_t* score,
+                       gsa_check_result* out, void* stream)
+{
+    if (!ctx || !seqY || !seqX || !subst || !score || !out) return GSA_ERROR_INVALID_VALUE;
+    int s = check_inputs(adjrows, adjcols, substsz);
+    if (s != GSA_SUCCESS) return s;
+    gsa::CheckArgs a {};
+    a.seqY = seqY;
+    a.seqX = seqX;
+    a.subst = subst;
+    a.substsz = substsz;
+    a.g = gapo;
+    a.adjrows = adjrows;
+    a.adjcols = adjcols;
+    a.score = score;
+    return run_check(ctx, a, false, pick_stream(ctx, stream), out);
+}
+
+int gsa_trace_sparse_dev(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, const int32_t* seqX, int32_t adjcols,
+                         const int32_t* subst, int32_t substsz, int32_t gapo, const gsa_sparse_geom* geom,
+                         const int32_t* hrow, const int32_t* hcol, char* edit, int64_t cap, int64_t* edit_len,
+                         uint32_t* trace_hash, int32_t* align_cost, void* stream)
+{
+    if (!ctx || !seqY || !seqX || !subst || !geom || !hrow || !hcol || !edit || !edit_len || !trace_hash)
+        return GSA_ERROR_INVALID_VALUE;
+    int s = check_inputs(adjrows, adjcols, substsz);
+    if (s != GSA_SUCCESS) return s;
+    gsa_sparse_geom g;
+    if ((s = gsa_sparse_geometry(adjrows, adjcols, geom->tileBx, &g)) != GSA_SUCCESS) return s;
+    if (std::memcmp(&g, geom, sizeof(g)) != 0) return GSA_ERROR_INVALID_VALUE;
+    hipError_t e = hipSetDevice(ctx->device);
+    if (e != hipSuccess) return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
+    hipStream_t st = pick_stream(ctx, stream);
+    // start: NwTrace2_GetTileAndElemIJ(adjrows-1, adjcols-1) with its saturation (nwtrace2_sparse.cpp:8-38)
+    const int64_t i0 = adjrows - 1, j0 = adjcols - 1;
+    int64_t iT = i0 / g.tileBy, jT = j0 / g.tileBx, iE = i0 % g.tileBy, jE = j0 % g.tileBx;
+    if (iT == g.tileHdrMatRows) { iT -= 1; iE += g.tileBy; }
+    if (jT == g.tileHdrMatCols) { jT -= 1; jE += g.tileBx; }
+    const size_t nmax = (size_t)i0 + (size_t)j0 + 1;
+    if (ctx->tmoves_cap < nmax)
+    {
+        if (ctx->tmoves) (void)hipFree(ctx->tmoves);
+        ctx->tmoves = nullptr;
+        ctx->tmoves_cap = 0;
+        if ((e = hipMalloc(&ctx->tmoves, nmax)) != hipSuccess) return fail(ctx, e, GSA_ERROR_MEMORY_ALLOCATION);
+        ctx->tmoves_cap = nmax;
+    }
+    if (!ctx->tres && (e = hipMalloc(&ctx->tres, 64)) != hipSuccess) return fail(ctx, e, GSA_ERROR_MEMORY_ALLOCATION);
+    const bool dirs_lds = gsa::trace_lds_bytes(g.tileBy, g.tileBx, substsz, true) <= 160 * 1024;
+    if (!dirs_lds)
+    {
+        const size_t bytes = gsa::trace_dir_words(g.tileBy, g.tileBx) * 4;
+        if (ctx->tdirs_cap < bytes)
+        {
+            if (ctx->tdirs) (void)hipFree(ctx->tdirs);
+            ctx->tdirs = nullptr;
+            ctx->tdirs_cap = 0;
+            if ((e = hipMalloc(&ctx->tdirs, bytes)) != hipSuccess) return fail(ctx, e, GSA_ERROR_MEMORY_ALLOCATION);
+            ctx->tdirs_cap = bytes;
+        }
+    }
+    gsa::TraceArgs a {};
+    a.seqY = seqY;
+    a.seqX = seqX;
+    a.subst = subst;
+    a.substsz = substsz;
+    a.g = gapo;
+    a.adjrows = adjrows;
+    a.adjcols = adjcols;
+    a.tBx = g.tileBx;
+    a.tBy = g.tileBy;
+    a.tcols = g.tileHdrMatCols;
+    a.hrow = hrow;
+    a.hcol = hcol;
+    a.iT0 = (int)iT;
+    a.jT0 = (int)jT;
+    a.iE0 = (int)iE;
+    a.jE0 = (int)jE;
+    a.edits = ctx->tmoves;
+    a.cap = (long long)nmax;
+    a.res = ctx->tres;
+    a.dirs_scratch = dirs_lds ? nullptr : ctx->tdirs;
+    if ((e = gsa::launch_trace_sparse(a, st)) != hipSuccess) return fail(ctx, e, GSA_ERROR_KERNEL_FAILURE);
+    long long res[2] = {0, 0};
+    if ((e = hipMemcpyAsync(res, ctx->tres, sizeof(res), hipMemcpyDeviceToHost, st)) != hipSuccess ||
+        (e = hipStreamSynchronize(st)) != hipSuccess)
+        return fail(ctx, e, GSA_ERROR_KERNEL_FAILURE);
+    if (res[0] < 0 || (size_t)res[0] > nmax) return GSA_ERROR_INVALID_RESULT;
+    std::vector<unsigned char> moves((size_t)res[0]);
+    if (res[0] > 0 && (e = hipMemcpy(moves.data(), ctx->tmoves, (size_t)res[0], hipMemcpyDeviceToHost)) != hipSuccess)
+        return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
+    if (align_cost) *align_cost = (int32_t)res[1];
+    return gsa::fold_moves(moves.data(), (int64_t)res[0], edit, cap, edit_len, trace_hash);
 }
 
 }  // extern "C"

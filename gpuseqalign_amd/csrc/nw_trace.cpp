@@ -116,6 +116,21 @@ SparseView make_view(const int32_t* hrow, const int32_t* hcol, const gsa_sparse_
 
 }  // namespace
 
+namespace gsa {
+
+// Moves of a device-side walk (nw_trace_dev.hip), in walk order, folded exactly as the host
+// traces fold theirs (the final '\0' push flushes the last run).
+int fold_moves(const unsigned char* moves, int64_t n, char* edit, int64_t cap, int64_t* edit_len, uint32_t* trace_hash)
+{
+    EditTrace t;
+    for (int64_t k = 0; k < n; k++) t.push((char)moves[k]);
+    t.push('\0');
+    *trace_hash = t.finish();
+    return emit(t, edit, cap, edit_len);
+}
+
+}  // namespace gsa
+
 extern "C" {
 
 uint32_t gsa_hash_full(const int32_t* score, int32_t adjrows, int32_t adjcols)

@@ -1,0 +1,255 @@
+// nw_trace_dev.hip -- sparse (mlsp) traceback on the device.
+//
+// NwTrace2_Sparse (nwtrace2_sparse.cpp:102-257) walks from (adjrows-1, adjcols-1) to (0,0)
+// and, each time it enters a tile, recomputes that tile from its header row and column
+// (NwTrace2_AlignTile, :40-96).  Here one workgroup does the same walk on the GPU:
+//   * the tile recompute is the row scan of nw_check.hip (lanes across 64-column panels,
+//     H'[j] = max(H[i][j0], prefix-max E'), 6 DPP steps), over rows 1..iE and columns
+//     1..jE only, and instead of the values it keeps, per cell, the move the walk would take
+//     there: DIAG if H[i-1][j-1] >= H[i-1][j] and >= H[i][j-1], else UP if H[i-1][j] >=
+//     H[i][j-1], else LEFT -- the reference's comparisons in its order (:144-176), 2 bits;
+//   * the walk itself is uniform scalar control flow reading those codes back from LDS
+//     (global scratch when the tile is wider than 512 columns) and emitting one edit byte per
+//     move ('=', 'X', 'I', 'D'), in walk order; the host folds them into the reference's
+//     run-length edit string and trace hash.
+// Cells outside the real matrix are never visited and never influence a visited cell (all
+// dependencies point up / left), so the padded tile (padding letter 0) gives the same moves
+// as the reference's zeroed artificial cells.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+
+#include "nw_trace_dev.h"
+
+namespace gsa {
+
+namespace {
+
+template <typename T>
+using gptr = __attribute__((address_space(1))) T*;
+template <typename T>
+__device__ __forceinline__ gptr<T> G(T* p)
+{
+    return (gptr<T>)p;
+}
+
+__device__ __forceinline__ int wave_prefix_max(int v)
+{
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, true));   // row_shr:1
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, true));   // row_shr:2
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, true));   // row_shr:4
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, true));   // row_shr:8
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false));  // row_bcast:15
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false));  // row_bcast:31
+    return v;
+}
+
+__device__ __forceinline__ int clamp_letter(int x, int substsz) { return ((unsigned)x < (unsigned)substsz) ? x : 0; }
+
+// move codes: diagonal with equal / different letters ('=' / 'X'), up ('I'), left ('D')
+constexpr int kDiagEq = 0, kDiagX = 1, kUp = 2, kLeft = 3;
+
+}  // namespace
+
+extern __shared__ __attribute__((aligned(16))) int tsm[];
+
+// Move codes of tile (iT, jT) for rows 1..iE, columns 1..jE:
+// word ((a-1)/16 * nP + (b-1)/64) * 64 + (b-1)%64 holds rows a..a+15 of column b, 2 bits each.
+template <bool DIRS_LDS>
+__device__ void tile_moves(const TraceArgs& a, int iT, int jT, int iE, int jE, int* sub, int* colbuf, int* yb,
+                           int* yraw, int* xraw, unsigned* dirs, int lane, bool first)
+{
+    const int g = a.g, tBx = a.tBx, tBy = a.tBy;
+    const long long W = tBx + 1, H = tBy + 1;
+    const long long k = (long long)iT * a.tcols + jT;
+    const gptr<const int> hr = G(a.hrow) + k * W;
+    const gptr<const int> hc = G(a.hcol) + k * H;
+    const long long rbase = (long long)iT * tBy, cbase = (long long)jT * tBx;
+    __syncthreads();
+    for (int e = lane; e <= iE; e += 64)
+    {
+        colbuf[e] = hc[e];
+        const long long r = rbase + e;
+        const int y = r < a.adjrows ? G(a.seqY)[r] : 0;
+        yraw[e] = y;
+        yb[e] = clamp_letter(y, a.substsz) * a.substsz;
+    }
+    for (int c = lane; c <= jE; c += 64) xraw[c] = G(a.seqX)[cbase + c];  // real columns only (c <= jE)
+    __syncthreads();
+    const int nP = (tBx + 63) / 64;
+    const int nPu = (jE + 63) / 64;  // panels the walk can reach
+    for (int p = 0; p < nPu; ++p)
+    {
+        const int j0 = 64 * p;
+        const int col = j0 + 1 + lane;
+        const bool valid = col <= tBx;
+        const long long gc = cbase + col;
+        const int xo = valid ? clamp_letter(gc < a.adjcols ? G(a.seqX)[gc] : 0, a.substsz) : 0;
+        int up = valid ? hr[col] : 0;
+        const int c1 = -(lane + 1) * g, c2 = -lane * g, c3 = (lane + 1) * g;
+        const int last = min(63, tBx - 1 - j0);
+        int Lprev = __builtin_amdgcn_readfirstlane(colbuf[0]);
+        const int top = __builtin_amdgcn_readlane(up, last);
+        __syncthreads();
+        if (lane == 0) colbuf[0] = top;
+        const int xr = (col <= jE) ? xraw[col] : -1;  // raw letter of this lane's column
+        unsigned word = 0;
+        // 64 rows at a time: left boundary and letters of row i0+r sit in lane r (readlane,
+        // no LDS latency per row); the substitution value is read one row ahead
+        for (int i0 = 1; i0 <= iE; i0 += 64)
+        {
+            const int nr = min(64, iE - i0 + 1);
+            const int Lv = (lane < nr) ? colbuf[i0 + lane] : 0;
+            const int yv = (lane < nr) ? yb[i0 + lane] : 0;
+            const int yrv = (lane < nr) ? yraw[i0 + lane] : 0;
+            int s_nx = sub[__builtin_amdgcn_readfirstlane(yv) + xo];
+            for (int r = 0; r < nr; ++r)
+            {
+                const int i = i0 + r;
+                const int L = __builtin_amdgcn_readlane(Lv, r);
+                const int s = s_nx;
+                if (r + 1 < nr) s_nx = sub[__builtin_amdgcn_readlane(yv, r + 1) + xo];
+                const int diag = __builtin_amdgcn_update_dpp(Lprev, up, 0x138, 0xf, 0xf, false);  // H[i-1][b-1]
+                const int m = max(max(diag + s + c1, up + c2), L) - L;
+                const int h = wave_prefix_max(m) + L + c3;
+                const int left = __builtin_amdgcn_update_dpp(L, h, 0x138, 0xf, 0xf, false);  // H[i][b-1]
+                const int bdu = max(diag, up);
+                int code = (diag < up) ? kUp : ((xr == __builtin_amdgcn_readlane(yrv, r)) ? kDiagEq : kDiagX);
+                code = (bdu < left) ? kLeft : code;
+                word |= (unsigned)code << (2 * ((i - 1) & 15));
+                if (((i - 1) & 15) == 15 || i == iE)
+                {
+                    dirs[((size_t)((i - 1) >> 4) * nP + p) * 64 + lane] = word;
+                    word = 0;
+                }
+                if (lane == last) colbuf[i] = h;
+                if (first && i == iE && col == jE) G(a.res)[1] = h;  // H[adjrows-1][adjcols-1] = align_cost
+                Lprev = L;
+                up = h;
+            }
+        }
+    }
+    __syncthreads();
+    (void)DIRS_LDS;
+}
+
+template <bool DIRS_LDS>
+__global__ void __launch_bounds__(64) trace_sparse_kernel(TraceArgs a)
+{
+    const int lane = threadIdx.x;
+    const int tBy = a.tBy;
+    const int nP = (a.tBx + 63) / 64;
+    int* sub = tsm;
+    int* colbuf = sub + 32 * 32;
+    int* yb = colbuf + (tBy + 1);
+    int* yraw = yb + (tBy + 1);
+    int* xraw = yraw + (tBy + 1);
+    unsigned* dirs = DIRS_LDS ? (unsigned*)(xraw + (a.tBx + 1)) : a.dirs_scratch;
+    for (int k = lane; k < a.substsz * a.substsz; k += 64) sub[k] = G(a.subst)[k];
+
+    int iT = a.iT0, jT = a.jT0, iE = a.iE0, jE = a.jE0;
+    const int Wm = a.tBx, Hm = a.tBy;  // hrowLen-1, hcolLen-1
+    long long n = 0;
+    bool done = false, first = true;
+    if (lane == 0 && (iE == 0 || jE == 0))
+    {
+        // start cell on a header of its tile (empty sequence): the value is stored there
+        const long long k = (long long)iT * a.tcols + jT;
+        G(a.res)[1] = (iE == 0) ? G(a.hrow)[k * (a.tBx + 1) + jE] : G(a.hcol)[k * (a.tBy + 1) + iE];
+    }
+    while (!done)
+    {
+        if (iE > 0 && jE > 0) tile_moves<DIRS_LDS>(a, iT, jT, iE, jE, sub, colbuf, yb, yraw, xraw, dirs, lane, first);
+        first = false;
+        for (;;)
+        {
+            int di = 0, dj = 0, e = 0;
+            if (iE > 0 && jE > 0)
+            {
+                const size_t wi = ((size_t)((iE - 1) >> 4) * nP + ((jE - 1) >> 6)) * 64 + ((jE - 1) & 63);
+                const unsigned w = __builtin_amdgcn_readfirstlane(dirs[wi]);
+                const int code = (w >> (2 * ((iE - 1) & 15))) & 3;
+                if (code <= kDiagX)
+                {
+                    di = dj = -1;
+                    e = (code == kDiagEq) ? '=' : 'X';  // seqX[j] == seqY[i]
+                }
+                else if (code == kUp)
+                {
+                    di = -1;
+                    e = 'I';
+                }
+                else
+                {
+                    dj = -1;
+                    e = 'D';
+                }
+            }
+            else if (iE > 0)
+            {
+                di = -1;
+                e = 'I';
+            }
+            else if (jE > 0)
+            {
+                dj = -1;
+                e = 'D';
+            }
+            if (di == 0 && dj == 0)
+            {
+                done = true;
+                break;
+            }
+            if (lane == 0 && n < a.cap) G(a.edits)[n] = (unsigned char)e;
+            ++n;
+            iE += di;
+            jE += dj;
+            // into the tile above / left / up-left on reaching its header (nwtrace2_sparse.cpp:195-214)
+            const int diT = (iE == 0 && iT > 0) ? 1 : 0;
+            const int djT = (jE == 0 && jT > 0) ? 1 : 0;
+            if (diT || djT)
+            {
+                iT -= diT;
+                jT -= djT;
+                if (iE == 0 && di != 0) iE = Hm;
+                if (jE == 0 && dj != 0) jE = Wm;
+                break;
+            }
+        }
+    }
+    if (lane == 0) G(a.res)[0] = n;
+}
+
+size_t trace_lds_bytes(int tBy, int tBx, int substsz, bool dirs_lds)
+{
+    (void)substsz;
+    const size_t base = (size_t)4 * (32 * 32 + 3 * (tBy + 1) + (tBx + 1));
+    return base + (dirs_lds ? trace_dir_words(tBy, tBx) * 4 : 0);
+}
+
+size_t trace_dir_words(int tBy, int tBx) { return (size_t)((tBy + 15) / 16) * ((tBx + 63) / 64) * 64; }
+
+hipError_t launch_trace_sparse(const TraceArgs& a, hipStream_t st)
+{
+    if (a.substsz > 32) return hipErrorInvalidValue;
+    const bool lds = a.dirs_scratch == nullptr;
+    const size_t bytes = trace_lds_bytes(a.tBy, a.tBx, a.substsz, lds);
+    if (lds)
+    {
+        hipError_t e = hipFuncSetAttribute((const void*)trace_sparse_kernel<true>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(trace_sparse_kernel<true>, dim3(1), dim3(64), bytes, st, a);
+    }
+    else
+    {
+        hipError_t e = hipFuncSetAttribute((const void*)trace_sparse_kernel<false>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(trace_sparse_kernel<false>, dim3(1), dim3(64), bytes, st, a);
+    }
+    return hipGetLastError();
+}
+
+}  // namespace gsa

@@ -142,6 +142,38 @@ int32_t gsa_sparse_align_cost(const int32_t* tileHrowMat, const int32_t* tileHco
                               const int32_t* seqY, int32_t adjrows, const int32_t* seqX, int32_t adjcols,
                               const int32_t* subst, int32_t substsz, int32_t gapo);
 
+/* ---- device-side verification ------------------------------------- */
+/* The reference compares a GPU fill only through align_cost and the score / trace hashes, so
+ * sparse header values off the trace path are never checked (nwtrace2_sparse.cpp:263-340).
+ * These check EVERY output value against the recurrence (nwalign_cpu1_st_row.cpp:4-10) on the
+ * device: a sparse result by tile consistency (each tile recomputed from its own header row
+ * and column must reproduce the headers of the tiles below and to the right; row 0 / column 0
+ * must be j*g / i*g; the two copies of each tile corner must agree), a full matrix cell by
+ * cell against its stored neighbours.  Zero mismatches implies every value is exact.
+ * Synchronous on `stream`; inputs are device pointers. */
+typedef struct gsa_check_result
+{
+    int64_t checked;    /* values compared */
+    int64_t mismatches; /* values inconsistent with the recurrence or the boundary */
+    int64_t first;      /* smallest mismatching index, -1 if none: full = i*adjcols+j;
+                           sparse = index into tileHrowMat, or hrowElems + index into tileHcolMat */
+} gsa_check_result;
+int gsa_check_sparse_dev(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, const int32_t* seqX, int32_t adjcols,
+                         const int32_t* subst, int32_t substsz, int32_t gapo, const gsa_sparse_geom* geom,
+                         const int32_t* tileHrowMat, const int32_t* tileHcolMat, gsa_check_result* out,
+                         void* stream);
+int gsa_check_full_dev(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, const int32_t* seqX, int32_t adjcols,
+                       const int32_t* subst, int32_t substsz, int32_t gapo, const int32_t* score,
+                       gsa_check_result* out, void* stream);
+
+/* NwTrace2_Sparse (src/nwtrace2_sparse.cpp:102-257) on the device: the walk and its tile
+ * recomputes run on the GPU from device-resident headers; outputs (edit string, trace hash,
+ * align_cost) are identical to gsa_trace_sparse.  Synchronous on `stream`. */
+int gsa_trace_sparse_dev(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, const int32_t* seqX, int32_t adjcols,
+                         const int32_t* subst, int32_t substsz, int32_t gapo, const gsa_sparse_geom* geom,
+                         const int32_t* tileHrowMat, const int32_t* tileHcolMat, char* edit, int64_t cap,
+                         int64_t* edit_len, uint32_t* trace_hash, int32_t* align_cost, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
