@@ -91,6 +91,12 @@ class CheckResult(ctypes.Structure):
         return {"checked": int(self.checked), "mismatches": int(self.mismatches), "first": int(self.first)}
 
 
+class ScoreResult(ctypes.Structure):
+    """gsa_score_result (include/gsa.h)."""
+    _fields_ = [("score", ctypes.c_int32), ("i_end", ctypes.c_int64), ("j_end", ctypes.c_int64),
+                ("calc_kernel_ms", ctypes.c_float)]
+
+
 _i32p = ctypes.POINTER(ctypes.c_int32)
 _vp = ctypes.c_void_p
 _i32 = ctypes.c_int32
@@ -128,6 +134,10 @@ SIGNATURES = {
                                             _vp, _vp, ctypes.POINTER(CheckResult), _vp]),
     "gsa_check_full_dev": (ctypes.c_int, [_vp, _vp, _i32, _vp, _i32, _vp, _i32, _i32, _vp,
                                           ctypes.POINTER(CheckResult), _vp]),
+    "gsa_score_dev": (ctypes.c_int, [_vp, _vp, _i32, _vp, _i32, _vp, _i32, _i32, _i32, _i32,
+                                     ctypes.POINTER(ScoreResult), _vp]),
+    "gsa_score": (ctypes.c_int, [_vp, _i32p, _i32, _i32p, _i32, _i32p, _i32, _i32, _i32, _i32,
+                                 ctypes.POINTER(ScoreResult), ctypes.POINTER(_Laps)]),
     "gsa_trace_sparse_dev": (ctypes.c_int, [_vp, _vp, _i32, _vp, _i32, _vp, _i32, _i32, ctypes.POINTER(SparseGeom),
                                             _vp, _vp, ctypes.c_char_p, _i64, ctypes.POINTER(ctypes.c_int64),
                                             ctypes.POINTER(ctypes.c_uint32), _i32p, _vp]),
@@ -294,7 +304,30 @@ class Engine:
     def sync(self, stream: Optional[int] = None):
         self._check(lib().gsa_sync(self._h, stream), "gsa_sync")
 
+    # -- score-only NW / SW, linear or affine gaps (BASELINE configs[4]) -----------------
+    def score(self, seqY, seqX, subst, gapo: int, gape: Optional[int] = None, local: bool = False) -> dict:
+        """Score-only alignment (host buffers): {"score", "i_end", "j_end", "laps"}; gape
+        defaults to gapo (linear gaps; global + linear = the reference's NW-LG align_cost)."""
+        seqY, seqX, subst = _c32(seqY), _c32(seqX), _c32(subst)
+        substsz = int(round(np.sqrt(subst.size)))
+        r = ScoreResult()
+        laps = _Laps()
+        st = lib().gsa_score(self._h, _p(seqY), len(seqY), _p(seqX), len(seqX), _p(subst), substsz, gapo,
+                             gapo if gape is None else gape, int(local), ctypes.byref(r), ctypes.byref(laps))
+        self._check(st, "gsa_score")
+        return {"score": int(r.score), "i_end": int(r.i_end), "j_end": int(r.j_end), "laps": laps.as_dict()}
+
+    def score_dev(self, seqY_ptr: int, adjrows: int, seqX_ptr: int, adjcols: int, subst_ptr: int, substsz: int,
+                  gapo: int, gape: int, local: bool = False, stream: Optional[int] = None) -> dict:
+        r = ScoreResult()
+        st = lib().gsa_score_dev(self._h, seqY_ptr, adjrows, seqX_ptr, adjcols, subst_ptr, substsz, gapo, gape,
+                                 int(local), ctypes.byref(r), stream)
+        self._check(st, "gsa_score_dev")
+        return {"score": int(r.score), "i_end": int(r.i_end), "j_end": int(r.j_end),
+                "kernel_ms": float(r.calc_kernel_ms)}
+
     # -- device-side verification (SURVEY.md 8(f)1) ---------------------------------------
+
     def check_sparse_dev(self, seqY_ptr: int, adjrows: int, seqX_ptr: int, adjcols: int, subst_ptr: int,
                          substsz: int, gapo: int, geom: SparseGeom, hrow_ptr: int, hcol_ptr: int,
                          stream: Optional[int] = None) -> dict:

@@ -19,6 +19,7 @@
 #include "nw_check.h"
 #include "nw_strip.h"
 #include "nw_trace_dev.h"
+#include "nw_scan.h"
 
 namespace gsa {
 int fold_moves(const unsigned char* moves, int64_t n, char* edit, int64_t cap, int64_t* edit_len, uint32_t* trace_hash);
@@ -56,6 +57,10 @@ struct gsa_ctx
     long long* tres = nullptr;
     unsigned* tdirs = nullptr;
     size_t tdirs_cap = 0;
+    // score-only fills (nw_scan.hip): boundary rows H/F, progress words, control words
+    int* sbnd = nullptr;
+    size_t sbnd_cap = 0;
+    unsigned long long* sctl = nullptr;  // [0] ticket|err, [1] best key, [2] result
 };
 
 namespace {
@@ -331,6 +336,8 @@ void gsa_ctx_destroy(gsa_ctx* ctx)
     if (ctx->tmoves) (void)hipFree(ctx->tmoves);
     if (ctx->tres) (void)hipFree(ctx->tres);
     if (ctx->tdirs) (void)hipFree(ctx->tdirs);
+    if (ctx->sbnd) (void)hipFree(ctx->sbnd);
+    if (ctx->sctl) (void)hipFree(ctx->sctl);
     for (int k = 0; k < gsa_ctx::kStage; ++k)
     {
         if (ctx->stage[k]) (void)hipHostFree(ctx->stage[k]);
@@ -633,6 +640,117 @@ int gsa_trace_sparse_dev(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, con
         return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
     if (align_cost) *align_cost = (int32_t)res[1];
     return gsa::fold_moves(moves.data(), (int64_t)res[0], edit, cap, edit_len, trace_hash);
+}
+
+int gsa_score_dev(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, const int32_t* seqX, int32_t adjcols,
+                  const int32_t* subst, int32_t substsz, int32_t gapo, int32_t gape, int32_t local,
+                  gsa_score_result* out, void* stream)
+{
+    if (!ctx || !seqY || !seqX || !subst || !out) return GSA_ERROR_INVALID_VALUE;
+    int s = check_inputs(adjrows, adjcols, substsz);
+    if (s != GSA_SUCCESS) return s;
+    if (gapo > gape || gape > 0) return GSA_ERROR_INVALID_VALUE;  // go <= ge <= 0 (nw_scan.hip)
+    const int64_t R = adjrows - 1, C = adjcols - 1;
+    out->calc_kernel_ms = 0.f;
+    if (R == 0 || C == 0)
+    {
+        // one boundary: nothing to fill (score_oracle.c semantics)
+        const int64_t k = R + C;
+        out->score = (local || k == 0) ? 0 : (int32_t)(gapo + (k - 1) * gape);
+        out->i_end = local ? 0 : R;
+        out->j_end = local ? 0 : C;
+        return GSA_SUCCESS;
+    }
+    hipError_t e = hipSetDevice(ctx->device);
+    if (e != hipSuccess) return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
+    hipStream_t st = pick_stream(ctx, stream);
+    const int64_t nTR = (R + 63) / 64;
+    const size_t bnd = (size_t)(nTR + 1) * (size_t)(C + 1);
+    const size_t need = 2 * bnd + (size_t)(nTR + 1);  // bh, bf, prog
+    if (ctx->sbnd_cap < need)
+    {
+        if (ctx->sbnd) (void)hipFree(ctx->sbnd);
+        ctx->sbnd = nullptr;
+        ctx->sbnd_cap = 0;
+        if ((e = hipMalloc(&ctx->sbnd, need * sizeof(int))) != hipSuccess)
+            return fail(ctx, e, GSA_ERROR_MEMORY_ALLOCATION);
+        ctx->sbnd_cap = need;
+    }
+    if (!ctx->sctl && (e = hipMalloc(&ctx->sctl, 64)) != hipSuccess) return fail(ctx, e, GSA_ERROR_MEMORY_ALLOCATION);
+    gsa::ScoreArgs a {};
+    a.seqY = seqY;
+    a.seqX = seqX;
+    a.subst = subst;
+    a.substsz = substsz;
+    a.go = gapo;
+    a.ge = gape;
+    a.R = R;
+    a.C = C;
+    a.nTR = (int)nTR;
+    a.bh = ctx->sbnd;
+    a.bf = ctx->sbnd + bnd;
+    a.prog = ctx->sbnd + 2 * bnd;
+    a.ticket = (unsigned*)ctx->sctl;
+    a.err = (unsigned*)ctx->sctl + 1;
+    a.best = ctx->sctl + 1;
+    a.result = (int*)(ctx->sctl + 2);
+    if ((e = hipMemsetAsync(a.prog, 0, (size_t)(nTR + 1) * sizeof(int), st)) != hipSuccess ||
+        (e = hipMemsetAsync(ctx->sctl, 0, 64, st)) != hipSuccess)
+        return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
+    (void)hipEventRecord(ctx->ev0, st);
+    if ((e = gsa::launch_score_scan(a, local, ctx->cu_count, st)) != hipSuccess)
+        return fail(ctx, e, GSA_ERROR_KERNEL_FAILURE);
+    (void)hipEventRecord(ctx->ev1, st);
+    unsigned long long ctl[3];
+    if ((e = hipMemcpyAsync(ctl, ctx->sctl, sizeof(ctl), hipMemcpyDeviceToHost, st)) != hipSuccess ||
+        (e = hipStreamSynchronize(st)) != hipSuccess)
+        return fail(ctx, e, GSA_ERROR_KERNEL_FAILURE);
+    (void)hipEventElapsedTime(&out->calc_kernel_ms, ctx->ev0, ctx->ev1);
+    if ((unsigned)(ctl[0] >> 32) != 0) return GSA_ERROR_KERNEL_FAILURE;  // a wait gave up
+    if (local)
+    {
+        const unsigned long long mask = (1ull << 40) - 1;
+        const unsigned long long idx = mask - (ctl[1] & mask);
+        out->score = (int32_t)(ctl[1] >> 40);
+        out->i_end = (int64_t)(idx / (unsigned long long)(C + 1));
+        out->j_end = (int64_t)(idx % (unsigned long long)(C + 1));
+    }
+    else
+    {
+        out->score = (int32_t)(uint32_t)ctl[2];
+        out->i_end = R;
+        out->j_end = C;
+    }
+    return GSA_SUCCESS;
+}
+
+int gsa_score(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, const int32_t* seqX, int32_t adjcols,
+              const int32_t* subst, int32_t substsz, int32_t gapo, int32_t gape, int32_t local,
+              gsa_score_result* out, gsa_laps* laps)
+{
+    if (!ctx || !seqY || !seqX || !subst || !out) return GSA_ERROR_INVALID_VALUE;
+    int s = check_inputs(adjrows, adjcols, substsz);
+    if (s != GSA_SUCCESS) return s;
+    gsa_laps L {};
+    auto t = Clock::now();
+    if ((s = ensure_dev(ctx, 0, (size_t)adjrows * 4)) || (s = ensure_dev(ctx, 1, (size_t)adjcols * 4)) ||
+        (s = ensure_dev(ctx, 2, (size_t)substsz * substsz * 4)))
+        return s;
+    L.alloc = ms_since(t);
+    hipError_t e;
+    if ((e = hipMemcpyAsync(ctx->dbuf[0], seqY, (size_t)adjrows * 4, hipMemcpyHostToDevice, ctx->stream)) ||
+        (e = hipMemcpyAsync(ctx->dbuf[1], seqX, (size_t)adjcols * 4, hipMemcpyHostToDevice, ctx->stream)) ||
+        (e = hipMemcpyAsync(ctx->dbuf[2], subst, (size_t)substsz * substsz * 4, hipMemcpyHostToDevice, ctx->stream)) ||
+        (e = hipStreamSynchronize(ctx->stream)))
+        return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
+    L.cpy_dev = ms_since(t);
+    s = gsa_score_dev(ctx, (const int32_t*)ctx->dbuf[0], adjrows, (const int32_t*)ctx->dbuf[1], adjcols,
+                      (const int32_t*)ctx->dbuf[2], substsz, gapo, gape, local, out, ctx->stream);
+    if (s != GSA_SUCCESS) return s;
+    L.calc = ms_since(t);
+    L.calc_kernel_ms = out->calc_kernel_ms;
+    if (laps) *laps = L;
+    return GSA_SUCCESS;
 }
 
 }  // extern "C"

@@ -174,6 +174,28 @@ int gsa_trace_sparse_dev(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, con
                          const int32_t* tileHrowMat, const int32_t* tileHcolMat, char* edit, int64_t cap,
                          int64_t* edit_len, uint32_t* trace_hash, int32_t* align_cost, void* stream);
 
+/* ---- score-only NW / SW, linear or affine gaps (BASELINE configs[4]) ---- */
+/* Not in the reference (README.md:7-23 marks AG/SW unimplemented; --gapeCost is unused,
+ * cmd_parser.cpp:143).  Semantics: oracle/score_oracle.c --
+ *   E = max(E_left + gape, H_left + gapo), F = max(F_up + gape, H_up + gapo),
+ *   H = max(H_diag + s, E, F [, 0 if local]); a gap of length L costs gapo + (L-1)*gape;
+ *   global: score = H[R][C], boundaries gapo + (k-1)*gape; local: max over H, end = first
+ *   cell in row-major order.  gapo == gape == g is the reference's NW-LG.  Requires
+ *   gapo <= gape <= 0.  Synchronous. */
+typedef struct gsa_score_result
+{
+    int32_t score;
+    int64_t i_end, j_end;  /* local: where the maximum first occurs; global: (adjrows-1, adjcols-1) */
+    float calc_kernel_ms;  /* hipEvent time of the fill kernel */
+} gsa_score_result;
+int gsa_score_dev(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, const int32_t* seqX, int32_t adjcols,
+                  const int32_t* subst, int32_t substsz, int32_t gapo, int32_t gape, int32_t local,
+                  gsa_score_result* out, void* stream);
+/* Host buffers (alloc, copy in, fill, laps as gsa_align_*). */
+int gsa_score(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, const int32_t* seqX, int32_t adjcols,
+              const int32_t* subst, int32_t substsz, int32_t gapo, int32_t gape, int32_t local,
+              gsa_score_result* out, gsa_laps* laps);
+
 #ifdef __cplusplus
 }
 #endif

@@ -22,8 +22,8 @@ _i64 = ctypes.c_int64
 def build() -> str:
     """Compile liborc.so (gcc) if missing or stale."""
     so = os.path.join(_HERE, "liborc.so")
-    src = os.path.join(_HERE, "nw_oracle.c")
-    if not os.path.exists(so) or os.path.getmtime(so) < os.path.getmtime(src):
+    srcs = [os.path.join(_HERE, f) for f in ("nw_oracle.c", "score_oracle.c", "Makefile")]
+    if not os.path.exists(so) or os.path.getmtime(so) < max(os.path.getmtime(f) for f in srcs):
         subprocess.check_call(["make", "-s", "-C", _HERE])
     return so
 
@@ -52,6 +52,13 @@ def lib():
         L.orc_trace_sparse.argtypes = [_i32p, _i32p, _i64, _i64, _i64, _i64, _i32p, _i64, _i32p, _i64, _i32p,
                                        ctypes.c_int32, ctypes.c_int32, ctypes.c_char_p, _i64,
                                        ctypes.POINTER(ctypes.c_int64), _i32p]
+        L.orc_score_ag.restype = ctypes.c_int32
+        L.orc_score_ag.argtypes = [_i32p, _i64, _i32p, _i64, _i32p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                   ctypes.c_int32, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]
+        L.orc_score_ag_mt.restype = ctypes.c_int32
+        L.orc_score_ag_mt.argtypes = [_i32p, _i64, _i32p, _i64, _i32p, ctypes.c_int32, ctypes.c_int32,
+                                      ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                      ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]
         _LIB = L
     return _LIB
 
@@ -152,3 +159,19 @@ def trace_sparse(hrow, hcol, trows, tcols, tBy, tBx, seqY, seqX, subst, g):
                                len(seqX), _p(subst), substsz, g, buf, cap, ctypes.byref(n), _p(cost))
     assert n.value >= 0
     return int(h), buf.raw[:n.value].decode(), int(cost[0])
+
+
+def score_ag(seqY, seqX, subst, go: int, ge: int, local: bool = False, mt: bool = False, blocksz: int = 256,
+             nthreads: int = 0):
+    """Score-only NW / SW with affine gaps (score_oracle.c; linear gaps: go == ge).
+    Returns (score, i_end, j_end).  Not in the reference: parity unpinned by it (see the C header)."""
+    y, x, s = (np.ascontiguousarray(a, dtype=np.int32) for a in (seqY, seqX, subst))
+    substsz = int(round(np.sqrt(s.size)))
+    ie, je = ctypes.c_int64(0), ctypes.c_int64(0)
+    if mt:
+        sc = lib().orc_score_ag_mt(_p(y), len(y), _p(x), len(x), _p(s.ravel()), substsz, go, ge, int(local), blocksz,
+                                   nthreads, ctypes.byref(ie), ctypes.byref(je))
+    else:
+        sc = lib().orc_score_ag(_p(y), len(y), _p(x), len(x), _p(s.ravel()), substsz, go, ge, int(local),
+                                ctypes.byref(ie), ctypes.byref(je))
+    return int(sc), int(ie.value), int(je.value)

@@ -1,0 +1,66 @@
+"""Score-only NW / SW with linear or affine gaps on the GPU (gsa_score, nw_scan.hip; BASELINE
+configs[4]) against the CPU restatement oracle/score_oracle.c (parity
+unpinned by the reference, which has no such mode; the oracle is pinned by
+tests/test_score_oracle.py)."""
+import numpy as np
+import pytest
+
+import gpuseqalign_amd as gsa
+from tests._data import random_pair, related_pair
+
+pytestmark = pytest.mark.gpu
+
+MODES = [(-11, -11, False), (-11, -1, False), (-5, -2, False), (-11, -11, True), (-11, -1, True), (-5, -2, True)]
+
+
+@pytest.mark.parametrize("R,C", [(1, 1), (1, 300), (300, 1), (63, 64), (64, 65), (65, 63), (130, 700), (700, 130),
+                                 (1000, 1500)])
+@pytest.mark.parametrize("go,ge,local", MODES)
+def test_score_matches_oracle(engine, golden, R, C, go, ge, local):
+    import oracle
+    Y, X = random_pair(R, C, 3 * R + C)
+    r = engine.score(Y, X, golden.blosum62, go, ge, local)
+    assert (r["score"], r["i_end"], r["j_end"]) == oracle.score_ag(Y, X, golden.blosum62, go, ge, local)
+
+
+@pytest.mark.parametrize("n", [200, 2000, 4097])
+@pytest.mark.parametrize("go,ge,local", MODES)
+def test_score_related_pairs(engine, golden, n, go, ge, local):
+    import oracle
+    Y, X = related_pair(n, n + 17)
+    r = engine.score(Y, X, golden.blosum62, go, ge, local)
+    assert (r["score"], r["i_end"], r["j_end"]) == oracle.score_ag(Y, X, golden.blosum62, go, ge, local)
+
+
+def test_empty_and_invalid(engine, golden):
+    import oracle
+    for R, C in [(0, 0), (0, 9), (7, 0)]:
+        Y, X = random_pair(R, C, 1)
+        for go, ge, local in MODES:
+            r = engine.score(Y, X, golden.blosum62, go, ge, local)
+            assert (r["score"], r["i_end"], r["j_end"]) == oracle.score_ag(Y, X, golden.blosum62, go, ge, local)
+    Y, X = random_pair(10, 10, 2)
+    for go, ge in [(-1, -11), (-3, 2)]:
+        with pytest.raises(gsa.NwError):
+            engine.score(Y, X, golden.blosum62, go, ge, False)
+
+
+def test_linear_global_equals_strip_fill(engine, golden):
+    """go == ge == g, global = the reference's NW-LG: same align_cost as the strip fill (config 2 pair)."""
+    Y, X = golden.pair("len12124[:10000] len15390[:10000]")
+    assert engine.score(Y, X, golden.blosum62, -11)["score"] == -4922
+    for k in golden.known["cases"]:
+        Y, X = golden.pair(k["pair"])
+        assert engine.score(Y, X, golden.blosum62, -11)["score"] == k["align_cost"]
+
+
+@pytest.mark.parametrize("go,ge,local", [(-11, -11, True), (-11, -1, False)])
+def test_config5_50k(engine, golden, go, ge, local):
+    """BASELINE configs[4]: 50k x 50k random pair (seed 200), SW-LG and NW-AG, against the
+    oracle's tiled OpenMP restatement (bit-identical to its row-streaming one)."""
+    import oracle
+    from gpuseqalign_amd import formats as F
+    Y, X = F.synthetic_seq(50000, 200), F.synthetic_seq(50000, 201)
+    r = engine.score(Y, X, golden.blosum62, go, ge, local)
+    ref = oracle.score_ag(Y, X, golden.blosum62, go, ge, local, mt=True, blocksz=256, nthreads=16)
+    assert (r["score"], r["i_end"], r["j_end"]) == ref

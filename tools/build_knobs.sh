@@ -10,6 +10,7 @@ for k in "$@"; do
   wait
   hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -c nw_check.hip -o build/knob/nw_check.o
 hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -c nw_trace_dev.hip -o build/knob/nw_trace_dev.o
+hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -c nw_scan.hip -o build/knob/nw_scan.o
   hipcc -O3 -std=c++17 -fPIC -c nw_trace.cpp -o build/knob/nw_trace.o
-  hipcc --offload-arch=gfx950 -shared -fPIC build/knob/gsa_capi.$k.o build/knob/nw_strip.$k.o build/knob/nw_trace.o build/knob/nw_check.o build/knob/nw_trace_dev.o -o ../libgsa_k$k.so
+  hipcc --offload-arch=gfx950 -shared -fPIC build/knob/gsa_capi.$k.o build/knob/nw_strip.$k.o build/knob/nw_trace.o build/knob/nw_check.o build/knob/nw_trace_dev.o build/knob/nw_scan.o -o ../libgsa_k$k.so
 done

@@ -6,6 +6,7 @@ cd "$(dirname "$0")/../gpuseqalign_amd/csrc"
 mkdir -p build/var
 hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -c nw_check.hip -o build/var/nw_check.o
 hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -c nw_trace_dev.hip -o build/var/nw_trace_dev.o
+hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -c nw_scan.hip -o build/var/nw_scan.o
 hipcc -O3 -std=c++17 -fPIC -c nw_trace.cpp -o build/var/nw_trace.o
 for spec in "$@"; do
   name="${spec%%:*}"; defs="${spec#*:}"
@@ -13,5 +14,5 @@ for spec in "$@"; do
     hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC $defs -c -x hip $f.hip -o build/var/$f.$name.o &
   done
   wait
-  hipcc --offload-arch=gfx950 -shared -fPIC build/var/gsa_capi.$name.o build/var/nw_strip.$name.o build/var/nw_trace.o build/var/nw_check.o build/var/nw_trace_dev.o -o ../libgsa_$name.so
+  hipcc --offload-arch=gfx950 -shared -fPIC build/var/gsa_capi.$name.o build/var/nw_strip.$name.o build/var/nw_trace.o build/var/nw_check.o build/var/nw_trace_dev.o build/var/nw_scan.o -o ../libgsa_$name.so
 done
