@@ -120,6 +120,8 @@ SIGNATURES = {
                                       ctypes.POINTER(_Laps)]),
     "gsa_align_sparse": (ctypes.c_int, [_vp, _i32p, _i32, _i32p, _i32, _i32p, _i32, _i32, _i32, _i32p, _i32p,
                                         ctypes.POINTER(SparseGeom), _i32p, ctypes.POINTER(_Laps)]),
+    "gsa_align_sparse_pt": (ctypes.c_int, [_vp, _i32p, _i32, _i32p, _i32, _i32p, _i32, _i32, _i32, _i32p, _i32p,
+                                           ctypes.POINTER(SparseGeom), _i32p, ctypes.POINTER(_Laps)]),
     "gsa_hash_full": (ctypes.c_uint32, [_i32p, _i32, _i32]),
     "gsa_trace_full": (ctypes.c_int, [_i32p, _i32p, _i32, _i32p, _i32, ctypes.c_char_p, _i64,
                                       ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_uint32)]),
@@ -255,8 +257,9 @@ class Engine:
         self._check(st, "gsa_align_full")
         return AlignResult(score, int(cost.value), laps.as_dict())
 
-    def align_sparse(self, seqY, seqX, subst, gapo: int, tileBx: int = 256) -> SparseResult:
-        """Tile-header (mlsp) representation (the gpu7..gpu9 family's tileHrowMat/tileHcolMat)."""
+    def align_sparse(self, seqY, seqX, subst, gapo: int, tileBx: int = 256, overlap: bool = False) -> SparseResult:
+        """Tile-header (mlsp) representation (the gpu7..gpu9 family's tileHrowMat/tileHcolMat).
+        overlap=True: mlsppt, the copy-back runs tile row by tile row during the fill."""
         seqY, seqX, subst = _c32(seqY), _c32(seqX), _c32(subst)
         substsz = int(round(np.sqrt(subst.size)))
         geom = sparse_geometry(len(seqY), len(seqX), tileBx)
@@ -264,10 +267,10 @@ class Engine:
         hcol = np.empty(geom.hcolElems, dtype=np.int32)
         cost = ctypes.c_int32(0)
         laps = _Laps()
-        st = lib().gsa_align_sparse(self._h, _p(seqY), len(seqY), _p(seqX), len(seqX), _p(subst), substsz, gapo,
-                                    tileBx, _p(hrow), _p(hcol), ctypes.byref(geom), ctypes.byref(cost),
-                                    ctypes.byref(laps))
-        self._check(st, "gsa_align_sparse")
+        fn = lib().gsa_align_sparse_pt if overlap else lib().gsa_align_sparse
+        st = fn(self._h, _p(seqY), len(seqY), _p(seqX), len(seqX), _p(subst), substsz, gapo, tileBx, _p(hrow),
+                _p(hcol), ctypes.byref(geom), ctypes.byref(cost), ctypes.byref(laps))
+        self._check(st, "gsa_align_sparse_pt" if overlap else "gsa_align_sparse")
         return SparseResult(hrow, hcol, geom, int(cost.value), laps.as_dict())
 
     # -- hot path on device-resident buffers (torch tensors or raw pointers) -------------
@@ -451,6 +454,11 @@ def _align_mlsp(engine: Engine, seqY, seqX, subst, gapo, tileBx=256, **_):
     return NwResult(align_cost=r.align_cost, laps=r.laps, payload=r)
 
 
+def _align_mlsppt(engine: Engine, seqY, seqX, subst, gapo, tileBx=256, **_):
+    r = engine.align_sparse(seqY, seqX, subst, gapo, tileBx=tileBx, overlap=True)
+    return NwResult(align_cost=r.align_cost, laps=r.laps, payload=r)
+
+
 def _trace1(res: NwResult, seqY, seqX, subst, gapo):
     res.trace_hash, res.edit_trace = trace_full(res.payload.score, seqY, seqX)
 
@@ -479,4 +487,7 @@ def get_nw_algorithm_map() -> Dict[str, NwAlgorithm]:
             "NwAlign_Gpu9_Mlsp_DiagDiagDiag"]
     m = {n: NwAlgorithm(n, _align_plain, _trace1, _hash1) for n in plain}
     m.update({n: NwAlgorithm(n, _align_mlsp, _trace2, _hash2, {"tileBx": [256]}) for n in mlsp})
+    # mlsppt (the reference's README.md:39 names it, never implemented): copy-back overlapped
+    m["NwAlign_Amd_Strip_Mlsppt"] = NwAlgorithm("NwAlign_Amd_Strip_Mlsppt", _align_mlsppt, _trace2, _hash2,
+                                                {"tileBx": [256]})
     return m

@@ -13,6 +13,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <new>
+#include <thread>
 #include <vector>
 
 #include "../../include/gsa.h"
@@ -60,6 +61,10 @@ struct gsa_ctx
     // score-only fills (nw_scan.hip): boundary rows H/F, progress words, control words
     int* sbnd = nullptr;
     size_t sbnd_cap = 0;
+    // mlsppt: host-mapped per-ticket completion flags and the copy-back stream
+    unsigned* ptflags = nullptr;
+    size_t ptflags_cap = 0;
+    hipStream_t cstream = nullptr;
     unsigned long long* sctl = nullptr;  // [0] ticket|err, [1] best key, [2] result
 };
 
@@ -169,7 +174,7 @@ int run_check(gsa_ctx* ctx, gsa::CheckArgs& a, bool sparse, hipStream_t st, gsa_
 // One batched launch: headers of every pair, then the persistent strip kernel over the
 // tickets of all pairs (pair-major).  `pairs` holds device pointers.
 int enqueue_batch(gsa_ctx* ctx, int mode, int npairs, const gsa_pair_dev* pairs, const int32_t* subst, int32_t substsz,
-                  int32_t gapo, int32_t tileBx, hipStream_t st)
+                  int32_t gapo, int32_t tileBx, hipStream_t st, unsigned* done = nullptr)
 {
     if (npairs < 1 || !pairs || !subst) return GSA_ERROR_INVALID_VALUE;
     if (substsz < 1 || substsz > 32) return GSA_ERROR_INVALID_VALUE;  // LDS profile holds <= 32 letters
@@ -265,6 +270,7 @@ int enqueue_batch(gsa_ctx* ctx, int mode, int npairs, const gsa_pair_dev* pairs,
     a.ticket = ctx->ctl;
     a.err = ctx->ctl + 1;
     a.dbg = ctx->dbg;
+    a.done = done;
     a.epoch = ++ctx->epoch;
     if (a.epoch == 0) a.epoch = ++ctx->epoch;  // 0 is the cleared-tag value
     e = hipMemsetAsync(ctx->ctl, 0, 16, st);
@@ -278,10 +284,10 @@ int enqueue_batch(gsa_ctx* ctx, int mode, int npairs, const gsa_pair_dev* pairs,
 
 int enqueue_fill(gsa_ctx* ctx, int mode, const int32_t* seqY, int32_t adjrows, const int32_t* seqX, int32_t adjcols,
                  const int32_t* subst, int32_t substsz, int32_t gapo, int32_t* score, int32_t tileBx, int32_t* hrow,
-                 int32_t* hcol, hipStream_t st)
+                 int32_t* hcol, hipStream_t st, unsigned* done = nullptr)
 {
     gsa_pair_dev p {seqY, adjrows, seqX, adjcols, score, hrow, hcol};
-    return enqueue_batch(ctx, mode, 1, &p, subst, substsz, gapo, tileBx, st);
+    return enqueue_batch(ctx, mode, 1, &p, subst, substsz, gapo, tileBx, st, done);
 }
 
 }  // namespace
@@ -338,6 +344,8 @@ void gsa_ctx_destroy(gsa_ctx* ctx)
     if (ctx->tdirs) (void)hipFree(ctx->tdirs);
     if (ctx->sbnd) (void)hipFree(ctx->sbnd);
     if (ctx->sctl) (void)hipFree(ctx->sctl);
+    if (ctx->ptflags) (void)hipHostFree(ctx->ptflags);
+    if (ctx->cstream) (void)hipStreamDestroy(ctx->cstream);
     for (int k = 0; k < gsa_ctx::kStage; ++k)
     {
         if (ctx->stage[k]) (void)hipHostFree(ctx->stage[k]);
@@ -749,6 +757,100 @@ int gsa_score(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, const int32_t*
     if (s != GSA_SUCCESS) return s;
     L.calc = ms_since(t);
     L.calc_kernel_ms = out->calc_kernel_ms;
+    if (laps) *laps = L;
+    return GSA_SUCCESS;
+}
+
+int gsa_align_sparse_pt(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, const int32_t* seqX, int32_t adjcols,
+                        const int32_t* subst, int32_t substsz, int32_t gapo, int32_t tileBx, int32_t* hrow_out,
+                        int32_t* hcol_out, gsa_sparse_geom* geom_out, int32_t* align_cost, gsa_laps* laps)
+{
+    if (!ctx || !seqY || !seqX || !subst || !hrow_out || !hcol_out) return GSA_ERROR_INVALID_VALUE;
+    int s = check_inputs(adjrows, adjcols, substsz);
+    if (s != GSA_SUCCESS) return s;
+    gsa_sparse_geom geom;
+    if ((s = gsa_sparse_geometry(adjrows, adjcols, tileBx, &geom)) != GSA_SUCCESS) return s;
+    gsa_laps L {};
+    auto t = Clock::now();
+    const size_t trows = (size_t)geom.tileHdrMatRows;
+    if ((s = ensure_dev(ctx, 0, (size_t)adjrows * 4)) || (s = ensure_dev(ctx, 1, (size_t)adjcols * 4)) ||
+        (s = ensure_dev(ctx, 2, (size_t)substsz * substsz * 4)) || (s = ensure_dev(ctx, 3, (size_t)geom.hrowElems * 4)) ||
+        (s = ensure_dev(ctx, 4, (size_t)geom.hcolElems * 4)))
+        return s;
+    hipError_t e;
+    if (ctx->ptflags_cap < trows)
+    {
+        if (ctx->ptflags) (void)hipHostFree(ctx->ptflags);
+        ctx->ptflags = nullptr;
+        ctx->ptflags_cap = 0;
+        if ((e = hipHostMalloc((void**)&ctx->ptflags, trows * sizeof(unsigned), hipHostMallocMapped)) != hipSuccess)
+            return fail(ctx, e, GSA_ERROR_MEMORY_ALLOCATION);
+        std::memset(ctx->ptflags, 0, trows * sizeof(unsigned));
+        ctx->ptflags_cap = trows;
+    }
+    if (!ctx->cstream && (e = hipStreamCreateWithFlags(&ctx->cstream, hipStreamNonBlocking)) != hipSuccess)
+        return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
+    unsigned* dflags = nullptr;
+    if ((e = hipHostGetDevicePointer((void**)&dflags, ctx->ptflags, 0)) != hipSuccess)
+        return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
+    L.alloc = ms_since(t);
+    if ((e = hipMemcpyAsync(ctx->dbuf[0], seqY, (size_t)adjrows * 4, hipMemcpyHostToDevice, ctx->stream)) ||
+        (e = hipMemcpyAsync(ctx->dbuf[1], seqX, (size_t)adjcols * 4, hipMemcpyHostToDevice, ctx->stream)) ||
+        (e = hipMemcpyAsync(ctx->dbuf[2], subst, (size_t)substsz * substsz * 4, hipMemcpyHostToDevice, ctx->stream)) ||
+        (e = hipStreamSynchronize(ctx->stream)))
+        return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
+    L.cpy_dev = ms_since(t);
+    int32_t* dhr = (int32_t*)ctx->dbuf[3];
+    int32_t* dhc = (int32_t*)ctx->dbuf[4];
+    (void)hipEventRecord(ctx->ev0, ctx->stream);
+    s = enqueue_fill(ctx, gsa::kModeSparse, (const int32_t*)ctx->dbuf[0], adjrows, (const int32_t*)ctx->dbuf[1],
+                     adjcols, (const int32_t*)ctx->dbuf[2], substsz, gapo, nullptr, tileBx, dhr, dhc, ctx->stream,
+                     dflags);
+    if (s != GSA_SUCCESS) return s;
+    (void)hipEventRecord(ctx->ev1, ctx->stream);
+    const unsigned epoch = ctx->epoch;
+    const size_t W = (size_t)geom.tileHrowLen * (size_t)geom.tileHdrMatCols;  // ints per tile row of hrow
+    const size_t H = (size_t)geom.tileHcolLen * (size_t)geom.tileHdrMatCols;  // ints per tile row of hcol
+    // tile rows whose headers are final: hrow row k+1 and hcol row k once super-strip k is done;
+    // hrow row 0 comes from the headers kernel before any super-strip starts
+    size_t done = 0, hrowCopied = 0, hcolCopied = 0;
+    const size_t chunk = std::max<size_t>(1, trows / 16);
+    auto copy_rows = [&](size_t hrUpTo, size_t hcUpTo) -> hipError_t {
+        hipError_t err = hipSuccess;
+        if (hrUpTo > hrowCopied)
+            err = hipMemcpyAsync(hrow_out + hrowCopied * W, dhr + hrowCopied * W, (hrUpTo - hrowCopied) * W * 4,
+                                 hipMemcpyDeviceToHost, ctx->cstream);
+        if (err == hipSuccess && hcUpTo > hcolCopied)
+            err = hipMemcpyAsync(hcol_out + hcolCopied * H, dhc + hcolCopied * H, (hcUpTo - hcolCopied) * H * 4,
+                                 hipMemcpyDeviceToHost, ctx->cstream);
+        if (err == hipSuccess) err = hipStreamSynchronize(ctx->cstream);
+        hrowCopied = std::max(hrowCopied, hrUpTo);
+        hcolCopied = std::max(hcolCopied, hcUpTo);
+        return err;
+    };
+    for (;;)
+    {
+        const hipError_t q = hipStreamQuery(ctx->stream);  // the fill (and its headers kernel) finished?
+        if (q != hipSuccess && q != hipErrorNotReady) return fail(ctx, q, GSA_ERROR_KERNEL_FAILURE);
+        while (done < trows && __atomic_load_n(ctx->ptflags + done, __ATOMIC_ACQUIRE) == epoch) ++done;
+        if (q == hipSuccess) break;
+        if (done >= hcolCopied + chunk)
+        {
+            if ((e = copy_rows(std::min(done + 1, trows), done)) != hipSuccess)
+                return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
+        }
+        else
+            std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
+    if ((s = gsa_sync(ctx, ctx->stream)) != GSA_SUCCESS) return s;
+    L.calc = ms_since(t);
+    (void)hipEventElapsedTime(&L.calc_kernel_ms, ctx->ev0, ctx->ev1);
+    if ((e = copy_rows(trows, trows)) != hipSuccess) return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
+    L.cpy_host = ms_since(t);
+    int32_t cost = gsa_sparse_align_cost(hrow_out, hcol_out, &geom, seqY, adjrows, seqX, adjcols, subst, substsz, gapo);
+    L.calc += ms_since(t);
+    if (align_cost) *align_cost = cost;
+    if (geom_out) *geom_out = geom;
     if (laps) *laps = L;
     return GSA_SUCCESS;
 }

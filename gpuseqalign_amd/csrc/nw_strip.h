@@ -54,6 +54,9 @@ struct StripArgs
     unsigned* err;
     unsigned epoch;
     unsigned long long* dbg;  // diagnostic builds only (GSA_STAMP): per-wave block time stamps
+    // mlsppt: host-mapped per-ticket flags, set to `epoch` once a super-strip's outputs are
+    // written back past L2 (null: no signalling)
+    unsigned* done;
     // batch: the per-pair fields above are loaded from pairs[] for every ticket
     const PairDesc* pairs;
     int nPairs;

@@ -755,9 +755,15 @@ __global__ void __launch_bounds__(64 * (NS + 1 + (MODE == kModeFull ? kStoreWave
     const int lane = threadIdx.x & 63;
     const Lds L = lds_layout<NS, MODE>(a.substsz);
     const uint32_t F = L.flags;
+    int prevTk = -1;  // global ticket this workgroup finished last (mlsppt signalling)
     for (;;)
     {
+        // mlsppt: every wave writes its stores of the finished ticket back past L2 (system-scope
+        // release), then one thread flags the ticket to the host, which copies it meanwhile
+        if (a.done && prevTk >= 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
         __syncthreads();
+        if (a.done && prevTk >= 0 && threadIdx.x == 0)
+            __hip_atomic_store(a.done + prevTk, a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         if (threadIdx.x == 0) lds_st(F + kFTicket, (err_set(a) ? a.nTicketsTotal : (int)atomicAdd(a.ticket, 1u)));
         __syncthreads();
         const int tkg = __builtin_amdgcn_readfirstlane(lds_ld(F + kFTicket));
@@ -776,6 +782,7 @@ __global__ void __launch_bounds__(64 * (NS + 1 + (MODE == kModeFull ? kStoreWave
             }
         }
         if (tkg >= a.nTicketsTotal) break;
+        prevTk = tkg;
         // pair of this ticket: last descriptor with ticketBase <= tkg (binary search, uniform)
         int lo = 0, hi = a.nPairs - 1;
         while (lo < hi)

@@ -178,7 +178,7 @@ NwStat NwAlign_Amd_Strip_Full(const NwAlgParams&, NwAlgInput& nw, NwAlgResult& r
 // Sparse family (NwAlign_Gpu7..9 slots): tile header matrices.  Parameter "tileBx" (a
 // multiple of 16, >= 64) selects the tile width; default 256.  The tile height is the
 // engine's super-strip height (gsa_sparse_tile_by()).
-NwStat NwAlign_Amd_Strip_Mlsp(const NwAlgParams& pr, NwAlgInput& nw, NwAlgResult& res)
+static NwStat align_mlsp(const NwAlgParams& pr, NwAlgInput& nw, NwAlgResult& res, bool overlap)
 {
     if (NwStat s = check_input(nw); s != NwStat::success) return s;
     int tileBx = 256;
@@ -200,9 +200,10 @@ NwStat NwAlign_Amd_Strip_Mlsp(const NwAlgParams& pr, NwAlgInput& nw, NwAlgResult
     }
     gsa_laps laps {};
     int cost = 0;
-    int st = gsa_align_sparse(nw.ctx, nw.seqY.data(), nw.adjrows, nw.seqX.data(), nw.adjcols, nw.subst.data(),
-                              nw.substsz, nw.gapoCost, tileBx, nw.tileHrowMat.data(), nw.tileHcolMat.data(), &g, &cost,
-                              &laps);
+    int st = (overlap ? gsa_align_sparse_pt : gsa_align_sparse)(nw.ctx, nw.seqY.data(), nw.adjrows, nw.seqX.data(),
+                                                                nw.adjcols, nw.subst.data(), nw.substsz, nw.gapoCost,
+                                                                tileBx, nw.tileHrowMat.data(), nw.tileHcolMat.data(),
+                                                                &g, &cost, &laps);
     res.hipStat = gsa_last_hip_error(nw.ctx);
     if (st != GSA_SUCCESS) return (NwStat)st;
     nw.geom = g;
@@ -215,6 +216,18 @@ NwStat NwAlign_Amd_Strip_Mlsp(const NwAlgParams& pr, NwAlgInput& nw, NwAlgResult
     res.globalMemPeakAllocs =
         std::max(res.globalMemPeakAllocs, (nw.tileHrowMat.size() + nw.tileHcolMat.size()) * sizeof(int));
     return NwStat::success;
+}
+
+NwStat NwAlign_Amd_Strip_Mlsp(const NwAlgParams& pr, NwAlgInput& nw, NwAlgResult& res)
+{
+    return align_mlsp(pr, nw, res, false);
+}
+
+// mlsppt ("multi-launch sparse with parallel transfer", README.md:39 of the reference, never
+// implemented there): the same outputs, the header copy-back overlapped with the fill.
+NwStat NwAlign_Amd_Strip_Mlsppt(const NwAlgParams& pr, NwAlgInput& nw, NwAlgResult& res)
+{
+    return align_mlsp(pr, nw, res, true);
 }
 
 // ---- trace / hash adapters (the reference's L4 consumers, host C++ in libgsa) -------------
@@ -315,6 +328,8 @@ void getNwAlgorithmMap(std::map<std::string, NwAlgorithm>& algMap)
 {
     const NwAlgorithm plain {NwAlign_Amd_Strip_Full, NwTrace1_Plain, NwHash1_Plain, NwPrintScore1_Plain,
                              NwPrintTrace1_Plain};
+    const NwAlgorithm sparse_pt {NwAlign_Amd_Strip_Mlsppt, NwTrace2_Sparse, NwHash2_Sparse, NwPrintScore2_Sparse,
+                                 NwPrintTrace1_Plain};
     const NwAlgorithm sparse {NwAlign_Amd_Strip_Mlsp, NwTrace2_Sparse, NwHash2_Sparse, NwPrintScore2_Sparse,
                               NwPrintTrace1_Plain};
     std::map<std::string, NwAlgorithm> m {
@@ -329,6 +344,7 @@ void getNwAlgorithmMap(std::map<std::string, NwAlgorithm>& algMap)
         {"NwAlign_Gpu9_Mlsp_DiagDiagDiag", sparse},
         {"NwAlign_Amd_Strip_Full", plain},
         {"NwAlign_Amd_Strip_Mlsp", sparse},
+        {"NwAlign_Amd_Strip_Mlsppt", sparse_pt},
     };
     algMap.swap(m);
 }

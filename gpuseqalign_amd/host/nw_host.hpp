@@ -190,6 +190,7 @@ void getNwAlgorithmMap(std::map<std::string, NwAlgorithm>& algMap);
 // Individual functions (the reference's nw_fns.hpp names).
 NwStat NwAlign_Amd_Strip_Full(const NwAlgParams& pr, NwAlgInput& nw, NwAlgResult& res);
 NwStat NwAlign_Amd_Strip_Mlsp(const NwAlgParams& pr, NwAlgInput& nw, NwAlgResult& res);
+NwStat NwAlign_Amd_Strip_Mlsppt(const NwAlgParams& pr, NwAlgInput& nw, NwAlgResult& res);
 NwStat NwTrace1_Plain(NwAlgInput& nw, NwAlgResult& res, bool calcDebugTrace);
 NwStat NwHash1_Plain(NwAlgInput& nw, NwAlgResult& res);
 NwStat NwTrace2_Sparse(NwAlgInput& nw, NwAlgResult& res, bool calcDebugTrace);

@@ -119,6 +119,15 @@ int gsa_align_sparse(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, const i
                      const int32_t* subst, int32_t substsz, int32_t gapo, int32_t tileBx, int32_t* tileHrowMat_out,
                      int32_t* tileHcolMat_out, gsa_sparse_geom* geom, int32_t* align_cost, gsa_laps* laps);
 
+/* mlsppt ("multi-launch sparse with parallel transfer", named in the reference's README.md:39,
+ * never implemented there): as gsa_align_sparse, but the header matrices are copied back to
+ * the host tile row by tile row WHILE the fill runs (the kernel flags each finished
+ * super-strip in host-mapped memory).  Same outputs; the laps' cpy_host is only the tail
+ * copied after the fill ends. */
+int gsa_align_sparse_pt(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, const int32_t* seqX, int32_t adjcols,
+                        const int32_t* subst, int32_t substsz, int32_t gapo, int32_t tileBx, int32_t* tileHrowMat_out,
+                        int32_t* tileHcolMat_out, gsa_sparse_geom* geom, int32_t* align_cost, gsa_laps* laps);
+
 /* ---- consumers (host), the reference's L4 ----------------------------------------- */
 /* NwHash1_Plain (src/nwtrace1_plain.cpp:133-154). */
 uint32_t gsa_hash_full(const int32_t* score, int32_t adjrows, int32_t adjcols);

@@ -126,14 +126,15 @@ def test_known_answers_end_to_end(gsa_nw, tmp_path):
     pf = tmp_path / "pairs.txt"
     pf.write_text("".join(c["pair"] + "\n" for c in known["cases"][:5]))
     pj = tmp_path / "params.json"
-    pj.write_text('{"NwAlign_Gpu3_Ml_DiagDiag": {}, "NwAlign_Gpu9_Mlsp_DiagDiagDiag": {"tileBx": [256, 64]}}')
+    pj.write_text('{"NwAlign_Gpu3_Ml_DiagDiag": {}, "NwAlign_Gpu9_Mlsp_DiagDiagDiag": {"tileBx": [256, 64]},'
+                  ' "NwAlign_Amd_Strip_Mlsppt": {"tileBx": [128]}}')
     out = tmp_path / "res.tsv"
     r = run(gsa_nw, "-b", os.path.join(RES, "subst.json"), "-r", str(pj), "-s", os.path.join(RES, "seq_generated.fa"),
             "-p", str(pf), "-o", str(out), "--fCalcScoreHash", "--fCalcTrace", "--warmupPerAlign", "1",
             "--samplesPerAlign", "2")
     assert r.returncode == 0, r.stderr
     rows = list(csv.DictReader(open(out), delimiter="\t"))
-    assert len(rows) == 5 * 3
+    assert len(rows) == 5 * 4
     by = {}
     for row in rows:
         assert row["err_step"] == "0" and row["nw_stat"] == "0"

@@ -60,3 +60,13 @@ _, t_fill = timed(lambda: (eng.fill_full_dev(*args, out.data_ptr()), eng.sync())
 chk, t_chk = timed(lambda: eng.check_full_dev(*args, out.data_ptr()))
 print(json.dumps({"R": 10000, "C": 10000, "full_fill_ms": round(t_fill, 3), "full_check_ms": round(t_chk, 3),
                   "check_GBps": round(2 * 4 * out.numel() / t_chk / 1e6, 1), **chk}), flush=True)
+
+# mlsppt: end-to-end host-buffer sparse align, plain vs overlapped copy-back (BASELINE configs[2])
+X = F.synthetic_seq(100000, 100)
+Y = F.mutate_seq(X, 101)
+for ov in (False, True, False, True):
+    t = time.perf_counter()
+    r = eng.align_sparse(Y, X, sub, -11, tileBx=256, overlap=ov)
+    tot = time.perf_counter() - t
+    print(json.dumps({"mlsp": "mlsppt" if ov else "mlsp", "R": 100000, "wall_ms": round(1e3 * tot, 2),
+                      "laps": {k: round(v, 3) for k, v in r.laps.items()}, "align_cost": r.align_cost}), flush=True)
