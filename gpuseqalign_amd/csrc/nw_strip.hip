@@ -195,10 +195,20 @@ __device__ __forceinline__ uint32_t ring_elem(int c)
 #ifndef GSA_STAMP
 #define GSA_STAMP 0
 #endif
+// Hand-off: the row above is checked (fresh word) and the next block's halo loaded at step group
+// GSA_HOP_Q of a block; GSA_MIDPUB also publishes the hand-off progress in mid-block.
+#ifndef GSA_HOP_Q
+#define GSA_HOP_Q 2
+#endif
+#ifndef GSA_MIDPUB
+#define GSA_MIDPUB 0
+#endif
 // Timing-experiment knobs (separate builds only; any set bit makes results WRONG):
 // 1 no halo loads, 2 no progress words / waits, 4 no sparse captures, 8 no hand-off writes,
 // 16 no output staging writes (full), 32 store waves store nothing (full), 64 store waves
-// read their LDS blocks but skip the global stores (full)
+// read their LDS blocks but skip the global stores (full), 128 store into one 16 KB window,
+// 256 4-byte stores, 512 no LDS reads by the store waves, 1024 store into a 256 KB ring per
+// workgroup (L2-resident) instead of the matrix
 #ifndef GSA_KNOB
 #define GSA_KNOB 0
 #endif
@@ -335,16 +345,20 @@ __device__ __forceinline__ void strip_wave(const StripArgs& a, const Lds& L, int
                                  __HIP_MEMORY_SCOPE_WORKGROUP);
     };
 
-    // block b may start once: the row above is valid up to the halo of block b+1, ring_out
-    // has room for block b, and (strip 0) the letters of block b+2 are published
-    // (full fills) and the loader has stored block b-2 whose staging slots block b reuses
-    auto ready = [&](int pin, int pco, int pxo, int psto, int b) {
+    // Block b may start once ring_out has room for it, (strip 0) the letters of block b+2 are
+    // published and (full fills) both store waves have drained the staging slots it reuses.
+    // The row above is checked separately, in the middle of block b, right before the halo of
+    // block b+1 is loaded (pin_ok): checked late and with a fresh word, it costs the hand-off
+    // ~20 steps less lag than a check at block start with a word read a block earlier.
+    auto pin_ok = [&](int pin, int b) { return (GSA_KNOB & 2) != 0 || pin >= min(16 * b + 32, Cp + 1); };
+    auto start_ok = [&](int pco, int pxo, int psto, int b) {
         if constexpr ((GSA_KNOB & 2) != 0) return true;
-        bool ok = pin >= min(16 * b + 32, Cp + 1) && pco >= 16 * b - 307;
+        bool ok = pco >= 16 * b - 307;
         if (w == 0) ok = ok && pxo >= min(16 * b + 48, Cp + 1);
         if constexpr (MODE == kModeFull) ok = ok && psto >= b - 1;
         return ok;
     };
+    auto ready = [&](int pin, int pco, int pxo, int psto, int b) { return pin_ok(pin, b) && start_ok(pco, pxo, psto, b); };
     // bounded spin until ready(b); false on time-out / error
     auto wait_ready = [&](int& pin, int& pco, int& pxo, int& psto, int b) {
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
@@ -357,6 +371,29 @@ __device__ __forceinline__ void strip_wave(const StripArgs& a, const Lds& L, int
                 return false;
             }
             pin = flag_ld(fin);
+            pco = flag_ld(fcout);
+            if (w == 0) pxo = flag_ld(F + kFXo);
+            if constexpr (MODE == kModeFull)
+            {
+                psto = flag_ld(fsto);
+#pragma unroll
+                for (int k = 1; k < kStoreWaves; ++k) psto = min(psto, flag_ld(fsto + 4 * k));
+            }
+        }
+        return true;
+    };
+
+    // bounded spin until start_ok(b)
+    auto wait_start = [&](int& pco, int& pxo, int& psto, int b) {
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        while (!start_ok(pco, pxo, psto, b))
+        {
+            __builtin_amdgcn_s_sleep(1);
+            if (__builtin_amdgcn_s_memrealtime() - t0 > kSpinLimit || err_set(a))
+            {
+                atomicOr(a.err, 1u);
+                return false;
+            }
             pco = flag_ld(fcout);
             if (w == 0) pxo = flag_ld(F + kFXo);
             if constexpr (MODE == kModeFull)
@@ -402,7 +439,13 @@ __device__ __forceinline__ void strip_wave(const StripArgs& a, const Lds& L, int
             const int t0 = 16 * b + 4 * q;
             lfree[q] = lds_ld4(xo_addr(t0 + 32));
 #pragma unroll
-            for (int u = 0; u < 4; ++u) snext[4 * q + u] = lds_ld2((uint32_t)lnext[q][u] + laneoff);
+            for (int u = 0; u < 4; ++u)
+            {
+                if constexpr ((GSA_KNOB & 16384) != 0)
+                    snext[4 * q + u] = int2v {lnext[q][u] & 0x00ff00ff, lnext[q][u] & 0x00ff00ff};  // timing: no profile reads
+                else
+                    snext[4 * q + u] = lds_ld2((uint32_t)lnext[q][u] + laneoff);
+            }
             int Xa[4], Xb[4], Xc[4], Xd[4];
 #pragma unroll
             for (int u = 0; u < 4; ++u)
@@ -445,12 +488,31 @@ __device__ __forceinline__ void strip_wave(const StripArgs& a, const Lds& L, int
                             int4v {X[k][0], X[k][1], X[k][2], X[k][3]});
                 }
             }
+            if (GSA_MIDPUB && q == 1) flag_st(F + kFProg + 4 * (w + 1), 16 * b + 8 - 63);  // steps < 16b+8 handed off
+            if (q == GSA_HOP_Q - 1) rpin = raw_ld(fin);
+            if (q == GSA_HOP_Q)
+            {
+                // halo of the next block, once the row above covers it
+                int pn = __builtin_amdgcn_readfirstlane(rpin);
+                if (!pin_ok(pn, b))
+                {
+                    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+                    while (!pin_ok(pn = flag_ld(fin), b))
+                    {
+                        __builtin_amdgcn_s_sleep(1);
+                        if (__builtin_amdgcn_s_memrealtime() - t0 > kSpinLimit || err_set(a))
+                        {
+                            atomicOr(a.err, 1u);
+                            break;
+                        }
+                    }
+                }
+                cbar();
+                hv_load(b + 1, hvnext);
+                flag_st(F + kFCons + 4 * w, 16 * (b + 1) - 3);  // after the halo reads (in order)
+            }
             if (q == 0)
             {
-                // halo of the next block (its progress was checked before this block)
-                hv_load(b + 1, hvnext);
-                flag_st(F + kFCons + 4 * w, 16 * (b + 1) - 3);
-                rpin = raw_ld(fin);
                 rpco = raw_ld(fcout);
                 if (w == 0) rpxo = raw_ld(F + kFXo);
                 if constexpr (MODE == kModeFull)
@@ -479,13 +541,12 @@ __device__ __forceinline__ void strip_wave(const StripArgs& a, const Lds& L, int
     auto run_block = [&](int b, int2v (&scur)[kBLK], int2v (&snext)[kBLK], int4v (&lnext)[4], int4v (&lfree)[4],
                          int (&hvcur)[kBLK], int (&hvnext)[kBLK]) {
         stamp(a, tk, w, b, 0, lane);
-        pin = __builtin_amdgcn_readfirstlane(rpin);
         pco = __builtin_amdgcn_readfirstlane(rpco);
         pxo = (w == 0) ? __builtin_amdgcn_readfirstlane(rpxo) : 0;
         psto = (MODE == kModeFull) ? __builtin_amdgcn_readfirstlane(rpsto) : 0;
-        if (!ready(pin, pco, pxo, psto, b))
+        if (!start_ok(pco, pxo, psto, b))
         {
-            if (!wait_ready(pin, pco, pxo, psto, b)) return false;
+            if (!wait_start(pco, pxo, psto, b)) return false;
         }
         cbar();
         stamp(a, tk, w, b, 1, lane);
@@ -683,6 +744,13 @@ __device__ __forceinline__ void store_wave(const StripArgs& a, const Lds& L, int
                     v = int4v {lane, j, bs, 0};
                 else
                     v = lds_ld4(ob + (uint32_t)rl * kOutRow + 16u * out_chunk(rl, ch + q));
+                if constexpr ((GSA_KNOB & 1024) != 0)
+                {
+                    // timing knob: a 256 KB ring per workgroup (L2-resident) instead of the matrix
+                    const size_t ri = ((size_t)(bs * 16 + j) * 64 + lane) & 16383;
+                    *(gptr<int4a>)(G(a.score) + (size_t)blockIdx.x * 65536 + 4 * ri) = int4a {v.x, v.y, v.z, v.w};
+                    continue;
+                }
                 if constexpr ((GSA_KNOB & 128) != 0)
                 {
                     // timing knob: stores into one 16 KB window (L2-resident) instead of the matrix
@@ -710,7 +778,12 @@ __device__ __forceinline__ void store_wave(const StripArgs& a, const Lds& L, int
                     if (c >= 1 && c + 3 <= a.C)
                     {
                         const int4a o {v.x + base, v.y + base + a.g, v.z + base + 2 * a.g, v.w + base + 3 * a.g};
-                        if constexpr (GSA_NT_STORE)
+                        if constexpr ((GSA_KNOB & 8192) != 0)
+                        {
+                            int4v ov {o.x, o.y, o.z, o.w};
+                            asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(dst), "v"(ov) : "memory");
+                        }
+                        else if constexpr (GSA_NT_STORE)
                             __builtin_nontemporal_store(o, (gptr<int4a>)dst);
                         else
                             *(gptr<int4a>)dst = o;
@@ -723,6 +796,8 @@ __device__ __forceinline__ void store_wave(const StripArgs& a, const Lds& L, int
                     }
                 }
             }
+            if constexpr ((GSA_KNOB & 2048) != 0) __builtin_amdgcn_s_waitcnt(0x0F78);  // vmcnt(8): bounded in-flight stores
+            if constexpr ((GSA_KNOB & 4096) != 0) __builtin_amdgcn_s_waitcnt(0x4F70);  // vmcnt(16)
             sb[w] = bs + 1;
             flag_st(F + kFSto + 16 * w + 4 * sw, sb[w]);  // after the block's LDS reads (in order)
             moved = true;

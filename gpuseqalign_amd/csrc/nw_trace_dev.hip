@@ -54,33 +54,52 @@ constexpr int kDiagEq = 0, kDiagX = 1, kUp = 2, kLeft = 3;
 
 extern __shared__ __attribute__((aligned(16))) int tsm[];
 
+constexpr int kTW = 4;  // waves per workgroup: the panels of a tile are pipelined over them
+
+__device__ __forceinline__ int lds_flag_ld(int* p)
+{
+    return __builtin_amdgcn_readfirstlane(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+}
+__device__ __forceinline__ void lds_flag_st(int* p, int v)
+{
+    asm volatile("" ::: "memory");  // the boundary values are written before the word (LDS executes in order)
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
 // Move codes of tile (iT, jT) for rows 1..iE, columns 1..jE:
 // word ((a-1)/16 * nP + (b-1)/64) * 64 + (b-1)%64 holds rows a..a+15 of column b, 2 bits each.
+// Wave w takes panels w, w+kTW, ...; panel p reads its left boundary column from slot p % (kTW+1)
+// and writes its right one to slot (p+1) % (kTW+1), publishing (panel << 16 | rows) every 16
+// rows, so consecutive panels run 16 rows apart.
 template <bool DIRS_LDS>
-__device__ void tile_moves(const TraceArgs& a, int iT, int jT, int iE, int jE, int* sub, int* colbuf, int* yb,
-                           int* yraw, int* xraw, unsigned* dirs, int lane, bool first)
+__device__ void tile_moves(const TraceArgs& a, int iT, int jT, int iE, int jE, int* sub, int* bnd, int* yraw,
+                           int* xraw, int* bprog, unsigned* dirs, int w, int lane, bool first)
 {
-    const int g = a.g, tBx = a.tBx, tBy = a.tBy;
+    const int g = a.g, tBx = a.tBx, tBy = a.tBy, BS = tBy + 1;
     const long long W = tBx + 1, H = tBy + 1;
     const long long k = (long long)iT * a.tcols + jT;
     const gptr<const int> hr = G(a.hrow) + k * W;
     const gptr<const int> hc = G(a.hcol) + k * H;
     const long long rbase = (long long)iT * tBy, cbase = (long long)jT * tBx;
-    __syncthreads();
-    for (int e = lane; e <= iE; e += 64)
+    const int tid = threadIdx.x;
+    __syncthreads();  // the previous walk has read its codes
+    for (int e = tid; e <= iE; e += 64 * kTW)
     {
-        colbuf[e] = hc[e];
+        bnd[e] = hc[e];  // slot 0: the tile's header column = left boundary of panel 0
         const long long r = rbase + e;
-        const int y = r < a.adjrows ? G(a.seqY)[r] : 0;
-        yraw[e] = y;
-        yb[e] = clamp_letter(y, a.substsz) * a.substsz;
+        yraw[e] = r < a.adjrows ? G(a.seqY)[r] : 0;
     }
-    for (int c = lane; c <= jE; c += 64) xraw[c] = G(a.seqX)[cbase + c];  // real columns only (c <= jE)
+    for (int c = tid; c <= jE; c += 64 * kTW) xraw[c] = G(a.seqX)[cbase + c];  // real columns only (c <= jE)
+    if (tid <= kTW) bprog[tid] = (tid == 0) ? iE : -1;  // boundary 0 complete, the others empty
     __syncthreads();
     const int nP = (tBx + 63) / 64;
     const int nPu = (jE + 63) / 64;  // panels the walk can reach
-    for (int p = 0; p < nPu; ++p)
+    for (int p = w; p < nPu; p += kTW)
     {
+        const int* bin = bnd + (p % (kTW + 1)) * BS;
+        int* bout = bnd + ((p + 1) % (kTW + 1)) * BS;
+        int* fin = bprog + p % (kTW + 1);
+        int* fout = bprog + (p + 1) % (kTW + 1);
         const int j0 = 64 * p;
         const int col = j0 + 1 + lane;
         const bool valid = col <= tBx;
@@ -89,33 +108,40 @@ __device__ void tile_moves(const TraceArgs& a, int iT, int jT, int iE, int jE, i
         int up = valid ? hr[col] : 0;
         const int c1 = -(lane + 1) * g, c2 = -lane * g, c3 = (lane + 1) * g;
         const int last = min(63, tBx - 1 - j0);
-        int Lprev = __builtin_amdgcn_readfirstlane(colbuf[0]);
-        const int top = __builtin_amdgcn_readlane(up, last);
-        __syncthreads();
-        if (lane == 0) colbuf[0] = top;
-        const int xr = (col <= jE) ? xraw[col] : -1;  // raw letter of this lane's column
+        int Lprev = __builtin_amdgcn_readfirstlane(hr[j0]);  // H[0][j0]
+        const int xr = (col <= jE) ? xraw[col] : -1;         // raw letter of this lane's column
         unsigned word = 0;
-        // 64 rows at a time: left boundary and letters of row i0+r sit in lane r (readlane,
-        // no LDS latency per row); the substitution value is read one row ahead
-        for (int i0 = 1; i0 <= iE; i0 += 64)
+        int avail = 0;  // rows of the left boundary known to be written
+        for (int i0 = 1; i0 <= iE; i0 += 16)
         {
-            const int nr = min(64, iE - i0 + 1);
-            const int Lv = (lane < nr) ? colbuf[i0 + lane] : 0;
-            const int yv = (lane < nr) ? yb[i0 + lane] : 0;
+            const int nr = min(16, iE - i0 + 1);
+            const int need = i0 + nr - 1;
+            while (avail < need)
+            {
+                const int v = lds_flag_ld(fin);
+                if ((v >> 16) == (p == 0 ? 0 : p) && (v & 0xffff) >= need && v >= 0)
+                    avail = v & 0xffff;
+                else
+                    __builtin_amdgcn_s_sleep(1);
+            }
+            // left boundary and letters of row i0+r in lane r (readlane, no LDS latency per row)
+            const int Lv = (lane < nr) ? bin[i0 + lane] : 0;
             const int yrv = (lane < nr) ? yraw[i0 + lane] : 0;
-            int s_nx = sub[__builtin_amdgcn_readfirstlane(yv) + xo];
+            int s_nx = sub[clamp_letter(__builtin_amdgcn_readfirstlane(yrv), a.substsz) * a.substsz + xo];
             for (int r = 0; r < nr; ++r)
             {
                 const int i = i0 + r;
                 const int L = __builtin_amdgcn_readlane(Lv, r);
+                const int yr = __builtin_amdgcn_readlane(yrv, r);
                 const int s = s_nx;
-                if (r + 1 < nr) s_nx = sub[__builtin_amdgcn_readlane(yv, r + 1) + xo];
+                if (r + 1 < nr)
+                    s_nx = sub[clamp_letter(__builtin_amdgcn_readlane(yrv, r + 1), a.substsz) * a.substsz + xo];
                 const int diag = __builtin_amdgcn_update_dpp(Lprev, up, 0x138, 0xf, 0xf, false);  // H[i-1][b-1]
                 const int m = max(max(diag + s + c1, up + c2), L) - L;
                 const int h = wave_prefix_max(m) + L + c3;
                 const int left = __builtin_amdgcn_update_dpp(L, h, 0x138, 0xf, 0xf, false);  // H[i][b-1]
                 const int bdu = max(diag, up);
-                int code = (diag < up) ? kUp : ((xr == __builtin_amdgcn_readlane(yrv, r)) ? kDiagEq : kDiagX);
+                int code = (diag < up) ? kUp : ((xr == yr) ? kDiagEq : kDiagX);
                 code = (bdu < left) ? kLeft : code;
                 word |= (unsigned)code << (2 * ((i - 1) & 15));
                 if (((i - 1) & 15) == 15 || i == iE)
@@ -123,11 +149,12 @@ __device__ void tile_moves(const TraceArgs& a, int iT, int jT, int iE, int jE, i
                     dirs[((size_t)((i - 1) >> 4) * nP + p) * 64 + lane] = word;
                     word = 0;
                 }
-                if (lane == last) colbuf[i] = h;
+                if (lane == last) bout[i] = h;
                 if (first && i == iE && col == jE) G(a.res)[1] = h;  // H[adjrows-1][adjcols-1] = align_cost
                 Lprev = L;
                 up = h;
             }
+            if (lane == 0) lds_flag_st(fout, ((p + 1) << 16) | need);
         }
     }
     __syncthreads();
@@ -135,96 +162,117 @@ __device__ void tile_moves(const TraceArgs& a, int iT, int jT, int iE, int jE, i
 }
 
 template <bool DIRS_LDS>
-__global__ void __launch_bounds__(64) trace_sparse_kernel(TraceArgs a)
+__global__ void __launch_bounds__(64 * kTW) trace_sparse_kernel(TraceArgs a)
 {
-    const int lane = threadIdx.x;
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     const int tBy = a.tBy;
     const int nP = (a.tBx + 63) / 64;
     int* sub = tsm;
-    int* colbuf = sub + 32 * 32;
-    int* yb = colbuf + (tBy + 1);
-    int* yraw = yb + (tBy + 1);
+    int* bnd = sub + 32 * 32;
+    int* yraw = bnd + (kTW + 1) * (tBy + 1);
     int* xraw = yraw + (tBy + 1);
-    unsigned* dirs = DIRS_LDS ? (unsigned*)(xraw + (a.tBx + 1)) : a.dirs_scratch;
-    for (int k = lane; k < a.substsz * a.substsz; k += 64) sub[k] = G(a.subst)[k];
+    int* bprog = xraw + (a.tBx + 1);
+    int* state = bprog + 8;  // walk state handed from wave 0 to the others
+    unsigned* dirs = DIRS_LDS ? (unsigned*)(state + 8) : a.dirs_scratch;
+    for (int k = tid; k < a.substsz * a.substsz; k += 64 * kTW) sub[k] = G(a.subst)[k];
 
     int iT = a.iT0, jT = a.jT0, iE = a.iE0, jE = a.jE0;
     const int Wm = a.tBx, Hm = a.tBy;  // hrowLen-1, hcolLen-1
     long long n = 0;
-    bool done = false, first = true;
-    if (lane == 0 && (iE == 0 || jE == 0))
+    bool first = true;
+    if (tid == 0 && (iE == 0 || jE == 0))
     {
         // start cell on a header of its tile (empty sequence): the value is stored there
         const long long k = (long long)iT * a.tcols + jT;
         G(a.res)[1] = (iE == 0) ? G(a.hrow)[k * (a.tBx + 1) + jE] : G(a.hcol)[k * (a.tBy + 1) + iE];
     }
-    while (!done)
+    for (;;)
     {
-        if (iE > 0 && jE > 0) tile_moves<DIRS_LDS>(a, iT, jT, iE, jE, sub, colbuf, yb, yraw, xraw, dirs, lane, first);
+        if (iE > 0 && jE > 0)
+            tile_moves<DIRS_LDS>(a, iT, jT, iE, jE, sub, bnd, yraw, xraw, bprog, dirs, w, lane, first);
         first = false;
-        for (;;)
+        int done = 0;
+        if (w == 0)
         {
-            int di = 0, dj = 0, e = 0;
-            if (iE > 0 && jE > 0)
+            for (;;)
             {
-                const size_t wi = ((size_t)((iE - 1) >> 4) * nP + ((jE - 1) >> 6)) * 64 + ((jE - 1) & 63);
-                const unsigned w = __builtin_amdgcn_readfirstlane(dirs[wi]);
-                const int code = (w >> (2 * ((iE - 1) & 15))) & 3;
-                if (code <= kDiagX)
+                int di = 0, dj = 0, e = 0;
+                if (iE > 0 && jE > 0)
                 {
-                    di = dj = -1;
-                    e = (code == kDiagEq) ? '=' : 'X';  // seqX[j] == seqY[i]
+                    const size_t wi = ((size_t)((iE - 1) >> 4) * nP + ((jE - 1) >> 6)) * 64 + ((jE - 1) & 63);
+                    const unsigned cw = __builtin_amdgcn_readfirstlane(dirs[wi]);
+                    const int code = (cw >> (2 * ((iE - 1) & 15))) & 3;
+                    if (code <= kDiagX)
+                    {
+                        di = dj = -1;
+                        e = (code == kDiagEq) ? '=' : 'X';  // seqX[j] == seqY[i]
+                    }
+                    else if (code == kUp)
+                    {
+                        di = -1;
+                        e = 'I';
+                    }
+                    else
+                    {
+                        dj = -1;
+                        e = 'D';
+                    }
                 }
-                else if (code == kUp)
+                else if (iE > 0)
                 {
                     di = -1;
                     e = 'I';
                 }
-                else
+                else if (jE > 0)
                 {
                     dj = -1;
                     e = 'D';
                 }
+                if (di == 0 && dj == 0)
+                {
+                    done = 1;
+                    break;
+                }
+                if (lane == 0 && n < a.cap) G(a.edits)[n] = (unsigned char)e;
+                ++n;
+                iE += di;
+                jE += dj;
+                // into the tile above / left / up-left on reaching its header (nwtrace2_sparse.cpp:195-214)
+                const int diT = (iE == 0 && iT > 0) ? 1 : 0;
+                const int djT = (jE == 0 && jT > 0) ? 1 : 0;
+                if (diT || djT)
+                {
+                    iT -= diT;
+                    jT -= djT;
+                    if (iE == 0 && di != 0) iE = Hm;
+                    if (jE == 0 && dj != 0) jE = Wm;
+                    break;
+                }
             }
-            else if (iE > 0)
+            if (lane == 0)
             {
-                di = -1;
-                e = 'I';
-            }
-            else if (jE > 0)
-            {
-                dj = -1;
-                e = 'D';
-            }
-            if (di == 0 && dj == 0)
-            {
-                done = true;
-                break;
-            }
-            if (lane == 0 && n < a.cap) G(a.edits)[n] = (unsigned char)e;
-            ++n;
-            iE += di;
-            jE += dj;
-            // into the tile above / left / up-left on reaching its header (nwtrace2_sparse.cpp:195-214)
-            const int diT = (iE == 0 && iT > 0) ? 1 : 0;
-            const int djT = (jE == 0 && jT > 0) ? 1 : 0;
-            if (diT || djT)
-            {
-                iT -= diT;
-                jT -= djT;
-                if (iE == 0 && di != 0) iE = Hm;
-                if (jE == 0 && dj != 0) jE = Wm;
-                break;
+                state[0] = iT;
+                state[1] = jT;
+                state[2] = iE;
+                state[3] = jE;
+                state[4] = done;
             }
         }
+        __syncthreads();
+        iT = state[0];
+        jT = state[1];
+        iE = state[2];
+        jE = state[3];
+        done = state[4];
+        if (done) break;
     }
-    if (lane == 0) G(a.res)[0] = n;
+    if (tid == 0) G(a.res)[0] = n;
 }
 
 size_t trace_lds_bytes(int tBy, int tBx, int substsz, bool dirs_lds)
 {
     (void)substsz;
-    const size_t base = (size_t)4 * (32 * 32 + 3 * (tBy + 1) + (tBx + 1));
+    const size_t base = (size_t)4 * (32 * 32 + (kTW + 1) * (tBy + 1) + (tBy + 1) + (tBx + 1) + 16);
     return base + (dirs_lds ? trace_dir_words(tBy, tBx) * 4 : 0);
 }
 
@@ -240,14 +288,14 @@ hipError_t launch_trace_sparse(const TraceArgs& a, hipStream_t st)
         hipError_t e = hipFuncSetAttribute((const void*)trace_sparse_kernel<true>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
         if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(trace_sparse_kernel<true>, dim3(1), dim3(64), bytes, st, a);
+        hipLaunchKernelGGL(trace_sparse_kernel<true>, dim3(1), dim3(64 * kTW), bytes, st, a);
     }
     else
     {
         hipError_t e = hipFuncSetAttribute((const void*)trace_sparse_kernel<false>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
         if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(trace_sparse_kernel<false>, dim3(1), dim3(64), bytes, st, a);
+        hipLaunchKernelGGL(trace_sparse_kernel<false>, dim3(1), dim3(64 * kTW), bytes, st, a);
     }
     return hipGetLastError();
 }
