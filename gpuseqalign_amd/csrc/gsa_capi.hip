@@ -63,6 +63,9 @@ struct gsa_ctx
     size_t sbnd_cap = 0;
     // mlsppt: host-mapped per-ticket completion flags and the copy-back stream
     unsigned* ptflags = nullptr;
+    // ring-mode full fills: ring + descriptors + head/tail/final words of the strip workgroups
+    int* ringbuf = nullptr;
+    size_t ringbuf_cap = 0;
     size_t ptflags_cap = 0;
     hipStream_t cstream = nullptr;
     unsigned long long* sctl = nullptr;  // [0] ticket|err, [1] best key, [2] result
@@ -143,6 +146,16 @@ int full_ns()
         return (v == 1 || v == 2) ? v : gsa::kFullNSDefault;
     }();
     return ns;
+}
+
+// Ring mode for full fills (nw_strip.hip): the output leaves the strip CUs through L2-resident
+// rings drained by copy workgroups on otherwise idle CUs.  Opt-in (GSA_FULL_RING=1, read per
+// launch): measured slower than the store waves -- the agent-scope
+// write-backs that make the ring visible across XCDs cost more than the strip saves.
+bool full_ring_enabled()
+{
+    const char* e = std::getenv("GSA_FULL_RING");
+    return e && std::atoi(e) == 1;
 }
 
 // NULL is the HIP null stream, as everywhere in HIP; the host-buffer entry points use the
@@ -276,8 +289,38 @@ int enqueue_batch(gsa_ctx* ctx, int mode, int npairs, const gsa_pair_dev* pairs,
     e = hipMemsetAsync(ctx->ctl, 0, 16, st);
     if (e != hipSuccess) return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
     // one pair: one workgroup per CU (its tickets are a chain); a batch: all resident slots
-    const int grid = (npairs == 1) ? std::max(1, std::min((int)tickets, ctx->cu_count)) : 0;
-    e = gsa::launch_strip_fill(a, mode, grid, st);
+    int grid = (npairs == 1) ? std::max(1, std::min((int)tickets, ctx->cu_count)) : 0;
+    int launchMode = mode;
+    if (mode == gsa::kModeFull && npairs == 1 && a.ns == 1 && !done && full_ring_enabled() && tickets >= 8 &&
+        2 * std::min<long long>(tickets, ctx->cu_count / 2) <= ctx->cu_count)
+    {
+        // nStrip a multiple of 8: copy workgroup nStrip+s then sits on strip s's XCD
+        int nStrip = (int)std::min<long long>(tickets, ctx->cu_count / 2);
+        nStrip -= nStrip % 8;
+        const size_t ringInts = (size_t)nStrip * gsa::kRingBlocks * 4096;
+        const size_t ctlInts = (size_t)nStrip * (gsa::kRingBlocks * 2 + 1 + gsa::kRingWaves + 1);
+        if (ctx->ringbuf_cap < ringInts + ctlInts)
+        {
+            if (ctx->ringbuf) (void)hipFree(ctx->ringbuf);
+            ctx->ringbuf = nullptr;
+            ctx->ringbuf_cap = 0;
+            if ((e = hipMalloc(&ctx->ringbuf, (ringInts + ctlInts) * sizeof(int))) != hipSuccess)
+                return fail(ctx, e, GSA_ERROR_MEMORY_ALLOCATION);
+            ctx->ringbuf_cap = ringInts + ctlInts;
+        }
+        a.ring = ctx->ringbuf;
+        a.rdesc = a.ring + ringInts;
+        a.rhead = a.rdesc + (size_t)nStrip * gsa::kRingBlocks * 2;
+        a.rtail = a.rhead + nStrip;
+        a.rfinal = a.rtail + (size_t)nStrip * gsa::kRingWaves;
+        a.nStrip = nStrip;
+        // head / tail / final words start at 0 every launch
+        e = hipMemsetAsync(a.rhead, 0, (size_t)nStrip * (2 + gsa::kRingWaves) * sizeof(int), st);
+        if (e != hipSuccess) return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
+        launchMode = gsa::kModeFullRing;
+        grid = 2 * nStrip;
+    }
+    e = gsa::launch_strip_fill(a, launchMode, grid, st);
     if (e != hipSuccess) return fail(ctx, e, GSA_ERROR_KERNEL_FAILURE);
     return GSA_SUCCESS;
 }
@@ -346,6 +389,7 @@ void gsa_ctx_destroy(gsa_ctx* ctx)
     if (ctx->sctl) (void)hipFree(ctx->sctl);
     if (ctx->ptflags) (void)hipHostFree(ctx->ptflags);
     if (ctx->cstream) (void)hipStreamDestroy(ctx->cstream);
+    if (ctx->ringbuf) (void)hipFree(ctx->ringbuf);
     for (int k = 0; k < gsa_ctx::kStage; ++k)
     {
         if (ctx->stage[k]) (void)hipHostFree(ctx->stage[k]);

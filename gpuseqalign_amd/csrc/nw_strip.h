@@ -8,6 +8,11 @@ namespace gsa {
 
 constexpr int kModeFull = 0;
 constexpr int kModeSparse = 1;
+// Full fill whose output leaves the strip's CU through an L2-resident ring: copy workgroups
+// on other CUs (same XCD) move it to the matrix (nw_strip.hip, "ring mode").
+constexpr int kModeFullRing = 2;
+constexpr int kRingBlocks = 16;  // ring slots (16-step blocks of 256 rows, 16 KB) per strip workgroup
+constexpr int kRingWaves = 4;    // waves per workgroup in ring mode (strip + loader + 2 idle / 4 copy)
 constexpr int kWaveRows = 256;                          // rows per strip (one wave, 4 rows per lane)
 constexpr int kSparseNS = 4;                            // strip waves per workgroup, sparse fills
 constexpr int kSparseTileBy = kWaveRows * kSparseNS;    // = tile height of the mlsp matrices
@@ -57,6 +62,16 @@ struct StripArgs
     // mlsppt: host-mapped per-ticket flags, set to `epoch` once a super-strip's outputs are
     // written back past L2 (null: no signalling)
     unsigned* done;
+    // ring mode (kModeFullRing): strip workgroups are blockIdx < nStrip, copy workgroup
+    // nStrip + s drains strip workgroup s's ring
+    int* ring;      // nStrip * kRingBlocks * 4096 ints (H', strip lane layout)
+    int* rdesc;     // nStrip * kRingBlocks * 2 ints: {global ticket, block}
+    int* rhead;     // nStrip: ring blocks published (agent release by the strip's loader)
+    int* rtail;     // nStrip * kRingWaves: ring blocks consumed, per copy wave
+    int* rfinal;    // nStrip: total blocks + 1 once the strip workgroup has no more tickets
+    int nStrip;
+    int ringBase;   // per ticket: ring blocks of this workgroup before this ticket
+    int ringTicket; // per ticket: its global ticket index (the copy workgroup maps it to rows)
     // batch: the per-pair fields above are loaded from pairs[] for every ticket
     const PairDesc* pairs;
     int nPairs;

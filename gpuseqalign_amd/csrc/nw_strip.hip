@@ -111,6 +111,8 @@ struct Lds
 //        xo_cols @ 64 (letter ring valid for columns < xo_cols), ticket @ 68,
 //        sto[w][s] @ 80+16w+4s (full fills: blocks of strip w stored to HBM by store wave s).
 constexpr uint32_t kFProg = 0, kFCons = 32, kFXo = 64, kFTicket = 68, kFSto = 80;
+// ring mode: ring blocks of this workgroup complete (strip -> loader), min consumed (loader mirror)
+constexpr uint32_t kFRingDone = 112, kFRingTail = 116;
 // Full fills: store waves per workgroup (<= 4; full fills use NS <= 2).  One wave sustains ~5.5 B/clk of 16-byte stores
 // whatever the pattern (tools/ubench/store_ubench.hip); a strip emits 1 KB per step.
 #ifndef GSA_STORE_WAVES
@@ -200,6 +202,12 @@ __device__ __forceinline__ uint32_t ring_elem(int c)
 #ifndef GSA_HOP_Q
 #define GSA_HOP_Q 2
 #endif
+#ifndef GSA_RING_PUB
+#define GSA_RING_PUB 2
+#endif
+#ifndef GSA_RING_FENCE
+#define GSA_RING_FENCE 1
+#endif
 #ifndef GSA_MIDPUB
 #define GSA_MIDPUB 0
 #endif
@@ -258,9 +266,10 @@ __device__ __forceinline__ void strip_wave(const StripArgs& a, const Lds& L, int
     const int Cp = a.Cp;
     const int r0 = tk * TR + kWaveRows * w + 1;  // first row of the strip
     const uint32_t F = L.flags;
-    if (MODE == kModeFull && r0 > a.R)
+    if (MODE != kModeSparse && r0 > a.R)
     {
         // nothing to store below the matrix: pass the (never read) hand-off through
+        if constexpr (MODE == kModeFullRing) flag_st(F + kFRingDone, a.ringBase + (Cp + 64 + kBLK - 1) / kBLK);
         flag_st(F + kFProg + 4 * (w + 1), kBig);
         flag_st(F + kFCons + 4 * w, kBig);
         return;
@@ -356,6 +365,7 @@ __device__ __forceinline__ void strip_wave(const StripArgs& a, const Lds& L, int
         bool ok = pco >= 16 * b - 307;
         if (w == 0) ok = ok && pxo >= min(16 * b + 48, Cp + 1);
         if constexpr (MODE == kModeFull) ok = ok && psto >= b - 1;
+        if constexpr (MODE == kModeFullRing) ok = ok && psto >= a.ringBase + b - kRingBlocks + 1;  // ring slot free
         return ok;
     };
     auto ready = [&](int pin, int pco, int pxo, int psto, int b) { return pin_ok(pin, b) && start_ok(pco, pxo, psto, b); };
@@ -379,6 +389,7 @@ __device__ __forceinline__ void strip_wave(const StripArgs& a, const Lds& L, int
 #pragma unroll
                 for (int k = 1; k < kStoreWaves; ++k) psto = min(psto, flag_ld(fsto + 4 * k));
             }
+            if constexpr (MODE == kModeFullRing) psto = flag_ld(F + kFRingTail);
         }
         return true;
     };
@@ -402,6 +413,7 @@ __device__ __forceinline__ void strip_wave(const StripArgs& a, const Lds& L, int
 #pragma unroll
                 for (int k = 1; k < kStoreWaves; ++k) psto = min(psto, flag_ld(fsto + 4 * k));
             }
+            if constexpr (MODE == kModeFullRing) psto = flag_ld(F + kFRingTail);
         }
         return true;
     };
@@ -477,7 +489,41 @@ __device__ __forceinline__ void strip_wave(const StripArgs& a, const Lds& L, int
             // hand-off: row D of 4 steps, slot (group - lane)
             if constexpr (!(GSA_KNOB & 8))
                 lds_st4(ring_out + 16u * (uint32_t)(((t0 >> 2) - lane) & (kRing - 1)), int4v {Xd[0], Xd[1], Xd[2], Xd[3]});
-            if constexpr (MODE == kModeFull && !(GSA_KNOB & 16))
+            if constexpr (MODE == kModeFullRing)
+            {
+                // H' of the 4 rows x 4 steps -> ring slot of this block, row-major [row][16 steps]:
+                // plain 16-byte global stores that stay in L2; the copy workgroup un-shifts them
+                const gptr<int> rb = G(a.ring) + ((size_t)blockIdx.x * kRingBlocks + (size_t)((a.ringBase + b) & (kRingBlocks - 1))) * 4096;
+#pragma unroll
+                for (int k = 0; k < kK; ++k)
+                {
+                    const int* X[kK] = {Xa, Xb, Xc, Xd};
+                    *(gptr<int4v>)(rb + (kK * lane + k) * 16 + 4 * q) = int4v {X[k][0], X[k][1], X[k][2], X[k][3]};
+                }
+            }
+            else if constexpr (MODE == kModeFull && (GSA_KNOB & (32768 | 65536)) != 0)
+            {
+                // timing knobs: the strip stores its 4x4 values itself (32768: a 256 KB ring per
+                // workgroup, L2-resident; 65536: the matrix rows, shifted values)
+#pragma unroll
+                for (int k = 0; k < kK; ++k)
+                {
+                    const int* X[kK] = {Xa, Xb, Xc, Xd};
+                    const int4a v4 {X[k][0], X[k][1], X[k][2], X[k][3]};
+                    if constexpr ((GSA_KNOB & 32768) != 0)
+                    {
+                        const size_t ri = ((size_t)(t0 >> 2) * 256 + kK * lane + k) & 16383;
+                        *(gptr<int4a>)(G(a.score) + (size_t)blockIdx.x * 65536 + 4 * ri) = v4;
+                    }
+                    else
+                    {
+                        const int r = r0 + kK * lane + k, c = t0 - lane;
+                        if (r <= a.R && c >= 1 && c + 3 <= a.C)
+                            *(gptr<int4a>)(G(a.score) + (size_t)r * (size_t)a.ld + c) = v4;
+                    }
+                }
+            }
+            else if constexpr (MODE == kModeFull && !(GSA_KNOB & 16))
             {
                 // stage H' of the 4 rows x 4 steps; the store waves un-shift and store them
 #pragma unroll
@@ -515,6 +561,7 @@ __device__ __forceinline__ void strip_wave(const StripArgs& a, const Lds& L, int
             {
                 rpco = raw_ld(fcout);
                 if (w == 0) rpxo = raw_ld(F + kFXo);
+                if constexpr (MODE == kModeFullRing) rpsto = raw_ld(F + kFRingTail);
                 if constexpr (MODE == kModeFull)
                 {
                     rpsto = raw_ld(fsto);
@@ -535,6 +582,17 @@ __device__ __forceinline__ void strip_wave(const StripArgs& a, const Lds& L, int
                 *(gptr<int4a>)(G(a.hcol) + ((size_t)tk * a.tcols + jT) * (size_t)(a.tBy + 1) + kWaveRows * w + kK * lane + 1) = v;
             }
         }
+        if constexpr (MODE == kModeFullRing)
+        {
+            const int gb = a.ringBase + b;
+            if (lane == 0)
+                *(gptr<int2v>)(G(a.rdesc) + 2 * ((size_t)blockIdx.x * kRingBlocks + (gb & (kRingBlocks - 1)))) =
+                    int2v {a.ringTicket, b};
+            // 17 stores per block (16 data + 1 descriptor) and nothing else on this wave's vmcnt:
+            // all blocks before this one are in L2 once at most 17 are outstanding
+            __builtin_amdgcn_s_waitcnt(0x4F71);  // vmcnt(17)
+            flag_st(F + kFRingDone, gb);
+        }
         flag_st(F + kFProg + 4 * (w + 1), b + 1 == NB ? kBig : 16 * (b + 1) - 63);
     };
 
@@ -543,7 +601,7 @@ __device__ __forceinline__ void strip_wave(const StripArgs& a, const Lds& L, int
         stamp(a, tk, w, b, 0, lane);
         pco = __builtin_amdgcn_readfirstlane(rpco);
         pxo = (w == 0) ? __builtin_amdgcn_readfirstlane(rpxo) : 0;
-        psto = (MODE == kModeFull) ? __builtin_amdgcn_readfirstlane(rpsto) : 0;
+        psto = (MODE != kModeSparse) ? __builtin_amdgcn_readfirstlane(rpsto) : 0;
         if (!start_ok(pco, pxo, psto, b))
         {
             if (!wait_start(pco, pxo, psto, b)) return false;
@@ -570,6 +628,11 @@ __device__ __forceinline__ void strip_wave(const StripArgs& a, const Lds& L, int
         if (b + 1 < NB && !run_block(b + 1, sB, sA, lxA, lxB, hvB, hvA)) return;
     }
     if (w == NS - 1) tstamp(a, tk, 2, lane);
+    if constexpr (MODE == kModeFullRing)
+    {
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): every block of this ticket is in L2
+        flag_st(F + kFRingDone, a.ringBase + NB);
+    }
     flag_st(F + kFCons + 4 * w, kBig);
 }
 
@@ -591,16 +654,49 @@ __device__ __forceinline__ void loader_wave(const StripArgs& a, const Lds& L, in
     const int hrowg = (tk + 1) * TR;  // global row of our last row
     // strips below the matrix (full mode, last super-strip) pass BIG through: the last
     // strip that computes is the one whose progress bounds the letter ring
-    const int nAct = (MODE == kModeFull) ? min(NS, (a.R - tk * TR + kWaveRows - 1) / kWaveRows) : NS;
+    const int nAct = (MODE != kModeSparse) ? min(NS, (a.R - tk * TR + kWaveRows - 1) / kWaveRows) : NS;
     const uint32_t ringN = L.ring + (uint32_t)nAct * (kRing * 16);
     int kx = 0;                       // next letter chunk (64 columns)
     int hnext = feed ? 0 : Cp + 1;    // next column of the row above to feed into ring 0
     int dnext = 0;                    // next column of our last row to drain
     int xl = load_letter(a, lane);
     uint64_t last = __builtin_amdgcn_s_memrealtime();
-    while (kx < nCh || hnext <= Cp || dnext <= Cp)
+    // ring mode: blocks of this ticket published to the copy workgroup, and its consumption
+    const int ringEnd = a.ringBase + (Cp + 64 + kBLK - 1) / kBLK;
+    int pubHead = a.ringBase;
+    int lastTail = (MODE == kModeFullRing) ? flag_ld(F + kFRingTail) : 0;
+    while (kx < nCh || hnext <= Cp || dnext <= Cp || (MODE == kModeFullRing && pubHead < ringEnd))
     {
         bool moved = false;
+        if constexpr (MODE == kModeFullRing)
+        {
+            // (0) ring blocks the strip has completed in L2 -> visible to the copy workgroup at agent
+            //     scope (release: L2 write-back), then the head word
+            const int rd = flag_ld(F + kFRingDone);
+            if (rd >= pubHead + GSA_RING_PUB || (rd > pubHead && rd == ringEnd))
+            {
+                if constexpr (GSA_RING_FENCE) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                if (lane == 0) __hip_atomic_store(G(a.rhead) + blockIdx.x, rd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                pubHead = rd;
+                moved = true;
+            }
+            // ring slots consumed: polled only when the strip gets within half a ring of them
+            if (pubHead - lastTail >= kRingBlocks / 2)
+            {
+                int t = kBig;
+#pragma unroll
+                for (int k = 0; k < kRingWaves; ++k)
+                    t = min(t, __hip_atomic_load(G(a.rtail) + (size_t)blockIdx.x * kRingWaves + k, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT));
+                t = __builtin_amdgcn_readfirstlane(t);
+                if (t > lastTail)
+                {
+                    lastTail = t;
+                    flag_st(F + kFRingTail, t);
+                    moved = true;
+                }
+            }
+        }
         const int pl = flag_ld(F + kFProg + 4 * nAct);
         const int cs0 = flag_ld(F + kFCons + 0);
         // (1) letters of chunk kx, once the last strip no longer reads the columns they replace
@@ -819,18 +915,126 @@ __device__ __forceinline__ void store_wave(const StripArgs& a, const Lds& L, int
         if (sink == 0x7fffffff) G(a.score)[0] = sink;  // keep the knob-64 reads alive
 }
 
+// ------------------------------------------------------------------------------------
+// ring mode: copy workgroup (on another CU of the strip's XCD when nStrip % 8 == 0, as
+// workgroups go to XCDs round-robin).  Wave w owns rows 64w..64w+63 of every ring block and
+// takes up to 4 published blocks per batch: 16 loads, the consumption word, then the
+// un-shifted 64-byte row segments to the matrix.  A wave's vmcnt retires in order, so a batch's
+// loads also wait for the previous batch's stores; batching keeps that below one block time.
+// Ring mode serves one pair (a.pairs[0]).
+// ------------------------------------------------------------------------------------
+template <int NS>
+__device__ void ring_copy_wg(const StripArgs& a)
+{
+    const int s = (int)blockIdx.x - a.nStrip;
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (w >= kRingWaves) return;
+    const PairDesc d = load_desc(a.pairs);
+    const gptr<const int> ringS = G((const int*)a.ring) + (size_t)s * kRingBlocks * 4096;
+    const gptr<int> score = G(d.score);
+    const int g = a.g;
+    int gb = 0;
+    uint64_t last = __builtin_amdgcn_s_memrealtime();
+    for (;;)
+    {
+        // relaxed polls; one acquire fence (cache invalidation) only once the head has moved
+        const int h = __builtin_amdgcn_readfirstlane(
+            __hip_atomic_load(G(a.rhead) + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        const int n = min(h - gb, 4);
+        if (n <= 0)
+        {
+            const int f = __builtin_amdgcn_readfirstlane(
+                __hip_atomic_load(G(a.rfinal) + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+            if (f > 0 && gb >= f - 1 && h <= gb) break;
+            if (__builtin_amdgcn_s_memrealtime() - last > kSpinLimit || err_set(a))
+            {
+                atomicOr(a.err, 1u);
+                return;
+            }
+            __builtin_amdgcn_s_sleep(2);
+            continue;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        last = __builtin_amdgcn_s_memrealtime();
+        int4v v[4][4];
+        int2v dd[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+        {
+            if (j >= n) break;
+            const size_t slot = (size_t)((gb + j) & (kRingBlocks - 1));
+            dd[j] = *(const gptr<int2v>)(G(a.rdesc) + 2 * ((size_t)s * kRingBlocks + slot));
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+            {
+                const int row = 64 * w + 16 * i + (lane >> 2);
+                v[j][i] = *(const gptr<int4v>)(ringS + slot * 4096 + row * 16 + 4 * (lane & 3));
+            }
+        }
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the ring slots are read
+        if (lane == 0)
+            __hip_atomic_store(G(a.rtail) + (size_t)s * kRingWaves + w, gb + n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+        {
+            if (j >= n) break;
+            const int tk = __builtin_amdgcn_readfirstlane(dd[j].x) - d.ticketBase;
+            const int b = __builtin_amdgcn_readfirstlane(dd[j].y);
+            const int r0w = tk * kWaveRows * NS + 1;
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+            {
+                const int row = 64 * w + 16 * i + (lane >> 2);
+                const int q = lane & 3;
+                const int r = r0w + row;
+                const int c = 16 * b + 4 * q - (row >> 2);  // column of .x: step 16b+4q of lane row/4
+                if (r <= d.R && c + 3 >= 1 && c <= d.C)
+                {
+                    const int4v x = v[j][i];
+                    const int base = (r + c) * g;
+                    const gptr<int> dst = score + (size_t)r * (size_t)d.ld + c;
+                    if (c >= 1 && c + 3 <= d.C)
+                        *(gptr<int4a>)dst = int4a {x.x + base, x.y + base + g, x.z + base + 2 * g, x.w + base + 3 * g};
+                    else
+                    {
+#pragma unroll
+                        for (int e = 0; e < 4; ++e)
+                            if (c + e >= 1 && c + e <= d.C) dst[e] = x[e] + base + e * g;
+                    }
+                }
+            }
+        }
+        gb += n;
+    }
+}
+
 // waves per workgroup: NS strips + loader (+ store waves for full fills)
 template <int NS, int MODE>
-constexpr int kWaves = NS + 1 + (MODE == kModeFull ? kStoreWaves : 0);
+constexpr int kWaves = MODE == kModeFullRing ? kRingWaves : NS + 1 + (MODE == kModeFull ? kStoreWaves : 0);
 
 template <int NS, int MODE>
-__global__ void __launch_bounds__(64 * (NS + 1 + (MODE == kModeFull ? kStoreWaves : 0))) nw_strip_kernel(StripArgs a)
+__global__ void __launch_bounds__(64 * (MODE == kModeFullRing ? kRingWaves : NS + 1 + (MODE == kModeFull ? kStoreWaves : 0)))
+    nw_strip_kernel(StripArgs a)
 {
     const int w = wave_role<NS, MODE>(__builtin_amdgcn_readfirstlane(threadIdx.x >> 6));
     const int lane = threadIdx.x & 63;
     const Lds L = lds_layout<NS, MODE>(a.substsz);
     const uint32_t F = L.flags;
     int prevTk = -1;  // global ticket this workgroup finished last (mlsppt signalling)
+    int ringBase = 0;  // ring mode: blocks this workgroup has put into its ring so far
+    if constexpr (MODE == kModeFullRing)
+    {
+        if ((int)blockIdx.x >= a.nStrip)
+        {
+            ring_copy_wg<NS>(a);
+            return;
+        }
+        if (threadIdx.x == 0)
+        {
+            lds_st(F + kFRingDone, 0);
+            lds_st(F + kFRingTail, 0);
+        }
+    }
     for (;;)
     {
         // mlsppt: every wave writes its stores of the finished ticket back past L2 (system-scope
@@ -856,7 +1060,13 @@ __global__ void __launch_bounds__(64 * (NS + 1 + (MODE == kModeFull ? kStoreWave
                 o[6] = (unsigned long long)a.ticket;
             }
         }
-        if (tkg >= a.nTicketsTotal) break;
+        if (tkg >= a.nTicketsTotal)
+        {
+            if constexpr (MODE == kModeFullRing)
+                if (threadIdx.x == 0)
+                    __hip_atomic_store(G(a.rfinal) + blockIdx.x, ringBase + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+        }
         prevTk = tkg;
         // pair of this ticket: last descriptor with ticketBase <= tkg (binary search, uniform)
         int lo = 0, hi = a.nPairs - 1;
@@ -884,6 +1094,9 @@ __global__ void __launch_bounds__(64 * (NS + 1 + (MODE == kModeFull ? kStoreWave
         pa.tcols = d.tcols;
         pa.gran = a.gran + d.granOff;
         pa.granStride = (long long)d.Cp + 1;
+        pa.ringBase = ringBase;
+        pa.ringTicket = tkg;
+        ringBase += (d.Cp + 64 + kBLK - 1) / kBLK;
         const int tk = tkg - d.ticketBase;
         if constexpr (GSA_STAMP)
         {
@@ -992,6 +1205,7 @@ hipError_t launch_headers(const StripArgs& a, int mode, long long maxWork, hipSt
 hipError_t launch_strip_fill(const StripArgs& a, int mode, int grid, hipStream_t stream)
 {
     if (mode == kModeSparse) return launch_strip<kSparseNS, kModeSparse>(a, grid, stream);
+    if (mode == kModeFullRing) return launch_strip<1, kModeFullRing>(a, grid, stream);
     if (a.ns == 2) return launch_strip<2, kModeFull>(a, grid, stream);
     return launch_strip<1, kModeFull>(a, grid, stream);
 }

@@ -147,3 +147,15 @@ def test_mlsp_40k_related(engine, golden):
     assert np.array_equal(rs.hrow, hr)
     assert np.array_equal(rs.hcol, hc)
     assert rs.align_cost == cost
+
+
+@pytest.mark.parametrize("R", [1800, 2049, 4097])
+@pytest.mark.parametrize("C", [1, 2, 63, 64, 65, 1000, 3001])
+def test_full_ring_mode_shapes(engine, golden, R, C, monkeypatch):
+    """Opt-in ring mode (GSA_FULL_RING=1; >= 8 strips: output through L2-resident rings drained
+    by copy workgroups, nw_strip.hip): every word against cpu1, ragged row and column counts."""
+    monkeypatch.setenv("GSA_FULL_RING", "1")
+    Y, X = random_pair(R, C, R + 7 * C)
+    r = engine.align_full(Y, X, golden.blosum62, -11)
+    S, cost = oracle.fill_full(Y, X, golden.blosum62, -11)
+    assert np.array_equal(r.score, S) and r.align_cost == cost
