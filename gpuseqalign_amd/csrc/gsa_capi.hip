@@ -184,6 +184,75 @@ int run_check(gsa_ctx* ctx, gsa::CheckArgs& a, bool sparse, hipStream_t st, gsa_
     return GSA_SUCCESS;
 }
 
+// Score-only kernels: global alignments run on the strip kernel in its affine mode (shifted
+// Gotoh, nw_strip.hip kModeScoreAG); local ones on the row scan (nw_scan.hip).  GSA_SCORE_SCAN=1
+// sends global ones to the row scan as well (tests compare the two).
+bool score_scan_forced()
+{
+    const char* e = std::getenv("GSA_SCORE_SCAN");
+    return e && std::atoi(e) == 1;
+}
+
+int score_ag_strip(gsa_ctx* ctx, const int32_t* seqY, int64_t R, const int32_t* seqX, int64_t C, const int32_t* subst,
+                   int32_t substsz, int32_t gapo, int32_t gape, gsa_score_result* out, hipStream_t st)
+{
+    const int64_t TR = (int64_t)gsa::kWaveRows * gsa::kSparseNS;
+    const int64_t tickets = (R + TR - 1) / TR;
+    if (tickets > (1ll << 30) || C > (1ll << 30)) return GSA_ERROR_INVALID_VALUE;
+    gsa::StripArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.subst = subst;
+    a.substsz = substsz;
+    a.g = gapo;
+    a.go = gapo;
+    a.ge = gape;
+    a.ns = gsa::kSparseNS;
+    gsa::PairDesc d;
+    std::memset(&d, 0, sizeof(d));
+    d.seqY = seqY;
+    d.seqX = seqX;
+    d.R = (int)R;
+    d.C = (int)C;
+    d.Cp = (int)C;
+    d.nTickets = (int)tickets;
+    int s = ensure_desc(ctx, 1);
+    if (s != GSA_SUCCESS) return s;
+    hipError_t e = hipMemcpyAsync(ctx->desc, &d, sizeof(d), hipMemcpyHostToDevice, st);
+    if (e != hipSuccess) return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
+    const size_t gran = (size_t)tickets * (size_t)(C + 1);
+    if ((s = ensure_gran(ctx, 2 * gran)) != GSA_SUCCESS) return s;
+    if (!ctx->sctl && (e = hipMalloc(&ctx->sctl, 64)) != hipSuccess) return fail(ctx, e, GSA_ERROR_MEMORY_ALLOCATION);
+    a.pairs = ctx->desc;
+    a.nPairs = 1;
+    a.nTicketsTotal = (int)tickets;
+    a.gran = ctx->gran;
+    a.gran2 = ctx->gran + gran;
+    a.ticket = ctx->ctl;
+    a.err = ctx->ctl + 1;
+    a.agResult = (int*)ctx->sctl;
+    a.epoch = ++ctx->epoch;
+    if (a.epoch == 0) a.epoch = ++ctx->epoch;
+    if ((e = hipMemsetAsync(ctx->ctl, 0, 16, st)) != hipSuccess) return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
+    (void)hipEventRecord(ctx->ev0, st);
+    const int grid = std::max(1, std::min((int)tickets, ctx->cu_count));
+    if ((e = gsa::launch_strip_fill(a, gsa::kModeScoreAG, grid, st)) != hipSuccess)
+        return fail(ctx, e, GSA_ERROR_KERNEL_FAILURE);
+    (void)hipEventRecord(ctx->ev1, st);
+    int res = 0;
+    unsigned flags[2] = {0, 0};
+    if ((e = hipMemcpyAsync(&res, ctx->sctl, sizeof(res), hipMemcpyDeviceToHost, st)) != hipSuccess ||
+        (e = hipMemcpyAsync(flags, ctx->ctl, sizeof(flags), hipMemcpyDeviceToHost, st)) != hipSuccess ||
+        (e = hipStreamSynchronize(st)) != hipSuccess)
+        return fail(ctx, e, GSA_ERROR_KERNEL_FAILURE);
+    (void)hipEventElapsedTime(&out->calc_kernel_ms, ctx->ev0, ctx->ev1);
+    if (flags[1] & 2u) return GSA_ERROR_INVALID_VALUE;  // a substitution value outside int16 after the shift
+    if (flags[1] != 0) return GSA_ERROR_KERNEL_FAILURE;
+    out->score = res;
+    out->i_end = R;
+    out->j_end = C;
+    return GSA_SUCCESS;
+}
+
 // One batched launch: headers of every pair, then the persistent strip kernel over the
 // tickets of all pairs (pair-major).  `pairs` holds device pointers.
 int enqueue_batch(gsa_ctx* ctx, int mode, int npairs, const gsa_pair_dev* pairs, const int32_t* subst, int32_t substsz,
@@ -716,6 +785,7 @@ int gsa_score_dev(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, const int3
     hipError_t e = hipSetDevice(ctx->device);
     if (e != hipSuccess) return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
     hipStream_t st = pick_stream(ctx, stream);
+    if (!local && !score_scan_forced()) return score_ag_strip(ctx, seqY, R, seqX, C, subst, substsz, gapo, gape, out, st);
     const int64_t nTR = (R + 63) / 64;
     const size_t bnd = (size_t)(nTR + 1) * (size_t)(C + 1);
     const size_t need = 2 * bnd + (size_t)(nTR + 1);  // bh, bf, prog

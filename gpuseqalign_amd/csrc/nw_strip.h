@@ -11,6 +11,9 @@ constexpr int kModeSparse = 1;
 // Full fill whose output leaves the strip's CU through an L2-resident ring: copy workgroups
 // on other CUs (same XCD) move it to the matrix (nw_strip.hip, "ring mode").
 constexpr int kModeFullRing = 2;
+// Score-only global alignment with affine gaps on the strip layout (gsa_score_dev, global):
+// shifted by (i+j)*gape, H', E', F' follow max recurrences with the constant d = gapo - gape.
+constexpr int kModeScoreAG = 3;
 constexpr int kRingBlocks = 16;  // ring slots (16-step blocks of 256 rows, 16 KB) per strip workgroup
 constexpr int kRingWaves = 4;    // waves per workgroup in ring mode (strip + loader + 2 idle / 4 copy)
 constexpr int kWaveRows = 256;                          // rows per strip (one wave, 4 rows per lane)
@@ -72,6 +75,10 @@ struct StripArgs
     int nStrip;
     int ringBase;   // per ticket: ring blocks of this workgroup before this ticket
     int ringTicket; // per ticket: its global ticket index (the copy workgroup maps it to rows)
+    // kModeScoreAG: gap open / extend, the F' hand-off granules (same layout as gran), result H[R][C]
+    int go, ge;
+    unsigned long long* gran2;
+    int* agResult;
     // batch: the per-pair fields above are loaded from pairs[] for every ticket
     const PairDesc* pairs;
     int nPairs;

@@ -104,6 +104,7 @@ __device__ __forceinline__ int shr1z(int v) { return __builtin_amdgcn_update_dpp
 struct Lds
 {
     uint32_t xo, ring, zero, flags, prof, psz, out;
+    uint32_t ring2;  // kModeScoreAG: the F' hand-off rings (same geometry as ring)
 };
 
 // flags: prog[i] @ 4i (ring i holds the row above strip i; valid for columns < prog[i]),
@@ -159,7 +160,8 @@ __device__ __forceinline__ Lds lds_layout(int substsz)
     L.psz = (uint32_t)(substsz + 1) * 512u;  // P[x][lane] = 4 x int16; row substsz = NEG
     L.xo = 0;
     L.ring = L.xo + 4 * kXCopy;
-    L.zero = L.ring + (NS + 1) * kRing * 16;
+    L.ring2 = L.ring + (NS + 1) * kRing * 16;
+    L.zero = L.ring2 + (MODE == kModeScoreAG ? (NS + 1) * kRing * 16 : 0);
     L.flags = L.zero + 16;
     L.prof = L.flags + 128;
     L.out = L.prof + NS * L.psz;
@@ -168,8 +170,8 @@ __device__ __forceinline__ Lds lds_layout(int substsz)
 
 size_t strip_lds_bytes(int ns, int substsz, int mode)
 {
-    return (size_t)4 * kXCopy + (size_t)(ns + 1) * kRing * 16 + 16 + 128 + (size_t)ns * (substsz + 1) * 512 +
-           (mode == kModeFull ? (size_t)ns * kOutStrip : 0);
+    return (size_t)4 * kXCopy + (size_t)(ns + 1) * kRing * 16 * (mode == kModeScoreAG ? 2 : 1) + 16 + 128 +
+           (size_t)ns * (substsz + 1) * 512 + (mode == kModeFull ? (size_t)ns * kOutStrip : 0);
 }
 
 __device__ __forceinline__ bool err_set(const StripArgs& a)
@@ -309,7 +311,8 @@ __device__ __forceinline__ void strip_wave(const StripArgs& a, const Lds& L, int
 #pragma unroll
             for (int k = 0; k < kK; ++k)
             {
-                v[k] = srow[k][x] - 2 * g;
+                // LG: s - 2g;  AG (H' = H - (i+j)ge, diagonal carried as Hgo' = H' + d): s - 2ge - d
+                v[k] = srow[k][x] - (MODE == kModeScoreAG ? a.ge + a.go : 2 * g);
                 bad |= (v[k] < -32767) || (v[k] > 32767);
             }
             int2v p;
@@ -329,6 +332,8 @@ __device__ __forceinline__ void strip_wave(const StripArgs& a, const Lds& L, int
     auto xo_addr = [&](int t0) { return xo_base + 16u * (uint32_t)(((t0 >> 2) + lanepos) & (kXR / 4 - 1)); };
     const uint32_t ring_in = L.ring + (uint32_t)w * (kRing * 16);
     const uint32_t ring_out = L.ring + (uint32_t)(w + 1) * (kRing * 16);
+    const uint32_t ring2_in = L.ring2 + (uint32_t)w * (kRing * 16);       // AG: F' of the row above
+    const uint32_t ring2_out = L.ring2 + (uint32_t)(w + 1) * (kRing * 16);
     const uint32_t fin = F + kFProg + 4 * w, fcout = F + kFCons + 4 * (w + 1), fsto = F + kFSto + 16 * w;
     const uint32_t out_w = L.out + (uint32_t)w * kOutStrip + (uint32_t)lane * 4 * kOutRow;
     const int out_key = (lane * 5) & 7;  // = ((row >> 2) * 5) & 7 for the lane's rows
@@ -344,6 +349,17 @@ __device__ __forceinline__ void strip_wave(const StripArgs& a, const Lds& L, int
         for (int u = 0; u < kBLK; ++u) hv[u] = win[(u + 3) >> 2][(u + 3) & 3];
         if constexpr (GSA_KNOB & 1)
             for (int u = 0; u < kBLK; ++u) hv[u] = 0;
+    };
+    auto hvf_load = [&](int b, int (&hv)[kBLK]) {
+        if constexpr (MODE == kModeScoreAG)
+        {
+            int4v win[5];
+#pragma unroll
+            for (int j = 0; j < 5; ++j)
+                win[j] = lds_ld4(lane == 0 ? ring2_in + 16u * (uint32_t)((4 * b - 48 + j) & (kRing - 1)) : L.zero);
+#pragma unroll
+            for (int u = 0; u < kBLK; ++u) hv[u] = win[(u + 3) >> 2][(u + 3) & 3];
+        }
     };
     auto letters_load = [&](int b, int4v (&lx)[4]) {
 #pragma unroll
@@ -424,10 +440,11 @@ __device__ __forceinline__ void strip_wave(const StripArgs& a, const Lds& L, int
     if (!wait_ready(pin, pco, pxo, psto, -1)) return;
     if (w == 0) tstamp(a, tk, 1, lane);
     cbar();
-    int hvA[kBLK], hvB[kBLK];
+    int hvA[kBLK], hvB[kBLK], hfA[kBLK], hfB[kBLK];
     int4v lxA[4], lxB[4];
     int2v sA[kBLK], sB[kBLK];
     hv_load(0, hvA);
+    hvf_load(0, hfA);
     letters_load(0, lxA);
     letters_load(1, lxB);
 #pragma unroll
@@ -435,16 +452,26 @@ __device__ __forceinline__ void strip_wave(const StripArgs& a, const Lds& L, int
 #pragma unroll
         for (int u = 0; u < 4; ++u) sA[4 * q + u] = lds_ld2((uint32_t)lxA[q][u] + laneoff);
 
-    int A = 0, B = 0, Cc = 0, D = 0, dA = 0;
+    // LG: H' of the 4 rows (0 = the shifted border).  AG: Hgo' of the 4 rows, E' of the 4 rows, F'
+    // of row D, all -inf before the matrix (kNegAG: far from overflow, never the maximum)
+    constexpr int kNegAG = -(1 << 29);
+    constexpr int i0v = (MODE == kModeScoreAG) ? kNegAG : 0;
+    int A = i0v, B = i0v, Cc = i0v, D = i0v, dA = i0v;
+    int EA = kNegAG, EB = kNegAG, EC = kNegAG, ED = kNegAG, FD = kNegAG;
+    const int dd = (MODE == kModeScoreAG) ? a.go - a.ge : 0;
+    // AG: the cell (R, C) lies in this strip iff r0 <= R < r0 + 256: lane, row, step of it
+    const int rR = a.R - r0;
+    const bool hasR = (MODE == kModeScoreAG) && rR >= 0 && rR < kWaveRows;
+    const int laneR = rR >> 2, kR = rR & 3, tStar = a.C + laneR;
     int cap[kK] = {0, 0, 0, 0};
     int rpin = pin, rpco = pco, rpxo = pxo, rpsto = psto;  // progress words as loaded, checked a block later
 
     // compute block b with (scur, hvcur); issue snext from lnext (letters of b+1), letters of
     // b+2 into lfree, and hvnext
     auto block = [&](int b, int2v (&scur)[kBLK], int2v (&snext)[kBLK], int4v (&lnext)[4], int4v (&lfree)[4],
-                     int (&hvcur)[kBLK], int (&hvnext)[kBLK], auto capT) {
+                     int (&hvcur)[kBLK], int (&hvnext)[kBLK], int (&hfcur)[kBLK], int (&hfnext)[kBLK], auto capT) {
         constexpr bool CAP = decltype(capT)::value;
-        const int cb = CAP ? ((16 * b) / a.tBx) * a.tBx : 0;
+        const int cb = (CAP && MODE == kModeSparse) ? ((16 * b) / a.tBx) * a.tBx : 0;
 #pragma unroll
         for (int q = 0; q < 4; ++q)
         {
@@ -458,11 +485,50 @@ __device__ __forceinline__ void strip_wave(const StripArgs& a, const Lds& L, int
                 else
                     snext[4 * q + u] = lds_ld2((uint32_t)lnext[q][u] + laneoff);
             }
-            int Xa[4], Xb[4], Xc[4], Xd[4];
+            int Xa[4], Xb[4], Xc[4], Xd[4], Fd[4];
 #pragma unroll
             for (int u = 0; u < 4; ++u)
             {
                 const int2v sv = scur[4 * q + u];
+                if constexpr (MODE == kModeScoreAG)
+                {
+                    // Gotoh in H' = H - (i+j)ge: E'(k,c) = max(E'(k,c-1), Hgo'(k,c-1)),
+                    // F'(k,c) = max(F'(k-1,c), Hgo'(k-1,c)), H' = max3(Hgo'diag + s'', E', F'),
+                    // Hgo' = H' + d; the row above comes from lane l-1 (DPP) or the halo
+                    const int upH = shr1z(D) + hvcur[4 * q + u];
+                    const int upF = shr1z(FD) + hfcur[4 * q + u];
+                    const int eA = max(EA, A), eB = max(EB, B), eC = max(EC, Cc), eD = max(ED, D);
+                    const int fA = max(upF, upH);
+                    const int hA = max(max(dA + (int)(short)sv.x, eA), fA);
+                    const int nA = hA + dd;
+                    const int fB = max(fA, nA);
+                    const int hB = max(max(A + (sv.x >> 16), eB), fB);
+                    const int nB = hB + dd;
+                    const int fC = max(fB, nB);
+                    const int hC = max(max(B + (int)(short)sv.y, eC), fC);
+                    const int nC = hC + dd;
+                    const int fD = max(fC, nC);
+                    const int hD = max(max(Cc + (sv.y >> 16), eD), fD);
+                    const int nD = hD + dd;
+                    if constexpr (CAP)
+                    {
+                        if (t0 + u == tStar && lane == laneR)
+                            G(a.agResult)[0] = (kR == 0 ? hA : kR == 1 ? hB : kR == 2 ? hC : hD) + (a.R + a.C) * a.ge;
+                    }
+                    dA = upH;
+                    A = nA;
+                    B = nB;
+                    Cc = nC;
+                    D = nD;
+                    EA = eA;
+                    EB = eB;
+                    EC = eC;
+                    ED = eD;
+                    FD = fD;
+                    Xd[u] = nD;
+                    Fd[u] = fD;
+                    continue;
+                }
                 const int up = shr1z(D) + hvcur[4 * q + u];
                 const int na = max(max(dA + (int)(short)sv.x, up), A);
                 const int nb = max(max(A + (sv.x >> 16), na), B);
@@ -489,6 +555,8 @@ __device__ __forceinline__ void strip_wave(const StripArgs& a, const Lds& L, int
             // hand-off: row D of 4 steps, slot (group - lane)
             if constexpr (!(GSA_KNOB & 8))
                 lds_st4(ring_out + 16u * (uint32_t)(((t0 >> 2) - lane) & (kRing - 1)), int4v {Xd[0], Xd[1], Xd[2], Xd[3]});
+            if constexpr (MODE == kModeScoreAG)
+                lds_st4(ring2_out + 16u * (uint32_t)(((t0 >> 2) - lane) & (kRing - 1)), int4v {Fd[0], Fd[1], Fd[2], Fd[3]});
             if constexpr (MODE == kModeFullRing)
             {
                 // H' of the 4 rows x 4 steps -> ring slot of this block, row-major [row][16 steps]:
@@ -555,6 +623,7 @@ __device__ __forceinline__ void strip_wave(const StripArgs& a, const Lds& L, int
                 }
                 cbar();
                 hv_load(b + 1, hvnext);
+                hvf_load(b + 1, hfnext);
                 flag_st(F + kFCons + 4 * w, 16 * (b + 1) - 3);  // after the halo reads (in order)
             }
             if (q == 0)
@@ -570,7 +639,7 @@ __device__ __forceinline__ void strip_wave(const StripArgs& a, const Lds& L, int
                 }
             }
         }
-        if constexpr (CAP)
+        if constexpr (CAP && MODE == kModeSparse)
         {
             if (16 * b + 15 == cb + 63)
             {
@@ -597,7 +666,7 @@ __device__ __forceinline__ void strip_wave(const StripArgs& a, const Lds& L, int
     };
 
     auto run_block = [&](int b, int2v (&scur)[kBLK], int2v (&snext)[kBLK], int4v (&lnext)[4], int4v (&lfree)[4],
-                         int (&hvcur)[kBLK], int (&hvnext)[kBLK]) {
+                         int (&hvcur)[kBLK], int (&hvnext)[kBLK], int (&hfcur)[kBLK], int (&hfnext)[kBLK]) {
         stamp(a, tk, w, b, 0, lane);
         pco = __builtin_amdgcn_readfirstlane(rpco);
         pxo = (w == 0) ? __builtin_amdgcn_readfirstlane(rpxo) : 0;
@@ -614,18 +683,19 @@ __device__ __forceinline__ void strip_wave(const StripArgs& a, const Lds& L, int
             const int jT = (16 * b) / a.tBx;
             capblk = !(GSA_KNOB & 4) && jT >= 1 && jT < a.tcols && 16 * b - jT * a.tBx < 64;
         }
+        if constexpr (MODE == kModeScoreAG) capblk = hasR && (tStar >> 4) == b;
         if (capblk)
-            block(b, scur, snext, lnext, lfree, hvcur, hvnext, std::integral_constant<bool, true>());
+            block(b, scur, snext, lnext, lfree, hvcur, hvnext, hfcur, hfnext, std::integral_constant<bool, true>());
         else
-            block(b, scur, snext, lnext, lfree, hvcur, hvnext, std::integral_constant<bool, false>());
+            block(b, scur, snext, lnext, lfree, hvcur, hvnext, hfcur, hfnext, std::integral_constant<bool, false>());
         stamp(a, tk, w, b, 3, lane);
         return true;
     };
 
     for (int b = 0; b < NB; b += 2)
     {
-        if (!run_block(b, sA, sB, lxB, lxA, hvA, hvB)) return;
-        if (b + 1 < NB && !run_block(b + 1, sB, sA, lxA, lxB, hvB, hvA)) return;
+        if (!run_block(b, sA, sB, lxB, lxA, hvA, hvB, hfA, hfB)) return;
+        if (b + 1 < NB && !run_block(b + 1, sB, sA, lxA, lxB, hvB, hvA, hfB, hfA)) return;
     }
     if (w == NS - 1) tstamp(a, tk, 2, lane);
     if constexpr (MODE == kModeFullRing)
@@ -646,16 +716,21 @@ __device__ __forceinline__ void loader_wave(const StripArgs& a, const Lds& L, in
     const int nCh = (Cp + 1 + 63) / 64;  // 64-column chunks covering columns 0..Cp
     const uint32_t F = L.flags;
     const uint32_t ring0 = L.ring;
-    const bool feed = tk > 0;
-    const unsigned long long* gprev = a.gran + (size_t)(feed ? tk - 1 : 0) * a.granStride;
+    // AG: ticket 0 is fed too, from the border row (Hgo' = d at column 0, 2d after it; F' = -inf)
+    const bool feed = tk > 0 || MODE == kModeScoreAG;
+    const unsigned long long* gprev = a.gran + (size_t)(tk > 0 ? tk - 1 : 0) * a.granStride;
     unsigned long long* gout = a.gran + (size_t)tk * a.granStride;
+    const unsigned long long* gprev2 = a.gran2 + (size_t)(tk > 0 ? tk - 1 : 0) * a.granStride;  // AG: F'
+    unsigned long long* gout2 = a.gran2 + (size_t)tk * a.granStride;
+    const uint32_t ring20 = L.ring2;
     const bool pub = tk + 1 < a.nTickets;
     constexpr int TR = kWaveRows * NS;
     const int hrowg = (tk + 1) * TR;  // global row of our last row
     // strips below the matrix (full mode, last super-strip) pass BIG through: the last
     // strip that computes is the one whose progress bounds the letter ring
-    const int nAct = (MODE != kModeSparse) ? min(NS, (a.R - tk * TR + kWaveRows - 1) / kWaveRows) : NS;
+    const int nAct = (MODE != kModeSparse) ? max(1, min(NS, (a.R - tk * TR + kWaveRows - 1) / kWaveRows)) : NS;
     const uint32_t ringN = L.ring + (uint32_t)nAct * (kRing * 16);
+    const uint32_t ringN2 = L.ring2 + (uint32_t)nAct * (kRing * 16);
     int kx = 0;                       // next letter chunk (64 columns)
     int hnext = feed ? 0 : Cp + 1;    // next column of the row above to feed into ring 0
     int dnext = 0;                    // next column of our last row to drain
@@ -717,13 +792,31 @@ __device__ __forceinline__ void loader_wave(const StripArgs& a, const Lds& L, in
         {
             const int c = hnext + lane;
             const bool in = c <= Cp;
-            unsigned long long q = in ? __hip_atomic_load(gprev + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
-            const bool good = in && (uint32_t)(q >> 32) == a.epoch;
+            unsigned long long q = 0ull, q2 = 0ull;
+            bool good;
+            if (MODE == kModeScoreAG && tk == 0)
+            {
+                const int dd = a.go - a.ge;
+                q = (uint32_t)(c == 0 ? dd : 2 * dd);
+                q2 = (uint32_t)(-(1 << 29));
+                good = in;
+            }
+            else
+            {
+                q = in ? __hip_atomic_load(gprev + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+                good = in && (uint32_t)(q >> 32) == a.epoch;
+                if constexpr (MODE == kModeScoreAG)
+                {
+                    q2 = in ? __hip_atomic_load(gprev2 + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+                    good = good && (uint32_t)(q2 >> 32) == a.epoch;
+                }
+            }
             const uint64_t badm = __ballot(!good);
             const int n = badm ? __builtin_ctzll(badm) : 64;  // granules arrive in column order
             if (n > 0)
             {
                 if (lane < n) lds_st(ring0 + ring_elem(c), (int)(uint32_t)q);
+                if (MODE == kModeScoreAG && lane < n) lds_st(ring20 + ring_elem(c), (int)(uint32_t)q2);
                 if (hnext == 0) tstamp(a, tk, 3, lane);
                 hnext += n;
                 flag_st(F + kFProg + 0, hnext > Cp ? kBig : hnext);
@@ -742,6 +835,13 @@ __device__ __forceinline__ void loader_wave(const StripArgs& a, const Lds& L, in
                 if (pub)
                     __hip_atomic_store(gout + c, ((unsigned long long)a.epoch << 32) | (uint32_t)v, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
+                if constexpr (MODE == kModeScoreAG)
+                {
+                    const int v2 = lds_ld(ringN2 + ring_elem(c));
+                    if (pub)
+                        __hip_atomic_store(gout2 + c, ((unsigned long long)a.epoch << 32) | (uint32_t)v2, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+                }
                 if constexpr (MODE == kModeSparse)
                 {
                     if (tk + 1 < a.trows)
@@ -1093,6 +1193,7 @@ __global__ void __launch_bounds__(64 * (MODE == kModeFullRing ? kRingWaves : NS 
         pa.trows = d.trows;
         pa.tcols = d.tcols;
         pa.gran = a.gran + d.granOff;
+        pa.gran2 = a.gran2 + d.granOff;
         pa.granStride = (long long)d.Cp + 1;
         pa.ringBase = ringBase;
         pa.ringTicket = tkg;
@@ -1119,7 +1220,7 @@ __global__ void __launch_bounds__(64 * (MODE == kModeFullRing ? kRingWaves : NS 
         if (threadIdx.x < 8)
         {
             // nothing valid yet: -64 < every column a lane can touch (lane 63 starts at -63)
-            lds_st(F + kFProg + 4 * threadIdx.x, (threadIdx.x == 0 && tk == 0) ? kBig : -64);
+            lds_st(F + kFProg + 4 * threadIdx.x, (threadIdx.x == 0 && tk == 0 && MODE != kModeScoreAG) ? kBig : -64);
             lds_st(F + kFCons + 4 * threadIdx.x, 0);
             lds_st(F + kFSto + 4 * threadIdx.x, 0);  // sto[0..1][0..3]
         }
@@ -1206,6 +1307,7 @@ hipError_t launch_strip_fill(const StripArgs& a, int mode, int grid, hipStream_t
 {
     if (mode == kModeSparse) return launch_strip<kSparseNS, kModeSparse>(a, grid, stream);
     if (mode == kModeFullRing) return launch_strip<1, kModeFullRing>(a, grid, stream);
+    if (mode == kModeScoreAG) return launch_strip<kSparseNS, kModeScoreAG>(a, grid, stream);
     if (a.ns == 2) return launch_strip<2, kModeFull>(a, grid, stream);
     return launch_strip<1, kModeFull>(a, grid, stream);
 }

@@ -64,3 +64,15 @@ def test_config5_50k(engine, golden, go, ge, local):
     r = engine.score(Y, X, golden.blosum62, go, ge, local)
     ref = oracle.score_ag(Y, X, golden.blosum62, go, ge, local, mt=True, blocksz=256, nthreads=16)
     assert (r["score"], r["i_end"], r["j_end"]) == ref
+
+
+@pytest.mark.parametrize("R,C", [(1, 300), (700, 130), (2049, 1500)])
+@pytest.mark.parametrize("go,ge", [(-11, -11), (-11, -1)])
+def test_global_row_scan_path(engine, golden, R, C, go, ge, monkeypatch):
+    """Global scores normally run on the strip kernel (affine mode); GSA_SCORE_SCAN=1 keeps the
+    row-scan kernel reachable for them: both equal the oracle."""
+    import oracle
+    monkeypatch.setenv("GSA_SCORE_SCAN", "1")
+    Y, X = random_pair(R, C, 5 * R + C)
+    r = engine.score(Y, X, golden.blosum62, go, ge, False)
+    assert (r["score"], r["i_end"], r["j_end"]) == oracle.score_ag(Y, X, golden.blosum62, go, ge, False)
