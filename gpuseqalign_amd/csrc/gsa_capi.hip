@@ -193,8 +193,18 @@ bool score_scan_forced()
     return e && std::atoi(e) == 1;
 }
 
+constexpr int kScoreTooLarge = 1000;  // internal: score_ag_strip -> row scan
+
+// SW end-cell keys: score << bits | (2^bits-1 - row-major index), bits = ceil(log2((R+1)(C+1)));
+// scores (< 2^31) keep 63 - bits >= 29 bits up to (R+1)(C+1) = 2^34
+int sw_idx_bits(int64_t R, int64_t C)
+{
+    const unsigned long long n = (unsigned long long)(R + 1) * (unsigned long long)(C + 1) - 1;
+    return n ? 64 - __builtin_clzll(n) : 1;
+}
+
 int score_ag_strip(gsa_ctx* ctx, const int32_t* seqY, int64_t R, const int32_t* seqX, int64_t C, const int32_t* subst,
-                   int32_t substsz, int32_t gapo, int32_t gape, gsa_score_result* out, hipStream_t st)
+                   int32_t substsz, int32_t gapo, int32_t gape, int32_t local, gsa_score_result* out, hipStream_t st)
 {
     const int64_t TR = (int64_t)gsa::kWaveRows * gsa::kSparseNS;
     const int64_t tickets = (R + TR - 1) / TR;
@@ -230,24 +240,39 @@ int score_ag_strip(gsa_ctx* ctx, const int32_t* seqY, int64_t R, const int32_t* 
     a.ticket = ctx->ctl;
     a.err = ctx->ctl + 1;
     a.agResult = (int*)ctx->sctl;
+    a.swBest = ctx->sctl + 1;
+    a.idxBits = sw_idx_bits(R, C);
     a.epoch = ++ctx->epoch;
     if (a.epoch == 0) a.epoch = ++ctx->epoch;
-    if ((e = hipMemsetAsync(ctx->ctl, 0, 16, st)) != hipSuccess) return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
+    if ((e = hipMemsetAsync(ctx->ctl, 0, 16, st)) != hipSuccess || (e = hipMemsetAsync(ctx->sctl, 0, 16, st)) != hipSuccess)
+        return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
     (void)hipEventRecord(ctx->ev0, st);
     const int grid = std::max(1, std::min((int)tickets, ctx->cu_count));
-    if ((e = gsa::launch_strip_fill(a, gsa::kModeScoreAG, grid, st)) != hipSuccess)
+    if ((e = gsa::launch_strip_fill(a, local ? gsa::kModeScoreSW : gsa::kModeScoreAG, grid, st)) != hipSuccess)
         return fail(ctx, e, GSA_ERROR_KERNEL_FAILURE);
     (void)hipEventRecord(ctx->ev1, st);
-    int res = 0;
+    unsigned long long res[2] = {0, 0};
     unsigned flags[2] = {0, 0};
-    if ((e = hipMemcpyAsync(&res, ctx->sctl, sizeof(res), hipMemcpyDeviceToHost, st)) != hipSuccess ||
+    if ((e = hipMemcpyAsync(res, ctx->sctl, sizeof(res), hipMemcpyDeviceToHost, st)) != hipSuccess ||
         (e = hipMemcpyAsync(flags, ctx->ctl, sizeof(flags), hipMemcpyDeviceToHost, st)) != hipSuccess ||
         (e = hipStreamSynchronize(st)) != hipSuccess)
         return fail(ctx, e, GSA_ERROR_KERNEL_FAILURE);
     (void)hipEventElapsedTime(&out->calc_kernel_ms, ctx->ev0, ctx->ev1);
     if (flags[1] & 2u) return GSA_ERROR_INVALID_VALUE;  // a substitution value outside int16 after the shift
     if (flags[1] != 0) return GSA_ERROR_KERNEL_FAILURE;
-    out->score = res;
+    if (local)
+    {
+        if (res[0] & 1u) return kScoreTooLarge;  // a score >= 2^26: the caller takes the row scan
+        // max key: score << idxBits | (2^idxBits-1 - row-major index); 0 = no positive cell -> (0, 0, 0)
+        const int bits = sw_idx_bits(R, C);
+        const unsigned long long mask = (1ull << bits) - 1;
+        const unsigned long long idx = res[1] ? mask - (res[1] & mask) : 0;
+        out->score = (int32_t)(res[1] >> bits);
+        out->i_end = (int64_t)(idx / (unsigned long long)(C + 1));
+        out->j_end = (int64_t)(idx % (unsigned long long)(C + 1));
+        return GSA_SUCCESS;
+    }
+    out->score = (int32_t)(uint32_t)res[0];
     out->i_end = R;
     out->j_end = C;
     return GSA_SUCCESS;
@@ -785,7 +810,13 @@ int gsa_score_dev(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, const int3
     hipError_t e = hipSetDevice(ctx->device);
     if (e != hipSuccess) return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
     hipStream_t st = pick_stream(ctx, stream);
-    if (!local && !score_scan_forced()) return score_ag_strip(ctx, seqY, R, seqX, C, subst, substsz, gapo, gape, out, st);
+    // the strip kernel's SW mode needs go < 0 (cells past C then never tie the maximum) and scores
+    // below 2^26 (packed with the step; it reports larger ones); otherwise the row scan
+    if (!score_scan_forced() && (!local || gapo < 0))
+    {
+        s = score_ag_strip(ctx, seqY, R, seqX, C, subst, substsz, gapo, gape, local, out, st);
+        if (s != kScoreTooLarge) return s;
+    }
     const int64_t nTR = (R + 63) / 64;
     const size_t bnd = (size_t)(nTR + 1) * (size_t)(C + 1);
     const size_t need = 2 * bnd + (size_t)(nTR + 1);  // bh, bf, prog
@@ -815,6 +846,7 @@ int gsa_score_dev(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, const int3
     a.ticket = (unsigned*)ctx->sctl;
     a.err = (unsigned*)ctx->sctl + 1;
     a.best = ctx->sctl + 1;
+    a.idxBits = sw_idx_bits(R, C);
     a.result = (int*)(ctx->sctl + 2);
     if ((e = hipMemsetAsync(a.prog, 0, (size_t)(nTR + 1) * sizeof(int), st)) != hipSuccess ||
         (e = hipMemsetAsync(ctx->sctl, 0, 64, st)) != hipSuccess)
@@ -831,9 +863,10 @@ int gsa_score_dev(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, const int3
     if ((unsigned)(ctl[0] >> 32) != 0) return GSA_ERROR_KERNEL_FAILURE;  // a wait gave up
     if (local)
     {
-        const unsigned long long mask = (1ull << 40) - 1;
+        const int bits = sw_idx_bits(R, C);
+        const unsigned long long mask = (1ull << bits) - 1;
         const unsigned long long idx = mask - (ctl[1] & mask);
-        out->score = (int32_t)(ctl[1] >> 40);
+        out->score = (int32_t)(ctl[1] >> bits);
         out->i_end = (int64_t)(idx / (unsigned long long)(C + 1));
         out->j_end = (int64_t)(idx % (unsigned long long)(C + 1));
     }

@@ -41,7 +41,6 @@ __device__ __forceinline__ gptr<T> G(T* p)
 
 constexpr int kNeg = -(1 << 29);
 constexpr uint64_t kSpin = 20000000ull;  // 0.2 s of s_memrealtime without progress
-constexpr uint64_t kIdxBits = 40;
 
 __device__ __forceinline__ int wave_prefix_max(int v)
 {
@@ -200,7 +199,7 @@ __global__ void __launch_bounds__(64) score_scan_kernel(ScoreArgs a)
     if (LOCAL)
     {
         const unsigned long long key =
-            ((unsigned long long)bv << kIdxBits) | (((1ull << kIdxBits) - 1) - bidx);
+            ((unsigned long long)bv << a.idxBits) | (((1ull << a.idxBits) - 1) - bidx);
         atomicMax(a.best, key);
     }
 }

@@ -14,6 +14,10 @@ constexpr int kModeFullRing = 2;
 // Score-only global alignment with affine gaps on the strip layout (gsa_score_dev, global):
 // shifted by (i+j)*gape, H', E', F' follow max recurrences with the constant d = gapo - gape.
 constexpr int kModeScoreAG = 3;
+// Score-only local alignment (Smith-Waterman) with affine gaps, same layout: the clamp at 0 is
+// a per-row floor (i+j)*(-gape) in the shifted space; the best cell goes to a packed atomicMax.
+constexpr int kModeScoreSW = 4;
+__host__ __device__ constexpr bool is_score_mode(int mode) { return mode == kModeScoreAG || mode == kModeScoreSW; }
 constexpr int kRingBlocks = 16;  // ring slots (16-step blocks of 256 rows, 16 KB) per strip workgroup
 constexpr int kRingWaves = 4;    // waves per workgroup in ring mode (strip + loader + 2 idle / 4 copy)
 constexpr int kWaveRows = 256;                          // rows per strip (one wave, 4 rows per lane)
@@ -79,6 +83,8 @@ struct StripArgs
     int go, ge;
     unsigned long long* gran2;
     int* agResult;
+    unsigned long long* swBest;  // kModeScoreSW: max of (score << idxBits | (2^idxBits-1 - row-major index))
+    int idxBits;
     // batch: the per-pair fields above are loaded from pairs[] for every ticket
     const PairDesc* pairs;
     int nPairs;

@@ -161,7 +161,7 @@ __device__ __forceinline__ Lds lds_layout(int substsz)
     L.xo = 0;
     L.ring = L.xo + 4 * kXCopy;
     L.ring2 = L.ring + (NS + 1) * kRing * 16;
-    L.zero = L.ring2 + (MODE == kModeScoreAG ? (NS + 1) * kRing * 16 : 0);
+    L.zero = L.ring2 + (is_score_mode(MODE) ? (NS + 1) * kRing * 16 : 0);
     L.flags = L.zero + 16;
     L.prof = L.flags + 128;
     L.out = L.prof + NS * L.psz;
@@ -170,7 +170,7 @@ __device__ __forceinline__ Lds lds_layout(int substsz)
 
 size_t strip_lds_bytes(int ns, int substsz, int mode)
 {
-    return (size_t)4 * kXCopy + (size_t)(ns + 1) * kRing * 16 * (mode == kModeScoreAG ? 2 : 1) + 16 + 128 +
+    return (size_t)4 * kXCopy + (size_t)(ns + 1) * kRing * 16 * (is_score_mode(mode) ? 2 : 1) + 16 + 128 +
            (size_t)ns * (substsz + 1) * 512 + (mode == kModeFull ? (size_t)ns * kOutStrip : 0);
 }
 
@@ -312,7 +312,7 @@ __device__ __forceinline__ void strip_wave(const StripArgs& a, const Lds& L, int
             for (int k = 0; k < kK; ++k)
             {
                 // LG: s - 2g;  AG (H' = H - (i+j)ge, diagonal carried as Hgo' = H' + d): s - 2ge - d
-                v[k] = srow[k][x] - (MODE == kModeScoreAG ? a.ge + a.go : 2 * g);
+                v[k] = srow[k][x] - (is_score_mode(MODE) ? a.ge + a.go : 2 * g);
                 bad |= (v[k] < -32767) || (v[k] > 32767);
             }
             int2v p;
@@ -351,7 +351,7 @@ __device__ __forceinline__ void strip_wave(const StripArgs& a, const Lds& L, int
             for (int u = 0; u < kBLK; ++u) hv[u] = 0;
     };
     auto hvf_load = [&](int b, int (&hv)[kBLK]) {
-        if constexpr (MODE == kModeScoreAG)
+        if constexpr (is_score_mode(MODE))
         {
             int4v win[5];
 #pragma unroll
@@ -455,14 +455,33 @@ __device__ __forceinline__ void strip_wave(const StripArgs& a, const Lds& L, int
     // LG: H' of the 4 rows (0 = the shifted border).  AG: Hgo' of the 4 rows, E' of the 4 rows, F'
     // of row D, all -inf before the matrix (kNegAG: far from overflow, never the maximum)
     constexpr int kNegAG = -(1 << 29);
-    constexpr int i0v = (MODE == kModeScoreAG) ? kNegAG : 0;
+    constexpr int i0v = is_score_mode(MODE) ? kNegAG : 0;
     int A = i0v, B = i0v, Cc = i0v, D = i0v, dA = i0v;
     int EA = kNegAG, EB = kNegAG, EC = kNegAG, ED = kNegAG, FD = kNegAG;
-    const int dd = (MODE == kModeScoreAG) ? a.go - a.ge : 0;
+    const int dd = is_score_mode(MODE) ? a.go - a.ge : 0;
     // AG: the cell (R, C) lies in this strip iff r0 <= R < r0 + 256: lane, row, step of it
     const int rR = a.R - r0;
     const bool hasR = (MODE == kModeScoreAG) && rR >= 0 && rR < kWaveRows;
     const int laneR = rR >> 2, kR = rR & 3, tStar = a.C + laneR;
+    // SW: floor of row k at the current step, H' >= -(i+j)ge (H >= 0).  Per row, the block's best
+    // as H << 4 | (15 - step in block) (one max per step: the larger H, then the earlier step) and,
+    // folded at each block end, the best H with the step it first appeared.  Rows below R start at
+    // a best nothing beats.  Columns past C are never the maximum: their E/F chains pay go < 0.
+    int zA = 0, zB = 0, zC = 0, zD = 0, pA = 0, pB = 0, pC = 0, pD = 0;
+    int bA = 0, bB = 0, bC = 0, bD = 0, tA = 0, tB = 0, tC = 0, tD = 0;
+    if constexpr (MODE == kModeScoreSW)
+    {
+        const int rb = r0 + kK * lane;  // row of k = A; i + j = rb + k + (t - lane)
+        constexpr int kOff = 0x7fffffff;
+        zA = -(rb - lane) * a.ge;
+        zB = zA - a.ge;
+        zC = zB - a.ge;
+        zD = zC - a.ge;
+        bA = (rb <= a.R) ? 0 : kOff;
+        bB = (rb + 1 <= a.R) ? 0 : kOff;
+        bC = (rb + 2 <= a.R) ? 0 : kOff;
+        bD = (rb + 3 <= a.R) ? 0 : kOff;
+    }
     int cap[kK] = {0, 0, 0, 0};
     int rpin = pin, rpco = pco, rpxo = pxo, rpsto = psto;  // progress words as loaded, checked a block later
 
@@ -490,7 +509,7 @@ __device__ __forceinline__ void strip_wave(const StripArgs& a, const Lds& L, int
             for (int u = 0; u < 4; ++u)
             {
                 const int2v sv = scur[4 * q + u];
-                if constexpr (MODE == kModeScoreAG)
+                if constexpr (is_score_mode(MODE))
                 {
                     // Gotoh in H' = H - (i+j)ge: E'(k,c) = max(E'(k,c-1), Hgo'(k,c-1)),
                     // F'(k,c) = max(F'(k-1,c), Hgo'(k-1,c)), H' = max3(Hgo'diag + s'', E', F'),
@@ -498,18 +517,33 @@ __device__ __forceinline__ void strip_wave(const StripArgs& a, const Lds& L, int
                     const int upH = shr1z(D) + hvcur[4 * q + u];
                     const int upF = shr1z(FD) + hfcur[4 * q + u];
                     const int eA = max(EA, A), eB = max(EB, B), eC = max(EC, Cc), eD = max(ED, D);
-                    const int fA = max(upF, upH);
+                    // SW: H >= 0 enters as F' >= floor (the max3 that forms F'): H = max(0, diag,
+                    // E, F) exactly, and a clamped F passes on at most ge <= 0, below the next floor
+                    constexpr bool SW = MODE == kModeScoreSW;
+                    const int fA = SW ? max(max(upF, upH), zA) : max(upF, upH);
                     const int hA = max(max(dA + (int)(short)sv.x, eA), fA);
                     const int nA = hA + dd;
-                    const int fB = max(fA, nA);
+                    const int fB = SW ? max(max(fA, nA), zB) : max(fA, nA);
                     const int hB = max(max(A + (sv.x >> 16), eB), fB);
                     const int nB = hB + dd;
-                    const int fC = max(fB, nB);
+                    const int fC = SW ? max(max(fB, nB), zC) : max(fB, nB);
                     const int hC = max(max(B + (int)(short)sv.y, eC), fC);
                     const int nC = hC + dd;
-                    const int fD = max(fC, nC);
+                    const int fD = SW ? max(max(fC, nC), zD) : max(fC, nC);
                     const int hD = max(max(Cc + (sv.y >> 16), eD), fD);
                     const int nD = hD + dd;
+                    if constexpr (SW)
+                    {
+                        const int bu = 15 - 4 * q - u;
+                        pA = max(pA, ((hA - zA) << 4) | bu);
+                        pB = max(pB, ((hB - zB) << 4) | bu);
+                        pC = max(pC, ((hC - zC) << 4) | bu);
+                        pD = max(pD, ((hD - zD) << 4) | bu);
+                        zA -= a.ge;
+                        zB -= a.ge;
+                        zC -= a.ge;
+                        zD -= a.ge;
+                    }
                     if constexpr (CAP)
                     {
                         if (t0 + u == tStar && lane == laneR)
@@ -555,7 +589,7 @@ __device__ __forceinline__ void strip_wave(const StripArgs& a, const Lds& L, int
             // hand-off: row D of 4 steps, slot (group - lane)
             if constexpr (!(GSA_KNOB & 8))
                 lds_st4(ring_out + 16u * (uint32_t)(((t0 >> 2) - lane) & (kRing - 1)), int4v {Xd[0], Xd[1], Xd[2], Xd[3]});
-            if constexpr (MODE == kModeScoreAG)
+            if constexpr (is_score_mode(MODE))
                 lds_st4(ring2_out + 16u * (uint32_t)(((t0 >> 2) - lane) & (kRing - 1)), int4v {Fd[0], Fd[1], Fd[2], Fd[3]});
             if constexpr (MODE == kModeFullRing)
             {
@@ -639,6 +673,20 @@ __device__ __forceinline__ void strip_wave(const StripArgs& a, const Lds& L, int
                 }
             }
         }
+        if constexpr (MODE == kModeScoreSW)
+        {
+            auto fold = [&](int& p, int& best, int& tb) {
+                const int v = p >> 4;
+                const bool up = v > best;
+                best = up ? v : best;
+                tb = up ? 16 * b + 15 - (p & 15) : tb;
+                p = 0;
+            };
+            fold(pA, bA, tA);
+            fold(pB, bB, tB);
+            fold(pC, bC, tC);
+            fold(pD, bD, tD);
+        }
         if constexpr (CAP && MODE == kModeSparse)
         {
             if (16 * b + 15 == cb + 63)
@@ -698,6 +746,28 @@ __device__ __forceinline__ void strip_wave(const StripArgs& a, const Lds& L, int
         if (b + 1 < NB && !run_block(b + 1, sB, sA, lxA, lxB, hvB, hvA, hfB, hfA)) return;
     }
     if (w == NS - 1) tstamp(a, tk, 2, lane);
+    if constexpr (MODE == kModeScoreSW)
+    {
+        // this lane's best cell, first in row-major order: rows in order, first step per row
+        const unsigned long long W = (unsigned long long)a.C + 1, mask = (1ull << a.idxBits) - 1;
+        const int bv[kK] = {bA, bB, bC, bD}, tv[kK] = {tA, tB, tC, tD};
+        unsigned long long key = 0;
+        bool big = false;
+#pragma unroll
+        for (int k = 0; k < kK; ++k)
+        {
+            // a score >= 2^26 (before the packing could wrap: one cell adds < 2^16) -> the host's row scan
+            big |= bv[k] >= (1 << 26) && r0 + kK * lane + k <= a.R;
+            if (bv[k] > 0 && r0 + kK * lane + k <= a.R)
+            {
+                const unsigned long long idx = (unsigned long long)(r0 + kK * lane + k) * W + (unsigned long long)(tv[k] - lane);
+                const unsigned long long kk = ((unsigned long long)bv[k] << a.idxBits) | (mask - idx);
+                key = kk > key ? kk : key;
+            }
+        }
+        if (key) atomicMax(a.swBest, key);
+        if (big) atomicOr((unsigned*)a.agResult, 1u);  // the AG result word, unused by SW
+    }
     if constexpr (MODE == kModeFullRing)
     {
         __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): every block of this ticket is in L2
@@ -717,7 +787,7 @@ __device__ __forceinline__ void loader_wave(const StripArgs& a, const Lds& L, in
     const uint32_t F = L.flags;
     const uint32_t ring0 = L.ring;
     // AG: ticket 0 is fed too, from the border row (Hgo' = d at column 0, 2d after it; F' = -inf)
-    const bool feed = tk > 0 || MODE == kModeScoreAG;
+    const bool feed = tk > 0 || is_score_mode(MODE);
     const unsigned long long* gprev = a.gran + (size_t)(tk > 0 ? tk - 1 : 0) * a.granStride;
     unsigned long long* gout = a.gran + (size_t)tk * a.granStride;
     const unsigned long long* gprev2 = a.gran2 + (size_t)(tk > 0 ? tk - 1 : 0) * a.granStride;  // AG: F'
@@ -794,10 +864,12 @@ __device__ __forceinline__ void loader_wave(const StripArgs& a, const Lds& L, in
             const bool in = c <= Cp;
             unsigned long long q = 0ull, q2 = 0ull;
             bool good;
-            if (MODE == kModeScoreAG && tk == 0)
+            if (is_score_mode(MODE) && tk == 0)
             {
+                // row 0 in the shifted space: global H'(0,c) = d for c >= 1 (0 at c = 0), local
+                // H'(0,c) = -c*ge (H = 0); carried as Hgo' = H' + d
                 const int dd = a.go - a.ge;
-                q = (uint32_t)(c == 0 ? dd : 2 * dd);
+                q = (uint32_t)(MODE == kModeScoreSW ? dd - c * a.ge : (c == 0 ? dd : 2 * dd));
                 q2 = (uint32_t)(-(1 << 29));
                 good = in;
             }
@@ -805,7 +877,7 @@ __device__ __forceinline__ void loader_wave(const StripArgs& a, const Lds& L, in
             {
                 q = in ? __hip_atomic_load(gprev + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
                 good = in && (uint32_t)(q >> 32) == a.epoch;
-                if constexpr (MODE == kModeScoreAG)
+                if constexpr (is_score_mode(MODE))
                 {
                     q2 = in ? __hip_atomic_load(gprev2 + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
                     good = good && (uint32_t)(q2 >> 32) == a.epoch;
@@ -816,7 +888,7 @@ __device__ __forceinline__ void loader_wave(const StripArgs& a, const Lds& L, in
             if (n > 0)
             {
                 if (lane < n) lds_st(ring0 + ring_elem(c), (int)(uint32_t)q);
-                if (MODE == kModeScoreAG && lane < n) lds_st(ring20 + ring_elem(c), (int)(uint32_t)q2);
+                if (is_score_mode(MODE) && lane < n) lds_st(ring20 + ring_elem(c), (int)(uint32_t)q2);
                 if (hnext == 0) tstamp(a, tk, 3, lane);
                 hnext += n;
                 flag_st(F + kFProg + 0, hnext > Cp ? kBig : hnext);
@@ -835,7 +907,7 @@ __device__ __forceinline__ void loader_wave(const StripArgs& a, const Lds& L, in
                 if (pub)
                     __hip_atomic_store(gout + c, ((unsigned long long)a.epoch << 32) | (uint32_t)v, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
-                if constexpr (MODE == kModeScoreAG)
+                if constexpr (is_score_mode(MODE))
                 {
                     const int v2 = lds_ld(ringN2 + ring_elem(c));
                     if (pub)
@@ -1215,12 +1287,17 @@ __global__ void __launch_bounds__(64 * (MODE == kModeFullRing ? kRingWaves : NS 
         }
         // per-super-strip state: letter ring = NEG, ring 0 = row 0 (H' = 0), progress words
         for (int k = threadIdx.x; k < kXCopy; k += 64 * kWaves<NS, MODE>) lds_st(L.xo + 4 * k, pa.substsz * 512);
-        for (int k = threadIdx.x; k < kRing * 4; k += 64 * kWaves<NS, MODE>) lds_st(L.ring + 4 * k, 0);
+        for (int k = threadIdx.x; k < kRing * 4; k += 64 * kWaves<NS, MODE>)
+        {
+            // score modes: Hgo' and F' of the row above = -inf past the columns the loader feeds
+            lds_st(L.ring + 4 * k, is_score_mode(MODE) ? -(1 << 29) : 0);
+            if constexpr (is_score_mode(MODE)) lds_st(L.ring2 + 4 * k, -(1 << 29));
+        }
         if (threadIdx.x < 4) lds_st(L.zero + 4 * threadIdx.x, 0);
         if (threadIdx.x < 8)
         {
             // nothing valid yet: -64 < every column a lane can touch (lane 63 starts at -63)
-            lds_st(F + kFProg + 4 * threadIdx.x, (threadIdx.x == 0 && tk == 0 && MODE != kModeScoreAG) ? kBig : -64);
+            lds_st(F + kFProg + 4 * threadIdx.x, (threadIdx.x == 0 && tk == 0 && !is_score_mode(MODE)) ? kBig : -64);
             lds_st(F + kFCons + 4 * threadIdx.x, 0);
             lds_st(F + kFSto + 4 * threadIdx.x, 0);  // sto[0..1][0..3]
         }
@@ -1308,6 +1385,7 @@ hipError_t launch_strip_fill(const StripArgs& a, int mode, int grid, hipStream_t
     if (mode == kModeSparse) return launch_strip<kSparseNS, kModeSparse>(a, grid, stream);
     if (mode == kModeFullRing) return launch_strip<1, kModeFullRing>(a, grid, stream);
     if (mode == kModeScoreAG) return launch_strip<kSparseNS, kModeScoreAG>(a, grid, stream);
+    if (mode == kModeScoreSW) return launch_strip<kSparseNS, kModeScoreSW>(a, grid, stream);
     if (a.ns == 2) return launch_strip<2, kModeFull>(a, grid, stream);
     return launch_strip<1, kModeFull>(a, grid, stream);
 }

@@ -67,12 +67,65 @@ def test_config5_50k(engine, golden, go, ge, local):
 
 
 @pytest.mark.parametrize("R,C", [(1, 300), (700, 130), (2049, 1500)])
-@pytest.mark.parametrize("go,ge", [(-11, -11), (-11, -1)])
-def test_global_row_scan_path(engine, golden, R, C, go, ge, monkeypatch):
-    """Global scores normally run on the strip kernel (affine mode); GSA_SCORE_SCAN=1 keeps the
-    row-scan kernel reachable for them: both equal the oracle."""
+@pytest.mark.parametrize("go,ge,local", MODES)
+def test_row_scan_path(engine, golden, R, C, go, ge, local, monkeypatch):
+    """Scores normally run on the strip kernel (affine / local modes); GSA_SCORE_SCAN=1 keeps the
+    row-scan kernel reachable: both equal the oracle."""
     import oracle
     monkeypatch.setenv("GSA_SCORE_SCAN", "1")
     Y, X = random_pair(R, C, 5 * R + C)
-    r = engine.score(Y, X, golden.blosum62, go, ge, False)
-    assert (r["score"], r["i_end"], r["j_end"]) == oracle.score_ag(Y, X, golden.blosum62, go, ge, False)
+    r = engine.score(Y, X, golden.blosum62, go, ge, local)
+    assert (r["score"], r["i_end"], r["j_end"]) == oracle.score_ag(Y, X, golden.blosum62, go, ge, local)
+
+
+@pytest.mark.parametrize("go,ge", [(-11, -11), (-11, -1), (-5, -2)])
+@pytest.mark.parametrize("gapR", [0, 37, 250, 3000])
+def test_local_ties_first_in_row_major(engine, golden, go, ge, gapR):
+    """SW: the same motif twice in Y (rows apart, across strip boundaries for the larger gaps),
+    flanked by a letter that scores -4 against everything (match +5, mismatch -4): two equal
+    maxima; the end cell reported is the first in row-major order, as the oracle's strict '>'
+    row sweep keeps."""
+    import oracle
+    n = int(round(np.sqrt(golden.blosum62.size)))
+    sub = np.full((n, n), -4, np.int32)
+    np.fill_diagonal(sub[:20, :20], 5)
+    sub = sub.reshape(golden.blosum62.shape)
+    rng = np.random.default_rng(gapR + 7)
+    motif = rng.integers(0, 20, 300).astype(np.int32)
+    fl = lambda k: np.full(k, 22, np.int32)
+    Y = np.concatenate([[0], fl(5), motif, fl(gapR + 1), motif, fl(9)]).astype(np.int32)
+    X = np.concatenate([[0], fl(50), motif, fl(40)]).astype(np.int32)
+    r = engine.score(Y, X, sub, go, ge, True)
+    ref = oracle.score_ag(Y, X, sub, go, ge, True)
+    assert ref == (1500, 305, 350)
+    assert (r["score"], r["i_end"], r["j_end"]) == ref
+
+
+def test_local_all_mismatch(engine, golden):
+    """SW with no positive cell: (0, 0, 0)."""
+    import oracle
+    sub = np.full_like(golden.blosum62, -4)
+    Y, X = random_pair(900, 1300, 3)
+    r = engine.score(Y, X, sub, -11, -1, True)
+    assert (r["score"], r["i_end"], r["j_end"]) == (0, 0, 0) == oracle.score_ag(Y, X, sub, -11, -1, True)
+
+
+def test_local_fallbacks_to_row_scan(engine, golden):
+    """SW takes the row scan when the strip kernel's conditions fail: go == 0 (cells past C could
+    tie the maximum) and scores >= 2^26 (the kernel flags them; packed with the step they would
+    wrap).  Both equal the oracle."""
+    import oracle
+    Y, X = random_pair(700, 900, 11)
+    for go, ge in [(0, 0)]:
+        r = engine.score(Y, X, golden.blosum62, go, ge, True)
+        assert (r["score"], r["i_end"], r["j_end"]) == oracle.score_ag(Y, X, golden.blosum62, go, ge, True)
+    n = int(round(np.sqrt(golden.blosum62.size)))
+    sub = np.full((n, n), -30000, np.int32)
+    np.fill_diagonal(sub, 30000)
+    sub = sub.reshape(golden.blosum62.shape)
+    Y, _ = random_pair(2600, 10, 12)
+    X = Y.copy()
+    ref = oracle.score_ag(Y, X, sub, -11, -1, True)
+    assert ref[0] >= 1 << 26
+    r = engine.score(Y, X, sub, -11, -1, True)
+    assert (r["score"], r["i_end"], r["j_end"]) == ref
