@@ -18,6 +18,7 @@
 
 #include "../../include/gsa.h"
 #include "nw_check.h"
+#include "nw_lane.h"
 #include "nw_strip.h"
 #include "nw_trace_dev.h"
 #include "nw_scan.h"
@@ -146,6 +147,22 @@ int full_ns()
         return (v == 1 || v == 2) ? v : gsa::kFullNSDefault;
     }();
     return ns;
+}
+
+// Full fills run on the one-row-per-lane kernel (nw_lane.hip) unless GSA_FULL_KERNEL=strip
+// selects the 4-rows-per-lane strip kernel (nw_strip.hip); GSA_LANE_NS = lane strips per
+// workgroup (1..4).  Both read per launch.
+bool full_lane_enabled()
+{
+    const char* e = std::getenv("GSA_FULL_KERNEL");
+    return !(e && std::strcmp(e, "strip") == 0);
+}
+
+int lane_ns()
+{
+    const char* e = std::getenv("GSA_LANE_NS");
+    const int v = e ? std::atoi(e) : gsa::kLaneNSDefault;
+    return (v >= 1 && v <= 4) ? v : gsa::kLaneNSDefault;
 }
 
 // Ring mode for full fills (nw_strip.hip): the output leaves the strip CUs through L2-resident
@@ -290,7 +307,9 @@ int enqueue_batch(gsa_ctx* ctx, int mode, int npairs, const gsa_pair_dev* pairs,
     a.subst = subst;
     a.substsz = substsz;
     a.g = gapo;
-    a.ns = (mode == gsa::kModeFull) ? full_ns() : gsa::kSparseNS;
+    const bool lane = mode == gsa::kModeFull && full_lane_enabled();
+    a.ns = (mode == gsa::kModeFull) ? (lane ? lane_ns() : full_ns()) : gsa::kSparseNS;
+    const int fullRows = lane ? gsa::kLaneRows * a.ns : gsa::kWaveRows * a.ns;  // rows per ticket
     if (mode == gsa::kModeSparse)
     {
         if (tileBx < 64 || tileBx % 16 != 0) return GSA_ERROR_INVALID_VALUE;
@@ -316,7 +335,7 @@ int enqueue_batch(gsa_ctx* ctx, int mode, int npairs, const gsa_pair_dev* pairs,
             d.ld = in.adjcols;
             d.Cp = d.C;
             // an empty row or column leaves nothing but headers to compute
-            d.nTickets = (d.C == 0) ? 0 : (d.R + gsa::kWaveRows * a.ns - 1) / (gsa::kWaveRows * a.ns);
+            d.nTickets = (d.C == 0) ? 0 : (d.R + fullRows - 1) / fullRows;
             maxWork = std::max<long long>(maxWork, (long long)std::max(d.R, d.C) + 1);
         }
         else
@@ -385,7 +404,7 @@ int enqueue_batch(gsa_ctx* ctx, int mode, int npairs, const gsa_pair_dev* pairs,
     // one pair: one workgroup per CU (its tickets are a chain); a batch: all resident slots
     int grid = (npairs == 1) ? std::max(1, std::min((int)tickets, ctx->cu_count)) : 0;
     int launchMode = mode;
-    if (mode == gsa::kModeFull && npairs == 1 && a.ns == 1 && !done && full_ring_enabled() && tickets >= 8 &&
+    if (mode == gsa::kModeFull && !lane && npairs == 1 && a.ns == 1 && !done && full_ring_enabled() && tickets >= 8 &&
         2 * std::min<long long>(tickets, ctx->cu_count / 2) <= ctx->cu_count)
     {
         // nStrip a multiple of 8: copy workgroup nStrip+s then sits on strip s's XCD
@@ -414,7 +433,7 @@ int enqueue_batch(gsa_ctx* ctx, int mode, int npairs, const gsa_pair_dev* pairs,
         launchMode = gsa::kModeFullRing;
         grid = 2 * nStrip;
     }
-    e = gsa::launch_strip_fill(a, launchMode, grid, st);
+    e = lane ? gsa::launch_lane_fill(a, a.ns, grid, st) : gsa::launch_strip_fill(a, launchMode, grid, st);
     if (e != hipSuccess) return fail(ctx, e, GSA_ERROR_KERNEL_FAILURE);
     return GSA_SUCCESS;
 }

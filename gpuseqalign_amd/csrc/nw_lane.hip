@@ -1,0 +1,641 @@
+// nw_lane.hip -- NW-LG full-matrix fill with ONE row per lane ("lane strips"), hand-written
+// wave64 HIP for gfx950 (MI355X).
+//
+// Replaces the plain fill family NwAlign_Gpu3..6 (nwalign_gpu3_ml_diagdiag.cu:288-596, the
+// per-diagonal kernels :11-287) and has their output contract: nw.score, the (R+1) x (C+1)
+// int32 matrix, row-major, unpadded.  Recurrence of UpdateScore (nwalign_cpu1_st_row.cpp:4-10).
+//
+// Why one row per lane.  A single pair is bounded by its wavefront's critical path,
+// (C + nStrips * hop) * t_step, not by HBM: with K rows per lane a step costs ~(a + b*K) cycles
+// and the hop is >= 64 steps (the lane skew) per 64*K rows.  The 4-row strips of nw_strip.hip
+// run ~200 cycles/step on full fills; one row per lane runs ~25-40 (tools/ubench/k1_ubench.hip),
+// which more than pays for 4x the strips.
+//
+// Step (unshifted values, gap folded into the operands, 4 VALU per cell):
+//     up' = dpp_shr1(H) + hv          hv = g; lane 0: H(row above, c) + g         v_add_u32_dpp
+//     t1  = U + q                     U = up' of the previous step, q = s(y, X[c]) - g
+//     H   = max3(t1, up', H + g)      = max3(H[i-1][j-1]+s, H[i-1][j]+g, H[i][j-1]+g)
+//     U   = up'
+// Lane l owns row r0 + l and at step t works on column t - l.  Columns <= 0 (the first 64
+// steps) are forced to the border r*g.
+//
+// Substitution scores come from a per-workgroup COLUMN profile Q[y][c] = s(y, X[c]) - g
+// (int32, a ring of kLW columns, rows kLQRS = kLW + 32 dwords apart): lane l reads Q[y_l][t-l],
+// bank (t - l) mod 32 whatever the row letters (conflict-free), at base + immediate offsets,
+// so a step spends no VALU on addressing.  The loader wave builds Q from seqX and the table.
+//
+// Hand-off: lane 63 of strip w writes its (H + g) values (the "left" operand it computes anyway)
+// into ring w+1, element e = column e - 64; lane 0 of strip w+1 reads them 8 at a time, one
+// block ahead.  Order is kept with LDS progress words (LDS ops of one wave execute in order).
+// Between super-strips (workgroups) the loader moves the last strip's row through 8-byte
+// {epoch, H+g} granules in HBM, as nw_strip.hip does.  The strips store their own output: two
+// dwordx4 per lane per 8-step block (the lane's row, 8 consecutive columns).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+
+#include "nw_lane.h"
+
+namespace gsa {
+namespace {
+
+constexpr int kLW = 512;           // Q ring columns (power of 2)
+constexpr int kLQRS = kLW + 32;    // Q row stride in dwords: == 0 mod 32, 32 guard columns
+constexpr int kLRing = 512;        // hand-off ring elements per strip boundary (power of 2)
+#ifndef GSA_LBLK
+#define GSA_LBLK 16
+#endif
+constexpr int kLBlk = GSA_LBLK;    // steps per block (8 or 16)
+static_assert(kLBlk == 8 || kLBlk == 16, "block");
+constexpr int kLH = kLBlk / 4;     // halo registers (int4) per block
+// Options (experiments): halo read by all lanes (lanes >= 1 read a row of g, no exec branch);
+// progress words read at block start (1) or in mid-block (0)
+#ifndef GSA_LHALO_ALL
+#define GSA_LHALO_ALL 0
+#endif
+#ifndef GSA_LFLAG_EARLY
+#define GSA_LFLAG_EARLY 0
+#endif
+// Output path: 0 = every lane stores its own row (dwordx4 stores, 64 rows per store
+// instruction); 1 = rows staged in LDS and stored row-contiguously (8 lanes x 16 B per row),
+// one pair of blocks behind.  1 measured slower on one strip (114 vs 78 cycles/step) with no
+// change in the hand-off lags (profiles/r01_lane_probe.jsonl), so 0 is the default.
+#ifndef GSA_LSTAGE
+#define GSA_LSTAGE 0
+#endif
+constexpr int kLBig = 0x3fffffff;  // "everything published"
+constexpr uint64_t kLSpin = 20000000ull;  // 0.2 s of s_memrealtime (100 MHz) without progress
+
+extern __shared__ __attribute__((aligned(16))) char lsm[];
+
+// Timing-experiment knobs (separate builds only; any set bit makes results WRONG):
+// 1 no global stores, 2 strips never wait, 4 no hand-off writes, 8 no halo reads, 16 no Q reads,
+// 32 no mid-block progress reads, 64 no progress stores by strips
+#ifndef GSA_LKNOB
+#define GSA_LKNOB 0
+#endif
+#ifndef GSA_STAMP
+#define GSA_STAMP 0
+#endif
+// Diagnostic stamps (separate build): s_memrealtime (100 MHz, one clock for all XCDs) at the start of every 8th block of the strip
+// waves of tickets 0..7, dbg[(ticket * 2 + w) * 160 + b / 8] (w < 2, b < 1280).
+__device__ __forceinline__ void lstamp(const StripArgs& a, int tk, int w, int b, int k, int lane)
+{
+    if constexpr (GSA_STAMP)
+    {
+        if (k == 0 && tk < 8 && w < 2 && (b & 7) == 0 && b < 1280 && lane == 0 && a.dbg)
+        {
+            unsigned long long t;
+            asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+            a.dbg[(size_t)(tk * 2 + w) * 160 + (b >> 3)] = t;
+        }
+    }
+}
+
+
+typedef int int4v __attribute__((ext_vector_type(4)));
+typedef int int4a __attribute__((ext_vector_type(4), aligned(4)));
+template <typename T>
+using gptr = __attribute__((address_space(1))) T*;
+template <typename T>
+__device__ __forceinline__ gptr<T> G(T* p)
+{
+    return (gptr<T>)p;
+}
+
+__device__ __forceinline__ int lds_ld(uint32_t a) { return *(const int*)(lsm + a); }
+__device__ __forceinline__ void lds_st(uint32_t a, int v) { *(int*)(lsm + a) = v; }
+__device__ __forceinline__ int4v lds_ld4(uint32_t a) { return *(const int4v*)(lsm + a); }
+__device__ __forceinline__ void lds_st4(uint32_t a, int4v v) { *(int4v*)(lsm + a) = v; }
+// progress words: relaxed workgroup-scope atomics (no waits; see nw_strip.hip)
+__device__ __forceinline__ int raw_ld(uint32_t a)
+{
+    return __hip_atomic_load((int*)__builtin_assume_aligned(lsm + a, 4), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ int flag_ld(uint32_t a) { return __builtin_amdgcn_readfirstlane(raw_ld(a)); }
+__device__ __forceinline__ void flag_st(uint32_t a, int v)
+{
+    asm volatile("" ::: "memory");  // data writes are issued before the word (LDS executes in order)
+    __hip_atomic_store((int*)__builtin_assume_aligned(lsm + a, 4), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ bool err_set(const StripArgs& a)
+{
+    return __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+}
+// lane l <- lane l-1, lane 0 <- 0 (DPP wave_shr:1, bound_ctrl zero)
+__device__ __forceinline__ int shr1z(int v) { return __builtin_amdgcn_update_dpp(0, v, 0x138, 0xF, 0xF, true); }
+
+// link stamps (stamp builds): s_memrealtime when the drain wave of ticket 0 has stored, and the
+// feed wave of ticket 1 has fed, the columns below 64k (dbg[2560 + k], dbg[2800 + k], k < 200)
+__device__ __forceinline__ void link_stamp(const StripArgs& a, int base, int oldc, int newc, int lane)
+{
+    if constexpr (GSA_STAMP)
+    {
+        if (lane == 0 && a.dbg && (oldc >> 6) != (newc >> 6) && (newc >> 6) < 200)
+        {
+            unsigned long long t;
+            asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+            for (int k = (oldc >> 6) + 1; k <= (newc >> 6) && k < 200; ++k) a.dbg[base + k] = t;
+        }
+    }
+}
+
+// LDS: Q profile, transposed substitution table subT[x][y] = s(y, x) - g (rows of kLSubRow
+// dwords, so one lane gathers 4 row letters per ds_read_b128), NS+1 hand-off rings, progress words.
+// flags: prog[i] @ 4i (ring i holds elements < prog[i]), cons[i] @ 32+4i (ring i's reader no
+// longer needs elements < cons[i]), xo @ 64 (Q holds columns < xo), ticket @ 68.
+struct LaneLds
+{
+    uint32_t q, stage, sub, ring, gfill, flags;
+};
+// Output stage per strip: 2 buffers of [64 rows][32 steps] int32 (128-byte rows of 8 16-byte
+// chunks, chunk index XOR row & 7: conflict-free for the strip's row writes and its row-segment
+// read-back, 8 lanes per row)
+constexpr uint32_t kStageBytes = 64u * 128u;
+constexpr uint32_t kFCons = 32, kFXo = 64, kFTicket = 68;
+constexpr int kLSubRow = 36;  // dwords per subT row: 32 letters + 4 (16-byte aligned rows)
+
+__host__ __device__ inline LaneLds lane_layout(int ns, int substsz)
+{
+    LaneLds L;
+    L.q = 0;
+    L.stage = (uint32_t)substsz * kLQRS * 4u;
+    L.sub = L.stage + (GSA_LSTAGE ? (uint32_t)ns * 2u * kStageBytes : 0u);
+    L.ring = L.sub + (uint32_t)substsz * kLSubRow * 4u;
+    L.gfill = L.ring + (uint32_t)(ns + 1) * kLRing * 4u;  // 16 x g: the "halo" of lanes >= 1
+    L.flags = L.gfill + 64u;
+    return L;
+}
+
+// ------------------------------------------------------------------------------------
+// strip wave: 64 rows, one per lane
+// ------------------------------------------------------------------------------------
+template <int NS>
+__device__ __forceinline__ void lane_strip(const StripArgs& a, const LaneLds& L, int tk, int w, int lane)
+{
+    const int g = a.g;
+    const int C = a.C;
+    const int r0 = tk * (kLaneRows * NS) + kLaneRows * w + 1;  // first row of the strip
+    const int r = r0 + lane;                                   // this lane's row
+    const bool live = r <= a.R;
+    int y = live ? G(a.seqY)[r] : 0;
+    y = ((unsigned)y < (unsigned)a.substsz) ? y : 0;
+    const uint32_t qrow = L.q + (uint32_t)y * (kLQRS * 4u);
+    const uint32_t ring_in = L.ring + (uint32_t)w * (kLRing * 4u);
+    const uint32_t ring_out = L.ring + (uint32_t)(w + 1) * (kLRing * 4u);
+    const uint32_t f_in = L.flags + 4u * w, f_out = L.flags + 4u * (w + 1);
+    const uint32_t c_in = L.flags + kFCons + 4u * w, c_out = L.flags + kFCons + 4u * (w + 1);
+    const uint32_t f_xo = L.flags + kFXo;
+    const int NB = (C + 65 + kLBlk - 1) / kLBlk;  // lane 63 reaches step C+64 (element of column C)
+    const int rg = r * g;
+    // output stage: this lane writes its row; for the read-back lane = 8 * srow + sq reads rows
+    // 8i + srow, chunk sq (steps 32p + 4sq ..) and stores them to columns 32p + 4sq - row
+    const uint32_t stg = L.stage + (uint32_t)w * (2u * kStageBytes);
+    const uint32_t stg_w = stg + 128u * (uint32_t)lane;
+    const int srow = lane >> 3, sq = lane & 7;
+    const uint32_t stg_r = stg + 128u * (uint32_t)srow + 16u * (uint32_t)(sq ^ srow);
+    const gptr<int> obase = G(a.score) + (size_t)(r0 + srow) * (size_t)a.ld;
+    const int rlim = a.R - r0 - srow;  // row 8i + srow of the strip is in the matrix iff 8i <= rlim
+    const gptr<int> orow = G(a.score) + (size_t)(live ? r : 0) * (size_t)a.ld;  // GSA_LSTAGE 0
+
+    // block b prefetches block b+1's inputs (ring elements < B(b+1)+64+B, Q columns < B(b+1)+B,
+    // B = kLBlk) and writes ring elements Bb .. Bb+B-1
+    auto ok = [&](int pin, int pco, int pxo, int b) {
+        if constexpr ((GSA_LKNOB & 2) != 0) return true;
+        return pin >= kLBlk * b + 64 + 2 * kLBlk && pco >= kLBlk * b + kLBlk - kLRing && (w != 0 || pxo >= kLBlk * b + 2 * kLBlk);
+    };
+    auto spin = [&](int b) {
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        for (;;)
+        {
+            const int pin = flag_ld(f_in), pco = flag_ld(c_out), pxo = (w == 0) ? flag_ld(f_xo) : 0;
+            if (ok(pin, pco, pxo, b)) return true;
+            __builtin_amdgcn_s_sleep(1);
+            if (__builtin_amdgcn_s_memrealtime() - t0 > kLSpin || err_set(a))
+            {
+                atomicOr(a.err, 1u);
+                return false;
+            }
+        }
+    };
+    // halo of block bb: ring elements B*bb+64 .. +B-1 (lane 0; lanes >= 1 keep / read g)
+    const uint32_t halo_base = (GSA_LHALO_ALL && lane != 0) ? L.gfill : ring_in;
+    auto halo_load = [&](int bb, int4v (&h)[kLH]) {
+        if constexpr (GSA_LHALO_ALL)
+        {
+            const uint32_t hb = halo_base + (lane == 0 ? 4u * (uint32_t)((kLBlk * bb + 64) & (kLRing - 1)) : 0u);
+#pragma unroll
+            for (int j = 0; j < kLH; ++j) h[j] = lds_ld4(hb + 16u * (lane == 0 ? j : 0));
+        }
+        else if (lane == 0)
+        {
+            const uint32_t hb = ring_in + 4u * (uint32_t)((kLBlk * bb + 64) & (kLRing - 1));
+#pragma unroll
+            for (int j = 0; j < kLH; ++j) h[j] = lds_ld4(hb + 16u * j);
+        }
+    };
+
+    int qA[kLBlk], qB[kLBlk];
+    int4v hA[kLH], hB[kLH];
+#pragma unroll
+    for (int j = 0; j < kLH; ++j) hA[j] = hB[j] = int4v {g, g, g, g};  // lanes >= 1 keep g
+    if (!spin(-1)) return;
+    {
+        const uint32_t qb = qrow + 4u * (uint32_t)((-lane) & (kLW - 1));
+#pragma unroll
+        for (int u = 0; u < kLBlk; ++u) qA[u] = lds_ld(qb + 4u * u);
+        halo_load(0, hA);
+    }
+    int H = rg, U = rg;
+    int rpin = 0, rpco = 0, rpxo = 0;  // progress words read in the previous block, checked now
+
+    auto block = [&](int b, int (&qc)[kLBlk], int (&qn)[kLBlk], int4v (&hc)[kLH], int4v (&hn)[kLH], auto rampT) {
+        constexpr bool RAMP = decltype(rampT)::value;
+        lstamp(a, tk, w, b, 0, lane);
+        {
+            const int pin = __builtin_amdgcn_readfirstlane(rpin), pco = __builtin_amdgcn_readfirstlane(rpco);
+            const int pxo = (w == 0) ? __builtin_amdgcn_readfirstlane(rpxo) : 0;
+            if (!ok(pin, pco, pxo, b) && !spin(b)) return false;
+        }
+        if (GSA_LFLAG_EARLY && !(GSA_LKNOB & 32))
+        {
+            rpin = raw_ld(f_in);
+            rpco = raw_ld(c_out);
+            rpxo = raw_ld(f_xo);
+        }
+        // prefetch block b+1: Q of columns B(b+1)-l .. +B-1, halo
+        {
+            const uint32_t qb = qrow + 4u * (uint32_t)((kLBlk * b + kLBlk - lane) & (kLW - 1));
+#pragma unroll
+            for (int u = 0; u < kLBlk; ++u) qn[u] = (GSA_LKNOB & 16) ? qc[u] ^ 1 : lds_ld(qb + 4u * u);
+            if constexpr (!(GSA_LKNOB & 8)) halo_load(b + 1, hn);
+            if constexpr (!(GSA_LKNOB & 64)) flag_st(c_in, kLBlk * b + 64 + 2 * kLBlk);
+        }
+        lstamp(a, tk, w, b, 1, lane);
+        int vals[kLBlk], lt[kLBlk];
+#pragma unroll
+        for (int u = 0; u < kLBlk; ++u)
+        {
+            const int up = shr1z(H) + hc[u >> 2][u & 3];
+            const int t1 = U + qc[u];
+            const int hg = H + g;
+            int h = max(max(t1, up), hg);
+            if constexpr (RAMP) h = (lane >= kLBlk * b + u) ? rg : h;  // column <= 0: the border
+            lt[u] = hg;
+            U = up;
+            H = h;
+            vals[u] = h;
+            if (!GSA_LFLAG_EARLY && !(GSA_LKNOB & 32) && u == kLBlk / 2 - 1)
+            {
+                rpin = raw_ld(f_in);
+                rpco = raw_ld(c_out);
+                rpxo = raw_ld(f_xo);
+            }
+        }
+        lstamp(a, tk, w, b, 2, lane);
+        // hand-off: lane 63's H + g of steps Bb-1 .. Bb+B-2 = ring elements Bb .. Bb+B-1 (columns
+        // Bb-64 ..); the last strip's ring is drained into granules by the drain wave
+        if (!(GSA_LKNOB & 4) && lane == 63)
+        {
+            const uint32_t eb = ring_out + 4u * (uint32_t)((kLBlk * b) & (kLRing - 1));
+#pragma unroll
+            for (int j = 0; j < kLH; ++j) lds_st4(eb + 16u * j, int4v {lt[4 * j], lt[4 * j + 1], lt[4 * j + 2], lt[4 * j + 3]});
+        }
+        if constexpr (!(GSA_LKNOB & 64)) flag_st(f_out, b + 1 == NB ? kLBig : kLBlk * b + kLBlk);
+        if constexpr (GSA_LSTAGE && !(GSA_LKNOB & 1))
+        {
+            // output: this lane's row into the stage (steps Bb .. Bb+B-1 = chunks 4(b&1) ..)
+            const uint32_t sb = stg_w + (uint32_t)((b >> 1) & 1) * kStageBytes;
+#pragma unroll
+            for (int j = 0; j < kLH; ++j)
+                lds_st4(sb + 16u * (uint32_t)((kLH * (b & 1) + j) ^ (lane & 7)),
+                        int4v {vals[4 * j], vals[4 * j + 1], vals[4 * j + 2], vals[4 * j + 3]});
+        }
+        if (!GSA_LSTAGE && !(GSA_LKNOB & 1) && live)
+        {
+            // output: this lane's row, columns Bb-l .. Bb-l+B-1 (column 0 is the header kernel's)
+            const int c0 = kLBlk * b - lane;
+            if (c0 >= 1 && c0 + kLBlk - 1 <= C)
+            {
+#pragma unroll
+                for (int j = 0; j < kLH; ++j)
+                    *(gptr<int4a>)(orow + c0 + 4 * j) = int4a {vals[4 * j], vals[4 * j + 1], vals[4 * j + 2], vals[4 * j + 3]};
+            }
+            else if (c0 + kLBlk - 1 >= 1 && c0 <= C)
+            {
+#pragma unroll
+                for (int e = 0; e < kLBlk; ++e)
+                    if (c0 + e >= 1 && c0 + e <= C) orow[c0 + e] = vals[e];
+            }
+        }
+        lstamp(a, tk, w, b, 3, lane);
+        return true;
+    };
+
+    // GSA_LSTAGE: stage read-back (8 rows x 128 B per read) and row-contiguous stores, one pair of blocks
+    // (32 steps) behind the compute: the reads of pair p are issued after its last block and
+    // stored after the next pair, so neither waits
+    static_assert(kLBlk == 16, "stage pairs are 2 blocks of 16 steps");
+    int4v Rg[8];
+    auto stage_read = [&](int p) {
+        if constexpr (GSA_LSTAGE && !(GSA_LKNOB & 1))
+        {
+            const uint32_t rb = stg_r + (uint32_t)(p & 1) * kStageBytes;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) Rg[i] = lds_ld4(rb + 1024u * i);
+        }
+    };
+    auto flush = [&](int p) {
+        if constexpr (GSA_LSTAGE && !(GSA_LKNOB & 1))
+        {
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+            {
+                const int c = 32 * p + 4 * sq - (8 * i + srow);  // column of Rg[i].x
+                if (8 * i <= rlim && c + 3 >= 1 && c <= C)
+                {
+                    const gptr<int> dst = obase + (size_t)(8 * i) * (size_t)a.ld + c;
+                    if (c >= 1 && c + 3 <= C)
+                        *(gptr<int4a>)dst = int4a {Rg[i].x, Rg[i].y, Rg[i].z, Rg[i].w};
+                    else
+                    {
+#pragma unroll
+                        for (int e = 0; e < 4; ++e)
+                            if (c + e >= 1 && c + e <= C) dst[e] = Rg[i][e];
+                    }
+                }
+            }
+        }
+    };
+
+    int b = 0;
+    constexpr int kRampBlocks = 64 / kLBlk;  // columns <= 0 occur only in the first 64 steps
+    for (; b < kRampBlocks; b += 2)
+    {
+        if (!block(b, qA, qB, hA, hB, std::integral_constant<bool, true>())) return;
+        if (!block(b + 1, qB, qA, hB, hA, std::integral_constant<bool, true>())) return;
+        if (b > 0) flush((b >> 1) - 1);
+        stage_read(b >> 1);
+    }
+    for (; b < NB; b += 2)
+    {
+        if (!block(b, qA, qB, hA, hB, std::integral_constant<bool, false>())) return;
+        if (b + 1 < NB && !block(b + 1, qB, qA, hB, hA, std::integral_constant<bool, false>())) return;
+        flush((b >> 1) - 1);
+        stage_read(b >> 1);
+    }
+    flush((NB - 1) >> 1);
+}
+
+// ------------------------------------------------------------------------------------
+// loader wave: Q profile, the row above strip 0 (granules of the previous super-strip, or
+// row 0), the drain of the last strip's row into granules for the next super-strip
+// ------------------------------------------------------------------------------------
+template <int NS>
+__device__ __forceinline__ void lane_loader(const StripArgs& a, const LaneLds& L, int tk, int lane)
+{
+    const int C = a.C, g = a.g;
+    const uint32_t F = L.flags;
+    const uint32_t ring0 = L.ring;
+    const gptr<const unsigned long long> gprev = G((const unsigned long long*)a.gran) + (size_t)(tk > 0 ? tk - 1 : 0) * a.granStride;
+    auto letter = [&](int c) {
+        int x = (c >= 1 && c <= C) ? G(a.seqX)[c] : 0;
+        return ((unsigned)x < (unsigned)a.substsz) ? x : 0;
+    };
+    int qn = 0;                    // Q holds columns < qn
+    int hnext = 0;                 // next column of the row above to feed into ring 0
+    int xl = letter(lane);
+    int pl = 0, c0 = 0;  // progress words, re-read only when their cached values block
+    uint64_t last = __builtin_amdgcn_s_memrealtime();
+    while (qn <= C || hnext <= C)
+    {
+        bool moved = false;
+        // (1) the row above strip 0 (H + g) -> ring 0 elements c + 64, as far as granules of the
+        //     previous super-strip are published (in column order) and ring 0 has room.  The
+        //     poll's own latency paces this loop (no sleep while granules are awaited).
+        if (hnext <= C && hnext + 128 > c0 + kLRing) c0 = flag_ld(F + kFCons);  // ring 0 consumed
+        if (hnext <= C && hnext + 128 <= c0 + kLRing)
+        {
+            const int c = hnext + lane;
+            const bool in = c <= C;
+            int v = 0;
+            bool good;
+            if (tk == 0)
+            {
+                v = c * g + g;  // row 0: H(0, c) = c*g
+                good = in;
+            }
+            else
+            {
+                const unsigned long long q = in ? __hip_atomic_load(gprev + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+                good = in && (uint32_t)(q >> 32) == a.epoch;
+                v = (int)(uint32_t)q;
+            }
+            const uint64_t badm = __ballot(!good);
+            const int n = badm ? __builtin_ctzll(badm) : 64;
+            if (n > 0)
+            {
+                if (lane < n) lds_st(ring0 + 4u * (uint32_t)((c + 64) & (kLRing - 1)), v);
+                if (tk == 1) link_stamp(a, 2800, hnext, hnext + n, lane);
+                hnext += n;
+                flag_st(F, hnext > C ? kLBig : hnext + 64);
+                moved = true;
+            }
+        }
+        // (2) Q columns qn .. qn+63: the columns they replace (<= qn+63-kLW) are dead once the
+        //     last strip has published elements pl (its next reads start at column pl-55).
+        //     Gather the lane's letter column of subT (8 x b128), then 32 straight-line writes.
+        if (qn <= C && qn > pl + kLW - 128) pl = flag_ld(F + 4u * NS);  // last strip's elements
+        if (qn <= C && qn <= pl + kLW - 128)
+        {
+            const uint32_t p = (uint32_t)((qn + lane) & (kLW - 1));
+            const uint32_t sb = L.sub + 4u * kLSubRow * (uint32_t)xl;
+            int4v v[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = lds_ld4(sb + 16u * j);
+            const uint32_t qa = L.q + 4u * p;
+#pragma unroll
+            for (int yy = 0; yy < 32; ++yy)
+                if (yy < a.substsz) lds_st(qa + 4u * kLQRS * yy, v[yy >> 2][yy & 3]);
+            if ((qn & (kLW - 1)) == 0 && lane < kLBlk)
+            {
+                // guard copy of columns p < kLBlk at p + kLW: a block's reads run past the wrap
+#pragma unroll
+                for (int yy = 0; yy < 32; ++yy)
+                    if (yy < a.substsz) lds_st(qa + 4u * (kLQRS * yy + kLW), v[yy >> 2][yy & 3]);
+            }
+            qn += 64;
+            xl = letter(qn + lane);
+            flag_st(F + kFXo, qn > C ? kLBig : qn);
+            moved = true;
+        }
+        const uint64_t now = __builtin_amdgcn_s_memrealtime();
+        if (moved)
+            last = now;
+        else
+        {
+            if (now - last > kLSpin || err_set(a))
+            {
+                atomicOr(a.err, 1u);
+                return;
+            }
+            if (tk == 0 || hnext > C) __builtin_amdgcn_s_sleep(1);
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// drain wave: the last strip's row (H + g, ring NS) -> granules for the next super-strip.  A
+// wave of its own: it issues no global loads, so its stores never wait (vmcnt is in order) and
+// the feed wave's granule polls never delay the drain.
+// ------------------------------------------------------------------------------------
+template <int NS>
+__device__ __forceinline__ void lane_drain(const StripArgs& a, const LaneLds& L, int tk, int lane)
+{
+    const int C = a.C;
+    const uint32_t F = L.flags, ringN = L.ring + (uint32_t)NS * (kLRing * 4u);
+    if (tk + 1 >= a.nTickets)
+    {
+        flag_st(F + kFCons + 4u * NS, kLBig);  // nobody reads our last row
+        return;
+    }
+    const gptr<unsigned long long> gout = G(a.gran) + (size_t)tk * a.granStride;
+    int dnext = 0;  // next column to drain
+    uint64_t last = __builtin_amdgcn_s_memrealtime();
+    while (dnext <= C)
+    {
+        const int avail = min(flag_ld(F + 4u * NS) - 64, C + 1);  // columns < avail are in ring NS
+        if (dnext < avail)
+        {
+            const int c = dnext + lane;
+            if (c < avail)
+            {
+                const int v = lds_ld(ringN + 4u * (uint32_t)((c + 64) & (kLRing - 1)));
+                __hip_atomic_store(gout + c, ((unsigned long long)a.epoch << 32) | (uint32_t)v, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            }
+            if (tk == 0) link_stamp(a, 2560, dnext, min(dnext + 64, avail), lane);
+            dnext = min(dnext + 64, avail);
+            flag_st(F + kFCons + 4u * NS, dnext > C ? kLBig : dnext + 64);
+            last = __builtin_amdgcn_s_memrealtime();
+        }
+        else
+        {
+            if (__builtin_amdgcn_s_memrealtime() - last > kLSpin || err_set(a))
+            {
+                atomicOr(a.err, 1u);
+                return;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+}
+
+__device__ __forceinline__ PairDesc lane_desc(const PairDesc* p)
+{
+    constexpr int N = sizeof(PairDesc) / 4;
+    const int* wds = (const int*)p;
+    union
+    {
+        int v[N];
+        PairDesc d;
+    } u;
+#pragma unroll
+    for (int k = 0; k < N; ++k) u.v[k] = __builtin_amdgcn_readfirstlane(G(wds)[k]);
+    return u.d;
+}
+
+template <int NS>
+__global__ void __launch_bounds__(64 * (NS + 2)) nw_lane_kernel(StripArgs a)
+{
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const LaneLds L = lane_layout(NS, a.substsz);
+    for (int k = threadIdx.x; k < a.substsz * kLSubRow; k += 64 * (NS + 2))
+    {
+        const int x = k / kLSubRow, yy = k % kLSubRow;
+        lds_st(L.sub + 4u * k, yy < a.substsz ? G(a.subst)[yy * a.substsz + x] - a.g : 0);
+    }
+    for (;;)
+    {
+        __syncthreads();
+        if (threadIdx.x == 0) lds_st(L.flags + kFTicket, err_set(a) ? a.nTicketsTotal : (int)atomicAdd(a.ticket, 1u));
+        __syncthreads();
+        const int tkg = __builtin_amdgcn_readfirstlane(lds_ld(L.flags + kFTicket));
+        if (tkg >= a.nTicketsTotal) break;
+        // pair of this ticket: last descriptor with ticketBase <= tkg (binary search, uniform)
+        int lo = 0, hi = a.nPairs - 1;
+        while (lo < hi)
+        {
+            const int mid = (lo + hi + 1) >> 1;
+            if (__builtin_amdgcn_readfirstlane(G(a.pairs)[mid].ticketBase) <= tkg)
+                lo = mid;
+            else
+                hi = mid - 1;
+        }
+        const PairDesc d = lane_desc(a.pairs + lo);
+        StripArgs pa = a;
+        pa.seqY = d.seqY;
+        pa.seqX = d.seqX;
+        pa.R = d.R;
+        pa.C = d.C;
+        pa.nTickets = d.nTickets;
+        pa.score = d.score;
+        pa.ld = d.ld;
+        pa.gran = a.gran + d.granOff;
+        pa.granStride = (long long)d.C + 1;
+        const int tk = tkg - d.ticketBase;
+        if (threadIdx.x < 16) lds_st(L.flags + 4u * threadIdx.x, 0);  // prog[], cons[]
+        if (threadIdx.x < 16) lds_st(L.gfill + 4u * threadIdx.x, a.g);
+        if (threadIdx.x == 0) lds_st(L.flags + kFXo, 0);
+        __syncthreads();
+        if (w == NS + 1)
+            lane_drain<NS>(pa, L, tk, lane);
+        else if (w == NS)
+            lane_loader<NS>(pa, L, tk, lane);
+        else
+        {
+            __builtin_amdgcn_s_setprio(3);
+            lane_strip<NS>(pa, L, tk, w, lane);
+            __builtin_amdgcn_s_setprio(0);
+        }
+    }
+}
+
+template <int NS>
+hipError_t launch_lane(const StripArgs& a, int grid, hipStream_t stream)
+{
+    const size_t lds = lane_lds_bytes(NS, a.substsz);
+    auto kern = nw_lane_kernel<NS>;
+    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+    if (grid <= 0)
+    {
+        int per_cu = 0, dev = 0, cus = 0;
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)kern, 64 * (NS + 2), lds);
+        if (e == hipSuccess) e = hipGetDevice(&dev);
+        if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        if (e != hipSuccess) return e;
+        grid = std::max(1, std::min(a.nTicketsTotal, std::max(1, per_cu) * cus));
+    }
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * (NS + 2)), lds, stream, a);
+    return hipGetLastError();
+}
+
+}  // namespace
+
+size_t lane_lds_bytes(int ns, int substsz)
+{
+    return (size_t)lane_layout(ns, substsz).flags + 128;
+}
+
+hipError_t launch_lane_fill(const StripArgs& a, int ns, int grid, hipStream_t stream)
+{
+    if (ns == 1) return launch_lane<1>(a, grid, stream);
+    if (ns == 3) return launch_lane<3>(a, grid, stream);
+    if (ns == 4) return launch_lane<4>(a, grid, stream);
+    return launch_lane<2>(a, grid, stream);
+}
+
+}  // namespace gsa

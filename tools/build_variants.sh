@@ -10,9 +10,9 @@ hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -c nw_scan.hip -o build/var/nw_
 hipcc -O3 -std=c++17 -fPIC -c nw_trace.cpp -o build/var/nw_trace.o
 for spec in "$@"; do
   name="${spec%%:*}"; defs="${spec#*:}"
-  for f in gsa_capi nw_strip; do
+  for f in gsa_capi nw_strip nw_lane; do
     hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC $defs -c -x hip $f.hip -o build/var/$f.$name.o &
   done
   wait
-  hipcc --offload-arch=gfx950 -shared -fPIC build/var/gsa_capi.$name.o build/var/nw_strip.$name.o build/var/nw_trace.o build/var/nw_check.o build/var/nw_trace_dev.o build/var/nw_scan.o -o ../libgsa_$name.so
+  hipcc --offload-arch=gfx950 -shared -fPIC build/var/gsa_capi.$name.o build/var/nw_strip.$name.o build/var/nw_lane.$name.o build/var/nw_trace.o build/var/nw_check.o build/var/nw_trace_dev.o build/var/nw_scan.o -o ../libgsa_$name.so
 done
