@@ -40,6 +40,14 @@ def load_pair(R, C):
     return Y, X, sd.matrix("blosum62"), src
 
 
+def full_kernel_name():
+    """Name of the full-fill kernel libgsa launches (gsa_capi.hip: GSA_FULL_KERNEL, GSA_LANE_NS)."""
+    if os.environ.get("GSA_FULL_KERNEL") == "strip":
+        return "gsa::nw_strip_kernel<%s,0> (full)" % os.environ.get("GSA_FULL_NS", "1")
+    ns = os.environ.get("GSA_LANE_NS", "2")
+    return "gsa::nw_lane_kernel<%s> (full, one row per lane)" % (ns if ns in ("1", "2", "3", "4") else "2")
+
+
 def cpu_baseline(Y, X, sub, budget_s=8.0, threads=None):
     """cpu4-mt-diagrow restatement (oracle/, test infrastructure) on a bounded sample."""
     import oracle
@@ -136,7 +144,7 @@ def main():
     if os.path.exists(tfile):
         try:
             tj = json.load(open(tfile))
-            if tj.get("R") == R and tj.get("C") == C:
+            if tj.get("R") == R and tj.get("C") == C and tj.get("kernel") == full_kernel_name():
                 traffic = tj.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
@@ -151,7 +159,7 @@ def main():
                        "parallelism": f"pair-sharded x{world}"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": PEAK_HBM_GBPS, "unit": "GB/s",
                          "frac": round(achieved / PEAK_HBM_GBPS, 4), "traffic": traffic,
-                         "kernel": "gsa::nw_strip_kernel<1,0> (full)", "kernel_ms": round(kern_ms, 4),
+                         "kernel": full_kernel_name(), "kernel_ms": round(kern_ms, 4),
                          "algorithmic_bytes_per_launch": bytes_per_launch},
             "align_costs": costs[:8],
         }

@@ -412,37 +412,15 @@ __device__ __forceinline__ void lane_loader(const StripArgs& a, const LaneLds& L
     {
         bool moved = false;
         // (1) the row above strip 0 (H + g) -> ring 0 elements c + 64, as far as granules of the
-        //     previous super-strip are published (in column order) and ring 0 has room.  The
-        //     poll's own latency paces this loop (no sleep while granules are awaited).
+        //     previous super-strip are published (in column order) and ring 0 has room.  The poll
+        //     is issued first and consumed after the Q work below, which runs under its latency;
+        //     that latency paces this loop (no sleep while granules are awaited).
         if (hnext <= C && hnext + 128 > c0 + kLRing) c0 = flag_ld(F + kFCons);  // ring 0 consumed
-        if (hnext <= C && hnext + 128 <= c0 + kLRing)
-        {
-            const int c = hnext + lane;
-            const bool in = c <= C;
-            int v = 0;
-            bool good;
-            if (tk == 0)
-            {
-                v = c * g + g;  // row 0: H(0, c) = c*g
-                good = in;
-            }
-            else
-            {
-                const unsigned long long q = in ? __hip_atomic_load(gprev + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
-                good = in && (uint32_t)(q >> 32) == a.epoch;
-                v = (int)(uint32_t)q;
-            }
-            const uint64_t badm = __ballot(!good);
-            const int n = badm ? __builtin_ctzll(badm) : 64;
-            if (n > 0)
-            {
-                if (lane < n) lds_st(ring0 + 4u * (uint32_t)((c + 64) & (kLRing - 1)), v);
-                if (tk == 1) link_stamp(a, 2800, hnext, hnext + n, lane);
-                hnext += n;
-                flag_st(F, hnext > C ? kLBig : hnext + 64);
-                moved = true;
-            }
-        }
+        const bool feed = hnext <= C && hnext + 128 <= c0 + kLRing;
+        const int c = hnext + lane;
+        const bool in = c <= C;
+        unsigned long long q = 0ull;
+        if (feed && tk > 0 && in) q = __hip_atomic_load(gprev + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         // (2) Q columns qn .. qn+63: the columns they replace (<= qn+63-kLW) are dead once the
         //     last strip has published elements pl (its next reads start at column pl-55).
         //     Gather the lane's letter column of subT (8 x b128), then 32 straight-line writes.
@@ -469,6 +447,31 @@ __device__ __forceinline__ void lane_loader(const StripArgs& a, const LaneLds& L
             xl = letter(qn + lane);
             flag_st(F + kFXo, qn > C ? kLBig : qn);
             moved = true;
+        }
+        if (feed)
+        {
+            int v = 0;
+            bool good;
+            if (tk == 0)
+            {
+                v = c * g + g;  // row 0: H(0, c) = c*g
+                good = in;
+            }
+            else
+            {
+                good = in && (uint32_t)(q >> 32) == a.epoch;
+                v = (int)(uint32_t)q;
+            }
+            const uint64_t badm = __ballot(!good);
+            const int n = badm ? __builtin_ctzll(badm) : 64;
+            if (n > 0)
+            {
+                if (lane < n) lds_st(ring0 + 4u * (uint32_t)((c + 64) & (kLRing - 1)), v);
+                if (tk == 1) link_stamp(a, 2800, hnext, hnext + n, lane);
+                hnext += n;
+                flag_st(F, hnext > C ? kLBig : hnext + 64);
+                moved = true;
+            }
         }
         const uint64_t now = __builtin_amdgcn_s_memrealtime();
         if (moved)
@@ -586,6 +589,13 @@ __global__ void __launch_bounds__(64 * (NS + 2)) nw_lane_kernel(StripArgs a)
         pa.gran = a.gran + d.granOff;
         pa.granStride = (long long)d.C + 1;
         const int tk = tkg - d.ticketBase;
+        if constexpr (GSA_STAMP)
+        {
+            // stamp builds: the XCD (XCC id) each ticket runs on, dbg[3100 + ticket]
+            unsigned xcc;
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+            if (threadIdx.x == 0 && tkg < 100 && a.dbg) a.dbg[3100 + tkg] = xcc & 0xf;
+        }
         if (threadIdx.x < 16) lds_st(L.flags + 4u * threadIdx.x, 0);  // prog[], cons[]
         if (threadIdx.x < 16) lds_st(L.gfill + 4u * threadIdx.x, a.g);
         if (threadIdx.x == 0) lds_st(L.flags + kFXo, 0);

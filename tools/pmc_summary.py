@@ -1,10 +1,12 @@
-"""Summarise tools/pmc_probe.sh output: per-counter value of the LAST nw_strip dispatch."""
+"""Summarise tools/pmc_probe.sh output: per-counter value of the LAST fill dispatch (kernel name
+containing argv[2], default nw_lane|nw_strip)."""
 import csv, collections, glob, json, sys
 out = {}
+keys = sys.argv[2].split("|") if len(sys.argv) > 2 else ["nw_lane", "nw_strip"]
 for f in sorted(glob.glob(sys.argv[1] + "/p*/run_counter_collection.csv")):
     agg = collections.defaultdict(float)
     for r in csv.DictReader(open(f)):
-        if "nw_strip" in r["Kernel_Name"]:
+        if any(k in r["Kernel_Name"] for k in keys):
             agg[(int(r["Dispatch_Id"]), r["Counter_Name"])] += float(r["Counter_Value"])
     if not agg:
         continue
