@@ -7,7 +7,7 @@
 namespace gsa {
 
 constexpr int kLaneRows = 64;       // rows per lane strip (one wave, one row per lane)
-constexpr int kLaneNSDefault = 2;   // lane strips per workgroup (super-strip = 128 rows)
+constexpr int kLaneNSDefault = 4;   // lane strips per workgroup (super-strip = 256 rows)
 
 // Workgroup LDS bytes for ns lane strips and a substitution alphabet of substsz letters.
 size_t lane_lds_bytes(int ns, int substsz);

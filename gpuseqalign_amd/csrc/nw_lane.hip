@@ -28,8 +28,11 @@
 // into ring w+1, element e = column e - 64; lane 0 of strip w+1 reads them 8 at a time, one
 // block ahead.  Order is kept with LDS progress words (LDS ops of one wave execute in order).
 // Between super-strips (workgroups) the loader moves the last strip's row through 8-byte
-// {epoch, H+g} granules in HBM, as nw_strip.hip does.  The strips store their own output: two
-// dwordx4 per lane per 8-step block (the lane's row, 8 consecutive columns).
+// {epoch, H+g} granules in HBM, as nw_strip.hip does.  The strips store their own output: per
+// 16-step block the lane's 16 values are transposed across lane bits 5 and 4 (16 permlane32/16
+// swaps) so each of the 4 dwordx4 stores writes 16 rows x 64 contiguous bytes.  One row per lane
+// per store cost a memory request per lane; with 3-4 strips per CU those requests slowed every
+// strip and the granule polls queued behind them (profiles/r01_xpose_probe.txt).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -43,12 +46,17 @@ namespace {
 constexpr int kLW = 512;           // Q ring columns (power of 2)
 constexpr int kLQRS = kLW + 32;    // Q row stride in dwords: == 0 mod 32, 32 guard columns
 constexpr int kLRing = 512;        // hand-off ring elements per strip boundary (power of 2)
+// Output transposed across lanes before the stores (1) or one row per lane per store (0)
+#ifndef GSA_LXPOSE
+#define GSA_LXPOSE 1
+#endif
 #ifndef GSA_LBLK
 #define GSA_LBLK 16
 #endif
 constexpr int kLBlk = GSA_LBLK;    // steps per block (8 or 16)
 static_assert(kLBlk == 8 || kLBlk == 16, "block");
 constexpr int kLH = kLBlk / 4;     // halo registers (int4) per block
+static_assert(!GSA_LXPOSE || kLBlk == 16, "transposed stores: 4 chunks per block");
 // Options (experiments): halo read by all lanes (lanes >= 1 read a row of g, no exec branch);
 // progress words read at block start (1) or in mid-block (0)
 #ifndef GSA_LHALO_ALL
@@ -79,16 +87,17 @@ extern __shared__ __attribute__((aligned(16))) char lsm[];
 #define GSA_STAMP 0
 #endif
 // Diagnostic stamps (separate build): s_memrealtime (100 MHz, one clock for all XCDs) at the start of every 8th block of the strip
-// waves of tickets 0..7, dbg[(ticket * 2 + w) * 160 + b / 8] (w < 2, b < 1280).
+// waves of the first 16 strips, dbg[(ticket * NS + w) * 160 + b / 8] (b < 1280).
+template <int NS>
 __device__ __forceinline__ void lstamp(const StripArgs& a, int tk, int w, int b, int k, int lane)
 {
     if constexpr (GSA_STAMP)
     {
-        if (k == 0 && tk < 8 && w < 2 && (b & 7) == 0 && b < 1280 && lane == 0 && a.dbg)
+        if (k == 0 && tk * NS + w < 16 && (b & 7) == 0 && b < 1280 && lane == 0 && a.dbg)
         {
             unsigned long long t;
             asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-            a.dbg[(size_t)(tk * 2 + w) * 160 + (b >> 3)] = t;
+            a.dbg[(size_t)(tk * NS + w) * 160 + (b >> 3)] = t;
         }
     }
 }
@@ -198,6 +207,10 @@ __device__ __forceinline__ void lane_strip(const StripArgs& a, const LaneLds& L,
     const gptr<int> obase = G(a.score) + (size_t)(r0 + srow) * (size_t)a.ld;
     const int rlim = a.R - r0 - srow;  // row 8i + srow of the strip is in the matrix iff 8i <= rlim
     const gptr<int> orow = G(a.score) + (size_t)(live ? r : 0) * (size_t)a.ld;  // GSA_LSTAGE 0
+    // GSA_LXPOSE: column 16b of row r0 + (lane & 15), shifted by the lane's chunk 4 * (lane >> 4)
+    // and the row's skew; + 16k(ld-1) for row r0 + 16k + (lane & 15)
+    const gptr<int> xbase = G(a.score) + (ptrdiff_t)(r0 + (lane & 15)) * a.ld + 4 * (lane >> 4) - (lane & 15);
+    const uint32_t xoff = (uint32_t)(lane & 15) * (uint32_t)(a.ld - 1) + 4u * (uint32_t)(lane >> 4);  // from row r0 + 16k
 
     // block b prefetches block b+1's inputs (ring elements < B(b+1)+64+B, Q columns < B(b+1)+B,
     // B = kLBlk) and writes ring elements Bb .. Bb+B-1
@@ -252,7 +265,7 @@ __device__ __forceinline__ void lane_strip(const StripArgs& a, const LaneLds& L,
 
     auto block = [&](int b, int (&qc)[kLBlk], int (&qn)[kLBlk], int4v (&hc)[kLH], int4v (&hn)[kLH], auto rampT) {
         constexpr bool RAMP = decltype(rampT)::value;
-        lstamp(a, tk, w, b, 0, lane);
+        lstamp<NS>(a, tk, w, b, 0, lane);
         {
             const int pin = __builtin_amdgcn_readfirstlane(rpin), pco = __builtin_amdgcn_readfirstlane(rpco);
             const int pxo = (w == 0) ? __builtin_amdgcn_readfirstlane(rpxo) : 0;
@@ -272,7 +285,7 @@ __device__ __forceinline__ void lane_strip(const StripArgs& a, const LaneLds& L,
             if constexpr (!(GSA_LKNOB & 8)) halo_load(b + 1, hn);
             if constexpr (!(GSA_LKNOB & 64)) flag_st(c_in, kLBlk * b + 64 + 2 * kLBlk);
         }
-        lstamp(a, tk, w, b, 1, lane);
+        lstamp<NS>(a, tk, w, b, 1, lane);
         int vals[kLBlk], lt[kLBlk];
 #pragma unroll
         for (int u = 0; u < kLBlk; ++u)
@@ -293,7 +306,7 @@ __device__ __forceinline__ void lane_strip(const StripArgs& a, const LaneLds& L,
                 rpxo = raw_ld(f_xo);
             }
         }
-        lstamp(a, tk, w, b, 2, lane);
+        lstamp<NS>(a, tk, w, b, 2, lane);
         // hand-off: lane 63's H + g of steps Bb-1 .. Bb+B-2 = ring elements Bb .. Bb+B-1 (columns
         // Bb-64 ..); the last strip's ring is drained into granules by the drain wave
         if (!(GSA_LKNOB & 4) && lane == 63)
@@ -312,7 +325,79 @@ __device__ __forceinline__ void lane_strip(const StripArgs& a, const LaneLds& L,
                 lds_st4(sb + 16u * (uint32_t)((kLH * (b & 1) + j) ^ (lane & 7)),
                         int4v {vals[4 * j], vals[4 * j + 1], vals[4 * j + 2], vals[4 * j + 3]});
         }
-        if (!GSA_LSTAGE && !(GSA_LKNOB & 1) && live)
+        if constexpr ((GSA_LKNOB & 1024) != 0)
+        {
+            // timing knob: the same bytes as lane-contiguous stores into the strip's own rows
+            // (64 lanes x 16 B = 1 KB contiguous per instruction); values land in wrong places
+            if (r0 + 63 <= a.R)
+            {
+#pragma unroll
+                for (int j = 0; j < kLH; ++j)
+                {
+                    const size_t off = ((size_t)b * kLBlk * 64 + (size_t)j * 256 + 4u * (uint32_t)lane) % ((size_t)64 * a.ld - 4);
+                    *(gptr<int4a>)(G(a.score) + (size_t)r0 * a.ld + off) = int4a {vals[4 * j], vals[4 * j + 1], vals[4 * j + 2], vals[4 * j + 3]};
+                }
+            }
+        }
+        else if constexpr (GSA_LXPOSE && !GSA_LSTAGE && !(GSA_LKNOB & 1))
+        {
+            // output, transposed in registers: the 4 chunks (4 columns each) of the block are
+            // exchanged across lane bits 5 and 4 (permlane32/16 swaps, 16 per block), so that
+            // store k has lane 16h+n write chunk h of row r0+16k+n: 16 rows x 64 contiguous bytes
+            // per store instead of 64 rows x 16 bytes (one row per lane pays one memory request
+            // per lane, and the CU's requests are shared by its strips and the granule polls)
+            int t[kLBlk];
+#pragma unroll
+            for (int e = 0; e < kLBlk; ++e) t[e] = vals[e];
+#pragma unroll
+            for (int k = 0; k < 2; ++k)
+#pragma unroll
+                for (int d = 0; d < 4; ++d)
+                {
+                    const auto sw = __builtin_amdgcn_permlane32_swap(t[4 * k + d], t[4 * (k + 2) + d], false, false);
+                    t[4 * k + d] = sw[0];
+                    t[4 * (k + 2) + d] = sw[1];
+                }
+#pragma unroll
+            for (int k = 0; k < 4; k += 2)
+#pragma unroll
+                for (int d = 0; d < 4; ++d)
+                {
+                    const auto sw = __builtin_amdgcn_permlane16_swap(t[4 * k + d], t[4 * (k + 1) + d], false, false);
+                    t[4 * k + d] = sw[0];
+                    t[4 * (k + 1) + d] = sw[1];
+                }
+            if (kLBlk * b - 63 >= 1 && kLBlk * b + kLBlk - 1 <= C && r0 + 63 <= a.R)
+            {
+                // interior block (uniform): every chunk is in the matrix; scalar row bases
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                {
+                    const gptr<int> ub = G(a.score) + ((ptrdiff_t)(r0 + 16 * k) * a.ld - 16 * k + kLBlk * b);
+                    *(gptr<int4a>)(ub + xoff) = int4a {t[4 * k], t[4 * k + 1], t[4 * k + 2], t[4 * k + 3]};
+                }
+            }
+            else
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+            {
+                const int rr = 16 * k + (lane & 15);  // row r0 + rr, columns xc .. xc+3
+                const int xc = kLBlk * b - rr + 4 * (lane >> 4);
+                if (r0 + rr <= a.R)
+                {
+                    const gptr<int> p = xbase + (size_t)k * 16u * (size_t)(a.ld - 1) + kLBlk * b;
+                    if (xc >= 1 && xc + 3 <= C)
+                        *(gptr<int4a>)p = int4a {t[4 * k], t[4 * k + 1], t[4 * k + 2], t[4 * k + 3]};
+                    else if (xc + 3 >= 1 && xc <= C)
+                    {
+#pragma unroll
+                        for (int e = 0; e < 4; ++e)
+                            if (xc + e >= 1 && xc + e <= C) p[e] = t[4 * k + e];
+                    }
+                }
+            }
+        }
+        else if (!GSA_LSTAGE && !(GSA_LKNOB & 1) && live)
         {
             // output: this lane's row, columns Bb-l .. Bb-l+B-1 (column 0 is the header kernel's)
             const int c0 = kLBlk * b - lane;
@@ -329,7 +414,7 @@ __device__ __forceinline__ void lane_strip(const StripArgs& a, const LaneLds& L,
                     if (c0 + e >= 1 && c0 + e <= C) orow[c0 + e] = vals[e];
             }
         }
-        lstamp(a, tk, w, b, 3, lane);
+        lstamp<NS>(a, tk, w, b, 3, lane);
         return true;
     };
 

@@ -25,11 +25,11 @@ allst = np.frombuffer(buf, dtype=np.uint64).astype(np.int64)
 xcc = allst[3100:3200]
 st = allst[:2560].reshape(16, 160)
 ns = int(os.environ.get("GSA_LANE_NS", "2"))
-rows = [(tk, w) for tk in range(8) for w in range(min(ns, 2))]
+rows = [(sidx // ns, sidx % ns) for sidx in range(16)]
 t0 = st[st > 0].min()
 prev = None
 for tk, w in rows:
-    s = st[tk * 2 + w]
+    s = st[tk * ns + w]
     ok = s > 0
     if ok.sum() < 4:
         continue
@@ -47,8 +47,8 @@ for tk, w in rows:
 # every 8 blocks; the others are interpolated.
 drain = allst[2560:2760]
 feed = allst[2800:3000]
-prod = st[0 * 2 + min(ns - 1, 1)].astype(float)
-cons = st[1 * 2 + 0].astype(float)
+prod = st[ns - 1].astype(float)
+cons = st[ns].astype(float)
 def at(s, blk):
     i = blk / 8.0
     lo = int(np.floor(i))
