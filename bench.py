@@ -44,8 +44,8 @@ def full_kernel_name():
     """Name of the full-fill kernel libgsa launches (gsa_capi.hip: GSA_FULL_KERNEL, GSA_LANE_NS)."""
     if os.environ.get("GSA_FULL_KERNEL") == "strip":
         return "gsa::nw_strip_kernel<%s,0> (full)" % os.environ.get("GSA_FULL_NS", "1")
-    ns = os.environ.get("GSA_LANE_NS", "2")
-    return "gsa::nw_lane_kernel<%s> (full, one row per lane)" % (ns if ns in ("1", "2", "3", "4") else "2")
+    ns = os.environ.get("GSA_LANE_NS", "4")   # nw_lane.h: kLaneNSDefault
+    return "gsa::nw_lane_kernel<%s> (full, one row per lane)" % (ns if ns in ("1", "2", "3", "4") else "4")
 
 
 def cpu_baseline(Y, X, sub, budget_s=8.0, threads=None):
