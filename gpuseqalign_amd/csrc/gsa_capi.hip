@@ -151,7 +151,7 @@ int full_ns()
 
 // Full fills run on the one-row-per-lane kernel (nw_lane.hip) unless GSA_FULL_KERNEL=strip
 // selects the 4-rows-per-lane strip kernel (nw_strip.hip); GSA_LANE_NS = lane strips per
-// workgroup (1..4).  Both read per launch.
+// workgroup (1..4, 6, 8).  Both read per launch.
 bool full_lane_enabled()
 {
     const char* e = std::getenv("GSA_FULL_KERNEL");
@@ -162,7 +162,7 @@ int lane_ns()
 {
     const char* e = std::getenv("GSA_LANE_NS");
     const int v = e ? std::atoi(e) : gsa::kLaneNSDefault;
-    return (v >= 1 && v <= 4) ? v : gsa::kLaneNSDefault;
+    return ((v >= 1 && v <= 4) || v == 6 || v == 8) ? v : gsa::kLaneNSDefault;
 }
 
 // Ring mode for full fills (nw_strip.hip): the output leaves the strip CUs through L2-resident

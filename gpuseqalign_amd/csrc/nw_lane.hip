@@ -20,7 +20,7 @@
 // steps) are forced to the border r*g.
 //
 // Substitution scores come from a per-workgroup COLUMN profile Q[y][c] = s(y, X[c]) - g
-// (int32, a ring of kLW columns, rows kLQRS = kLW + 32 dwords apart): lane l reads Q[y_l][t-l],
+// (int32, a ring of kLW = 512 or 1024 columns, rows kLW + 32 dwords apart): lane l reads Q[y_l][t-l],
 // bank (t - l) mod 32 whatever the row letters (conflict-free), at base + immediate offsets,
 // so a step spends no VALU on addressing.  The loader wave builds Q from seqX and the table.
 //
@@ -43,8 +43,10 @@
 namespace gsa {
 namespace {
 
-constexpr int kLW = 512;           // Q ring columns (power of 2)
-constexpr int kLQRS = kLW + 32;    // Q row stride in dwords: == 0 mod 32, 32 guard columns
+// Q ring columns (power of 2).  The ring spans the first strip's frontier back to the last
+// strip's oldest column, ~(NS - 1) hops of ~100 columns + the lane skew: 1024 from NS = 5 on.
+__host__ __device__ constexpr int lane_lw(int ns) { return ns >= 5 ? 1024 : 512; }
+__host__ __device__ constexpr int lane_qrs(int ns) { return lane_lw(ns) + 32; }  // Q row stride in dwords: == 0 mod 32, 32 guard columns
 constexpr int kLRing = 512;        // hand-off ring elements per strip boundary (power of 2)
 // Output transposed across lanes before the stores (1) or one row per lane per store (0)
 #ifndef GSA_LXPOSE
@@ -65,6 +67,13 @@ static_assert(!GSA_LXPOSE || kLBlk == 16, "transposed stores: 4 chunks per block
 #ifndef GSA_LFLAG_EARLY
 #define GSA_LFLAG_EARLY 0
 #endif
+// Halo (row above, lane 0) of block b read at the start of block b (1) or prefetched during
+// block b-1 (0).  The prefetch makes each strip wait one more block (16 steps) for the strip
+// above on every hop.
+#ifndef GSA_LHALO_JIT
+#define GSA_LHALO_JIT 1
+#endif
+constexpr int kLHaloAhead = GSA_LHALO_JIT ? 1 : 2;  // halo blocks needed at block start
 // Output path: 0 = every lane stores its own row (dwordx4 stores, 64 rows per store
 // instruction); 1 = rows staged in LDS and stored row-contiguously (8 lanes x 16 B per row),
 // one pair of blocks behind.  1 measured slower on one strip (114 vs 78 cycles/step) with no
@@ -87,17 +96,21 @@ extern __shared__ __attribute__((aligned(16))) char lsm[];
 #define GSA_STAMP 0
 #endif
 // Diagnostic stamps (separate build): s_memrealtime (100 MHz, one clock for all XCDs) at the start of every 8th block of the strip
-// waves of the first 16 strips, dbg[(ticket * NS + w) * 160 + b / 8] (b < 1280).
+// waves of strips s = 0, S, .., 15S (S = GSA_STAMP_STRIDE), dbg[(s / S) * 160 + b / 8] (b < 1280).
+#ifndef GSA_STAMP_STRIDE
+#define GSA_STAMP_STRIDE 1
+#endif
 template <int NS>
 __device__ __forceinline__ void lstamp(const StripArgs& a, int tk, int w, int b, int k, int lane)
 {
     if constexpr (GSA_STAMP)
     {
-        if (k == 0 && tk * NS + w < 16 && (b & 7) == 0 && b < 1280 && lane == 0 && a.dbg)
+        const int s = tk * NS + w;
+        if (k == 0 && s % GSA_STAMP_STRIDE == 0 && s < 16 * GSA_STAMP_STRIDE && (b & 7) == 0 && b < 1280 && lane == 0 && a.dbg)
         {
             unsigned long long t;
             asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-            a.dbg[(size_t)(tk * NS + w) * 160 + (b >> 3)] = t;
+            a.dbg[(size_t)(s / GSA_STAMP_STRIDE) * 160 + (b >> 3)] = t;
         }
     }
 }
@@ -152,8 +165,8 @@ __device__ __forceinline__ void link_stamp(const StripArgs& a, int base, int old
 
 // LDS: Q profile, transposed substitution table subT[x][y] = s(y, x) - g (rows of kLSubRow
 // dwords, so one lane gathers 4 row letters per ds_read_b128), NS+1 hand-off rings, progress words.
-// flags: prog[i] @ 4i (ring i holds elements < prog[i]), cons[i] @ 32+4i (ring i's reader no
-// longer needs elements < cons[i]), xo @ 64 (Q holds columns < xo), ticket @ 68.
+// flags: prog[i] @ 4i (ring i holds elements < prog[i]), cons[i] @ 64+4i (ring i's reader no
+// longer needs elements < cons[i]), xo @ 128 (Q holds columns < xo), ticket @ 132.
 struct LaneLds
 {
     uint32_t q, stage, sub, ring, gfill, flags;
@@ -162,14 +175,14 @@ struct LaneLds
 // chunks, chunk index XOR row & 7: conflict-free for the strip's row writes and its row-segment
 // read-back, 8 lanes per row)
 constexpr uint32_t kStageBytes = 64u * 128u;
-constexpr uint32_t kFCons = 32, kFXo = 64, kFTicket = 68;
+constexpr uint32_t kFCons = 64, kFXo = 128, kFTicket = 132;  // prog/cons: NS + 1 <= 16 words each
 constexpr int kLSubRow = 36;  // dwords per subT row: 32 letters + 4 (16-byte aligned rows)
 
 __host__ __device__ inline LaneLds lane_layout(int ns, int substsz)
 {
     LaneLds L;
     L.q = 0;
-    L.stage = (uint32_t)substsz * kLQRS * 4u;
+    L.stage = (uint32_t)substsz * lane_qrs(ns) * 4u;
     L.sub = L.stage + (GSA_LSTAGE ? (uint32_t)ns * 2u * kStageBytes : 0u);
     L.ring = L.sub + (uint32_t)substsz * kLSubRow * 4u;
     L.gfill = L.ring + (uint32_t)(ns + 1) * kLRing * 4u;  // 16 x g: the "halo" of lanes >= 1
@@ -190,6 +203,7 @@ __device__ __forceinline__ void lane_strip(const StripArgs& a, const LaneLds& L,
     const bool live = r <= a.R;
     int y = live ? G(a.seqY)[r] : 0;
     y = ((unsigned)y < (unsigned)a.substsz) ? y : 0;
+    constexpr int kLW = lane_lw(NS), kLQRS = lane_qrs(NS);
     const uint32_t qrow = L.q + (uint32_t)y * (kLQRS * 4u);
     const uint32_t ring_in = L.ring + (uint32_t)w * (kLRing * 4u);
     const uint32_t ring_out = L.ring + (uint32_t)(w + 1) * (kLRing * 4u);
@@ -216,7 +230,7 @@ __device__ __forceinline__ void lane_strip(const StripArgs& a, const LaneLds& L,
     // B = kLBlk) and writes ring elements Bb .. Bb+B-1
     auto ok = [&](int pin, int pco, int pxo, int b) {
         if constexpr ((GSA_LKNOB & 2) != 0) return true;
-        return pin >= kLBlk * b + 64 + 2 * kLBlk && pco >= kLBlk * b + kLBlk - kLRing && (w != 0 || pxo >= kLBlk * b + 2 * kLBlk);
+        return pin >= kLBlk * b + 64 + kLHaloAhead * kLBlk && pco >= kLBlk * b + kLBlk - kLRing && (w != 0 || pxo >= kLBlk * b + 2 * kLBlk);
     };
     auto spin = [&](int b) {
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
@@ -258,7 +272,7 @@ __device__ __forceinline__ void lane_strip(const StripArgs& a, const LaneLds& L,
         const uint32_t qb = qrow + 4u * (uint32_t)((-lane) & (kLW - 1));
 #pragma unroll
         for (int u = 0; u < kLBlk; ++u) qA[u] = lds_ld(qb + 4u * u);
-        halo_load(0, hA);
+        if constexpr (!GSA_LHALO_JIT) halo_load(0, hA);
     }
     int H = rg, U = rg;
     int rpin = 0, rpco = 0, rpxo = 0;  // progress words read in the previous block, checked now
@@ -277,13 +291,14 @@ __device__ __forceinline__ void lane_strip(const StripArgs& a, const LaneLds& L,
             rpco = raw_ld(c_out);
             rpxo = raw_ld(f_xo);
         }
-        // prefetch block b+1: Q of columns B(b+1)-l .. +B-1, halo
+        if constexpr (GSA_LHALO_JIT && !(GSA_LKNOB & 8)) halo_load(b, hc);
+        // prefetch block b+1: Q of columns B(b+1)-l .. +B-1 (and the halo unless GSA_LHALO_JIT)
         {
             const uint32_t qb = qrow + 4u * (uint32_t)((kLBlk * b + kLBlk - lane) & (kLW - 1));
 #pragma unroll
             for (int u = 0; u < kLBlk; ++u) qn[u] = (GSA_LKNOB & 16) ? qc[u] ^ 1 : lds_ld(qb + 4u * u);
-            if constexpr (!(GSA_LKNOB & 8)) halo_load(b + 1, hn);
-            if constexpr (!(GSA_LKNOB & 64)) flag_st(c_in, kLBlk * b + 64 + 2 * kLBlk);
+            if constexpr (!(GSA_LKNOB & 8) && !GSA_LHALO_JIT) halo_load(b + 1, hn);
+            if constexpr (!(GSA_LKNOB & 64)) flag_st(c_in, kLBlk * b + 64 + kLHaloAhead * kLBlk);
         }
         lstamp<NS>(a, tk, w, b, 1, lane);
         int vals[kLBlk], lt[kLBlk];
@@ -481,6 +496,7 @@ template <int NS>
 __device__ __forceinline__ void lane_loader(const StripArgs& a, const LaneLds& L, int tk, int lane)
 {
     const int C = a.C, g = a.g;
+    constexpr int kLW = lane_lw(NS), kLQRS = lane_qrs(NS);
     const uint32_t F = L.flags;
     const uint32_t ring0 = L.ring;
     const gptr<const unsigned long long> gprev = G((const unsigned long long*)a.gran) + (size_t)(tk > 0 ? tk - 1 : 0) * a.granStride;
@@ -681,7 +697,7 @@ __global__ void __launch_bounds__(64 * (NS + 2)) nw_lane_kernel(StripArgs a)
             asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
             if (threadIdx.x == 0 && tkg < 100 && a.dbg) a.dbg[3100 + tkg] = xcc & 0xf;
         }
-        if (threadIdx.x < 16) lds_st(L.flags + 4u * threadIdx.x, 0);  // prog[], cons[]
+        if (threadIdx.x < 32) lds_st(L.flags + 4u * threadIdx.x, 0);  // prog[], cons[]
         if (threadIdx.x < 16) lds_st(L.gfill + 4u * threadIdx.x, a.g);
         if (threadIdx.x == 0) lds_st(L.flags + kFXo, 0);
         __syncthreads();
@@ -722,7 +738,7 @@ hipError_t launch_lane(const StripArgs& a, int grid, hipStream_t stream)
 
 size_t lane_lds_bytes(int ns, int substsz)
 {
-    return (size_t)lane_layout(ns, substsz).flags + 128;
+    return (size_t)lane_layout(ns, substsz).flags + 256;
 }
 
 hipError_t launch_lane_fill(const StripArgs& a, int ns, int grid, hipStream_t stream)
@@ -730,6 +746,8 @@ hipError_t launch_lane_fill(const StripArgs& a, int ns, int grid, hipStream_t st
     if (ns == 1) return launch_lane<1>(a, grid, stream);
     if (ns == 3) return launch_lane<3>(a, grid, stream);
     if (ns == 4) return launch_lane<4>(a, grid, stream);
+    if (ns == 6) return launch_lane<6>(a, grid, stream);
+    if (ns == 8) return launch_lane<8>(a, grid, stream);
     return launch_lane<2>(a, grid, stream);
 }
 

@@ -25,11 +25,12 @@ allst = np.frombuffer(buf, dtype=np.uint64).astype(np.int64)
 xcc = allst[3100:3200]
 st = allst[:2560].reshape(16, 160)
 ns = int(os.environ.get("GSA_LANE_NS", "2"))
-rows = [(sidx // ns, sidx % ns) for sidx in range(16)]
+stride = int(os.environ.get("STRIDE", "1"))  # the stamp build's GSA_STAMP_STRIDE
+rows = [(sidx * stride // ns, sidx * stride % ns) for sidx in range(16)]
 t0 = st[st > 0].min()
 prev = None
-for tk, w in rows:
-    s = st[tk * ns + w]
+for i, (tk, w) in enumerate(rows):
+    s = st[i]
     ok = s > 0
     if ok.sum() < 4:
         continue
@@ -45,6 +46,8 @@ for tk, w in rows:
 # link ticket 0 -> 1.  Column 64k is written by the producer (ticket 0's last strip) in block
 # 4k+4 and computed by the consumer (ticket 1, strip 0) in block 4k.  Block starts are stamped
 # every 8 blocks; the others are interpolated.
+if stride != 1:
+    sys.exit(0)
 drain = allst[2560:2760]
 feed = allst[2800:3000]
 prod = st[ns - 1].astype(float)
