@@ -509,6 +509,8 @@ __device__ __forceinline__ void lane_loader(const StripArgs& a, const LaneLds& L
     int xl = letter(lane);
     int pl = 0, c0 = 0;  // progress words, re-read only when their cached values block
     uint64_t last = __builtin_amdgcn_s_memrealtime();
+    int npoll = 0;       // stamp builds: polls of ticket 1 (issue / return times, dbg[4000 + 3k])
+    uint64_t tpoll = 0;
     while (qn <= C || hnext <= C)
     {
         bool moved = false;
@@ -521,6 +523,8 @@ __device__ __forceinline__ void lane_loader(const StripArgs& a, const LaneLds& L
         const int c = hnext + lane;
         const bool in = c <= C;
         unsigned long long q = 0ull;
+        if constexpr (GSA_STAMP)
+            if (feed && tk == 1) tpoll = __builtin_amdgcn_s_memrealtime();
         if (feed && tk > 0 && in) q = __hip_atomic_load(gprev + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         // (2) Q columns qn .. qn+63: the columns they replace (<= qn+63-kLW) are dead once the
         //     last strip has published elements pl (its next reads start at column pl-55).
@@ -565,6 +569,18 @@ __device__ __forceinline__ void lane_loader(const StripArgs& a, const LaneLds& L
             }
             const uint64_t badm = __ballot(!good);
             const int n = badm ? __builtin_ctzll(badm) : 64;
+            if constexpr (GSA_STAMP)
+            {
+                if (tk == 1 && npoll < 1000 && lane == 0 && a.dbg)
+                {
+                    unsigned long long t;
+                    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+                    a.dbg[4000 + 3 * npoll] = tpoll;
+                    a.dbg[4001 + 3 * npoll] = t;
+                    a.dbg[4002 + 3 * npoll] = (unsigned long long)(hnext + n);
+                }
+                ++npoll;
+            }
             if (n > 0)
             {
                 if (lane < n) lds_st(ring0 + 4u * (uint32_t)((c + 64) & (kLRing - 1)), v);
@@ -606,6 +622,7 @@ __device__ __forceinline__ void lane_drain(const StripArgs& a, const LaneLds& L,
     }
     const gptr<unsigned long long> gout = G(a.gran) + (size_t)tk * a.granStride;
     int dnext = 0;  // next column to drain
+    int ndr = 0;    // stamp builds: drain stores
     uint64_t last = __builtin_amdgcn_s_memrealtime();
     while (dnext <= C)
     {
@@ -620,6 +637,18 @@ __device__ __forceinline__ void lane_drain(const StripArgs& a, const LaneLds& L,
                                    __HIP_MEMORY_SCOPE_AGENT);
             }
             if (tk == 0) link_stamp(a, 2560, dnext, min(dnext + 64, avail), lane);
+            if constexpr (GSA_STAMP)
+            {
+                // stamp builds: drain stores of ticket 0 (time, columns < value), dbg[8000 + 2m]
+                if (tk == 0 && lane == 0 && a.dbg && ndr < 2000)
+                {
+                    unsigned long long t;
+                    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+                    a.dbg[8000 + 2 * ndr] = t;
+                    a.dbg[8001 + 2 * ndr] = (unsigned long long)min(dnext + 64, avail);
+                }
+                ++ndr;
+            }
             dnext = min(dnext + 64, avail);
             flag_st(F + kFCons + 4u * NS, dnext > C ? kLBig : dnext + 64);
             last = __builtin_amdgcn_s_memrealtime();
