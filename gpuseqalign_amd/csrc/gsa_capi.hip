@@ -359,26 +359,49 @@ int enqueue_batch(gsa_ctx* ctx, int mode, int npairs, const gsa_pair_dev* pairs,
         gran += (long long)d.nTickets * ((long long)d.Cp + 1);
         if (tickets > (1ll << 30)) return GSA_ERROR_INVALID_VALUE;
     }
+    // batch schedule (more than one pair): round-robin over the pairs, longest first, so the
+    // resident workgroups run the first tickets of every pair side by side instead of one pair's
+    // chain of dependent tickets; ticket j of a pair stays behind its ticket j-1
+    std::vector<int> sched;
+    const char* order = std::getenv("GSA_BATCH_ORDER");  // "pair": pair-major (comparisons)
+    if (npairs > 1 && !(order && std::strcmp(order, "pair") == 0))
+    {
+        std::vector<int> ord((size_t)npairs);
+        for (int p = 0; p < npairs; ++p) ord[(size_t)p] = p;
+        std::stable_sort(ord.begin(), ord.end(), [&](int x, int y) { return hd[(size_t)x].nTickets > hd[(size_t)y].nTickets; });
+        sched.reserve(2 * (size_t)tickets);
+        for (int j = 0; j < hd[(size_t)ord[0]].nTickets; ++j)
+            for (int p : ord)
+            {
+                if (hd[(size_t)p].nTickets <= j) break;
+                sched.push_back(p);
+                sched.push_back(j);
+            }
+    }
+    // descriptors, then the schedule, in one device buffer (units of PairDesc)
+    const size_t schedUnits = (sched.size() * sizeof(int) + sizeof(gsa::PairDesc) - 1) / sizeof(gsa::PairDesc);
+    const size_t units = (size_t)npairs + schedUnits;
     hipError_t e = hipSetDevice(ctx->device);
     if (e != hipSuccess) return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
-    int s = ensure_desc(ctx, (size_t)npairs);
+    int s = ensure_desc(ctx, units);
     if (s != GSA_SUCCESS) return s;
     // stage the descriptors in a pinned slot and copy them in stream order
     const int slot = ctx->stage_next;
     ctx->stage_next = (slot + 1) % gsa_ctx::kStage;
     if (ctx->stage_used[slot] && (e = hipEventSynchronize(ctx->stage_ev[slot])) != hipSuccess)
         return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
-    if (ctx->stage_cap[slot] < (size_t)npairs)
+    if (ctx->stage_cap[slot] < units)
     {
         if (ctx->stage[slot]) (void)hipHostFree(ctx->stage[slot]);
         ctx->stage[slot] = nullptr;
         ctx->stage_cap[slot] = 0;
-        if ((e = hipHostMalloc((void**)&ctx->stage[slot], (size_t)npairs * sizeof(gsa::PairDesc))) != hipSuccess)
+        if ((e = hipHostMalloc((void**)&ctx->stage[slot], units * sizeof(gsa::PairDesc))) != hipSuccess)
             return fail(ctx, e, GSA_ERROR_MEMORY_ALLOCATION);
-        ctx->stage_cap[slot] = (size_t)npairs;
+        ctx->stage_cap[slot] = units;
     }
     std::memcpy(ctx->stage[slot], hd.data(), (size_t)npairs * sizeof(gsa::PairDesc));
-    e = hipMemcpyAsync(ctx->desc, ctx->stage[slot], (size_t)npairs * sizeof(gsa::PairDesc), hipMemcpyHostToDevice, st);
+    if (!sched.empty()) std::memcpy(ctx->stage[slot] + npairs, sched.data(), sched.size() * sizeof(int));
+    e = hipMemcpyAsync(ctx->desc, ctx->stage[slot], units * sizeof(gsa::PairDesc), hipMemcpyHostToDevice, st);
     if (e == hipSuccess) e = hipEventRecord(ctx->stage_ev[slot], st);
     if (e != hipSuccess) return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
     ctx->stage_used[slot] = true;
@@ -386,6 +409,7 @@ int enqueue_batch(gsa_ctx* ctx, int mode, int npairs, const gsa_pair_dev* pairs,
     a.pairs = ctx->desc;
     a.nPairs = npairs;
     a.nTicketsTotal = (int)tickets;
+    a.sched = sched.empty() ? nullptr : (const int*)(ctx->desc + npairs);
     e = gsa::launch_headers(a, mode, maxWork, st);
     if (e != hipSuccess) return fail(ctx, e, GSA_ERROR_KERNEL_FAILURE);
     if (tickets == 0) return GSA_SUCCESS;

@@ -697,15 +697,25 @@ __global__ void __launch_bounds__(64 * (NS + 2)) nw_lane_kernel(StripArgs a)
         __syncthreads();
         const int tkg = __builtin_amdgcn_readfirstlane(lds_ld(L.flags + kFTicket));
         if (tkg >= a.nTicketsTotal) break;
-        // pair of this ticket: last descriptor with ticketBase <= tkg (binary search, uniform)
-        int lo = 0, hi = a.nPairs - 1;
-        while (lo < hi)
+        // pair of this ticket: the batch schedule, or the last descriptor with ticketBase <= tkg
+        // (binary search, uniform)
+        int lo = 0, tks = -1;
+        if (a.sched)
         {
-            const int mid = (lo + hi + 1) >> 1;
-            if (__builtin_amdgcn_readfirstlane(G(a.pairs)[mid].ticketBase) <= tkg)
-                lo = mid;
-            else
-                hi = mid - 1;
+            lo = __builtin_amdgcn_readfirstlane(G(a.sched)[2 * tkg]);
+            tks = __builtin_amdgcn_readfirstlane(G(a.sched)[2 * tkg + 1]);
+        }
+        else
+        {
+            int hi = a.nPairs - 1;
+            while (lo < hi)
+            {
+                const int mid = (lo + hi + 1) >> 1;
+                if (__builtin_amdgcn_readfirstlane(G(a.pairs)[mid].ticketBase) <= tkg)
+                    lo = mid;
+                else
+                    hi = mid - 1;
+            }
         }
         const PairDesc d = lane_desc(a.pairs + lo);
         StripArgs pa = a;
@@ -718,7 +728,7 @@ __global__ void __launch_bounds__(64 * (NS + 2)) nw_lane_kernel(StripArgs a)
         pa.ld = d.ld;
         pa.gran = a.gran + d.granOff;
         pa.granStride = (long long)d.C + 1;
-        const int tk = tkg - d.ticketBase;
+        const int tk = (tks >= 0) ? tks : tkg - d.ticketBase;
         if constexpr (GSA_STAMP)
         {
             // stamp builds: the XCD (XCC id) each ticket runs on, dbg[3100 + ticket]

@@ -89,6 +89,9 @@ struct StripArgs
     const PairDesc* pairs;
     int nPairs;
     int nTicketsTotal;
+    // batch schedule: {pair, ticket within the pair} of every global ticket, round-robin over the
+    // pairs (null: pair-major by ticketBase).  Ticket j of a pair always follows its ticket j-1.
+    const int* sched;
 };
 
 size_t strip_lds_bytes(int ns, int substsz, int mode);

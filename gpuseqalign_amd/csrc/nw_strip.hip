@@ -1240,15 +1240,25 @@ __global__ void __launch_bounds__(64 * (MODE == kModeFullRing ? kRingWaves : NS 
             break;
         }
         prevTk = tkg;
-        // pair of this ticket: last descriptor with ticketBase <= tkg (binary search, uniform)
-        int lo = 0, hi = a.nPairs - 1;
-        while (lo < hi)
+        // pair of this ticket: the batch schedule, or the last descriptor with ticketBase <= tkg
+        // (binary search, uniform)
+        int lo = 0, tks = -1;
+        if (a.sched)
         {
-            const int mid = (lo + hi + 1) >> 1;
-            if (__builtin_amdgcn_readfirstlane(a.pairs[mid].ticketBase) <= tkg)
-                lo = mid;
-            else
-                hi = mid - 1;
+            lo = __builtin_amdgcn_readfirstlane(a.sched[2 * tkg]);
+            tks = __builtin_amdgcn_readfirstlane(a.sched[2 * tkg + 1]);
+        }
+        else
+        {
+            int hi = a.nPairs - 1;
+            while (lo < hi)
+            {
+                const int mid = (lo + hi + 1) >> 1;
+                if (__builtin_amdgcn_readfirstlane(a.pairs[mid].ticketBase) <= tkg)
+                    lo = mid;
+                else
+                    hi = mid - 1;
+            }
         }
         const PairDesc d = load_desc(a.pairs + lo);
         StripArgs pa = a;
@@ -1270,7 +1280,7 @@ __global__ void __launch_bounds__(64 * (MODE == kModeFullRing ? kRingWaves : NS 
         pa.ringBase = ringBase;
         pa.ringTicket = tkg;
         ringBase += (d.Cp + 64 + kBLK - 1) / kBLK;
-        const int tk = tkg - d.ticketBase;
+        const int tk = (tks >= 0) ? tks : tkg - d.ticketBase;
         if constexpr (GSA_STAMP)
         {
             // diagnostic builds: the per-pair arguments as this workgroup sees them
