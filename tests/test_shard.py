@@ -128,12 +128,16 @@ def test_gpu_batch_matches_oracle(golden, mode):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("order", ["round-robin", "pair"])
 @pytest.mark.parametrize("mode", ["full", "sparse"])
-def test_batched_launch_equals_single_fills(engine, golden, mode):
-    """Every output word of a batched launch equals the single-pair fill of the same pair."""
+def test_batched_launch_equals_single_fills(engine, golden, mode, order, monkeypatch):
+    """Every output word of a batched launch equals the single-pair fill of the same pair, with
+    the tickets scheduled round-robin over the pairs (default) or pair-major (GSA_BATCH_ORDER)."""
+    monkeypatch.setenv("GSA_BATCH_ORDER", order)
     import torch
     import gpuseqalign_amd as gsa
-    pairs = _pairs()
+    # + pairs of 2-5 tickets (256-row super-strips), so the schedule interleaves their chains
+    pairs = _pairs() + [random_pair(r, c, 5 * r + c) for r, c in [(700, 300), (1030, 200), (600, 900), (300, 77)]]
     dev = torch.device("cuda:0")
     ts = torch.from_numpy(golden.blosum62).to(dev)
     ins = [(torch.from_numpy(y).to(dev), torch.from_numpy(x).to(dev)) for y, x in pairs]
