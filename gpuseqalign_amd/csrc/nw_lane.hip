@@ -67,6 +67,14 @@ static_assert(!GSA_LXPOSE || kLBlk == 16, "transposed stores: 4 chunks per block
 #ifndef GSA_LFLAG_EARLY
 #define GSA_LFLAG_EARLY 0
 #endif
+// Lane 63's hand-off writes: all lanes write (the others into a per-strip sink), so the 4
+// ds_write_b128 need no exec mask (1), or lane 63 alone (0)
+#ifndef GSA_LHAND_ALL
+#define GSA_LHAND_ALL 1
+#endif
+#ifndef GSA_LSCHED_BARRIER
+#define GSA_LSCHED_BARRIER 0
+#endif
 // Halo (row above, lane 0) of block b read at the start of block b (1) or prefetched during
 // block b-1 (0).  The prefetch makes each strip wait one more block (16 steps) for the strip
 // above on every hop.
@@ -169,7 +177,7 @@ __device__ __forceinline__ void link_stamp(const StripArgs& a, int base, int old
 // longer needs elements < cons[i]), xo @ 128 (Q holds columns < xo), ticket @ 132.
 struct LaneLds
 {
-    uint32_t q, stage, sub, ring, gfill, flags;
+    uint32_t q, stage, sub, ring, gfill, sink, flags;
 };
 // Output stage per strip: 2 buffers of [64 rows][32 steps] int32 (128-byte rows of 8 16-byte
 // chunks, chunk index XOR row & 7: conflict-free for the strip's row writes and its row-segment
@@ -186,7 +194,8 @@ __host__ __device__ inline LaneLds lane_layout(int ns, int substsz)
     L.sub = L.stage + (GSA_LSTAGE ? (uint32_t)ns * 2u * kStageBytes : 0u);
     L.ring = L.sub + (uint32_t)substsz * kLSubRow * 4u;
     L.gfill = L.ring + (uint32_t)(ns + 1) * kLRing * 4u;  // 16 x g: the "halo" of lanes >= 1
-    L.flags = L.gfill + 64u;
+    L.sink = L.gfill + 64u;                                // GSA_LHAND_ALL: lanes 0..62's hand-off writes
+    L.flags = L.sink + (GSA_LHAND_ALL ? (uint32_t)ns * 1024u : 0u);
     return L;
 }
 
@@ -210,6 +219,7 @@ __device__ __forceinline__ void lane_strip(const StripArgs& a, const LaneLds& L,
     const uint32_t f_in = L.flags + 4u * w, f_out = L.flags + 4u * (w + 1);
     const uint32_t c_in = L.flags + kFCons + 4u * w, c_out = L.flags + kFCons + 4u * (w + 1);
     const uint32_t f_xo = L.flags + kFXo;
+    const uint32_t hsink = L.sink + (uint32_t)w * 1024u + 16u * (uint32_t)lane;
     const int NB = (C + 65 + kLBlk - 1) / kLBlk;  // lane 63 reaches step C+64 (element of column C)
     const int rg = r * g;
     // output stage: this lane writes its row; for the read-back lane = 8 * srow + sq reads rows
@@ -322,9 +332,20 @@ __device__ __forceinline__ void lane_strip(const StripArgs& a, const LaneLds& L,
             }
         }
         lstamp<NS>(a, tk, w, b, 2, lane);
+#if GSA_LSCHED_BARRIER
+        __builtin_amdgcn_sched_barrier(0);  // keep the hand-off writes and swaps out of the step chain
+#endif
         // hand-off: lane 63's H + g of steps Bb-1 .. Bb+B-2 = ring elements Bb .. Bb+B-1 (columns
         // Bb-64 ..); the last strip's ring is drained into granules by the drain wave
-        if (!(GSA_LKNOB & 4) && lane == 63)
+        if constexpr (GSA_LHAND_ALL && !(GSA_LKNOB & 4))
+        {
+            // every lane writes (no exec mask): lane 63 into the ring, the others into a sink
+            const uint32_t eb = (lane == 63) ? ring_out + 4u * (uint32_t)((kLBlk * b) & (kLRing - 1)) : hsink;
+#pragma unroll
+            for (int j = 0; j < kLH; ++j)
+                lds_st4(eb + ((lane == 63) ? 16u * j : 0u), int4v {lt[4 * j], lt[4 * j + 1], lt[4 * j + 2], lt[4 * j + 3]});
+        }
+        else if (!(GSA_LKNOB & 4) && lane == 63)
         {
             const uint32_t eb = ring_out + 4u * (uint32_t)((kLBlk * b) & (kLRing - 1));
 #pragma unroll
