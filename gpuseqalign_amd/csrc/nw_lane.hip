@@ -75,6 +75,12 @@ static_assert(!GSA_LXPOSE || kLBlk == 16, "transposed stores: 4 chunks per block
 #ifndef GSA_LSCHED_BARRIER
 #define GSA_LSCHED_BARRIER 0
 #endif
+// interior output stores as buffer stores (scalar base + 32-bit lane offsets) (1) or global
+// stores with 64-bit lane addresses (0, default: 1 measured 3.6 % slower on one 10k pair and
+// ~5 % faster on a 64-pair batch, profiles/r01_lane_knobs_handoff.txt)
+#ifndef GSA_LBUFST
+#define GSA_LBUFST 0
+#endif
 // Halo (row above, lane 0) of block b read at the start of block b (1) or prefetched during
 // block b-1 (0).  The prefetch makes each strip wait one more block (16 steps) for the strip
 // above on every hop.
@@ -126,6 +132,7 @@ __device__ __forceinline__ void lstamp(const StripArgs& a, int tk, int w, int b,
 
 typedef int int4v __attribute__((ext_vector_type(4)));
 typedef int int4a __attribute__((ext_vector_type(4), aligned(4)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 template <typename T>
 using gptr = __attribute__((address_space(1))) T*;
 template <typename T>
@@ -235,6 +242,9 @@ __device__ __forceinline__ void lane_strip(const StripArgs& a, const LaneLds& L,
     // and the row's skew; + 16k(ld-1) for row r0 + 16k + (lane & 15)
     const gptr<int> xbase = G(a.score) + (ptrdiff_t)(r0 + (lane & 15)) * a.ld + 4 * (lane >> 4) - (lane & 15);
     const uint32_t xoff = (uint32_t)(lane & 15) * (uint32_t)(a.ld - 1) + 4u * (uint32_t)(lane >> 4);  // from row r0 + 16k
+    // GSA_LBUFST: the strip's 64 rows as one buffer resource (interior blocks only: r0 + 63 <= R)
+    const __amdgpu_buffer_rsrc_t srsrc = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(a.score + (size_t)r0 * (size_t)a.ld), 0, (int)min((long long)64 * a.ld * 4, 0x7fffffffll), 0x00020000);
 
     // block b prefetches block b+1's inputs (ring elements < B(b+1)+64+B, Q columns < B(b+1)+B,
     // B = kLBlk) and writes ring elements Bb .. Bb+B-1
@@ -409,8 +419,18 @@ __device__ __forceinline__ void lane_strip(const StripArgs& a, const LaneLds& L,
 #pragma unroll
                 for (int k = 0; k < 4; ++k)
                 {
-                    const gptr<int> ub = G(a.score) + ((ptrdiff_t)(r0 + 16 * k) * a.ld - 16 * k + kLBlk * b);
-                    *(gptr<int4a>)(ub + xoff) = int4a {t[4 * k], t[4 * k + 1], t[4 * k + 2], t[4 * k + 3]};
+                    if constexpr (GSA_LBUFST)
+                    {
+                        // buffer store: per-lane 32-bit offset + scalar offset, no 64-bit VALU address
+                        const int so = 4 * (int)((long long)(16 * k) * a.ld - 16 * k + kLBlk * b);
+                        __builtin_amdgcn_raw_buffer_store_b128(u32x4 {(unsigned)t[4 * k], (unsigned)t[4 * k + 1], (unsigned)t[4 * k + 2], (unsigned)t[4 * k + 3]},
+                                                               srsrc, (int)(4u * xoff), so, 0);
+                    }
+                    else
+                    {
+                        const gptr<int> ub = G(a.score) + ((ptrdiff_t)(r0 + 16 * k) * a.ld - 16 * k + kLBlk * b);
+                        *(gptr<int4a>)(ub + xoff) = int4a {t[4 * k], t[4 * k + 1], t[4 * k + 2], t[4 * k + 3]};
+                    }
                 }
             }
             else
