@@ -162,12 +162,13 @@ def test_full_ring_mode_shapes(engine, golden, R, C, monkeypatch):
     assert np.array_equal(r.score, S) and r.align_cost == cost
 
 
-@pytest.mark.parametrize("kernel,ns", [("lane", "1"), ("lane", "2"), ("lane", "3"), ("lane", "4"), ("strip", "1")])
+@pytest.mark.parametrize("kernel,ns", [("lane", "1"), ("lane", "2"), ("lane", "3"), ("lane", "4"), ("lane", "6"), ("lane", "8"),
+                                       ("strip", "1")])
 @pytest.mark.parametrize("R,C", [(1, 1), (1, 700), (63, 64), (64, 65), (127, 300), (128, 128), (129, 1029),
                                  (300, 1), (385, 1500), (1100, 2222), (2049, 777)])
 def test_full_kernels_shapes(engine, golden, kernel, ns, R, C, monkeypatch):
     """Both full-fill kernels (GSA_FULL_KERNEL, read per launch): the one-row-per-lane kernel
-    (nw_lane.hip) with 1..4 strips per workgroup (GSA_LANE_NS: every super-strip boundary,
+    (nw_lane.hip) with 1..4, 6, 8 strips per workgroup (GSA_LANE_NS: every super-strip boundary,
     ragged last strips, rows beyond R) and the 4-rows-per-lane strip kernel, every word."""
     monkeypatch.setenv("GSA_FULL_KERNEL", kernel)
     monkeypatch.setenv("GSA_LANE_NS", ns)
@@ -177,9 +178,10 @@ def test_full_kernels_shapes(engine, golden, kernel, ns, R, C, monkeypatch):
     assert np.array_equal(r.score, S) and r.align_cost == cost
 
 
-@pytest.mark.parametrize("ns", ["1", "2", "3"])
+@pytest.mark.parametrize("ns", ["1", "2", "3", "4", "8"])
 def test_lane_kernel_wide_pair(engine, golden, ns, monkeypatch):
-    """Columns past the 512-column profile ring and its guard copies, several super-strips."""
+    """Columns past the profile ring (512 columns, 1024 from NS = 5) and its guard copies,
+    several super-strips."""
     monkeypatch.setenv("GSA_FULL_KERNEL", "lane")
     monkeypatch.setenv("GSA_LANE_NS", ns)
     Y, X = related_pair(5000, 17)
