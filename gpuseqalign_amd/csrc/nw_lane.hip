@@ -77,8 +77,8 @@ static_assert(!GSA_LXPOSE || kLBlk == 16, "transposed stores: 4 chunks per block
 #define GSA_LSCHED_BARRIER 0
 #endif
 // interior output stores as buffer stores (scalar base + 32-bit lane offsets) (1) or global
-// stores with 64-bit lane addresses (0, default: 1 measured 3.6 % slower on one 10k pair and
-// ~5 % faster on a 64-pair batch, profiles/r01_lane_knobs_handoff.txt)
+// stores with 64-bit lane addresses (0, default: 1 measured 1-4 % slower on one 10k pair and
+// ~9 % slower on a 64-pair batch in same-box A/B runs, profiles/r01_lane_knobs_handoff.txt)
 #ifndef GSA_LBUFST
 #define GSA_LBUFST 0
 #endif
