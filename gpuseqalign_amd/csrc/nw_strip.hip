@@ -213,6 +213,13 @@ __device__ __forceinline__ uint32_t ring_elem(int c)
 #ifndef GSA_MIDPUB
 #define GSA_MIDPUB 0
 #endif
+// Smith-Waterman mode: the halo of block b is read at the start of block b (1) instead of in the
+// middle of block b-1 (0): one halo buffer live instead of two, so the SW strip no longer spills
+// (256 VGPRs + 36 spilled -> 235).  50k SW 7.64 -> 7.01 ms; NW-AG, which spilled 8, got slower
+// (5.13 -> 5.46 ms) and keeps the prefetch (profiles/r01_score_jit.txt)
+#ifndef GSA_SCORE_JIT
+#define GSA_SCORE_JIT 1
+#endif
 // Timing-experiment knobs (separate builds only; any set bit makes results WRONG):
 // 1 no halo loads, 2 no progress words / waits, 4 no sparse captures, 8 no hand-off writes,
 // 16 no output staging writes (full), 32 store waves store nothing (full), 64 store waves
@@ -638,7 +645,7 @@ __device__ __forceinline__ void strip_wave(const StripArgs& a, const Lds& L, int
             }
             if (GSA_MIDPUB && q == 1) flag_st(F + kFProg + 4 * (w + 1), 16 * b + 8 - 63);  // steps < 16b+8 handed off
             if (q == GSA_HOP_Q - 1) rpin = raw_ld(fin);
-            if (q == GSA_HOP_Q)
+            if (q == GSA_HOP_Q && !(GSA_SCORE_JIT && MODE == kModeScoreSW))
             {
                 // halo of the next block, once the row above covers it
                 int pn = __builtin_amdgcn_readfirstlane(rpin);
@@ -722,6 +729,31 @@ __device__ __forceinline__ void strip_wave(const StripArgs& a, const Lds& L, int
         if (!start_ok(pco, pxo, psto, b))
         {
             if (!wait_start(pco, pxo, psto, b)) return false;
+        }
+        if constexpr (GSA_SCORE_JIT && MODE == kModeScoreSW)
+        {
+            // halo of this block (block 0's came with the prologue), once the row above covers it
+            if (b > 0)
+            {
+                int pn = __builtin_amdgcn_readfirstlane(rpin);
+                if (!pin_ok(pn, b - 1))
+                {
+                    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+                    while (!pin_ok(pn = flag_ld(fin), b - 1))
+                    {
+                        __builtin_amdgcn_s_sleep(1);
+                        if (__builtin_amdgcn_s_memrealtime() - t0 > kSpinLimit || err_set(a))
+                        {
+                            atomicOr(a.err, 1u);
+                            return false;
+                        }
+                    }
+                }
+                cbar();
+                hv_load(b, hvcur);
+                hvf_load(b, hfcur);
+                flag_st(F + kFCons + 4 * w, 16 * b - 3);  // after the halo reads (in order)
+            }
         }
         cbar();
         stamp(a, tk, w, b, 1, lane);
