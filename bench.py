@@ -1,15 +1,27 @@
 #!/usr/bin/env python3
 """bench.py -- NW-LG fill throughput (GCUPS) on MI355X, driver contract.
 
-Workload (BASELINE.json configs[1]): one NW-LG 10k x 10k pair per rank and step, full int32
-score matrix written to HBM (the plain/gpu3-6 representation), blosum62, gapo -11.  Inputs
-(sequences, substitution table) are resident in HBM before the timed region; the output
-matrix buffer is preallocated.  N>1: one process per GPU (torch.distributed, RCCL), pairs
-shard across ranks with no data-path collective (weak scaling); RCCL only broadcasts the
-substitution table and gathers per-pair align_costs.
+Headline workload (BASELINE.json north_star / configs[2]): ONE NW-LG
+100k x 100k related pair per rank and step -- seqX = splitmix64 seed 100, seqY = seqX with 15 %
+substitutions + 2 % indels (seed 101) -- filled into the sparse tile-header (mlsp) form
+(tileHrowMat / tileHcolMat, tileBx 256), blosum62, gapo -11.  The path replaced is
+NwAlign_Gpu9_Mlsp_DiagDiagDiag (nwalign_gpu9_mlsp_diagdiagdiag.cu:368-722) timed as align.calc
+(benchmark.cpp:473).  Inputs (sequences, substitution table) are resident in HBM before the
+timed region; the header buffers are preallocated.  The fill's align_cost is checked against
+the oracle golden tests/golden/config3_100k.json (data; no oracle code runs here).
 
-Prints ONE JSON line (rank 0) with roofline (HBM-write bound, 4 B/cell) and cpu_baseline
-(oracle restatement of cpu4-mt-diagrow, test infrastructure, timed on this host).
+N>1: one process per GPU (torch.distributed, RCCL); every rank fills its own config-3 pair
+(weak scaling, no data-path collective: RCCL only broadcasts the substitution table and
+gathers align_costs / max-reduces the time).  The `config4` field is BASELINE configs[3]: the
+512 pairs of 18-22k (shard.synthetic_batch, seeds 1000+k) LPT-sharded over the N ranks
+(strong scaling: fixed total work), each rank's share in one persistent batched launch, every
+align_cost checked against tests/golden/config4_pairs.json.  `fill_10k_full` is configs[1].
+
+Roofline: the sparse fill does not stream HBM (headers are ~0.07 B/cell); it is bound by int32
+VALU issue.  Algorithmic work = 5 int ops per cell (3 add + 2 max, UpdateScore,
+nwalign_cpu1_st_row.cpp:4-10); peak = 256 CU x 4 SIMD x 32 lanes x 2.4 GHz = 78.6 T lane-ops/s
+(MI355X_MICROARCH.md: SIMD-32, wave64 VALU over 2 cycles).  cpu_baseline: the oracle's
+cpu4-mt-diagrow restatement (test infrastructure) on a bounded 20k x 20k prefix of the same pair.
 """
 import argparse
 import json
@@ -23,46 +35,159 @@ sys.path.insert(0, ROOT)
 import numpy as np
 
 METRIC = "GCUPS (DP cell updates/s) + peak HBM GB/s, NW-LG N×M fill, 1/2/4/8 MI355X"
-PEAK_HBM_GBPS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+PEAK_HBM_GBPS = 8000.0                       # MI355X_MICROARCH.md chip table (spec)
+PEAK_VALU_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12  # int32 lane-ops/s, 78.6 T
+OPS_PER_CELL = 5
+TILE_BX = 256
 
 
-def load_pair(R, C):
+def subst_blosum62():
+    from gpuseqalign_amd import formats as F
+    return F.read_subst_json(os.path.join(ROOT, "tests", "golden", "resrc", "subst.json")).matrix("blosum62")
+
+
+def config3_pair():
+    from gpuseqalign_amd import formats as F
+    X = F.synthetic_seq(100000, 100)
+    return F.mutate_seq(X, 101), X
+
+
+def config2_pair():
     from gpuseqalign_amd import formats as F
     res = os.path.join(ROOT, "tests", "golden", "resrc")
     sd = F.read_subst_json(os.path.join(res, "subst.json"))
-    if (R, C) == (10000, 10000):
-        seqs = F.read_fasta(os.path.join(res, "seq_generated.fa"), sd.letter_map)
-        Y, X = F.pair_arrays(F.parse_pair_line("len12124[:10000] len15390[:10000]", seqs), seqs)
-        src = "reference resrc/seq_generated.fa: len12124[:10000] x len15390[:10000]"
-    else:
-        Y, X = F.synthetic_seq(R, 2), F.synthetic_seq(C, 3)
-        src = "splitmix64 synthetic (seeds 2, 3)"
-    return Y, X, sd.matrix("blosum62"), src
+    seqs = F.read_fasta(os.path.join(res, "seq_generated.fa"), sd.letter_map)
+    return F.pair_arrays(F.parse_pair_line("len12124[:10000] len15390[:10000]", seqs), seqs)
 
 
-def full_kernel_name():
-    """Name of the full-fill kernel libgsa launches (gsa_capi.hip: GSA_FULL_KERNEL, GSA_LANE_NS)."""
-    if os.environ.get("GSA_FULL_KERNEL") == "strip":
-        return "gsa::nw_strip_kernel<%s,0> (full)" % os.environ.get("GSA_FULL_NS", "1")
-    ns = os.environ.get("GSA_LANE_NS", "4")   # nw_lane.h: kLaneNSDefault
-    return "gsa::nw_lane_kernel<%s> (full, one row per lane)" % (ns if ns in ("1", "2", "3", "4") else "4")
+def load_golden(name):
+    p = os.path.join(ROOT, "tests", "golden", name)
+    if not os.path.exists(p):
+        return None
+    with open(p) as f:
+        return json.load(f)
 
 
-def cpu_baseline(Y, X, sub, budget_s=8.0, threads=None):
-    """cpu4-mt-diagrow restatement (oracle/, test infrastructure) on a bounded sample."""
+def sparse_kernel_name():
+    return "gsa::nw_strip_kernel<4,1> (sparse, 4 rows per lane)"
+
+
+def cpu_topology():
+    """(usable logical CPUs, physical cores among them, cgroup CPU quota or None, nproc)."""
+    try:
+        cpus = sorted(os.sched_getaffinity(0))
+    except AttributeError:
+        cpus = list(range(os.cpu_count() or 1))
+    phys = set()
+    try:
+        cur = {}
+        with open("/proc/cpuinfo") as f:
+            for line in f.read().split("\n\n"):
+                d = dict(kv.split(":", 1) for kv in line.split("\n") if ":" in kv)
+                d = {k.strip(): v.strip() for k, v in d.items()}
+                if "processor" in d and int(d["processor"]) in cpus:
+                    phys.add((d.get("physical id", "0"), d.get("core id", d["processor"])))
+        del cur
+    except Exception:
+        phys = set()
+    quota = None
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(p)
+    except Exception:
+        pass
+    return len(cpus), (len(phys) or len(cpus)), quota, os.cpu_count()
+
+
+def cpu_baseline(Y, X, sub, budget_s=20.0, n=20000):
+    """cpu4-mt-diagrow restatement (oracle/, test infrastructure) on a bounded n x n prefix of the
+    headline pair, timed at the physical core count and at the process's CPU share."""
     import oracle
-    threads = threads or min(16, os.cpu_count() or 1)
-    t_end = time.time() + budget_s
-    reps, cells, t_tot = 0, 0, 0.0
-    while time.time() < t_end or reps == 0:
+    ncpu, phys, quota, nproc = cpu_topology()
+    share = max(1, min(phys, int(quota) if quota else phys))
+    Yp, Xp = Y[:n + 1], X[:n + 1]
+    cands = sorted({phys, share, min(16, phys)}, reverse=True)
+    runs = {}
+    for th in cands:
+        t_end = time.time() + budget_s / len(cands)
+        reps, t_tot = 0, 0.0
+        while time.time() < t_end or reps == 0:
+            t0 = time.perf_counter()
+            oracle.fill_full_mt(Yp, Xp, sub, -11, blocksz=256, nthreads=th)
+            t_tot += time.perf_counter() - t0
+            reps += 1
+        runs[th] = (n * n * reps / t_tot / 1e9, reps, t_tot)
+    best = max(runs, key=lambda t: runs[t][0])
+    v, reps, t_tot = runs[best]
+    return {"value": round(v, 4), "unit": "GCUPS", "cores": best, "kind": "port",
+            "sample": (f"oracle cpu4-mt-diagrow restatement (blocksz 256, OpenMP), {reps} fills of the "
+                       f"{n}x{n} prefix of the config-3 pair in {t_tot:.1f} s at {best} threads; host: nproc "
+                       f"{nproc}, {ncpu} CPUs in the affinity mask, {phys} physical cores, cgroup quota "
+                       f"{quota if quota else 'none'}; threads tried: "
+                       + ", ".join(f"{t}: {runs[t][0]:.3f} GCUPS" for t in sorted(runs)))}
+
+
+def timed_steps(step, stream, dev, steps, warmup, world, eng):
+    import torch
+    import torch.distributed as dist
+    with torch.cuda.stream(stream):
+        for _ in range(warmup):
+            step()
+        eng.sync(stream.cuda_stream)
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
-        oracle.fill_full_mt(Y, X, sub, -11, blocksz=256, nthreads=threads)
-        t_tot += time.perf_counter() - t0
-        reps += 1
-        cells += (len(Y) - 1) * (len(X) - 1)
-    return {"value": round(cells / t_tot / 1e9, 4), "unit": "GCUPS", "cores": threads, "kind": "port",
-            "sample": f"oracle cpu4-mt-diagrow restatement (blocksz 256, {threads} OpenMP threads), "
-                      f"{reps} fills of the same {len(Y) - 1}x{len(X) - 1} pair, {t_tot:.1f} s"}
+        for e0, e1 in evs:
+            e0.record(stream)
+            step()
+            e1.record(stream)
+        eng.sync(stream.cuda_stream)
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+    kern_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs]))
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed, kern_ms
+
+
+def traffic_for(name, R, C, kernel):
+    p = os.path.join(ROOT, "profiles", name)
+    if not os.path.exists(p):
+        return None
+    try:
+        tj = json.load(open(p))
+        if tj.get("R") == R and tj.get("C") == C and tj.get("kernel") == kernel:
+            return tj.get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+    return None
+
+
+def bench_config4(world, rank, local, n_pairs):
+    """BASELINE configs[3]: n_pairs pairs of 18-22k, LPT-sharded over the ranks (strong scaling)."""
+    from gpuseqalign_amd import shard
+    pairs = shard.synthetic_batch(n_pairs, 18000, 22000, seed0=1000)
+    sub = subst_blosum62()
+    rep = shard.shard_align(pairs, sub, -11, shard.gpu_batch_align(device=local, mode="sparse", tileBx=TILE_BX),
+                            device=f"cuda:{local}" if world > 1 else None)
+    gold = load_golden("config4_pairs.json")
+    costs = [r.align_cost for r in rep.results]
+    match = None
+    if gold is not None and gold.get("n_pairs", 0) >= n_pairs:
+        match = sum(int(a == b) for a, b in zip(costs, gold["align_cost"][:n_pairs]))
+    return {"workload": f"BASELINE configs[3]: {n_pairs} NW-LG pairs, lengths uniform in [18000, 22000] "
+                        f"(seeds 1000+k), sparse tile headers (tileBx {TILE_BX}), LPT-sharded over {world} rank(s), "
+                        "one persistent batched launch per rank",
+            "value": round(rep.gcups, 2), "unit": "GCUPS", "scaling": "strong", "cells": rep.cells,
+            "seconds": round(rep.elapsed_s, 4), "pairs": n_pairs,
+            "pairs_matching_golden": match, "golden_pairs": None if gold is None else gold.get("n_pairs")}
 
 
 def main():
@@ -70,10 +195,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--R", type=int, default=10000)
-    ap.add_argument("--C", type=int, default=10000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-budget", type=float, default=8.0)
+    ap.add_argument("--cpu-budget", type=float, default=20.0)
+    ap.add_argument("--config4-pairs", type=int, default=512, help="0 = skip the configs[3] batch field")
+    ap.add_argument("--no-10k", action="store_true", help="skip the configs[1] full-matrix field")
     a = ap.parse_args()
 
     import torch
@@ -88,87 +213,110 @@ def main():
         dist.init_process_group("nccl")
     dev = torch.device("cuda", local if world > 1 else 0)
 
-    Y, X, sub, src = load_pair(a.R, a.C)
-    R, C = len(Y) - 1, len(X) - 1
-    tY = torch.from_numpy(Y).to(dev)
-    tX = torch.from_numpy(X).to(dev)
+    sub = subst_blosum62()
     tS = torch.from_numpy(sub).to(dev)
     if world > 1:
         dist.broadcast(tS, src=0)  # substitution table from rank 0 (RCCL over xGMI)
-    score = torch.empty((R + 1) * (C + 1), dtype=torch.int32, device=dev)
     eng = gsa.Engine(dev.index)
     stream = torch.cuda.Stream(device=dev)
     sh = stream.cuda_stream
 
-    def step():
-        eng.fill_full_dev(tY.data_ptr(), R + 1, tX.data_ptr(), C + 1, tS.data_ptr(), 25, -11, score.data_ptr(), sh)
+    # ---- headline: config 3, 100k x 100k sparse fill --------------------------------------
+    Y, X = config3_pair()
+    R, C = len(Y) - 1, len(X) - 1
+    tY, tX = torch.from_numpy(Y).to(dev), torch.from_numpy(X).to(dev)
+    geom = gsa.sparse_geometry(R + 1, C + 1, TILE_BX)
+    hrow = torch.empty(geom.hrowElems, dtype=torch.int32, device=dev)
+    hcol = torch.empty(geom.hcolElems, dtype=torch.int32, device=dev)
 
-    with torch.cuda.stream(stream):
-        for _ in range(a.warmup):
-            step()
-        eng.sync(sh)
-        # per-launch kernel time (HIP events on the launch stream)
-        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize(dev)
-        t0 = time.perf_counter()
-        for e0, e1 in evs:
-            e0.record(stream)
-            step()
-            e1.record(stream)
-        eng.sync(sh)
-        torch.cuda.synchronize(dev)
-        if world > 1:
-            dist.barrier()
-        elapsed = time.perf_counter() - t0
-    kern_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs]))
+    def step():
+        eng.fill_sparse_dev(tY.data_ptr(), R + 1, tX.data_ptr(), C + 1, tS.data_ptr(), 25, -11, TILE_BX,
+                            hrow.data_ptr(), hcol.data_ptr(), sh)
+
+    elapsed, kern_ms = timed_steps(step, stream, dev, a.steps, a.warmup, world, eng)
+    # align_cost as the reference's mlsp align computes it (recompute of the last tile from its
+    # headers, nwalign_gpu9_mlsp_diagdiagdiag.cu:713-716): only the last tile's headers come back
+    last = geom.tileHdrMatRows * geom.tileHdrMatCols - 1
+    hr = np.zeros(geom.hrowElems, dtype=np.int32)
+    hc = np.zeros(geom.hcolElems, dtype=np.int32)
+    hr[last * geom.tileHrowLen:] = hrow[last * geom.tileHrowLen:].cpu().numpy()
+    hc[last * geom.tileHcolLen:] = hcol[last * geom.tileHcolLen:].cpu().numpy()
+    cost = gsa.sparse_align_cost(gsa.SparseResult(hr, hc, geom, 0, {}), Y, X, sub, -11)
+    del hr, hc
+    costs = [cost]
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        cost = score[-1:].clone()
-        costs = [torch.zeros_like(cost) for _ in range(world)]
-        dist.all_gather(costs, cost)
-        costs = [int(c.item()) for c in costs]
-    else:
-        costs = [int(score[-1].item())]
+        t = torch.tensor([cost], dtype=torch.int64, device=dev)
+        lst = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(lst, t)
+        costs = [int(v.item()) for v in lst]
+    gold = load_golden("config3_100k.json")
+    gold_cost = None if gold is None else gold["pairs"]["related"]["align_cost"]
 
     cells = float(R) * float(C)
-    ms_per_step = elapsed * 1e3 / a.steps
     value = world * cells * a.steps / elapsed / 1e9
-    bytes_per_launch = 4.0 * (R + 1) * (C + 1)
-    achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
-    traffic = None
-    tfile = os.path.join(ROOT, "profiles", "traffic.json")
-    if os.path.exists(tfile):
-        try:
-            tj = json.load(open(tfile))
-            if tj.get("R") == R and tj.get("C") == C and tj.get("kernel") == full_kernel_name():
-                traffic = tj.get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
+    ops_achieved = OPS_PER_CELL * cells / (kern_ms * 1e-3) / 1e12
+    hdr_bytes = 4.0 * (geom.hrowElems + geom.hcolElems)
+    kname = sparse_kernel_name()
+    del hrow, hcol
+    torch.cuda.empty_cache()
+
+    # ---- configs[1]: 10k x 10k full matrix (secondary field) ------------------------------
+    full10k = None
+    if not a.no_10k:
+        Y2, X2 = config2_pair()
+        R2, C2 = len(Y2) - 1, len(X2) - 1
+        tY2, tX2 = torch.from_numpy(Y2).to(dev), torch.from_numpy(X2).to(dev)
+        score = torch.empty((R2 + 1) * (C2 + 1), dtype=torch.int32, device=dev)
+
+        def step2():
+            eng.fill_full_dev(tY2.data_ptr(), R2 + 1, tX2.data_ptr(), C2 + 1, tS.data_ptr(), 25, -11,
+                              score.data_ptr(), sh)
+
+        el2, km2 = timed_steps(step2, stream, dev, a.steps, a.warmup, world, eng)
+        b2 = 4.0 * (R2 + 1) * (C2 + 1)
+        full10k = {"workload": "BASELINE configs[1]: NW-LG len12124[:10000] x len15390[:10000] "
+                               "(resrc/seq_generated.fa), full int32 score matrix in HBM",
+                   "value": round(world * R2 * C2 * a.steps / el2 / 1e9, 2), "unit": "GCUPS",
+                   "ms_per_step": round(el2 * 1e3 / a.steps, 4), "kernel_ms": round(km2, 4),
+                   "kernel": "gsa::nw_lane_kernel<4> (full, one row per lane)",
+                   "hbm_write_GBps": round(b2 / (km2 * 1e-3) / 1e9, 1),
+                   "hbm_frac": round(b2 / (km2 * 1e-3) / 1e9 / PEAK_HBM_GBPS, 4),
+                   "align_cost": int(score[-1].item()), "golden_align_cost": -4922}
+        del score
+        torch.cuda.empty_cache()
+    eng.sync(sh)
+    eng.close()
+
+    # ---- configs[3]: 512 pairs, LPT-sharded (strong scaling field) ------------------------
+    cfg4 = bench_config4(world, rank, local, a.config4_pairs) if a.config4_pairs > 0 else None
 
     if rank == 0:
         out = {
             "metric": METRIC, "value": round(value, 3), "unit": "GCUPS", "n_gpus": world, "steps": a.steps,
-            "warmup": a.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "int32", "data": f"synthetic ({src}); blosum62, gapo -11",
-            "config": {"workload": f"NW-LG {R}x{C} full int32 score matrix in HBM (BASELINE configs[1])",
-                       "R": R, "C": C, "pairs_per_rank": 1, "representation": "full (plain family)",
+            "warmup": a.warmup, "ms_per_step": round(elapsed * 1e3 / a.steps, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "int32",
+            "data": "synthetic (splitmix64: seqX seed 100, seqY = seqX mutated seed 101); blosum62, gapo -11",
+            "config": {"workload": f"BASELINE configs[2]: NW-LG {R}x{C} related pair, sparse tile-header (mlsp) "
+                                   f"fill, tileBx {TILE_BX} x tileBy {geom.tileHcolLen - 1}, headers only in HBM",
+                       "R": R, "C": C, "pairs_per_rank": 1, "representation": "sparse tile headers (mlsp)",
                        "parallelism": f"pair-sharded x{world}"},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": PEAK_HBM_GBPS, "unit": "GB/s",
-                         "frac": round(achieved / PEAK_HBM_GBPS, 4), "traffic": traffic,
-                         "kernel": full_kernel_name(), "kernel_ms": round(kern_ms, 4),
-                         "algorithmic_bytes_per_launch": bytes_per_launch},
-            "align_costs": costs[:8],
+            "roofline": {"bound": "valu", "achieved": round(ops_achieved, 3), "peak": round(PEAK_VALU_TOPS, 2),
+                         "unit": "T int32 lane-ops/s", "frac": round(ops_achieved / PEAK_VALU_TOPS, 4),
+                         "traffic": traffic_for("traffic_config3.json", R, C, kname),
+                         "kernel": kname, "kernel_ms": round(kern_ms, 4), "ops_per_cell": OPS_PER_CELL,
+                         "algorithmic_ops_per_launch": OPS_PER_CELL * cells,
+                         "header_bytes_per_launch": hdr_bytes,
+                         "header_GBps": round(hdr_bytes / (kern_ms * 1e-3) / 1e9, 1),
+                         "hbm_frac": round(hdr_bytes / (kern_ms * 1e-3) / 1e9 / PEAK_HBM_GBPS, 5)},
+            "align_costs": costs[:8], "golden_align_cost": gold_cost,
+            "golden_match": None if gold_cost is None else all(c == gold_cost for c in costs),
+            "fill_10k_full": full10k, "config4": cfg4,
         }
         if not a.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(Y, X, sub, budget_s=a.cpu_budget)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
-    eng.close()
 
 
 if __name__ == "__main__":

@@ -91,6 +91,15 @@ class CheckResult(ctypes.Structure):
         return {"checked": int(self.checked), "mismatches": int(self.mismatches), "first": int(self.first)}
 
 
+class MemStats(ctypes.Structure):
+    """gsa_mem_stats: the reference's NwAlgResult peak-alloc columns (nwalign_shared.cpp:5-25)."""
+    _fields_ = [("glmem_peak_allocs", ctypes.c_int64), ("shmem_peak_allocs", ctypes.c_int64),
+                ("locmem_peak_allocs", ctypes.c_int64), ("regmem_peak_allocs", ctypes.c_int64)]
+
+    def as_dict(self):
+        return {k: int(getattr(self, k)) for k, _ in self._fields_}
+
+
 class ScoreResult(ctypes.Structure):
     """gsa_score_result (include/gsa.h)."""
     _fields_ = [("score", ctypes.c_int32), ("i_end", ctypes.c_int64), ("j_end", ctypes.c_int64),
@@ -114,6 +123,9 @@ SIGNATURES = {
     "gsa_fill_full_dev": (ctypes.c_int, [_vp, _vp, _i32, _vp, _i32, _vp, _i32, _i32, _vp, _vp]),
     "gsa_fill_sparse_dev": (ctypes.c_int, [_vp, _vp, _i32, _vp, _i32, _vp, _i32, _i32, _i32, _vp, _vp, _vp]),
     "gsa_sync": (ctypes.c_int, [_vp, _vp]),
+    "gsa_set_watchdog": (ctypes.c_int, [_vp, _i64]),
+    "gsa_mem_stats_get": (ctypes.c_int, [_vp, ctypes.POINTER(MemStats)]),
+    "gsa_mem_stats_reset": (ctypes.c_int, [_vp]),
     "gsa_fill_full_batch_dev": (ctypes.c_int, [_vp, _i32, ctypes.POINTER(PairDev), _vp, _i32, _i32, _vp]),
     "gsa_fill_sparse_batch_dev": (ctypes.c_int, [_vp, _i32, ctypes.POINTER(PairDev), _vp, _i32, _i32, _i32, _vp]),
     "gsa_align_full": (ctypes.c_int, [_vp, _i32p, _i32, _i32p, _i32, _i32p, _i32, _i32, _i32p, _i32p,
@@ -305,7 +317,21 @@ class Engine:
         self._check(st, "gsa_fill_%s_batch_dev" % mode)
 
     def sync(self, stream: Optional[int] = None):
+        """Wait for `stream`; raises NwError if a hand-off of ANY fill enqueued since the last
+        sync gave up (the error word is sticky until this call clears it)."""
         self._check(lib().gsa_sync(self._h, stream), "gsa_sync")
+
+    def set_watchdog(self, microseconds: int):
+        """No-progress limit of every wait inside later fills (default 1 s)."""
+        self._check(lib().gsa_set_watchdog(self._h, int(microseconds)), "gsa_set_watchdog")
+
+    def mem_stats(self) -> dict:
+        m = MemStats()
+        self._check(lib().gsa_mem_stats_get(self._h, ctypes.byref(m)), "gsa_mem_stats_get")
+        return m.as_dict()
+
+    def reset_mem_stats(self):
+        self._check(lib().gsa_mem_stats_reset(self._h), "gsa_mem_stats_reset")
 
     # -- score-only NW / SW, linear or affine gaps (BASELINE configs[4]) -----------------
     def score(self, seqY, seqX, subst, gapo: int, gape: Optional[int] = None, local: bool = False) -> dict:

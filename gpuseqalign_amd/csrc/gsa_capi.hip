@@ -32,7 +32,10 @@ struct gsa_ctx
     int device = 0;
     int cu_count = 0;
     hipStream_t stream = nullptr;
-    unsigned* ctl = nullptr;  // [0] ticket, [1] error flags (16 B, zeroed per launch)
+    // [0] ticket (zeroed per launch), [1] error flags: sticky across launches, read and cleared
+    // by gsa_sync (or by the synchronous call that reports them)
+    unsigned* ctl = nullptr;
+    unsigned long long spin_ticks = 100000000ull;  // watchdog: 1 s of s_memrealtime (100 MHz)
     unsigned long long* gran = nullptr;
     size_t gran_elems = 0;
     unsigned epoch = 0;
@@ -70,6 +73,7 @@ struct gsa_ctx
     size_t ptflags_cap = 0;
     hipStream_t cstream = nullptr;
     unsigned long long* sctl = nullptr;  // [0] ticket|err, [1] best key, [2] result
+    gsa_mem_stats mem {};  // peak resource use of the fills since creation / gsa_mem_stats_reset
 };
 
 namespace {
@@ -102,7 +106,7 @@ int ensure_dev(gsa_ctx* ctx, int slot, size_t bytes)
     return GSA_SUCCESS;
 }
 
-int ensure_gran(gsa_ctx* ctx, size_t elems)
+int ensure_gran(gsa_ctx* ctx, size_t elems, hipStream_t st)
 {
     if (ctx->gran_elems >= elems && ctx->gran) return GSA_SUCCESS;
     if (ctx->gran) (void)hipFree(ctx->gran);
@@ -110,8 +114,9 @@ int ensure_gran(gsa_ctx* ctx, size_t elems)
     ctx->gran_elems = 0;
     hipError_t e = hipMalloc(&ctx->gran, elems * sizeof(unsigned long long));
     if (e != hipSuccess) return fail(ctx, e, GSA_ERROR_MEMORY_ALLOCATION);
-    // tags must never match a live epoch by accident: clear once per allocation
-    e = hipMemset(ctx->gran, 0, elems * sizeof(unsigned long long));
+    // tags must never match a live epoch by accident: clear once per allocation, in stream order
+    // before the launch that uses it (a non-blocking stream is not ordered behind the null stream)
+    e = hipMemsetAsync(ctx->gran, 0, elems * sizeof(unsigned long long), st);
     if (e != hipSuccess) return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
     ctx->gran_elems = elems;
     return GSA_SUCCESS;
@@ -178,6 +183,42 @@ bool full_ring_enabled()
 // NULL is the HIP null stream, as everywhere in HIP; the host-buffer entry points use the
 // context's own stream explicitly.
 hipStream_t pick_stream(gsa_ctx*, void* stream) { return (hipStream_t)stream; }
+
+// Device bytes this context holds (scratch, hand-off granules, the host entry points' I/O buffers).
+long long held_bytes(const gsa_ctx* c)
+{
+    long long b = 256 + 64 + (long long)c->gran_elems * 8 + (long long)c->desc_cap * (long long)sizeof(gsa::PairDesc) +
+                  (long long)c->tmoves_cap + (long long)c->tdirs_cap * 4 + (long long)c->sbnd_cap * 4 +
+                  (long long)c->ringbuf_cap * 4;
+    for (size_t k : c->dcap) b += (long long)k;
+    return b;
+}
+
+// Fold the footprint of the fill just launched (gsa::g_last_foot) into the context's peaks, as
+// updateNwAlgPeakMemUsage does per launch (nwalign_shared.cpp:5-25).
+void note_launch(gsa_ctx* c)
+{
+    const gsa::LaunchFoot& f = gsa::g_last_foot;
+    c->mem.glmem_peak_allocs = std::max<int64_t>(c->mem.glmem_peak_allocs, held_bytes(c));
+    c->mem.shmem_peak_allocs = std::max<int64_t>(c->mem.shmem_peak_allocs, f.lds_per_wg * f.active_wgs);
+    c->mem.locmem_peak_allocs =
+        std::max<int64_t>(c->mem.locmem_peak_allocs, f.scratch_per_lane * f.threads_per_wg * f.active_wgs);
+    c->mem.regmem_peak_allocs =
+        std::max<int64_t>(c->mem.regmem_peak_allocs, f.regs_per_lane * 4 * f.threads_per_wg * f.active_wgs);
+}
+
+// Read the sticky error word (after the caller's stream sync) and clear it if set.
+hipError_t take_err(gsa_ctx* ctx, hipStream_t st, unsigned* err)
+{
+    hipError_t e = hipMemcpyAsync(err, ctx->ctl + 1, sizeof(unsigned), hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e == hipSuccess && *err != 0)
+    {
+        e = hipMemsetAsync(ctx->ctl + 1, 0, sizeof(unsigned), st);
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
+    }
+    return e;
+}
 
 // Verification launch (nw_check.hip): zero the result words, launch, read them back.
 int run_check(gsa_ctx* ctx, gsa::CheckArgs& a, bool sparse, hipStream_t st, gsa_check_result* out)
@@ -247,7 +288,7 @@ int score_ag_strip(gsa_ctx* ctx, const int32_t* seqY, int64_t R, const int32_t* 
     hipError_t e = hipMemcpyAsync(ctx->desc, &d, sizeof(d), hipMemcpyHostToDevice, st);
     if (e != hipSuccess) return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
     const size_t gran = (size_t)tickets * (size_t)(C + 1);
-    if ((s = ensure_gran(ctx, 2 * gran)) != GSA_SUCCESS) return s;
+    if ((s = ensure_gran(ctx, 2 * gran, st)) != GSA_SUCCESS) return s;
     if (!ctx->sctl && (e = hipMalloc(&ctx->sctl, 64)) != hipSuccess) return fail(ctx, e, GSA_ERROR_MEMORY_ALLOCATION);
     a.pairs = ctx->desc;
     a.nPairs = 1;
@@ -256,27 +297,30 @@ int score_ag_strip(gsa_ctx* ctx, const int32_t* seqY, int64_t R, const int32_t* 
     a.gran2 = ctx->gran + gran;
     a.ticket = ctx->ctl;
     a.err = ctx->ctl + 1;
+    a.spin = ctx->spin_ticks;
     a.agResult = (int*)ctx->sctl;
     a.swBest = ctx->sctl + 1;
     a.idxBits = sw_idx_bits(R, C);
     a.epoch = ++ctx->epoch;
     if (a.epoch == 0) a.epoch = ++ctx->epoch;
-    if ((e = hipMemsetAsync(ctx->ctl, 0, 16, st)) != hipSuccess || (e = hipMemsetAsync(ctx->sctl, 0, 16, st)) != hipSuccess)
+    if ((e = hipMemsetAsync(ctx->ctl, 0, 4, st)) != hipSuccess || (e = hipMemsetAsync(ctx->sctl, 0, 16, st)) != hipSuccess)
         return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
     (void)hipEventRecord(ctx->ev0, st);
     const int grid = std::max(1, std::min((int)tickets, ctx->cu_count));
     if ((e = gsa::launch_strip_fill(a, local ? gsa::kModeScoreSW : gsa::kModeScoreAG, grid, st)) != hipSuccess)
         return fail(ctx, e, GSA_ERROR_KERNEL_FAILURE);
+    note_launch(ctx);
     (void)hipEventRecord(ctx->ev1, st);
     unsigned long long res[2] = {0, 0};
-    unsigned flags[2] = {0, 0};
+    unsigned err = 0;
     if ((e = hipMemcpyAsync(res, ctx->sctl, sizeof(res), hipMemcpyDeviceToHost, st)) != hipSuccess ||
-        (e = hipMemcpyAsync(flags, ctx->ctl, sizeof(flags), hipMemcpyDeviceToHost, st)) != hipSuccess ||
         (e = hipStreamSynchronize(st)) != hipSuccess)
         return fail(ctx, e, GSA_ERROR_KERNEL_FAILURE);
+    if ((e = take_err(ctx, st, &err)) != hipSuccess) return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
     (void)hipEventElapsedTime(&out->calc_kernel_ms, ctx->ev0, ctx->ev1);
-    if (flags[1] & 2u) return GSA_ERROR_INVALID_VALUE;  // a substitution value outside int16 after the shift
-    if (flags[1] != 0) return GSA_ERROR_KERNEL_FAILURE;
+    // a substitution value outside int16 after the shift: the int32 row scan computes it
+    if (err == 2u) return kScoreTooLarge;
+    if (err != 0) return GSA_ERROR_KERNEL_FAILURE;
     if (local)
     {
         if (res[0] & 1u) return kScoreTooLarge;  // a score >= 2^26: the caller takes the row scan
@@ -415,15 +459,16 @@ int enqueue_batch(gsa_ctx* ctx, int mode, int npairs, const gsa_pair_dev* pairs,
     if (tickets == 0) return GSA_SUCCESS;
 
     // granule stride (Cp+1) and base are per pair: the kernel takes them from the descriptor
-    if ((s = ensure_gran(ctx, (size_t)gran)) != GSA_SUCCESS) return s;
+    if ((s = ensure_gran(ctx, (size_t)gran, st)) != GSA_SUCCESS) return s;
     a.gran = ctx->gran;
     a.ticket = ctx->ctl;
     a.err = ctx->ctl + 1;
+    a.spin = ctx->spin_ticks;
     a.dbg = ctx->dbg;
     a.done = done;
     a.epoch = ++ctx->epoch;
     if (a.epoch == 0) a.epoch = ++ctx->epoch;  // 0 is the cleared-tag value
-    e = hipMemsetAsync(ctx->ctl, 0, 16, st);
+    e = hipMemsetAsync(ctx->ctl, 0, 4, st);  // the ticket; the error word stays sticky
     if (e != hipSuccess) return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
     // one pair: one workgroup per CU (its tickets are a chain); a batch: all resident slots
     int grid = (npairs == 1) ? std::max(1, std::min((int)tickets, ctx->cu_count)) : 0;
@@ -459,6 +504,7 @@ int enqueue_batch(gsa_ctx* ctx, int mode, int npairs, const gsa_pair_dev* pairs,
     }
     e = lane ? gsa::launch_lane_fill(a, a.ns, grid, st) : gsa::launch_strip_fill(a, launchMode, grid, st);
     if (e != hipSuccess) return fail(ctx, e, GSA_ERROR_KERNEL_FAILURE);
+    note_launch(ctx);
     return GSA_SUCCESS;
 }
 
@@ -614,12 +660,34 @@ int gsa_fill_sparse_batch_dev(gsa_ctx* ctx, int32_t npairs, const gsa_pair_dev* 
 int gsa_sync(gsa_ctx* ctx, void* stream)
 {
     if (!ctx) return GSA_ERROR_INVALID_VALUE;
-    hipError_t e = hipStreamSynchronize(pick_stream(ctx, stream));
+    const hipStream_t st = pick_stream(ctx, stream);
+    hipError_t e = hipStreamSynchronize(st);
     if (e != hipSuccess) return fail(ctx, e, GSA_ERROR_KERNEL_FAILURE);
-    unsigned flags[2] = {0, 0};
-    e = hipMemcpy(flags, ctx->ctl, sizeof(flags), hipMemcpyDeviceToHost);
-    if (e != hipSuccess) return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
-    if (flags[1] != 0) return GSA_ERROR_KERNEL_FAILURE;  // a hand-off spin gave up
+    unsigned err = 0;
+    if ((e = take_err(ctx, st, &err)) != hipSuccess) return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
+    // a hand-off spin of ANY launch since the last sync gave up (the word is sticky)
+    if (err != 0) return GSA_ERROR_KERNEL_FAILURE;
+    return GSA_SUCCESS;
+}
+
+int gsa_mem_stats_get(const gsa_ctx* ctx, gsa_mem_stats* out)
+{
+    if (!ctx || !out) return GSA_ERROR_INVALID_VALUE;
+    *out = ctx->mem;
+    return GSA_SUCCESS;
+}
+
+int gsa_mem_stats_reset(gsa_ctx* ctx)
+{
+    if (!ctx) return GSA_ERROR_INVALID_VALUE;
+    ctx->mem = gsa_mem_stats {};
+    return GSA_SUCCESS;
+}
+
+int gsa_set_watchdog(gsa_ctx* ctx, int64_t microseconds)
+{
+    if (!ctx || microseconds < 0 || microseconds > 3600ll * 1000000ll) return GSA_ERROR_INVALID_VALUE;
+    ctx->spin_ticks = (unsigned long long)microseconds * 100ull;  // s_memrealtime: 100 MHz
     return GSA_SUCCESS;
 }
 
@@ -853,9 +921,27 @@ int gsa_score_dev(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, const int3
     hipError_t e = hipSetDevice(ctx->device);
     if (e != hipSuccess) return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
     hipStream_t st = pick_stream(ctx, stream);
+    // value ranges: the largest |substitution value| bounds every score and shifted value
+    std::vector<int32_t> sub((size_t)substsz * (size_t)substsz);
+    if ((e = hipMemcpyAsync(sub.data(), subst, sub.size() * 4, hipMemcpyDeviceToHost, st)) != hipSuccess ||
+        (e = hipStreamSynchronize(st)) != hipSuccess)
+        return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
+    long long smax = 1;
+    for (int32_t v : sub) smax = std::max<long long>(smax, v < 0 ? -(long long)v : (long long)v);
+    const long long span = (R + C) * (long long)(-gape) + (long long)(gape - gapo) + smax;
+    // unshifted int32 (row scan): |H| <= smax*min(R,C) + |go| + (R+C)|ge|
+    if (smax * std::min(R, C) + (long long)(-gapo) + (R + C) * (long long)(-gape) >= (1ll << 30))
+        return GSA_ERROR_INVALID_VALUE;
+    const int bits = sw_idx_bits(R, C);
+    const long long scoreBound = std::min<long long>((1ll << 31) - 1, smax * std::min(R, C));
+    const int scoreBits = scoreBound > 0 ? 64 - __builtin_clzll((unsigned long long)scoreBound) : 1;
+    // SW end-cell keys (score << bits | ~index) must fit 64 bits: the row scan packs full scores
+    if (local && bits + scoreBits > 63) return GSA_ERROR_INVALID_VALUE;
     // the strip kernel's SW mode needs go < 0 (cells past C then never tie the maximum) and scores
-    // below 2^26 (packed with the step; it reports larger ones); otherwise the row scan
-    if (!score_scan_forced() && (!local || gapo < 0))
+    // below 2^26 packed with bits index bits (it reports larger ones); both modes keep shifted
+    // values (i+j)*ge apart within int32 with margin; otherwise the row scan
+    const bool stripOk = (!local || (gapo < 0 && bits + 27 <= 63)) && span < (1ll << 28);
+    if (!score_scan_forced() && stripOk)
     {
         s = score_ag_strip(ctx, seqY, R, seqX, C, subst, substsz, gapo, gape, local, out, st);
         if (s != kScoreTooLarge) return s;
@@ -888,6 +974,7 @@ int gsa_score_dev(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, const int3
     a.prog = ctx->sbnd + 2 * bnd;
     a.ticket = (unsigned*)ctx->sctl;
     a.err = (unsigned*)ctx->sctl + 1;
+    a.spin = ctx->spin_ticks;
     a.best = ctx->sctl + 1;
     a.idxBits = sw_idx_bits(R, C);
     a.result = (int*)(ctx->sctl + 2);

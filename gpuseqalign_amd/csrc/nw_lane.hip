@@ -97,7 +97,6 @@ constexpr int kLHaloAhead = GSA_LHALO_JIT ? 1 : 2;  // halo blocks needed at blo
 #define GSA_LSTAGE 0
 #endif
 constexpr int kLBig = 0x3fffffff;  // "everything published"
-constexpr uint64_t kLSpin = 20000000ull;  // 0.2 s of s_memrealtime (100 MHz) without progress
 
 extern __shared__ __attribute__((aligned(16))) char lsm[];
 
@@ -260,7 +259,7 @@ __device__ __forceinline__ void lane_strip(const StripArgs& a, const LaneLds& L,
             const int pin = flag_ld(f_in), pco = flag_ld(c_out), pxo = (w == 0) ? flag_ld(f_xo) : 0;
             if (ok(pin, pco, pxo, b)) return true;
             __builtin_amdgcn_s_sleep(1);
-            if (__builtin_amdgcn_s_memrealtime() - t0 > kLSpin || err_set(a))
+            if (__builtin_amdgcn_s_memrealtime() - t0 > a.spin || err_set(a))
             {
                 atomicOr(a.err, 1u);
                 return false;
@@ -637,7 +636,7 @@ __device__ __forceinline__ void lane_loader(const StripArgs& a, const LaneLds& L
             last = now;
         else
         {
-            if (now - last > kLSpin || err_set(a))
+            if (now - last > a.spin || err_set(a))
             {
                 atomicOr(a.err, 1u);
                 return;
@@ -697,7 +696,7 @@ __device__ __forceinline__ void lane_drain(const StripArgs& a, const LaneLds& L,
         }
         else
         {
-            if (__builtin_amdgcn_s_memrealtime() - last > kLSpin || err_set(a))
+            if (__builtin_amdgcn_s_memrealtime() - last > a.spin || err_set(a))
             {
                 atomicOr(a.err, 1u);
                 return;
@@ -811,6 +810,7 @@ hipError_t launch_lane(const StripArgs& a, int grid, hipStream_t stream)
         if (e != hipSuccess) return e;
         grid = std::max(1, std::min(a.nTicketsTotal, std::max(1, per_cu) * cus));
     }
+    if ((e = record_foot((const void*)kern, lds, 64 * (NS + 2), grid)) != hipSuccess) return e;
     hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * (NS + 2)), lds, stream, a);
     return hipGetLastError();
 }

@@ -19,6 +19,7 @@ struct ScoreArgs
     int* prog;               // (nTR+1) progress words: boundary row b valid for columns < prog[b]
     unsigned* ticket;
     unsigned* err;
+    unsigned long long spin;   // watchdog ticks (100 MHz) without progress
     unsigned long long* best;  // local: max of (score << idxBits | (2^idxBits-1 - row-major index))
     int idxBits;               // local: bits of the row-major index, ceil(log2((R+1)(C+1)))
     int* result;             // global: H[R][C]

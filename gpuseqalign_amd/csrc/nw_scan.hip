@@ -40,7 +40,6 @@ __device__ __forceinline__ gptr<T> G(T* p)
 }
 
 constexpr int kNeg = -(1 << 29);
-constexpr uint64_t kSpin = 20000000ull;  // 0.2 s of s_memrealtime without progress
 
 __device__ __forceinline__ int wave_prefix_max(int v)
 {
@@ -114,7 +113,7 @@ __global__ void __launch_bounds__(64) score_scan_kernel(ScoreArgs a)
                     seen = __builtin_amdgcn_readfirstlane(
                         __hip_atomic_load(G(a.prog) + tk, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT));
                     if (seen >= need) break;
-                    if (__builtin_amdgcn_s_memrealtime() - t0 > kSpin || err_set(a))
+                    if (__builtin_amdgcn_s_memrealtime() - t0 > a.spin || err_set(a))
                     {
                         if (lane == 0) atomicOr(a.err, 1u);
                         return;

@@ -63,7 +63,8 @@ struct StripArgs
     unsigned long long* gran;
     long long granStride;
     unsigned* ticket;
-    unsigned* err;
+    unsigned* err;      // sticky: set by a spin that gave up, cleared by gsa_sync after reading
+    unsigned long long spin;  // watchdog: s_memrealtime ticks (100 MHz) a wait may go without progress
     unsigned epoch;
     unsigned long long* dbg;  // diagnostic builds only (GSA_STAMP): per-wave block time stamps
     // mlsppt: host-mapped per-ticket flags, set to `epoch` once a super-strip's outputs are
@@ -93,6 +94,21 @@ struct StripArgs
     // pairs (null: pair-major by ticketBase).  Ticket j of a pair always follows its ticket j-1.
     const int* sched;
 };
+
+// Resource footprint of the last fill launched from this host thread: what the reference's
+// updateNwAlgPeakMemUsage (nwalign_shared.cpp:5-25) multiplies out -- kernel attributes
+// (hipFuncGetAttributes) and the workgroups resident at once (min(grid, occupancy x CUs)).
+struct LaunchFoot
+{
+    long long lds_per_wg;       // static + dynamic LDS bytes per workgroup
+    long long scratch_per_lane; // private (scratch) bytes per lane
+    long long regs_per_lane;    // VGPRs per lane (numRegs)
+    long long threads_per_wg;
+    long long active_wgs;
+};
+extern thread_local LaunchFoot g_last_foot;
+// fill g_last_foot for a launch of `kern` (dynamic LDS `lds`, `threads` per workgroup, `grid`)
+hipError_t record_foot(const void* kern, size_t lds, int threads, int grid);
 
 size_t strip_lds_bytes(int ns, int substsz, int mode);
 // headers of every pair of the batch (grid.y = pair); maxWork = largest per-pair element count

@@ -58,7 +58,8 @@ constexpr int kXCopy = kXR * 4 + 256;
 __host__ __device__ constexpr uint32_t xcopy_base(int m) { return (uint32_t)m * kXCopy + (m == 0 ? 0 : m == 1 ? 208 : m == 2 ? 144 : 80); }
 constexpr int kRing = 128;          // hand-off ring slots (16 B) per strip boundary
 constexpr int kBig = 0x3fffffff;    // "everything published"
-constexpr uint64_t kSpinLimit = 20000000ull;  // 0.2 s of s_memrealtime (100 MHz) without progress
+// Every spin gives up after StripArgs::spin ticks of s_memrealtime (100 MHz) without progress
+// (gsa_set_watchdog; default 1 s) and sets the error word.
 
 
 extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -398,7 +399,7 @@ __device__ __forceinline__ void strip_wave(const StripArgs& a, const Lds& L, int
         while (!ready(pin, pco, pxo, psto, b))
         {
             __builtin_amdgcn_s_sleep(1);
-            if (__builtin_amdgcn_s_memrealtime() - t0 > kSpinLimit || err_set(a))
+            if (__builtin_amdgcn_s_memrealtime() - t0 > a.spin || err_set(a))
             {
                 atomicOr(a.err, 1u);
                 return false;
@@ -423,7 +424,7 @@ __device__ __forceinline__ void strip_wave(const StripArgs& a, const Lds& L, int
         while (!start_ok(pco, pxo, psto, b))
         {
             __builtin_amdgcn_s_sleep(1);
-            if (__builtin_amdgcn_s_memrealtime() - t0 > kSpinLimit || err_set(a))
+            if (__builtin_amdgcn_s_memrealtime() - t0 > a.spin || err_set(a))
             {
                 atomicOr(a.err, 1u);
                 return false;
@@ -655,7 +656,7 @@ __device__ __forceinline__ void strip_wave(const StripArgs& a, const Lds& L, int
                     while (!pin_ok(pn = flag_ld(fin), b))
                     {
                         __builtin_amdgcn_s_sleep(1);
-                        if (__builtin_amdgcn_s_memrealtime() - t0 > kSpinLimit || err_set(a))
+                        if (__builtin_amdgcn_s_memrealtime() - t0 > a.spin || err_set(a))
                         {
                             atomicOr(a.err, 1u);
                             break;
@@ -742,7 +743,7 @@ __device__ __forceinline__ void strip_wave(const StripArgs& a, const Lds& L, int
                     while (!pin_ok(pn = flag_ld(fin), b - 1))
                     {
                         __builtin_amdgcn_s_sleep(1);
-                        if (__builtin_amdgcn_s_memrealtime() - t0 > kSpinLimit || err_set(a))
+                        if (__builtin_amdgcn_s_memrealtime() - t0 > a.spin || err_set(a))
                         {
                             atomicOr(a.err, 1u);
                             return false;
@@ -968,7 +969,7 @@ __device__ __forceinline__ void loader_wave(const StripArgs& a, const Lds& L, in
             last = now;
         else
         {
-            if (now - last > kSpinLimit || err_set(a))
+            if (now - last > a.spin || err_set(a))
             {
                 atomicOr(a.err, 1u);
                 return;
@@ -1107,7 +1108,7 @@ __device__ __forceinline__ void store_wave(const StripArgs& a, const Lds& L, int
             last = now;
         else
         {
-            if (now - last > kSpinLimit || err_set(a))
+            if (now - last > a.spin || err_set(a))
             {
                 atomicOr(a.err, 1u);
                 return;
@@ -1150,7 +1151,7 @@ __device__ void ring_copy_wg(const StripArgs& a)
             const int f = __builtin_amdgcn_readfirstlane(
                 __hip_atomic_load(G(a.rfinal) + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
             if (f > 0 && gb >= f - 1 && h <= gb) break;
-            if (__builtin_amdgcn_s_memrealtime() - last > kSpinLimit || err_set(a))
+            if (__builtin_amdgcn_s_memrealtime() - last > a.spin || err_set(a))
             {
                 atomicOr(a.err, 1u);
                 return;
@@ -1411,8 +1412,28 @@ static hipError_t launch_strip(const StripArgs& a, int grid, hipStream_t stream)
         if (e != hipSuccess) return e;
         grid = std::max(1, std::min(a.nTicketsTotal, std::max(1, per_cu) * cus));
     }
+    if ((e = record_foot((const void*)kern, lds, 64 * kWaves<NS, MODE>, grid)) != hipSuccess) return e;
     hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * kWaves<NS, MODE>), lds, stream, a);
     return hipGetLastError();
+}
+
+thread_local LaunchFoot g_last_foot {};
+
+hipError_t record_foot(const void* kern, size_t lds, int threads, int grid)
+{
+    hipFuncAttributes at {};
+    int per_cu = 0, dev = 0, cus = 0;
+    hipError_t e = hipFuncGetAttributes(&at, kern);
+    if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, threads, lds);
+    if (e == hipSuccess) e = hipGetDevice(&dev);
+    if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (e != hipSuccess) return e;
+    g_last_foot.lds_per_wg = (long long)at.sharedSizeBytes + (long long)lds;
+    g_last_foot.scratch_per_lane = (long long)at.localSizeBytes;
+    g_last_foot.regs_per_lane = (long long)at.numRegs;
+    g_last_foot.threads_per_wg = threads;
+    g_last_foot.active_wgs = std::min<long long>(grid, (long long)std::max(1, per_cu) * cus);
+    return hipSuccess;
 }
 
 hipError_t launch_headers(const StripArgs& a, int mode, long long maxWork, hipStream_t stream)

@@ -149,6 +149,18 @@ NwStat check_input(const NwAlgInput& nw)
 
 }  // namespace
 
+// Peak-alloc columns from the context's launch footprints (updateNwAlgPeakMemUsage,
+// nwalign_shared.cpp:5-25): kernel attributes x resident workgroups of every fill so far.
+static void update_peak_mem(const NwAlgInput& nw, NwAlgResult& res)
+{
+    gsa_mem_stats m {};
+    if (gsa_mem_stats_get(nw.ctx, &m) != GSA_SUCCESS) return;
+    res.globalMemPeakAllocs = std::max(res.globalMemPeakAllocs, (size_t)m.glmem_peak_allocs);
+    res.sharedMemPeakAllocs = std::max(res.sharedMemPeakAllocs, (size_t)m.shmem_peak_allocs);
+    res.localMemPeakAllocs = std::max(res.localMemPeakAllocs, (size_t)m.locmem_peak_allocs);
+    res.regMemPeakAllocs = std::max(res.regMemPeakAllocs, (size_t)m.regmem_peak_allocs);
+}
+
 // Plain family (NwAlign_Gpu1..6 slots): the full (adjrows x adjcols) matrix in nw.score.
 // No tunables: the strip geometry is fixed by the hardware; parameters the
 // reference's files list for these slots are accepted and ignored.
@@ -165,6 +177,7 @@ NwStat NwAlign_Amd_Strip_Full(const NwAlgParams&, NwAlgInput& nw, NwAlgResult& r
     }
     gsa_laps laps {};
     int cost = 0;
+    gsa_mem_stats_reset(nw.ctx);  // peaks of this call only (res keeps the max over runs)
     int st = gsa_align_full(nw.ctx, nw.seqY.data(), nw.adjrows, nw.seqX.data(), nw.adjcols, nw.subst.data(), nw.substsz,
                             nw.gapoCost, nw.score.data(), &cost, &laps);
     res.hipStat = gsa_last_hip_error(nw.ctx);
@@ -172,6 +185,7 @@ NwStat NwAlign_Amd_Strip_Full(const NwAlgParams&, NwAlgInput& nw, NwAlgResult& r
     copy_laps(laps, res.sw_align);
     res.align_cost = cost;
     res.globalMemPeakAllocs = std::max(res.globalMemPeakAllocs, nw.score.size() * sizeof(int));
+    update_peak_mem(nw, res);
     return NwStat::success;
 }
 
@@ -200,6 +214,7 @@ static NwStat align_mlsp(const NwAlgParams& pr, NwAlgInput& nw, NwAlgResult& res
     }
     gsa_laps laps {};
     int cost = 0;
+    gsa_mem_stats_reset(nw.ctx);
     int st = (overlap ? gsa_align_sparse_pt : gsa_align_sparse)(nw.ctx, nw.seqY.data(), nw.adjrows, nw.seqX.data(),
                                                                 nw.adjcols, nw.subst.data(), nw.substsz, nw.gapoCost,
                                                                 tileBx, nw.tileHrowMat.data(), nw.tileHcolMat.data(),
@@ -215,6 +230,7 @@ static NwStat align_mlsp(const NwAlgParams& pr, NwAlgInput& nw, NwAlgResult& res
     res.align_cost = cost;
     res.globalMemPeakAllocs =
         std::max(res.globalMemPeakAllocs, (nw.tileHrowMat.size() + nw.tileHcolMat.size()) * sizeof(int));
+    update_peak_mem(nw, res);
     return NwStat::success;
 }
 
@@ -725,9 +741,9 @@ NwStat writeNwResultToTsv(std::ostream& os, const NwAlgResult& res, const TsvPri
     field("sm_count", res.sm_count);
     field("ram_peak_allocs", res.ramPeakAllocs);
     field("glmem_peak_allocs", res.globalMemPeakAllocs);
-    field("shmem_peak_allocs", 0);
-    field("locmem_peak_allocs", 0);
-    field("regmem_peak_allocs", 0);
+    field("shmem_peak_allocs", res.sharedMemPeakAllocs);
+    field("locmem_peak_allocs", res.localMemPeakAllocs);
+    field("regmem_peak_allocs", res.regMemPeakAllocs);
     field("align.alloc", ms(res.sw_align.get_or_default("align.alloc")));
     field("align.cpy_dev", ms(res.sw_align.get_or_default("align.cpy_dev")));
     field("align.init_hdr", ms(res.sw_align.get_or_default("align.init_hdr")));

@@ -142,6 +142,9 @@ struct NwAlgResult
     size_t sm_count = 0;
     size_t ramPeakAllocs = 0;
     size_t globalMemPeakAllocs = 0;
+    size_t sharedMemPeakAllocs = 0;
+    size_t localMemPeakAllocs = 0;
+    size_t regMemPeakAllocs = 0;
 
     Laps sw_align, sw_hash, sw_trace;
 };

@@ -80,13 +80,32 @@ int gsa_sparse_geometry(int32_t adjrows, int32_t adjcols, int32_t tileBx, gsa_sp
 
 /* ---- hot path, device-resident buffers (inputs already in HBM) --------------------- */
 /* Enqueue the fill on `stream` (a hipStream_t; NULL = the HIP null stream); asynchronous.  Call
- * gsa_sync() before reading outputs: it also reports hand-off time-outs. */
+ * gsa_sync() before reading outputs: it also reports hand-off time-outs.  The context's error word
+ * is STICKY: a time-out in any launch enqueued since the last gsa_sync() makes that gsa_sync()
+ * return GSA_ERROR_KERNEL_FAILURE (launches enqueued behind the failed one give up at once), and
+ * gsa_sync() then clears it, so the context is usable again.  One stream per context at a time
+ * (the launches share the context's ticket word). */
 int gsa_fill_full_dev(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, const int32_t* seqX, int32_t adjcols,
                       const int32_t* subst, int32_t substsz, int32_t gapo, int32_t* score, void* stream);
 int gsa_fill_sparse_dev(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, const int32_t* seqX, int32_t adjcols,
                         const int32_t* subst, int32_t substsz, int32_t gapo, int32_t tileBx, int32_t* tileHrowMat,
                         int32_t* tileHcolMat, void* stream);
 int gsa_sync(gsa_ctx* ctx, void* stream);
+/* Peak resource use of the fills launched on this context since its creation or the last reset:
+ * the reference's NwAlgResult peak-alloc columns (updateNwAlgPeakMemUsage, nwalign_shared.cpp:5-25).
+ * shmem/locmem/regmem = per-workgroup LDS, per-lane scratch x threads, per-lane VGPRs x 4 B x
+ * threads, each times the workgroups resident at once; glmem = device bytes the context holds
+ * (scratch and hand-off buffers, plus the host-buffer entry points' input/output copies). */
+typedef struct gsa_mem_stats
+{
+    int64_t glmem_peak_allocs, shmem_peak_allocs, locmem_peak_allocs, regmem_peak_allocs;
+} gsa_mem_stats;
+int gsa_mem_stats_get(const gsa_ctx* ctx, gsa_mem_stats* out);
+int gsa_mem_stats_reset(gsa_ctx* ctx);
+/* Hand-off watchdog: a wait inside a fill that sees no progress for this long gives up and sets
+ * the error word (default 1 s; 0 = give up at the first unmet poll, for tests of the error path).
+ * Applies to launches enqueued after the call. */
+int gsa_set_watchdog(gsa_ctx* ctx, int64_t microseconds);
 
 /* ---- batched fills: many independent pairs in ONE persistent launch ------------------- */
 /* Device pointers of one pair: score for full fills (adjrows*adjcols), the two header

@@ -147,3 +147,7 @@ def test_known_answers_end_to_end(gsa_nw, tmp_path):
             if "edit_trace" in c:
                 assert row["edit_trace"] == c["edit_trace"]
             assert float(row["align.calc"]) > 0
+            # peak-alloc columns from the launch footprints (nwalign_shared.cpp:5-25)
+            for col in ("glmem_peak_allocs", "shmem_peak_allocs", "regmem_peak_allocs"):
+                assert int(row[col]) > 0, (col, row[col])
+            assert int(row["locmem_peak_allocs"]) >= 0
