@@ -19,6 +19,7 @@
 #include "../../include/gsa.h"
 #include "nw_check.h"
 #include "nw_lane.h"
+#include "nw_pair2.h"
 #include "nw_strip.h"
 #include "nw_trace_dev.h"
 #include "nw_scan.h"
@@ -161,6 +162,25 @@ bool full_lane_enabled()
 {
     const char* e = std::getenv("GSA_FULL_KERNEL");
     return !(e && std::strcmp(e, "strip") == 0);
+}
+
+// Sparse fills: the two-rows-per-lane kernel (nw_pair2.hip) for single pairs, the 4-rows-per-lane
+// strip kernel (nw_strip.hip) for batches, where many pairs fill the chip and fewer VALU per cell
+// win.  GSA_SPARSE_KERNEL=strip|pair2 forces one (read per launch); GSA_PAIR2_NS = strips per
+// workgroup (2, 4).
+bool sparse_pair2(int npairs)
+{
+    const char* e = std::getenv("GSA_SPARSE_KERNEL");
+    if (e && std::strcmp(e, "strip") == 0) return false;
+    if (e && std::strcmp(e, "pair2") == 0) return true;
+    return npairs == 1;
+}
+
+int pair2_ns()
+{
+    const char* e = std::getenv("GSA_PAIR2_NS");
+    const int v = e ? std::atoi(e) : gsa::kPair2NSDefault;
+    return gsa::pair2_ns_ok(v) ? v : gsa::kPair2NSDefault;
 }
 
 int lane_ns()
@@ -352,7 +372,10 @@ int enqueue_batch(gsa_ctx* ctx, int mode, int npairs, const gsa_pair_dev* pairs,
     a.substsz = substsz;
     a.g = gapo;
     const bool lane = mode == gsa::kModeFull && full_lane_enabled();
-    a.ns = (mode == gsa::kModeFull) ? (lane ? lane_ns() : full_ns()) : gsa::kSparseNS;
+    const bool pair2 = mode == gsa::kModeSparse && !done && sparse_pair2(npairs);  // mlsppt: per-tile-row flags of the strip kernel
+    a.ns = (mode == gsa::kModeFull) ? (lane ? lane_ns() : full_ns()) : (pair2 ? pair2_ns() : gsa::kSparseNS);
+    // sparse tickets per tile row: the pair2 kernel's super-strip is a fraction of the tile height
+    const int perTileRow = pair2 ? gsa::kSparseTileBy / (gsa::kPair2Rows * a.ns) : 1;
     const int fullRows = lane ? gsa::kLaneRows * a.ns : gsa::kWaveRows * a.ns;  // rows per ticket
     if (mode == gsa::kModeSparse)
     {
@@ -393,7 +416,7 @@ int enqueue_batch(gsa_ctx* ctx, int mode, int npairs, const gsa_pair_dev* pairs,
             d.trows = geom.tileHdrMatRows;
             d.tcols = geom.tileHdrMatCols;
             d.Cp = d.tcols * tileBx;
-            d.nTickets = d.trows;
+            d.nTickets = d.trows * perTileRow;
             maxWork = std::max<long long>(maxWork, std::max((long long)d.tcols * (tileBx + 1),
                                                             (long long)d.trows * (gsa::kSparseTileBy + 1)));
         }
@@ -502,7 +525,9 @@ int enqueue_batch(gsa_ctx* ctx, int mode, int npairs, const gsa_pair_dev* pairs,
         launchMode = gsa::kModeFullRing;
         grid = 2 * nStrip;
     }
-    e = lane ? gsa::launch_lane_fill(a, a.ns, grid, st) : gsa::launch_strip_fill(a, launchMode, grid, st);
+    e = lane    ? gsa::launch_lane_fill(a, a.ns, grid, st)
+        : pair2 ? gsa::launch_pair2_fill(a, a.ns, grid, st)
+                : gsa::launch_strip_fill(a, launchMode, grid, st);
     if (e != hipSuccess) return fail(ctx, e, GSA_ERROR_KERNEL_FAILURE);
     note_launch(ctx);
     return GSA_SUCCESS;
