@@ -19,6 +19,7 @@
 #include "../../include/gsa.h"
 #include "nw_check.h"
 #include "nw_lane.h"
+#include "nw_krow.h"
 #include "nw_pair2.h"
 #include "nw_strip.h"
 #include "nw_trace_dev.h"
@@ -164,17 +165,27 @@ bool full_lane_enabled()
     return !(e && std::strcmp(e, "strip") == 0);
 }
 
-// Sparse fills: the two-rows-per-lane kernel (nw_pair2.hip) for single pairs, the 4-rows-per-lane
-// strip kernel (nw_strip.hip) for batches, where many pairs fill the chip and fewer VALU per cell
-// win.  GSA_SPARSE_KERNEL=strip|pair2 forces one (read per launch); GSA_PAIR2_NS = strips per
-// workgroup (2, 4).
-bool sparse_pair2(int npairs)
+// Sparse fills: the K-rows-per-lane kernel (nw_krow.hip) for single pairs, the strip kernel
+// (nw_strip.hip) for batches, where many pairs fill the chip and fewer VALU per cell win.
+// GSA_SPARSE_KERNEL=strip|krow|pair2 forces one (read per launch); GSA_KROW_K (2, 4) and
+// GSA_KROW_NS (2, 4) pick the K-rows geometry, GSA_PAIR2_NS the pair2 one.
+enum SparseKern { kSpStrip, kSpKrow, kSpPair2 };
+SparseKern sparse_kernel(int npairs)
 {
     const char* e = std::getenv("GSA_SPARSE_KERNEL");
-    if (e && std::strcmp(e, "strip") == 0) return false;
-    if (e && std::strcmp(e, "pair2") == 0) return true;
-    return npairs == 1;
+    if (e && std::strcmp(e, "strip") == 0) return kSpStrip;
+    if (e && std::strcmp(e, "krow") == 0) return kSpKrow;
+    if (e && std::strcmp(e, "pair2") == 0) return kSpPair2;
+    return npairs == 1 ? kSpKrow : kSpStrip;
 }
+
+int env_int(const char* name, int dflt)
+{
+    const char* e = std::getenv(name);
+    return e ? std::atoi(e) : dflt;
+}
+
+bool sparse_pair2(int npairs) { return sparse_kernel(npairs) == kSpPair2; }
 
 int pair2_ns()
 {
@@ -372,10 +383,24 @@ int enqueue_batch(gsa_ctx* ctx, int mode, int npairs, const gsa_pair_dev* pairs,
     a.substsz = substsz;
     a.g = gapo;
     const bool lane = mode == gsa::kModeFull && full_lane_enabled();
-    const bool pair2 = mode == gsa::kModeSparse && !done && sparse_pair2(npairs);  // mlsppt: per-tile-row flags of the strip kernel
-    a.ns = (mode == gsa::kModeFull) ? (lane ? lane_ns() : full_ns()) : (pair2 ? pair2_ns() : gsa::kSparseNS);
-    // sparse tickets per tile row: the pair2 kernel's super-strip is a fraction of the tile height
-    const int perTileRow = pair2 ? gsa::kSparseTileBy / (gsa::kPair2Rows * a.ns) : 1;
+    // mlsppt (done flags per tile row) stays on the strip kernel
+    const SparseKern sk = (mode == gsa::kModeSparse && !done) ? sparse_kernel(npairs) : kSpStrip;
+    const bool pair2 = mode == gsa::kModeSparse && sk == kSpPair2;
+    const bool krow = mode == gsa::kModeSparse && sk == kSpKrow;
+    int krowK = env_int("GSA_KROW_K", gsa::kKrowKDefault), krowNS = env_int("GSA_KROW_NS", gsa::kKrowNSDefault);
+    if (!gsa::krow_ok(krowNS, krowK))
+    {
+        krowK = gsa::kKrowKDefault;
+        krowNS = gsa::kKrowNSDefault;
+    }
+    a.ns = (mode == gsa::kModeFull) ? (lane ? lane_ns() : full_ns())
+           : pair2                  ? pair2_ns()
+           : krow                   ? krowNS
+                                    : gsa::kSparseNS;
+    // sparse tickets per tile row: a K-rows / pair2 super-strip is a fraction of the tile height
+    const int perTileRow = pair2  ? gsa::kSparseTileBy / (gsa::kPair2Rows * a.ns)
+                           : krow ? gsa::kSparseTileBy / gsa::krow_ticket_rows(krowNS, krowK)
+                                  : 1;
     const int fullRows = lane ? gsa::kLaneRows * a.ns : gsa::kWaveRows * a.ns;  // rows per ticket
     if (mode == gsa::kModeSparse)
     {
@@ -526,6 +551,7 @@ int enqueue_batch(gsa_ctx* ctx, int mode, int npairs, const gsa_pair_dev* pairs,
         grid = 2 * nStrip;
     }
     e = lane    ? gsa::launch_lane_fill(a, a.ns, grid, st)
+        : krow  ? gsa::launch_krow_fill(a, krowNS, krowK, grid, st)
         : pair2 ? gsa::launch_pair2_fill(a, a.ns, grid, st)
                 : gsa::launch_strip_fill(a, launchMode, grid, st);
     if (e != hipSuccess) return fail(ctx, e, GSA_ERROR_KERNEL_FAILURE);

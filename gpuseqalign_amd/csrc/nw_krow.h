@@ -1,0 +1,23 @@
+// nw_krow.h -- launch interface of the K-rows-per-lane sparse (mlsp) fill (nw_krow.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+
+#include "nw_strip.h"
+
+namespace gsa {
+
+constexpr int kKrowKDefault = 4;   // rows per lane
+constexpr int kKrowNSDefault = 4;  // strip waves per workgroup
+
+// (ns, k) pairs the library instantiates: a ticket = ns * 64 * k rows, which must divide the
+// sparse tile height kSparseTileBy (1024).
+__host__ __device__ constexpr bool krow_ok(int ns, int k) { return (k == 2 || k == 4) && (ns == 2 || ns == 4); }
+__host__ __device__ constexpr int krow_ticket_rows(int ns, int k) { return ns * 64 * k; }
+size_t krow_lds_bytes(int ns, int k, int substsz);
+// StripArgs / PairDesc / granule contract as launch_strip_fill (sparse mode, a.tBx, a.tBy,
+// per-pair hrow/hcol/trows/tcols/Cp); tickets of a pair = trows * tBy / krow_ticket_rows.
+// Every |s - 2g| must fit int16 (checked by the host).  grid <= 0: every resident slot.
+hipError_t launch_krow_fill(const StripArgs& a, int ns, int k, int grid, hipStream_t stream);
+
+}  // namespace gsa

@@ -1,0 +1,626 @@
+// nw_krow.hip -- NW-LG sparse (mlsp tile-header) fill with K rows per lane (K = 2 or 4),
+// hand-written wave64 HIP for gfx950 (MI355X).
+//
+// Replaces the sparse family NwAlign_Gpu7..9 (nwalign_gpu9_mlsp_diagdiagdiag.cu:368-722, kernels
+// :15-360) for single pairs and has their output contract: tileHrowMat / tileHcolMat, tile-major
+// k = tcols*iT + jT, 1+tBx resp. 1+tBy ints per tile, element 0 the corner, the padded region
+// computed with letter 0 (nwalign_gpu9_mlsp_diagdiagdiag.cu:147-171, 471-478).  Recurrence of
+// UpdateScore (nwalign_cpu1_st_row.cpp:4-10).
+//
+// Cost model of one pair.  The fill is a wavefront: strip waves of 64K rows (lane l owns rows
+// r0+Kl .. r0+Kl+K-1 and at step t works on column t-l) follow each other ~6 blocks of 16 steps
+// apart (the 64-lane skew, one block of hand-off granularity, the progress check), so a pair
+// takes (C/16 + 6 * R/(64K)) block times.  A block costs ~16 * (K+1) dependent VALU of step
+// chain plus a fixed ~700 cycles of side work (halo and profile reads, hand-off writes, progress
+// words, header-column capture; measured with tools/p2_stamps.py), so the side work, not the
+// arithmetic, sets the block time, and more rows per lane cut the lag term: K = 4 is ~2x fewer
+// strips than K = 2 for a block ~10 % longer (profiles/r02_sparse_kernels.txt).
+//
+// Step, shifted values H' = H - (i+j)*g (borders 0), K+1 dependent VALU + K adds:
+//     up    = dpp_shr1(H[K-1]) + halo    lane 0: H'(row above, c) from the ring; others + 0
+//     H[0]' = max3(D + q0, up, H[0])     D = up of the previous step (= H'(r0+Kl-1, c-1))
+//     H[k]' = max3(H[k-1] + qk, H[k-1]', H[k])
+// q = s(y, X[c]) - 2g (int16) from a per-workgroup column profile in LDS: two copies shifted by
+// one column, dword d of copy p holding columns (2d-p, 2d-p+1), so every lane reads its 16 columns
+// of a block as 8 aligned dwords at base + immediate offsets (copy = lane parity): no VALU
+// addressing, 8*K/2 ds_read2 per block; the halves are taken by SDWA operands of the adds.
+//
+// Sparse output.  Header rows (the last row of a tile row) are the last row of a ticket: the
+// drain wave writes them with the granules.  Header columns are captured by the strips: in a
+// block whose 79-column window holds a tile boundary, each lane picks its (H[0..K-1]) at its
+// boundary step with a 4-level v_cndmask tree over the block's 16 steps and stores K ints.
+//
+// Hand-off between strips: lane 63 writes its old H[K-1] (column t-64) into the next strip's
+// ring (all lanes write, the others into a sink: no exec mask), behind the next block's halo
+// reads; lane 0 of the next strip reads block b's 16 halo values at the start of block b.  LDS
+// progress words keep the order (a wave's LDS operations execute in order).  Between
+// super-strips (workgroups) the drain wave moves the last row through 8-byte {epoch, H'}
+// granules in HBM (sc1 atomics), polled by the next super-strip's loader wave
+// (MI355X_MICROARCH.md, handoff-1to1).  Every wait is bounded (StripArgs::spin, error word).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+
+#include "nw_krow.h"
+
+namespace gsa {
+namespace {
+
+__host__ __device__ constexpr int kr_lw(int ns, int k) { return ns * k >= 8 ? 1024 : 512; }  // profile ring columns
+__host__ __device__ constexpr int kr_qrs(int ns, int k) { return kr_lw(ns, k) / 2 + 16; }     // dwords per profile row (+ guard)
+constexpr int kBlk = 16;          // steps per block
+constexpr int kHalo = kBlk / 4;   // halo registers (int4) per block
+constexpr int kRing = 512;        // hand-off ring elements per strip boundary (power of 2)
+constexpr int kBig = 0x3fffffff;  // "everything published"
+constexpr int kSubRow = 36;       // dwords per subT row (32 letters + 4)
+constexpr int kBatch = 128;       // profile columns the loader adds per pass (2 per lane)
+constexpr uint32_t kFCons = 64, kFXo = 128, kFTicket = 132;
+
+extern __shared__ __attribute__((aligned(16))) char krsm[];
+
+typedef int int4v __attribute__((ext_vector_type(4)));
+template <typename T>
+using gptr = __attribute__((address_space(1))) T*;
+template <typename T>
+__device__ __forceinline__ gptr<T> G(T* p)
+{
+    return (gptr<T>)p;
+}
+
+__device__ __forceinline__ int lds_ld(uint32_t a) { return *(const int*)(krsm + a); }
+__device__ __forceinline__ void lds_st(uint32_t a, int v) { *(int*)(krsm + a) = v; }
+__device__ __forceinline__ int4v lds_ld4(uint32_t a) { return *(const int4v*)(krsm + a); }
+__device__ __forceinline__ void lds_st4(uint32_t a, int4v v) { *(int4v*)(krsm + a) = v; }
+// progress words: relaxed workgroup-scope atomics (no vmcnt drains, unlike volatile accesses)
+__device__ __forceinline__ int raw_ld(uint32_t a)
+{
+    return __hip_atomic_load((int*)__builtin_assume_aligned(krsm + a, 4), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ int flag_ld(uint32_t a) { return __builtin_amdgcn_readfirstlane(raw_ld(a)); }
+__device__ __forceinline__ void flag_st(uint32_t a, int v)
+{
+    asm volatile("" ::: "memory");  // data writes are issued before the word (LDS executes in order)
+    __hip_atomic_store((int*)__builtin_assume_aligned(krsm + a, 4), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ bool err_set(const StripArgs& a)
+{
+    return __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+}
+// lane l <- lane l-1, lane 0 <- 0 (DPP wave_shr:1, bound_ctrl zero)
+__device__ __forceinline__ int shr1z(int v) { return __builtin_amdgcn_update_dpp(0, v, 0x138, 0xF, 0xF, true); }
+__device__ __forceinline__ int max3i(int a, int b, int c) { return max(max(a, b), c); }
+// m ? b : a per lane, m a lane mask in an SGPR pair: one v_cndmask (a ?: tree over an array is
+// turned into a dynamically indexed array in scratch)
+__device__ __forceinline__ int sel(uint64_t m, int a, int b)
+{
+    int r;
+    asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(m));
+    return r;
+}
+// int16 half of a profile dword: column 2d-p (lo) or 2d-p+1 (hi)
+__device__ __forceinline__ int qlo(int v) { return (int)(short)v; }
+__device__ __forceinline__ int qhi(int v) { return v >> 16; }
+
+// LDS: profile (2 copies x substsz rows x kr_qrs dwords), subT[x][y] = s(y, x) - 2g, NS+1
+// hand-off rings, 16 zeros (the halo of lanes >= 1), the hand-off sink, progress words:
+// prog[i] @ 4i (ring i holds elements < prog[i]), cons[i] @ 64+4i (ring i's reader no longer
+// needs elements < cons[i]), xo @ 128 (the profile holds columns < xo), ticket @ 132.
+struct KrLds
+{
+    uint32_t q, sub, ring, zfill, sink, flags;
+};
+
+__host__ __device__ inline KrLds kr_layout(int ns, int k, int substsz)
+{
+    KrLds L;
+    L.q = 0;
+    L.sub = 2u * (uint32_t)substsz * kr_qrs(ns, k) * 4u;
+    L.ring = L.sub + (uint32_t)substsz * kSubRow * 4u;
+    L.zfill = L.ring + (uint32_t)(ns + 1) * kRing * 4u;
+    L.sink = L.zfill + 64u;
+    L.flags = L.sink + (uint32_t)ns * 1024u;
+    return L;
+}
+
+// ------------------------------------------------------------------------------------
+// strip wave: 64K rows, K per lane
+// ------------------------------------------------------------------------------------
+template <int NS, int K>
+__device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int tk, int w, int lane)
+{
+    const int g = a.g;
+    const int Cp = a.Cp;
+    const int tBx = a.tBx, tBy = a.tBy, tcols = a.tcols;
+    const int r0 = tk * (64 * K * NS) + 64 * K * w + 1;  // first row of the strip
+    const int rl = r0 + K * lane;                          // this lane's first row
+    constexpr int kLW = kr_lw(NS, K), kQRS = kr_qrs(NS, K);
+    constexpr int kQW = kLW / 2;  // profile dwords per copy row (ring)
+    uint32_t qrow[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+    {
+        const int r = rl + k;
+        int y = (r <= a.R) ? G(a.seqY)[r] : 0;
+        y = ((unsigned)y < (unsigned)a.substsz) ? y : 0;
+        qrow[k] = L.q + (uint32_t)((lane & 1) * a.substsz + y) * (kQRS * 4u);
+    }
+    const uint32_t ring_in = L.ring + (uint32_t)w * (kRing * 4u);
+    const uint32_t ring_out = L.ring + (uint32_t)(w + 1) * (kRing * 4u);
+    const uint32_t f_in = L.flags + 4u * w, f_out = L.flags + 4u * (w + 1);
+    const uint32_t c_in = L.flags + kFCons + 4u * w, c_out = L.flags + kFCons + 4u * (w + 1);
+    const uint32_t f_xo = L.flags + kFXo;
+    const uint32_t hsink = L.sink + (uint32_t)w * 1024u + 16u * (uint32_t)lane;
+    const int NB = (Cp + 65 + kBlk - 1) / kBlk;  // lane 63 reaches step Cp+64 (element of column Cp)
+    // header-column slots of this lane's rows: tile row iT, elements ea .. ea+K-1 (one tile)
+    const int iT = (rl - 1) / tBy;
+    const int ea = rl - iT * tBy;
+    const gptr<int> hcolT = G(a.hcol) + (size_t)iT * (size_t)tcols * (size_t)(tBy + 1) + ea;
+
+    // block b needs its halo (ring elements 16b+64 .. 16b+79), room in ring_out for elements
+    // 16b .. 16b+15, and (strip 0; the others trail it) the profile of block b+1 (columns < 16b+32)
+    auto ok = [&](int pin, int pco, int pxo, int b) {
+        return pin >= kBlk * b + 64 + kBlk && pco >= kBlk * b + kBlk - kRing && (w != 0 || pxo >= kBlk * b + 2 * kBlk);
+    };
+    // the error word is a global load, which waits for this wave's outstanding header stores
+    // (vmcnt retires in order): polled once per 32 LDS polls
+    auto spin = [&](int b) {
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        for (int it = 1;; ++it)
+        {
+            const int pin = flag_ld(f_in), pco = flag_ld(c_out), pxo = (w == 0) ? flag_ld(f_xo) : 0;
+            if (ok(pin, pco, pxo, b)) return true;
+            __builtin_amdgcn_s_sleep(1);
+            if (__builtin_amdgcn_s_memrealtime() - t0 > a.spin || ((it & 31) == 0 && err_set(a)))
+            {
+                atomicOr(a.err, 1u);
+                return false;
+            }
+        }
+    };
+    // halo of block b: lane 0 reads ring elements 16b+64 .. +15, lanes >= 1 a row of zeros (no branch)
+    int4v hc[kHalo];
+    auto halo_load = [&](int b) {
+        const uint32_t hb = (lane == 0) ? ring_in + 4u * (uint32_t)((kBlk * b + 64) & (kRing - 1)) : L.zfill;
+#pragma unroll
+        for (int j = 0; j < kHalo; ++j) hc[j] = lds_ld4(hb + 16u * (lane == 0 ? j : 0));
+    };
+    // profile dwords of block b: columns 16b - lane .. +15 are dwords 8b - lane/2 .. +7 of copy
+    // (lane & 1); reads past the ring's end hit the guard copy
+    auto q_off = [&](int b) { return 4u * (uint32_t)((8 * b - (lane >> 1)) & (kQW - 1)); };
+    int qA[K][8], qB[K][8];
+    {
+        const uint32_t p = q_off(0);
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) qA[k][j] = 0;
+        if (!spin(-1)) return;
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) qA[k][j] = lds_ld(qrow[k] + p + 4u * j);
+    }
+    int H[K], D = 0;
+#pragma unroll
+    for (int k = 0; k < K; ++k) H[k] = 0;
+    int lt[kBlk];  // lane 63's hand-off values of the last block (H[K-1] of columns t-64)
+    // hand-off of block bb: every lane writes (lane 63 into the ring, the others into the sink,
+    // no exec mask), then the progress word
+    auto handoff = [&](int bb) {
+        const uint32_t eb = (lane == 63) ? ring_out + 4u * (uint32_t)((kBlk * bb) & (kRing - 1)) : hsink;
+#pragma unroll
+        for (int j = 0; j < kHalo; ++j)
+            lds_st4(eb + ((lane == 63) ? 16u * j : 0u), int4v {lt[4 * j], lt[4 * j + 1], lt[4 * j + 2], lt[4 * j + 3]});
+        flag_st(f_out, bb + 1 == NB ? kBig : kBlk * bb + kBlk);
+    };
+    int rpin = 0, rpco = 0, rpxo = 0;  // progress words read in mid-block, checked at the next block
+    int nb0 = tBx, jb0 = 1;             // smallest tile boundary column >= 16b - 63 (uniform)
+
+    // One body for blocks with and without a header-column capture (cap, uniform): separate
+    // bodies get different register assignments and ~100 v_mov per block to reconcile them.
+    auto block = [&](int b, int (&qc)[K][8], int (&qn)[K][8], auto rampT, bool cap) {
+        constexpr bool RAMP = decltype(rampT)::value;
+        constexpr bool CAP = !RAMP;  // ramp blocks hold no boundary (tBx >= 64)
+        {
+            const int pin = __builtin_amdgcn_readfirstlane(rpin), pco = __builtin_amdgcn_readfirstlane(rpco);
+            const int pxo = (w == 0) ? __builtin_amdgcn_readfirstlane(rpxo) : 0;
+            if (!ok(pin, pco, pxo, b) && !spin(b)) return false;
+        }
+        halo_load(b);
+        // block b-1's hand-off, behind this block's halo reads (LDS executes a wave's operations in
+        // order: written before them, the halo would wait for the writes)
+        if (b > 0) handoff(b - 1);
+        flag_st(c_in, kBlk * b + 64 + kBlk);
+        const uint32_t pn = q_off(b + 1);
+        int va[CAP ? K : 1][CAP ? kBlk : 1];
+#pragma unroll
+        for (int u = 0; u < kBlk; ++u)
+        {
+            int nh[K];
+            const int up = shr1z(H[K - 1]) + hc[u >> 2][u & 3];
+            {
+                const int q = (u & 1) ? qhi(qc[0][u >> 1]) : qlo(qc[0][u >> 1]);
+                nh[0] = max3i(D + q, up, H[0]);
+            }
+#pragma unroll
+            for (int k = 1; k < K; ++k)
+            {
+                const int q = (u & 1) ? qhi(qc[k][u >> 1]) : qlo(qc[k][u >> 1]);
+                nh[k] = max3i(H[k - 1] + q, nh[k - 1], H[k]);
+            }
+            if constexpr (RAMP)
+            {
+                // column t - lane <= 0: the border (H' = 0)
+                const bool border = lane >= kBlk * b + u;
+#pragma unroll
+                for (int k = 0; k < K; ++k) nh[k] = border ? 0 : nh[k];
+            }
+            // profile of block b+1: K dwords per step over the first half of the block
+            if (u < 8)
+#pragma unroll
+                for (int k = 0; k < K; ++k) qn[k][u] = lds_ld(qrow[k] + pn + 4u * u);
+            lt[u] = H[K - 1];  // column t-64 of the lane's last row: ring element t
+            D = up;
+#pragma unroll
+            for (int k = 0; k < K; ++k)
+            {
+                H[k] = nh[k];
+                if constexpr (CAP) va[k][u] = nh[k];
+            }
+            if (u == kBlk / 2)
+            {
+                rpin = raw_ld(f_in);
+                rpco = raw_ld(c_out);
+                rpxo = raw_ld(f_xo);
+            }
+        }
+        if (CAP && cap)
+        {
+            // this lane's columns lo .. lo+15; boundaries nb0 (>= 16b-63) and nb0 + tBx
+            const int lo = kBlk * b - lane;
+            int bc = nb0, jT = jb0;
+            if (bc < lo)
+            {
+                bc += tBx;
+                ++jT;
+            }
+            const int s = bc - lo;
+            if (s <= kBlk - 1 && jT < tcols)
+            {
+                // 16 -> 1 by the bits of s (v_cndmask tree, 15 per row)
+                const uint64_t m1 = __builtin_amdgcn_ballot_w64((s & 1) != 0), m2 = __builtin_amdgcn_ballot_w64((s & 2) != 0);
+                const uint64_t m4 = __builtin_amdgcn_ballot_w64((s & 4) != 0), m8 = __builtin_amdgcn_ballot_w64((s & 8) != 0);
+                const gptr<int> dst = hcolT + (size_t)jT * (size_t)(tBy + 1);
+#pragma unroll
+                for (int k = 0; k < K; ++k)
+                {
+                    int x[8];
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) x[i] = sel(m1, va[k][2 * i], va[k][2 * i + 1]);
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) x[i] = sel(m2, x[2 * i], x[2 * i + 1]);
+#pragma unroll
+                    for (int i = 0; i < 2; ++i) x[i] = sel(m4, x[2 * i], x[2 * i + 1]);
+                    dst[k] = sel(m8, x[0], x[1]) + (rl + k + bc) * g;
+                }
+            }
+        }
+        return true;
+    };
+
+    // the window of block b holds a tile boundary iff nb0 <= 16b+15 (uniform)
+    auto advance = [&](int b) {
+        if (nb0 < kBlk * b - 63)  // the window moves 16 columns per block and tBx >= 64
+        {
+            nb0 += tBx;
+            ++jb0;
+        }
+        return nb0 <= kBlk * b + kBlk - 1 && jb0 < tcols;
+    };
+    using T = std::integral_constant<bool, true>;
+    using F = std::integral_constant<bool, false>;
+    constexpr int kRampBlocks = 64 / kBlk;  // columns <= 0 occur only in the first 64 steps
+    int b = 0;
+    for (; b < kRampBlocks; b += 2)
+    {
+        if (!block(b, qA, qB, T(), false)) return;
+        if (!block(b + 1, qB, qA, T(), false)) return;
+    }
+    for (; b < NB; b += 2)
+    {
+        if (!block(b, qA, qB, F(), advance(b))) return;
+        if (b + 1 >= NB) break;
+        if (!block(b + 1, qB, qA, F(), advance(b + 1))) return;
+    }
+    handoff(NB - 1);
+}
+
+// ------------------------------------------------------------------------------------
+// loader wave: the column profile and the row above strip 0 (granules of the previous
+// super-strip, or row 0)
+// ------------------------------------------------------------------------------------
+template <int NS, int K>
+__device__ __forceinline__ void kr_loader(const StripArgs& a, const KrLds& L, int tk, int lane)
+{
+    const int Cp = a.Cp, C = a.C;
+    constexpr int kLW = kr_lw(NS, K), kQRS = kr_qrs(NS, K), kQW = kLW / 2;
+    const uint32_t F = L.flags;
+    const uint32_t ring0 = L.ring;
+    const gptr<const unsigned long long> gprev = G((const unsigned long long*)a.gran) + (size_t)(tk > 0 ? tk - 1 : 0) * a.granStride;
+    auto letter = [&](int c) {
+        int x = (c >= 1 && c <= C) ? G(a.seqX)[c] : 0;  // padded columns: letter 0
+        return ((unsigned)x < (unsigned)a.substsz) ? x : 0;
+    };
+    auto subrow = [&](int x, int4v (&v)[8]) {
+        const uint32_t sb = L.sub + 4u * kSubRow * (uint32_t)x;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = lds_ld4(sb + 16u * j);
+    };
+    int qn = 0;     // the profile holds columns < qn
+    int hnext = 0;  // next column of the row above to feed into ring 0
+    int pl = 0, c0 = 0;  // progress words, re-read only when their cached values block
+    uint64_t last = __builtin_amdgcn_s_memrealtime();
+    while (qn <= Cp || hnext <= Cp)
+    {
+        bool moved = false;
+        // (1) the row above strip 0 -> ring 0 elements c + 64, as far as granules of the previous
+        //     super-strip are published (in column order) and ring 0 has room.  The poll is issued
+        //     first and consumed after the profile work, which runs under its latency.
+        if (hnext <= Cp && hnext + 128 > c0 + kRing) c0 = flag_ld(F + kFCons);
+        const bool feed = hnext <= Cp && hnext + 128 <= c0 + kRing;
+        const int c = hnext + lane;
+        const bool in = c <= Cp;
+        unsigned long long q = 0ull;
+        if (feed && tk > 0 && in) q = __hip_atomic_load(gprev + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // (2) profile columns qn .. qn+127 (lane l: qn+2l-1 .. qn+2l+1): the ring slots they take
+        //     held columns <= qn+127-kLW, dead once the last strip has published elements pl (it
+        //     then reads columns >= pl-47)
+        if (qn <= Cp && qn + 192 > pl + kLW) pl = flag_ld(F + 4u * NS);
+        if (qn <= Cp && qn + 192 <= pl + kLW)
+        {
+            const int cl = qn + 2 * lane;
+            int4v vm[8], v0[8], v1[8];
+            subrow(letter(cl - 1), vm);
+            subrow(letter(cl), v0);
+            subrow(letter(cl + 1), v1);
+            const uint32_t d = (uint32_t)((qn / 2 + lane) & (kQW - 1));  // dword of columns (cl, cl+1) / (cl-1, cl)
+            const bool guard = d < 8;                                     // ring head: also the guard copy at d + kQW
+#pragma unroll
+            for (int yy = 0; yy < 32; ++yy)
+            {
+                if (yy < a.substsz)
+                {
+                    const int s0 = v0[yy >> 2][yy & 3];
+                    const int p0 = (s0 & 0xffff) | (v1[yy >> 2][yy & 3] << 16);  // copy 0: (cl, cl+1)
+                    const int p1 = (vm[yy >> 2][yy & 3] & 0xffff) | (s0 << 16);  // copy 1: (cl-1, cl)
+                    const uint32_t r0a = L.q + 4u * (kQRS * (uint32_t)yy + d);
+                    const uint32_t r1a = L.q + 4u * (kQRS * (uint32_t)(a.substsz + yy) + d);
+                    lds_st(r0a, p0);
+                    lds_st(r1a, p1);
+                    if (guard)
+                    {
+                        lds_st(r0a + 4u * kQW, p0);
+                        lds_st(r1a + 4u * kQW, p1);
+                    }
+                }
+            }
+            qn += kBatch;
+            flag_st(F + kFXo, qn > Cp ? kBig : qn);
+            moved = true;
+        }
+        if (feed)
+        {
+            int v = 0;  // row 0: H' = 0
+            bool good = in;
+            if (tk > 0)
+            {
+                good = in && (uint32_t)(q >> 32) == a.epoch;
+                v = (int)(uint32_t)q;
+            }
+            const uint64_t badm = __ballot(!good);
+            const int n = badm ? __builtin_ctzll(badm) : 64;
+            if (n > 0)
+            {
+                if (lane < n) lds_st(ring0 + 4u * (uint32_t)((c + 64) & (kRing - 1)), v);
+                hnext += n;
+                flag_st(F, hnext > Cp ? kBig : hnext + 64);
+                moved = true;
+            }
+        }
+        const uint64_t now = __builtin_amdgcn_s_memrealtime();
+        if (moved)
+            last = now;
+        else
+        {
+            if (now - last > a.spin || err_set(a))
+            {
+                atomicOr(a.err, 1u);
+                return;
+            }
+            if (tk == 0 || hnext > Cp) __builtin_amdgcn_s_sleep(1);
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// drain wave: the last strip's row (ring NS) -> granules for the next super-strip and, when the
+// row closes a tile row, the header row of the tiles below (unshifted) with its duplicates: the
+// last element of the tile to the left and the corner of the header column
+// (nwalign_gpu9_mlsp_diagdiagdiag.cu:214-218, 253-257).  It issues no global loads, so its stores
+// never wait behind a poll.
+// ------------------------------------------------------------------------------------
+template <int NS, int K>
+__device__ __forceinline__ void kr_drain(const StripArgs& a, const KrLds& L, int tk, int lane)
+{
+    const int Cp = a.Cp, g = a.g, tBx = a.tBx, tBy = a.tBy, tcols = a.tcols;
+    const uint32_t F = L.flags, ringN = L.ring + (uint32_t)NS * (kRing * 4u);
+    if (tk + 1 >= a.nTickets)
+    {
+        flag_st(F + kFCons + 4u * NS, kBig);  // nobody reads our last row
+        return;
+    }
+    const gptr<unsigned long long> gout = G(a.gran) + (size_t)tk * a.granStride;
+    const int rowEnd = (tk + 1) * (64 * K * NS);  // the row this ticket hands down
+    const bool hdr = rowEnd % tBy == 0;
+    const size_t rowbase = (size_t)(rowEnd / tBy) * (size_t)tcols;  // tile index of (iT+1, 0)
+    int dnext = 0;  // next column to drain
+    uint64_t last = __builtin_amdgcn_s_memrealtime();
+    while (dnext <= Cp)
+    {
+        const int avail = min(flag_ld(F + 4u * NS) - 64, Cp + 1);  // columns < avail are in ring NS
+        if (dnext < avail)
+        {
+            const int c = dnext + lane;
+            if (c < avail)
+            {
+                const int v = lds_ld(ringN + 4u * (uint32_t)((c + 64) & (kRing - 1)));
+                __hip_atomic_store(gout + c, ((unsigned long long)a.epoch << 32) | (uint32_t)v, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+                if (hdr)
+                {
+                    const int hv = v + (rowEnd + c) * g;
+                    const int jT = c / tBx, jj = c - jT * tBx;
+                    if (jT < tcols) G(a.hrow)[(rowbase + jT) * (size_t)(tBx + 1) + jj] = hv;
+                    if (jj == 0 && jT > 0)
+                    {
+                        G(a.hrow)[(rowbase + jT - 1) * (size_t)(tBx + 1) + tBx] = hv;
+                        if (jT < tcols) G(a.hcol)[(rowbase + jT) * (size_t)(tBy + 1)] = hv;
+                    }
+                }
+            }
+            dnext = min(dnext + 64, avail);
+            flag_st(F + kFCons + 4u * NS, dnext > Cp ? kBig : dnext + 64);
+            last = __builtin_amdgcn_s_memrealtime();
+        }
+        else
+        {
+            if (__builtin_amdgcn_s_memrealtime() - last > a.spin || err_set(a))
+            {
+                atomicOr(a.err, 1u);
+                return;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+}
+
+__device__ __forceinline__ PairDesc kr_desc(const PairDesc* p)
+{
+    constexpr int N = sizeof(PairDesc) / 4;
+    const int* wds = (const int*)p;
+    union
+    {
+        int v[N];
+        PairDesc d;
+    } u;
+#pragma unroll
+    for (int k = 0; k < N; ++k) u.v[k] = __builtin_amdgcn_readfirstlane(G(wds)[k]);
+    return u.d;
+}
+
+template <int NS, int K>
+__global__ void __launch_bounds__(64 * (NS + 2)) nw_krow_kernel(StripArgs a)
+{
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const KrLds L = kr_layout(NS, K, a.substsz);
+    bool bad = false;
+    for (int k = threadIdx.x; k < a.substsz * kSubRow; k += 64 * (NS + 2))
+    {
+        const int x = k / kSubRow, yy = k % kSubRow;
+        const int v = yy < a.substsz ? G(a.subst)[yy * a.substsz + x] - 2 * a.g : 0;
+        bad |= v < -32768 || v > 32767;  // the profile holds int16
+        lds_st(L.sub + 4u * k, v);
+    }
+    if (bad) atomicOr(a.err, 2u);
+    if (threadIdx.x < 16) lds_st(L.zfill + 4u * threadIdx.x, 0);
+    for (;;)
+    {
+        __syncthreads();
+        if (threadIdx.x == 0) lds_st(L.flags + kFTicket, err_set(a) ? a.nTicketsTotal : (int)atomicAdd(a.ticket, 1u));
+        __syncthreads();
+        const int tkg = __builtin_amdgcn_readfirstlane(lds_ld(L.flags + kFTicket));
+        if (tkg >= a.nTicketsTotal) break;
+        // pair of this ticket: the batch schedule, or the last descriptor with ticketBase <= tkg
+        int lo = 0, tks = -1;
+        if (a.sched)
+        {
+            lo = __builtin_amdgcn_readfirstlane(G(a.sched)[2 * tkg]);
+            tks = __builtin_amdgcn_readfirstlane(G(a.sched)[2 * tkg + 1]);
+        }
+        else
+        {
+            int hi = a.nPairs - 1;
+            while (lo < hi)
+            {
+                const int mid = (lo + hi + 1) >> 1;
+                if (__builtin_amdgcn_readfirstlane(G(a.pairs)[mid].ticketBase) <= tkg)
+                    lo = mid;
+                else
+                    hi = mid - 1;
+            }
+        }
+        const PairDesc d = kr_desc(a.pairs + lo);
+        StripArgs pa = a;
+        pa.seqY = d.seqY;
+        pa.seqX = d.seqX;
+        pa.R = d.R;
+        pa.C = d.C;
+        pa.Cp = d.Cp;
+        pa.nTickets = d.nTickets;
+        pa.hrow = d.hrow;
+        pa.hcol = d.hcol;
+        pa.trows = d.trows;
+        pa.tcols = d.tcols;
+        pa.gran = a.gran + d.granOff;
+        pa.granStride = (long long)d.Cp + 1;
+        const int tk = (tks >= 0) ? tks : tkg - d.ticketBase;
+        if (threadIdx.x < 32) lds_st(L.flags + 4u * threadIdx.x, 0);  // prog[], cons[]
+        if (threadIdx.x == 0) lds_st(L.flags + kFXo, 0);
+        __syncthreads();
+        if (w == NS + 1)
+            kr_drain<NS, K>(pa, L, tk, lane);
+        else if (w == NS)
+            kr_loader<NS, K>(pa, L, tk, lane);
+        else
+        {
+            __builtin_amdgcn_s_setprio(3);
+            kr_strip<NS, K>(pa, L, tk, w, lane);
+            __builtin_amdgcn_s_setprio(0);
+        }
+    }
+}
+
+template <int NS, int K>
+hipError_t launch_kr(const StripArgs& a, int grid, hipStream_t stream)
+{
+    const size_t lds = krow_lds_bytes(NS, K, a.substsz);
+    auto kern = nw_krow_kernel<NS, K>;
+    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+    if (grid <= 0)
+    {
+        int per_cu = 0, dev = 0, cus = 0;
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)kern, 64 * (NS + 2), lds);
+        if (e == hipSuccess) e = hipGetDevice(&dev);
+        if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        if (e != hipSuccess) return e;
+        grid = std::max(1, std::min(a.nTicketsTotal, std::max(1, per_cu) * cus));
+    }
+    if ((e = record_foot((const void*)kern, lds, 64 * (NS + 2), grid)) != hipSuccess) return e;
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * (NS + 2)), lds, stream, a);
+    return hipGetLastError();
+}
+
+}  // namespace
+
+size_t krow_lds_bytes(int ns, int k, int substsz) { return (size_t)kr_layout(ns, k, substsz).flags + 256; }
+
+hipError_t launch_krow_fill(const StripArgs& a, int ns, int k, int grid, hipStream_t stream)
+{
+    if (k == 2) return ns == 2 ? launch_kr<2, 2>(a, grid, stream) : launch_kr<4, 2>(a, grid, stream);
+    return ns == 2 ? launch_kr<2, 4>(a, grid, stream) : launch_kr<4, 4>(a, grid, stream);
+}
+
+}  // namespace gsa

@@ -62,6 +62,11 @@ extern __shared__ __attribute__((aligned(16))) char p2sm[];
 #ifndef GSA_P2KNOB
 #define GSA_P2KNOB 0
 #endif
+// Diagnostic stamps (separate build, tools/p2_stamps.py): s_memtime at 4 points of blocks
+// 64..319 of the strips of tickets 0 and 1, dbg[(tk*NS + w)*1024 + (b-64)*4 + k]
+#ifndef GSA_P2STAMP
+#define GSA_P2STAMP 0
+#endif
 
 typedef int int4v __attribute__((ext_vector_type(4)));
 template <typename T>
@@ -221,11 +226,18 @@ __device__ __forceinline__ void p2_strip(const StripArgs& a, const P2Lds& L, int
                      auto rampT, bool cap) {
         constexpr bool RAMP = decltype(rampT)::value;
         constexpr bool CAP = !RAMP && (GSA_P2KNOB & 32) == 0;  // ramp blocks hold no boundary (tBx >= 64)
+        auto stamp = [&](int k) {
+            if constexpr (GSA_P2STAMP != 0)
+                if (tk < 2 && b >= 64 && b < 320 && lane == 0 && a.dbg)
+                    a.dbg[(size_t)(tk * NS + w) * 1024 + (b - 64) * 4 + k] = __builtin_amdgcn_s_memtime();
+        };
+        stamp(0);
         {
             const int pin = __builtin_amdgcn_readfirstlane(rpin), pco = __builtin_amdgcn_readfirstlane(rpco);
             const int pxo = (w == 0) ? __builtin_amdgcn_readfirstlane(rpxo) : 0;
             if (!ok(pin, pco, pxo, b) && !spin(b)) return false;
         }
+        stamp(1);
         if constexpr ((GSA_P2KNOB & 1) == 0) halo_load(b, hc);
         // block b-1's hand-off, behind this block's halo reads (LDS executes a wave's operations in
         // order: written before them, the halo would wait for the writes)
@@ -248,15 +260,25 @@ __device__ __forceinline__ void p2_strip(const StripArgs& a, const P2Lds& L, int
                 ha = border ? 0 : ha;
                 hb = border ? 0 : hb;
             }
-            if constexpr ((GSA_P2KNOB & 2) == 0)
+            // Q of block b+1 in the first half of the block (4 columns per step), so the reads have
+            // returned when the next block starts (a wave's LDS operations return in order, and the
+            // block start waits on the progress reads issued after them)
+            if (u < kP2Blk / 2)
             {
-                qna[u] = lds_ld(qrowA + pn + 4u * u);
-                qnb[u] = lds_ld(qrowB + pn + 4u * u);
-            }
-            else
-            {
-                qna[u] = qca[u] ^ 1;
-                qnb[u] = qcb[u] ^ 1;
+#pragma unroll
+                for (int e = 2 * u; e < 2 * u + 2; ++e)
+                {
+                    if constexpr ((GSA_P2KNOB & 2) == 0)
+                    {
+                        qna[e] = lds_ld(qrowA + pn + 4u * e);
+                        qnb[e] = lds_ld(qrowB + pn + 4u * e);
+                    }
+                    else
+                    {
+                        qna[e] = qca[e] ^ 1;
+                        qnb[e] = qcb[e] ^ 1;
+                    }
+                }
             }
             lt[u] = Hb;  // column t-64 of row b: ring element t
             Da = up;
@@ -274,6 +296,7 @@ __device__ __forceinline__ void p2_strip(const StripArgs& a, const P2Lds& L, int
                 rpxo = raw_ld(f_xo);
             }
         }
+        stamp(2);
         if (CAP && cap)
         {
             // this lane's columns lo .. lo+15; boundaries nb0 (>= 16b-63) and nb0 + tBx
@@ -321,6 +344,7 @@ __device__ __forceinline__ void p2_strip(const StripArgs& a, const P2Lds& L, int
                     lds_st(hsink, sa + sb);
             }
         }
+        stamp(3);
         return true;
     };
 

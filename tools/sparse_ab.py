@@ -33,9 +33,12 @@ for shp in shapes:
   st = torch.cuda.current_stream()
   R, C = len(Y) - 1, len(X) - 1
   for v in a.variants.split(","):
-      kern, ns = v.split(":")
-      os.environ["GSA_SPARSE_KERNEL"] = kern
-      os.environ["GSA_PAIR2_NS"] = ns
+      parts = v.split(":")  # kernel:ns[:k]
+      os.environ["GSA_SPARSE_KERNEL"] = parts[0]
+      os.environ["GSA_PAIR2_NS"] = parts[1]
+      os.environ["GSA_KROW_NS"] = parts[1]
+      if len(parts) > 2:
+          os.environ["GSA_KROW_K"] = parts[2]
       fn = lambda: eng.fill_sparse_dev(y.data_ptr(), len(Y), x.data_ptr(), len(X), s.data_ptr(), 25, -11, a.tileBx,
                                        hr.data_ptr(), hc.data_ptr(), st.cuda_stream)
       fn(); eng.sync(st.cuda_stream)
