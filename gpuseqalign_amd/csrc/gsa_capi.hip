@@ -20,7 +20,6 @@
 #include "nw_check.h"
 #include "nw_lane.h"
 #include "nw_krow.h"
-#include "nw_pair2.h"
 #include "nw_strip.h"
 #include "nw_trace_dev.h"
 #include "nw_scan.h"
@@ -165,18 +164,15 @@ bool full_lane_enabled()
     return !(e && std::strcmp(e, "strip") == 0);
 }
 
-// Sparse fills: the K-rows-per-lane kernel (nw_krow.hip) for single pairs, the strip kernel
-// (nw_strip.hip) for batches, where many pairs fill the chip and fewer VALU per cell win.
-// GSA_SPARSE_KERNEL=strip|krow|pair2 forces one (read per launch); GSA_KROW_K (2, 4) and
-// GSA_KROW_NS (2, 4) pick the K-rows geometry, GSA_PAIR2_NS the pair2 one.
-enum SparseKern { kSpStrip, kSpKrow, kSpPair2 };
-SparseKern sparse_kernel(int npairs)
+// Sparse fills run on the K-rows-per-lane kernel (nw_krow.hip, K = 4): 6.8 vs 8.0 ms for the
+// 100k pair and 5.2 vs 4.3 TCUPS for 512 pairs of 20k against the strip kernel (nw_strip.hip),
+// which mlsppt keeps.  GSA_SPARSE_KERNEL=strip forces the strip kernel (read per launch, tested);
+// GSA_KROW_K (2, 4) and GSA_KROW_NS (2, 4) pick the K-rows geometry.
+enum SparseKern { kSpStrip, kSpKrow };
+SparseKern sparse_kernel()
 {
     const char* e = std::getenv("GSA_SPARSE_KERNEL");
-    if (e && std::strcmp(e, "strip") == 0) return kSpStrip;
-    if (e && std::strcmp(e, "krow") == 0) return kSpKrow;
-    if (e && std::strcmp(e, "pair2") == 0) return kSpPair2;
-    return npairs == 1 ? kSpKrow : kSpStrip;
+    return (e && std::strcmp(e, "strip") == 0) ? kSpStrip : kSpKrow;
 }
 
 int env_int(const char* name, int dflt)
@@ -185,14 +181,6 @@ int env_int(const char* name, int dflt)
     return e ? std::atoi(e) : dflt;
 }
 
-bool sparse_pair2(int npairs) { return sparse_kernel(npairs) == kSpPair2; }
-
-int pair2_ns()
-{
-    const char* e = std::getenv("GSA_PAIR2_NS");
-    const int v = e ? std::atoi(e) : gsa::kPair2NSDefault;
-    return gsa::pair2_ns_ok(v) ? v : gsa::kPair2NSDefault;
-}
 
 int lane_ns()
 {
@@ -384,23 +372,16 @@ int enqueue_batch(gsa_ctx* ctx, int mode, int npairs, const gsa_pair_dev* pairs,
     a.g = gapo;
     const bool lane = mode == gsa::kModeFull && full_lane_enabled();
     // mlsppt (done flags per tile row) stays on the strip kernel
-    const SparseKern sk = (mode == gsa::kModeSparse && !done) ? sparse_kernel(npairs) : kSpStrip;
-    const bool pair2 = mode == gsa::kModeSparse && sk == kSpPair2;
-    const bool krow = mode == gsa::kModeSparse && sk == kSpKrow;
+    const bool krow = mode == gsa::kModeSparse && !done && sparse_kernel() == kSpKrow;
     int krowK = env_int("GSA_KROW_K", gsa::kKrowKDefault), krowNS = env_int("GSA_KROW_NS", gsa::kKrowNSDefault);
     if (!gsa::krow_ok(krowNS, krowK))
     {
         krowK = gsa::kKrowKDefault;
         krowNS = gsa::kKrowNSDefault;
     }
-    a.ns = (mode == gsa::kModeFull) ? (lane ? lane_ns() : full_ns())
-           : pair2                  ? pair2_ns()
-           : krow                   ? krowNS
-                                    : gsa::kSparseNS;
-    // sparse tickets per tile row: a K-rows / pair2 super-strip is a fraction of the tile height
-    const int perTileRow = pair2  ? gsa::kSparseTileBy / (gsa::kPair2Rows * a.ns)
-                           : krow ? gsa::kSparseTileBy / gsa::krow_ticket_rows(krowNS, krowK)
-                                  : 1;
+    a.ns = (mode == gsa::kModeFull) ? (lane ? lane_ns() : full_ns()) : krow ? krowNS : gsa::kSparseNS;
+    // sparse tickets per tile row: a K-rows super-strip can be a fraction of the tile height
+    const int perTileRow = krow ? gsa::kSparseTileBy / gsa::krow_ticket_rows(krowNS, krowK) : 1;
     const int fullRows = lane ? gsa::kLaneRows * a.ns : gsa::kWaveRows * a.ns;  // rows per ticket
     if (mode == gsa::kModeSparse)
     {
@@ -551,8 +532,7 @@ int enqueue_batch(gsa_ctx* ctx, int mode, int npairs, const gsa_pair_dev* pairs,
         grid = 2 * nStrip;
     }
     e = lane    ? gsa::launch_lane_fill(a, a.ns, grid, st)
-        : krow  ? gsa::launch_krow_fill(a, krowNS, krowK, grid, st)
-        : pair2 ? gsa::launch_pair2_fill(a, a.ns, grid, st)
+        : krow  ? gsa::launch_krow_fill(a, krowNS, krowK, 0, grid, st)
                 : gsa::launch_strip_fill(a, launchMode, grid, st);
     if (e != hipSuccess) return fail(ctx, e, GSA_ERROR_KERNEL_FAILURE);
     note_launch(ctx);

@@ -14,10 +14,11 @@ constexpr int kKrowNSDefault = 4;  // strip waves per workgroup
 // sparse tile height kSparseTileBy (1024).
 __host__ __device__ constexpr bool krow_ok(int ns, int k) { return (k == 2 || k == 4) && (ns == 2 || ns == 4); }
 __host__ __device__ constexpr int krow_ticket_rows(int ns, int k) { return ns * 64 * k; }
-size_t krow_lds_bytes(int ns, int k, int substsz);
+size_t krow_lds_bytes(int ns, int lw, int substsz);
 // StripArgs / PairDesc / granule contract as launch_strip_fill (sparse mode, a.tBx, a.tBy,
 // per-pair hrow/hcol/trows/tcols/Cp); tickets of a pair = trows * tBy / krow_ticket_rows.
-// Every |s - 2g| must fit int16 (checked by the host).  grid <= 0: every resident slot.
-hipError_t launch_krow_fill(const StripArgs& a, int ns, int k, int grid, hipStream_t stream);
+// Every |s - 2g| must fit int16 (the kernel sets error bit 2 otherwise).  grid <= 0: every resident slot.
+// The profile ring holds 1024 columns for (ns, k) = (4, 4), 512 otherwise (lw is reserved).
+hipError_t launch_krow_fill(const StripArgs& a, int ns, int k, int lw, int grid, hipStream_t stream);
 
 }  // namespace gsa

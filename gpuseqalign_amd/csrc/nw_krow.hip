@@ -47,8 +47,7 @@
 namespace gsa {
 namespace {
 
-__host__ __device__ constexpr int kr_lw(int ns, int k) { return ns * k >= 8 ? 1024 : 512; }  // profile ring columns
-__host__ __device__ constexpr int kr_qrs(int ns, int k) { return kr_lw(ns, k) / 2 + 16; }     // dwords per profile row (+ guard)
+__host__ __device__ constexpr int kr_qrs(int lw) { return lw / 2 + 16; }  // dwords per profile row (ring + guard)
 constexpr int kBlk = 16;          // steps per block
 constexpr int kHalo = kBlk / 4;   // halo registers (int4) per block
 constexpr int kRing = 512;        // hand-off ring elements per strip boundary (power of 2)
@@ -58,6 +57,18 @@ constexpr int kBatch = 128;       // profile columns the loader adds per pass (2
 constexpr uint32_t kFCons = 64, kFXo = 128, kFTicket = 132;
 
 extern __shared__ __attribute__((aligned(16))) char krsm[];
+
+// Diagnostic stamps (separate build, tools/p2_stamps.py): s_memtime at 4 points of blocks
+// 64..319 of the strips of tickets 0 and 1, dbg[(tk*NS + w)*1024 + (b-64)*4 + k]
+#ifndef GSA_KRSTAMP
+#define GSA_KRSTAMP 0
+#endif
+// Timing-experiment knobs (tools/build_kr_knobs.sh; any set bit makes results WRONG): 1 no halo
+// reads, 4 no hand-off writes, 8 strips never wait, 16 no mid-block progress reads, 32 no
+// header-column capture
+#ifndef GSA_KRKNOB
+#define GSA_KRKNOB 0
+#endif
 
 typedef int int4v __attribute__((ext_vector_type(4)));
 template <typename T>
@@ -111,11 +122,11 @@ struct KrLds
     uint32_t q, sub, ring, zfill, sink, flags;
 };
 
-__host__ __device__ inline KrLds kr_layout(int ns, int k, int substsz)
+__host__ __device__ inline KrLds kr_layout(int ns, int lw, int substsz)
 {
     KrLds L;
     L.q = 0;
-    L.sub = 2u * (uint32_t)substsz * kr_qrs(ns, k) * 4u;
+    L.sub = 2u * (uint32_t)substsz * kr_qrs(lw) * 4u;
     L.ring = L.sub + (uint32_t)substsz * kSubRow * 4u;
     L.zfill = L.ring + (uint32_t)(ns + 1) * kRing * 4u;
     L.sink = L.zfill + 64u;
@@ -126,7 +137,7 @@ __host__ __device__ inline KrLds kr_layout(int ns, int k, int substsz)
 // ------------------------------------------------------------------------------------
 // strip wave: 64K rows, K per lane
 // ------------------------------------------------------------------------------------
-template <int NS, int K>
+template <int NS, int K, int LW>
 __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int tk, int w, int lane)
 {
     const int g = a.g;
@@ -134,7 +145,7 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
     const int tBx = a.tBx, tBy = a.tBy, tcols = a.tcols;
     const int r0 = tk * (64 * K * NS) + 64 * K * w + 1;  // first row of the strip
     const int rl = r0 + K * lane;                          // this lane's first row
-    constexpr int kLW = kr_lw(NS, K), kQRS = kr_qrs(NS, K);
+    constexpr int kLW = LW, kQRS = kr_qrs(LW);
     constexpr int kQW = kLW / 2;  // profile dwords per copy row (ring)
     uint32_t qrow[K];
 #pragma unroll
@@ -160,6 +171,7 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
     // block b needs its halo (ring elements 16b+64 .. 16b+79), room in ring_out for elements
     // 16b .. 16b+15, and (strip 0; the others trail it) the profile of block b+1 (columns < 16b+32)
     auto ok = [&](int pin, int pco, int pxo, int b) {
+        if constexpr ((GSA_KRKNOB & 8) != 0) return true;
         return pin >= kBlk * b + 64 + kBlk && pco >= kBlk * b + kBlk - kRing && (w != 0 || pxo >= kBlk * b + 2 * kBlk);
     };
     // the error word is a global load, which waits for this wave's outstanding header stores
@@ -180,6 +192,8 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
     };
     // halo of block b: lane 0 reads ring elements 16b+64 .. +15, lanes >= 1 a row of zeros (no branch)
     int4v hc[kHalo];
+#pragma unroll
+    for (int j = 0; j < kHalo; ++j) hc[j] = int4v {0, 0, 0, 0};
     auto halo_load = [&](int b) {
         const uint32_t hb = (lane == 0) ? ring_in + 4u * (uint32_t)((kBlk * b + 64) & (kRing - 1)) : L.zfill;
 #pragma unroll
@@ -208,10 +222,13 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
     // hand-off of block bb: every lane writes (lane 63 into the ring, the others into the sink,
     // no exec mask), then the progress word
     auto handoff = [&](int bb) {
+        if constexpr ((GSA_KRKNOB & 4) == 0)
+        {
         const uint32_t eb = (lane == 63) ? ring_out + 4u * (uint32_t)((kBlk * bb) & (kRing - 1)) : hsink;
 #pragma unroll
         for (int j = 0; j < kHalo; ++j)
             lds_st4(eb + ((lane == 63) ? 16u * j : 0u), int4v {lt[4 * j], lt[4 * j + 1], lt[4 * j + 2], lt[4 * j + 3]});
+        }
         flag_st(f_out, bb + 1 == NB ? kBig : kBlk * bb + kBlk);
     };
     int rpin = 0, rpco = 0, rpxo = 0;  // progress words read in mid-block, checked at the next block
@@ -221,13 +238,20 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
     // bodies get different register assignments and ~100 v_mov per block to reconcile them.
     auto block = [&](int b, int (&qc)[K][8], int (&qn)[K][8], auto rampT, bool cap) {
         constexpr bool RAMP = decltype(rampT)::value;
-        constexpr bool CAP = !RAMP;  // ramp blocks hold no boundary (tBx >= 64)
+        constexpr bool CAP = !RAMP && (GSA_KRKNOB & 32) == 0;  // ramp blocks hold no boundary (tBx >= 64)
+        auto stamp = [&](int k) {
+            if constexpr (GSA_KRSTAMP != 0)
+                if (tk < 2 && b >= 64 && b < 320 && lane == 0 && a.dbg)
+                    a.dbg[(size_t)(tk * NS + w) * 1024 + (b - 64) * 4 + k] = __builtin_amdgcn_s_memtime();
+        };
+        stamp(0);
         {
             const int pin = __builtin_amdgcn_readfirstlane(rpin), pco = __builtin_amdgcn_readfirstlane(rpco);
             const int pxo = (w == 0) ? __builtin_amdgcn_readfirstlane(rpxo) : 0;
             if (!ok(pin, pco, pxo, b) && !spin(b)) return false;
         }
-        halo_load(b);
+        stamp(1);
+        if constexpr ((GSA_KRKNOB & 1) == 0) halo_load(b);
         // block b-1's hand-off, behind this block's halo reads (LDS executes a wave's operations in
         // order: written before them, the halo would wait for the writes)
         if (b > 0) handoff(b - 1);
@@ -268,13 +292,14 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
                 H[k] = nh[k];
                 if constexpr (CAP) va[k][u] = nh[k];
             }
-            if (u == kBlk / 2)
+            if ((GSA_KRKNOB & 16) == 0 && u == kBlk / 2)
             {
                 rpin = raw_ld(f_in);
                 rpco = raw_ld(c_out);
                 rpxo = raw_ld(f_xo);
             }
         }
+        stamp(2);
         if (CAP && cap)
         {
             // this lane's columns lo .. lo+15; boundaries nb0 (>= 16b-63) and nb0 + tBx
@@ -306,6 +331,7 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
                 }
             }
         }
+        stamp(3);
         return true;
     };
 
@@ -340,11 +366,11 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
 // loader wave: the column profile and the row above strip 0 (granules of the previous
 // super-strip, or row 0)
 // ------------------------------------------------------------------------------------
-template <int NS, int K>
+template <int NS, int K, int LW>
 __device__ __forceinline__ void kr_loader(const StripArgs& a, const KrLds& L, int tk, int lane)
 {
     const int Cp = a.Cp, C = a.C;
-    constexpr int kLW = kr_lw(NS, K), kQRS = kr_qrs(NS, K), kQW = kLW / 2;
+    constexpr int kLW = LW, kQRS = kr_qrs(LW), kQW = kLW / 2;
     const uint32_t F = L.flags;
     const uint32_t ring0 = L.ring;
     const gptr<const unsigned long long> gprev = G((const unsigned long long*)a.gran) + (size_t)(tk > 0 ? tk - 1 : 0) * a.granStride;
@@ -450,7 +476,7 @@ __device__ __forceinline__ void kr_loader(const StripArgs& a, const KrLds& L, in
 // (nwalign_gpu9_mlsp_diagdiagdiag.cu:214-218, 253-257).  It issues no global loads, so its stores
 // never wait behind a poll.
 // ------------------------------------------------------------------------------------
-template <int NS, int K>
+template <int NS, int K, int LW>
 __device__ __forceinline__ void kr_drain(const StripArgs& a, const KrLds& L, int tk, int lane)
 {
     const int Cp = a.Cp, g = a.g, tBx = a.tBx, tBy = a.tBy, tcols = a.tcols;
@@ -519,12 +545,12 @@ __device__ __forceinline__ PairDesc kr_desc(const PairDesc* p)
     return u.d;
 }
 
-template <int NS, int K>
+template <int NS, int K, int LW>
 __global__ void __launch_bounds__(64 * (NS + 2)) nw_krow_kernel(StripArgs a)
 {
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
-    const KrLds L = kr_layout(NS, K, a.substsz);
+    const KrLds L = kr_layout(NS, LW, a.substsz);
     bool bad = false;
     for (int k = threadIdx.x; k < a.substsz * kSubRow; k += 64 * (NS + 2))
     {
@@ -580,23 +606,23 @@ __global__ void __launch_bounds__(64 * (NS + 2)) nw_krow_kernel(StripArgs a)
         if (threadIdx.x == 0) lds_st(L.flags + kFXo, 0);
         __syncthreads();
         if (w == NS + 1)
-            kr_drain<NS, K>(pa, L, tk, lane);
+            kr_drain<NS, K, LW>(pa, L, tk, lane);
         else if (w == NS)
-            kr_loader<NS, K>(pa, L, tk, lane);
+            kr_loader<NS, K, LW>(pa, L, tk, lane);
         else
         {
             __builtin_amdgcn_s_setprio(3);
-            kr_strip<NS, K>(pa, L, tk, w, lane);
+            kr_strip<NS, K, LW>(pa, L, tk, w, lane);
             __builtin_amdgcn_s_setprio(0);
         }
     }
 }
 
-template <int NS, int K>
+template <int NS, int K, int LW>
 hipError_t launch_kr(const StripArgs& a, int grid, hipStream_t stream)
 {
-    const size_t lds = krow_lds_bytes(NS, K, a.substsz);
-    auto kern = nw_krow_kernel<NS, K>;
+    const size_t lds = krow_lds_bytes(NS, LW, a.substsz);
+    auto kern = nw_krow_kernel<NS, K, LW>;
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     if (grid <= 0)
@@ -615,12 +641,14 @@ hipError_t launch_kr(const StripArgs& a, int grid, hipStream_t stream)
 
 }  // namespace
 
-size_t krow_lds_bytes(int ns, int k, int substsz) { return (size_t)kr_layout(ns, k, substsz).flags + 256; }
+size_t krow_lds_bytes(int ns, int lw, int substsz) { return (size_t)kr_layout(ns, lw, substsz).flags + 256; }
 
-hipError_t launch_krow_fill(const StripArgs& a, int ns, int k, int grid, hipStream_t stream)
+hipError_t launch_krow_fill(const StripArgs& a, int ns, int k, int lw, int grid, hipStream_t stream)
 {
-    if (k == 2) return ns == 2 ? launch_kr<2, 2>(a, grid, stream) : launch_kr<4, 2>(a, grid, stream);
-    return ns == 2 ? launch_kr<2, 4>(a, grid, stream) : launch_kr<4, 4>(a, grid, stream);
+    if (k == 2) return ns == 2 ? launch_kr<2, 2, 512>(a, grid, stream) : launch_kr<4, 2, 1024>(a, grid, stream);
+    (void)lw;  // 512 for (4, 4) measured slower for one pair and for batches (the first strip
+               // is throttled by the window): 1024
+    return ns == 2 ? launch_kr<2, 4, 512>(a, grid, stream) : launch_kr<4, 4, 1024>(a, grid, stream);
 }
 
 }  // namespace gsa

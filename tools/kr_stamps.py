@@ -1,5 +1,5 @@
-"""Diagnostic: per-block timings of the pair2 strips (stamp build: GSA_LIB=.../libgsa_p2stamp.so,
-nw_pair2.hip GSA_P2STAMP).  One R x C random sparse fill; for strips 0..7 (tickets 0, 1) and
+"""Diagnostic: per-block timings of the K-rows strips (stamp build tools/build_stamp_lib.sh: GSA_LIB=.../libgsa_p2stamp.so,
+nw_krow.hip GSA_KRSTAMP).  One R x C random sparse fill; for strips 0..7 (tickets 0, 1) and
 blocks 64..319: block period, wait at block start, 16 steps, capture pick, and the rest."""
 import ctypes, os, sys, json
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))

@@ -10,7 +10,7 @@ import gpuseqalign_amd as gsa
 import bench
 
 ap = argparse.ArgumentParser()
-ap.add_argument("--variants", default="strip:4,pair2:2,pair2:4,pair2:8")
+ap.add_argument("--variants", default="strip:4,krow:4:4,krow:4:2,krow:2:4")
 ap.add_argument("--reps", type=int, default=10)
 ap.add_argument("--tileBx", type=int, default=256)
 ap.add_argument("--shapes", default="", help="RxC,...: random pairs instead of the config-3 pair")
