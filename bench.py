@@ -69,7 +69,7 @@ def load_golden(name):
 
 
 def sparse_kernel_name():
-    return "gsa::nw_strip_kernel<4,1> (sparse, 4 rows per lane)"
+    return "gsa::nw_krow_kernel<4,4,1024> (sparse, K = 4 rows per lane)"
 
 
 def cpu_topology():

@@ -47,7 +47,11 @@
 namespace gsa {
 namespace {
 
-__host__ __device__ constexpr int kr_qrs(int lw) { return lw / 2 + 16; }  // dwords per profile row (ring + guard)
+// dwords per profile row: the ring + a guard, == 0 mod 32 (the row letter never moves a lane's bank)
+__host__ __device__ constexpr int kr_qrs(int lw) { return lw / 2 + 32; }
+// copy 1 starts 16 dwords past a multiple of 32: lanes 2m (copy 0) and 2m+1 (copy 1) read the same
+// dword index d, so copy 1 must sit in the other half of the banks (d and d + 16)
+__host__ __device__ constexpr uint32_t kr_copy1(int lw, int substsz) { return (uint32_t)substsz * kr_qrs(lw) + 16u; }
 constexpr int kBlk = 16;          // steps per block
 constexpr int kHalo = kBlk / 4;   // halo registers (int4) per block
 constexpr int kRing = 512;        // hand-off ring elements per strip boundary (power of 2)
@@ -113,7 +117,7 @@ __device__ __forceinline__ int sel(uint64_t m, int a, int b)
 __device__ __forceinline__ int qlo(int v) { return (int)(short)v; }
 __device__ __forceinline__ int qhi(int v) { return v >> 16; }
 
-// LDS: profile (2 copies x substsz rows x kr_qrs dwords), subT[x][y] = s(y, x) - 2g, NS+1
+// LDS: profile (2 copies x substsz rows x kr_qrs dwords, copy 1 at kr_copy1), subT[x][y] = s(y, x) - 2g, NS+1
 // hand-off rings, 16 zeros (the halo of lanes >= 1), the hand-off sink, progress words:
 // prog[i] @ 4i (ring i holds elements < prog[i]), cons[i] @ 64+4i (ring i's reader no longer
 // needs elements < cons[i]), xo @ 128 (the profile holds columns < xo), ticket @ 132.
@@ -126,7 +130,7 @@ __host__ __device__ inline KrLds kr_layout(int ns, int lw, int substsz)
 {
     KrLds L;
     L.q = 0;
-    L.sub = 2u * (uint32_t)substsz * kr_qrs(lw) * 4u;
+    L.sub = (kr_copy1(lw, substsz) + (uint32_t)substsz * kr_qrs(lw) + 16u) * 4u;
     L.ring = L.sub + (uint32_t)substsz * kSubRow * 4u;
     L.zfill = L.ring + (uint32_t)(ns + 1) * kRing * 4u;
     L.sink = L.zfill + 64u;
@@ -154,7 +158,7 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
         const int r = rl + k;
         int y = (r <= a.R) ? G(a.seqY)[r] : 0;
         y = ((unsigned)y < (unsigned)a.substsz) ? y : 0;
-        qrow[k] = L.q + (uint32_t)((lane & 1) * a.substsz + y) * (kQRS * 4u);
+        qrow[k] = L.q + 4u * ((lane & 1) * kr_copy1(LW, a.substsz) + (uint32_t)y * kQRS);
     }
     const uint32_t ring_in = L.ring + (uint32_t)w * (kRing * 4u);
     const uint32_t ring_out = L.ring + (uint32_t)(w + 1) * (kRing * 4u);
@@ -421,7 +425,7 @@ __device__ __forceinline__ void kr_loader(const StripArgs& a, const KrLds& L, in
                     const int p0 = (s0 & 0xffff) | (v1[yy >> 2][yy & 3] << 16);  // copy 0: (cl, cl+1)
                     const int p1 = (vm[yy >> 2][yy & 3] & 0xffff) | (s0 << 16);  // copy 1: (cl-1, cl)
                     const uint32_t r0a = L.q + 4u * (kQRS * (uint32_t)yy + d);
-                    const uint32_t r1a = L.q + 4u * (kQRS * (uint32_t)(a.substsz + yy) + d);
+                    const uint32_t r1a = L.q + 4u * (kr_copy1(LW, a.substsz) + kQRS * (uint32_t)yy + d);
                     lds_st(r0a, p0);
                     lds_st(r1a, p1);
                     if (guard)
