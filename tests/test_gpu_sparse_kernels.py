@@ -11,16 +11,23 @@ from tests._data import random_pair, related_pair
 
 pytestmark = pytest.mark.gpu
 
+# (kernel, strips per workgroup, rows per lane)
 KERNELS = [("krow", 4, 4), ("krow", 4, 2), ("krow", 2, 4), ("krow", 2, 2), ("strip", 4, 4)]
+
+
+def _select(monkeypatch, kern, ns, k):
+    monkeypatch.setenv("GSA_SPARSE_KERNEL", kern)
+    monkeypatch.setenv("GSA_KROW_NS", str(ns))
+    monkeypatch.setenv("GSA_KROW_K", str(k))
 
 
 @pytest.mark.parametrize("kern,ns,k", KERNELS)
 @pytest.mark.parametrize("R,C,tBx,related", [(1, 1, 64, False), (63, 2000, 64, False), (1500, 700, 80, True),
-                                             (2049, 3001, 256, True), (4100, 1030, 512, False)])
+                                             (2049, 3001, 256, True), (4100, 1030, 512, False),
+                                             (700, 1900, 96, True), (1100, 1777, 112, False), (3000, 2500, 128, True),
+                                             (130, 5000, 64, True)])
 def test_sparse_kernel_matches_oracle(engine, golden, monkeypatch, kern, ns, k, R, C, tBx, related):
-    monkeypatch.setenv("GSA_SPARSE_KERNEL", kern)
-    monkeypatch.setenv("GSA_KROW_NS", str(ns))
-    monkeypatch.setenv("GSA_KROW_K", str(k))
+    _select(monkeypatch, kern, ns, k)
     Y, X = related_pair(max(R, C), 31) if related else random_pair(R, C, 17)
     Y, X = Y[:R + 1], X[:C + 1]
     res = engine.align_sparse(Y, X, golden.blosum62, -11, tileBx=tBx)
@@ -34,9 +41,7 @@ def test_sparse_kernel_batch_matches_oracle(golden, monkeypatch, kern, ns, k):
     """A batched launch (tickets of several pairs interleaved) in each geometry."""
     import torch
     from gpuseqalign_amd import shard
-    monkeypatch.setenv("GSA_SPARSE_KERNEL", kern)
-    monkeypatch.setenv("GSA_KROW_NS", str(ns))
-    monkeypatch.setenv("GSA_KROW_K", str(k))
+    _select(monkeypatch, kern, ns, k)
     if not torch.cuda.is_available():
         pytest.skip("no GPU visible")
     pairs = shard.synthetic_batch(12, 300, 2600, seed0=77)
