@@ -256,9 +256,6 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
         }
         stamp(1);
         if constexpr ((GSA_KRKNOB & 1) == 0) halo_load(b);
-        // block b-1's hand-off, behind this block's halo reads (LDS executes a wave's operations in
-        // order: written before them, the halo would wait for the writes)
-        if (b > 0) handoff(b - 1);
         flag_st(c_in, kBlk * b + 64 + kBlk);
         const uint32_t pn = q_off(b + 1);
         int va[CAP ? K : 1][CAP ? kBlk : 1];
@@ -304,6 +301,10 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
             }
         }
         stamp(2);
+        // the block's hand-off at its end (the next strip sees it a block earlier than when it is
+        // written behind the next block's halo reads: measured 1 % faster at 100k, slightly slower
+        // per block)
+        handoff(b);
         if (CAP && cap)
         {
             // this lane's columns lo .. lo+15; boundaries nb0 (>= 16b-63) and nb0 + tBx
@@ -363,7 +364,6 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
         if (b + 1 >= NB) break;
         if (!block(b + 1, qB, qA, F(), advance(b + 1))) return;
     }
-    handoff(NB - 1);
 }
 
 // ------------------------------------------------------------------------------------

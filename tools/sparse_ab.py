@@ -13,11 +13,11 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--variants", default="strip:4,krow:4:4,krow:4:2,krow:2:4")
 ap.add_argument("--reps", type=int, default=10)
 ap.add_argument("--tileBx", type=int, default=256)
-ap.add_argument("--shapes", default="", help="RxC,...: random pairs instead of the config-3 pair")
+ap.add_argument("--shapes", default="", help="RxC,... (random pairs) or config3 (the headline pair); default config3")
 a = ap.parse_args()
 from gpuseqalign_amd import formats as F
 sub = bench.subst_blosum62()
-shapes = [tuple(map(int, t.split("x"))) for t in a.shapes.split(",") if t] or [None]
+shapes = [None if t == "config3" else tuple(map(int, t.split("x"))) for t in a.shapes.split(",") if t] or [None]
 for shp in shapes:
   if shp:
     Y, X = F.synthetic_seq(shp[0], 11), F.synthetic_seq(shp[1], 12)
