@@ -312,7 +312,7 @@ def main():
             "golden_match": None if gold_cost is None else all(c == gold_cost for c in costs),
             "fill_10k_full": full10k, "config4": cfg4,
         }
-        if not a.no_cpu_baseline:
+        if not a.no_cpu_baseline and world == 1:  # the CPU leg runs on rank 0 at N = 1 only
             out["cpu_baseline"] = cpu_baseline(Y, X, sub, budget_s=a.cpu_budget)
         print(json.dumps(out), flush=True)
     if world > 1:

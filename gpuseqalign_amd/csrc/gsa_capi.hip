@@ -42,7 +42,6 @@ struct gsa_ctx
     unsigned epoch = 0;
     int last_hip_error = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
-    unsigned long long* dbg = nullptr;  // stamp buffer of diagnostic builds
     // scratch buffers for the host-buffer entry points (grow-only, like DeviceArray::init)
     void* dbuf[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
     size_t dcap[5] = {0, 0, 0, 0, 0};
@@ -68,9 +67,6 @@ struct gsa_ctx
     size_t sbnd_cap = 0;
     // mlsppt: host-mapped per-ticket completion flags and the copy-back stream
     unsigned* ptflags = nullptr;
-    // ring-mode full fills: ring + descriptors + head/tail/final words of the strip workgroups
-    int* ringbuf = nullptr;
-    size_t ringbuf_cap = 0;
     size_t ptflags_cap = 0;
     hipStream_t cstream = nullptr;
     unsigned long long* sctl = nullptr;  // [0] ticket|err, [1] best key, [2] result
@@ -143,27 +139,6 @@ int check_inputs(int32_t adjrows, int32_t adjcols, int32_t substsz)
     return GSA_SUCCESS;
 }
 
-// Strip waves per workgroup of full fills (1 or 2: each strip stages its output in 36 KB of
-// LDS); GSA_FULL_NS overrides the default for experiments.
-int full_ns()
-{
-    static int ns = [] {
-        const char* e = std::getenv("GSA_FULL_NS");
-        int v = e ? std::atoi(e) : gsa::kFullNSDefault;
-        return (v == 1 || v == 2) ? v : gsa::kFullNSDefault;
-    }();
-    return ns;
-}
-
-// Full fills run on the one-row-per-lane kernel (nw_lane.hip) unless GSA_FULL_KERNEL=strip
-// selects the 4-rows-per-lane strip kernel (nw_strip.hip); GSA_LANE_NS = lane strips per
-// workgroup (1..4, 6, 8).  Both read per launch.
-bool full_lane_enabled()
-{
-    const char* e = std::getenv("GSA_FULL_KERNEL");
-    return !(e && std::strcmp(e, "strip") == 0);
-}
-
 // Sparse fills run on the K-rows-per-lane kernel (nw_krow.hip, K = 4): 6.8 vs 8.0 ms for the
 // 100k pair and 5.2 vs 4.3 TCUPS for 512 pairs of 20k against the strip kernel (nw_strip.hip),
 // which mlsppt keeps.  GSA_SPARSE_KERNEL=strip forces the strip kernel (read per launch, tested);
@@ -182,21 +157,13 @@ int env_int(const char* name, int dflt)
 }
 
 
+// Full fills run on the one-row-per-lane kernel (nw_lane.hip); GSA_LANE_NS = lane strips per
+// workgroup (1..4, 6, 8; read per launch, tested; 4 is the default and the fastest measured).
 int lane_ns()
 {
     const char* e = std::getenv("GSA_LANE_NS");
     const int v = e ? std::atoi(e) : gsa::kLaneNSDefault;
     return ((v >= 1 && v <= 4) || v == 6 || v == 8) ? v : gsa::kLaneNSDefault;
-}
-
-// Ring mode for full fills (nw_strip.hip): the output leaves the strip CUs through L2-resident
-// rings drained by copy workgroups on otherwise idle CUs.  Opt-in (GSA_FULL_RING=1, read per
-// launch): measured slower than the store waves -- the agent-scope
-// write-backs that make the ring visible across XCDs cost more than the strip saves.
-bool full_ring_enabled()
-{
-    const char* e = std::getenv("GSA_FULL_RING");
-    return e && std::atoi(e) == 1;
 }
 
 // NULL is the HIP null stream, as everywhere in HIP; the host-buffer entry points use the
@@ -207,8 +174,7 @@ hipStream_t pick_stream(gsa_ctx*, void* stream) { return (hipStream_t)stream; }
 long long held_bytes(const gsa_ctx* c)
 {
     long long b = 256 + 64 + (long long)c->gran_elems * 8 + (long long)c->desc_cap * (long long)sizeof(gsa::PairDesc) +
-                  (long long)c->tmoves_cap + (long long)c->tdirs_cap * 4 + (long long)c->sbnd_cap * 4 +
-                  (long long)c->ringbuf_cap * 4;
+                  (long long)c->tmoves_cap + (long long)c->tdirs_cap * 4 + (long long)c->sbnd_cap * 4;
     for (size_t k : c->dcap) b += (long long)k;
     return b;
 }
@@ -370,7 +336,7 @@ int enqueue_batch(gsa_ctx* ctx, int mode, int npairs, const gsa_pair_dev* pairs,
     a.subst = subst;
     a.substsz = substsz;
     a.g = gapo;
-    const bool lane = mode == gsa::kModeFull && full_lane_enabled();
+    const bool lane = mode == gsa::kModeFull;
     // mlsppt (done flags per tile row) stays on the strip kernel
     const bool krow = mode == gsa::kModeSparse && !done && sparse_kernel() == kSpKrow;
     int krowK = env_int("GSA_KROW_K", gsa::kKrowKDefault), krowNS = env_int("GSA_KROW_NS", gsa::kKrowNSDefault);
@@ -379,10 +345,10 @@ int enqueue_batch(gsa_ctx* ctx, int mode, int npairs, const gsa_pair_dev* pairs,
         krowK = gsa::kKrowKDefault;
         krowNS = gsa::kKrowNSDefault;
     }
-    a.ns = (mode == gsa::kModeFull) ? (lane ? lane_ns() : full_ns()) : krow ? krowNS : gsa::kSparseNS;
+    a.ns = lane ? lane_ns() : krow ? krowNS : gsa::kSparseNS;
     // sparse tickets per tile row: a K-rows super-strip can be a fraction of the tile height
     const int perTileRow = krow ? gsa::kSparseTileBy / gsa::krow_ticket_rows(krowNS, krowK) : 1;
-    const int fullRows = lane ? gsa::kLaneRows * a.ns : gsa::kWaveRows * a.ns;  // rows per ticket
+    const int fullRows = gsa::kLaneRows * a.ns;  // rows per ticket of a full fill
     if (mode == gsa::kModeSparse)
     {
         if (tileBx < 64 || tileBx % 16 != 0) return GSA_ERROR_INVALID_VALUE;
@@ -493,7 +459,6 @@ int enqueue_batch(gsa_ctx* ctx, int mode, int npairs, const gsa_pair_dev* pairs,
     a.ticket = ctx->ctl;
     a.err = ctx->ctl + 1;
     a.spin = ctx->spin_ticks;
-    a.dbg = ctx->dbg;
     a.done = done;
     a.epoch = ++ctx->epoch;
     if (a.epoch == 0) a.epoch = ++ctx->epoch;  // 0 is the cleared-tag value
@@ -501,39 +466,9 @@ int enqueue_batch(gsa_ctx* ctx, int mode, int npairs, const gsa_pair_dev* pairs,
     if (e != hipSuccess) return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
     // one pair: one workgroup per CU (its tickets are a chain); a batch: all resident slots
     int grid = (npairs == 1) ? std::max(1, std::min((int)tickets, ctx->cu_count)) : 0;
-    int launchMode = mode;
-    if (mode == gsa::kModeFull && !lane && npairs == 1 && a.ns == 1 && !done && full_ring_enabled() && tickets >= 8 &&
-        2 * std::min<long long>(tickets, ctx->cu_count / 2) <= ctx->cu_count)
-    {
-        // nStrip a multiple of 8: copy workgroup nStrip+s then sits on strip s's XCD
-        int nStrip = (int)std::min<long long>(tickets, ctx->cu_count / 2);
-        nStrip -= nStrip % 8;
-        const size_t ringInts = (size_t)nStrip * gsa::kRingBlocks * 4096;
-        const size_t ctlInts = (size_t)nStrip * (gsa::kRingBlocks * 2 + 1 + gsa::kRingWaves + 1);
-        if (ctx->ringbuf_cap < ringInts + ctlInts)
-        {
-            if (ctx->ringbuf) (void)hipFree(ctx->ringbuf);
-            ctx->ringbuf = nullptr;
-            ctx->ringbuf_cap = 0;
-            if ((e = hipMalloc(&ctx->ringbuf, (ringInts + ctlInts) * sizeof(int))) != hipSuccess)
-                return fail(ctx, e, GSA_ERROR_MEMORY_ALLOCATION);
-            ctx->ringbuf_cap = ringInts + ctlInts;
-        }
-        a.ring = ctx->ringbuf;
-        a.rdesc = a.ring + ringInts;
-        a.rhead = a.rdesc + (size_t)nStrip * gsa::kRingBlocks * 2;
-        a.rtail = a.rhead + nStrip;
-        a.rfinal = a.rtail + (size_t)nStrip * gsa::kRingWaves;
-        a.nStrip = nStrip;
-        // head / tail / final words start at 0 every launch
-        e = hipMemsetAsync(a.rhead, 0, (size_t)nStrip * (2 + gsa::kRingWaves) * sizeof(int), st);
-        if (e != hipSuccess) return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
-        launchMode = gsa::kModeFullRing;
-        grid = 2 * nStrip;
-    }
     e = lane    ? gsa::launch_lane_fill(a, a.ns, grid, st)
         : krow  ? gsa::launch_krow_fill(a, krowNS, krowK, 0, grid, st)
-                : gsa::launch_strip_fill(a, launchMode, grid, st);
+                : gsa::launch_strip_fill(a, mode, grid, st);
     if (e != hipSuccess) return fail(ctx, e, GSA_ERROR_KERNEL_FAILURE);
     note_launch(ctx);
     return GSA_SUCCESS;
@@ -571,10 +506,6 @@ int gsa_ctx_create(int device, gsa_ctx** out)
     if (e == hipSuccess) e = hipEventCreate(&ctx->ev1);
     for (int k = 0; k < gsa_ctx::kStage && e == hipSuccess; ++k)
         e = hipEventCreateWithFlags(&ctx->stage_ev[k], hipEventDisableTiming);
-#if defined(GSA_STAMP) && GSA_STAMP
-    if (e == hipSuccess) e = hipMalloc(&ctx->dbg, 16 * 256 * 4 * sizeof(unsigned long long));
-    if (e == hipSuccess) e = hipMemset(ctx->dbg, 0, 16 * 256 * 4 * sizeof(unsigned long long));
-#endif
     if (e != hipSuccess)
     {
         int code = (int)e;
@@ -603,13 +534,11 @@ void gsa_ctx_destroy(gsa_ctx* ctx)
     if (ctx->sctl) (void)hipFree(ctx->sctl);
     if (ctx->ptflags) (void)hipHostFree(ctx->ptflags);
     if (ctx->cstream) (void)hipStreamDestroy(ctx->cstream);
-    if (ctx->ringbuf) (void)hipFree(ctx->ringbuf);
     for (int k = 0; k < gsa_ctx::kStage; ++k)
     {
         if (ctx->stage[k]) (void)hipHostFree(ctx->stage[k]);
         if (ctx->stage_ev[k]) (void)hipEventDestroy(ctx->stage_ev[k]);
     }
-    if (ctx->dbg) (void)hipFree(ctx->dbg);
     if (ctx->ctl) (void)hipFree(ctx->ctl);
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
@@ -619,15 +548,6 @@ void gsa_ctx_destroy(gsa_ctx* ctx)
 
 int gsa_last_hip_error(const gsa_ctx* ctx) { return ctx ? ctx->last_hip_error : 0; }
 
-#if defined(GSA_STAMP) && GSA_STAMP
-// diagnostic builds only: copy the stamp buffer out
-int gsa_debug_stamps(gsa_ctx* ctx, unsigned long long* out, int n)
-{
-    if (!ctx || !ctx->dbg) return GSA_ERROR_INVALID_VALUE;
-    hipError_t e = hipMemcpy(out, ctx->dbg, (size_t)n * sizeof(unsigned long long), hipMemcpyDeviceToHost);
-    return e == hipSuccess ? GSA_SUCCESS : GSA_ERROR_MEMORY_TRANSFER;
-}
-#endif
 
 int gsa_device_cu_count(const gsa_ctx* ctx) { return ctx ? ctx->cu_count : 0; }
 

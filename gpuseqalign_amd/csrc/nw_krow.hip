@@ -10,11 +10,14 @@
 // Cost model of one pair.  The fill is a wavefront: strip waves of 64K rows (lane l owns rows
 // r0+Kl .. r0+Kl+K-1 and at step t works on column t-l) follow each other ~6 blocks of 16 steps
 // apart (the 64-lane skew, one block of hand-off granularity, the progress check), so a pair
-// takes (C/16 + 6 * R/(64K)) block times.  A block costs ~16 * (K+1) dependent VALU of step
-// chain plus a fixed ~700 cycles of side work (halo and profile reads, hand-off writes, progress
-// words, header-column capture; measured with tools/p2_stamps.py), so the side work, not the
-// arithmetic, sets the block time, and more rows per lane cut the lag term: K = 4 is ~2x fewer
-// strips than K = 2 for a block ~10 % longer (profiles/r02_sparse_kernels.txt).
+// takes (C/16 + 6 * R/(64K)) block times.  One wave issues at most one VALU per ~4.5 cycles, so
+// the 2K+1 VALU of a step cost ~41 cycles at K = 4 whatever the dependency chain (splitting the
+// lane's rows into two groups a column apart halves the chain and changes nothing); the LDS
+// side work of a block (16 profile reads, 4 halo reads, 4 hand-off writes, 5 progress words)
+// costs ~12-40 cycles per instruction of the wave's time and, with the header-column capture
+// and the block's scalar control, about as much as the 16 steps (tools/ubench/lds_ubench.hip,
+// profiles/r02_krow_breakdown.txt, profiles/r02_krow_probes.txt).  K = 4 halves the strips of
+// K = 2 for a block ~25 % longer.
 //
 // Step, shifted values H' = H - (i+j)*g (borders 0), K+1 dependent VALU + K adds:
 //     up    = dpp_shr1(H[K-1]) + halo    lane 0: H'(row above, c) from the ring; others + 0
@@ -62,17 +65,6 @@ constexpr uint32_t kFCons = 64, kFXo = 128, kFTicket = 132;
 
 extern __shared__ __attribute__((aligned(16))) char krsm[];
 
-// Diagnostic stamps (separate build, tools/p2_stamps.py): s_memtime at 4 points of blocks
-// 64..319 of the strips of tickets 0 and 1, dbg[(tk*NS + w)*1024 + (b-64)*4 + k]
-#ifndef GSA_KRSTAMP
-#define GSA_KRSTAMP 0
-#endif
-// Timing-experiment knobs (tools/build_kr_knobs.sh; any set bit makes results WRONG): 1 no halo
-// reads, 4 no hand-off writes, 8 strips never wait, 16 no mid-block progress reads, 32 no
-// header-column capture
-#ifndef GSA_KRKNOB
-#define GSA_KRKNOB 0
-#endif
 
 typedef int int4v __attribute__((ext_vector_type(4)));
 template <typename T>
@@ -175,7 +167,6 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
     // block b needs its halo (ring elements 16b+64 .. 16b+79), room in ring_out for elements
     // 16b .. 16b+15, and (strip 0; the others trail it) the profile of block b+1 (columns < 16b+32)
     auto ok = [&](int pin, int pco, int pxo, int b) {
-        if constexpr ((GSA_KRKNOB & 8) != 0) return true;
         return pin >= kBlk * b + 64 + kBlk && pco >= kBlk * b + kBlk - kRing && (w != 0 || pxo >= kBlk * b + 2 * kBlk);
     };
     // the error word is a global load, which waits for this wave's outstanding header stores
@@ -226,13 +217,10 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
     // hand-off of block bb: every lane writes (lane 63 into the ring, the others into the sink,
     // no exec mask), then the progress word
     auto handoff = [&](int bb) {
-        if constexpr ((GSA_KRKNOB & 4) == 0)
-        {
         const uint32_t eb = (lane == 63) ? ring_out + 4u * (uint32_t)((kBlk * bb) & (kRing - 1)) : hsink;
 #pragma unroll
         for (int j = 0; j < kHalo; ++j)
             lds_st4(eb + ((lane == 63) ? 16u * j : 0u), int4v {lt[4 * j], lt[4 * j + 1], lt[4 * j + 2], lt[4 * j + 3]});
-        }
         flag_st(f_out, bb + 1 == NB ? kBig : kBlk * bb + kBlk);
     };
     int rpin = 0, rpco = 0, rpxo = 0;  // progress words read in mid-block, checked at the next block
@@ -242,20 +230,13 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
     // bodies get different register assignments and ~100 v_mov per block to reconcile them.
     auto block = [&](int b, int (&qc)[K][8], int (&qn)[K][8], auto rampT, bool cap) {
         constexpr bool RAMP = decltype(rampT)::value;
-        constexpr bool CAP = !RAMP && (GSA_KRKNOB & 32) == 0;  // ramp blocks hold no boundary (tBx >= 64)
-        auto stamp = [&](int k) {
-            if constexpr (GSA_KRSTAMP != 0)
-                if (tk < 2 && b >= 64 && b < 320 && lane == 0 && a.dbg)
-                    a.dbg[(size_t)(tk * NS + w) * 1024 + (b - 64) * 4 + k] = __builtin_amdgcn_s_memtime();
-        };
-        stamp(0);
+        constexpr bool CAP = !RAMP;  // ramp blocks hold no boundary (tBx >= 64)
         {
             const int pin = __builtin_amdgcn_readfirstlane(rpin), pco = __builtin_amdgcn_readfirstlane(rpco);
             const int pxo = (w == 0) ? __builtin_amdgcn_readfirstlane(rpxo) : 0;
             if (!ok(pin, pco, pxo, b) && !spin(b)) return false;
         }
-        stamp(1);
-        if constexpr ((GSA_KRKNOB & 1) == 0) halo_load(b);
+        halo_load(b);
         flag_st(c_in, kBlk * b + 64 + kBlk);
         const uint32_t pn = q_off(b + 1);
         int va[CAP ? K : 1][CAP ? kBlk : 1];
@@ -293,14 +274,13 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
                 H[k] = nh[k];
                 if constexpr (CAP) va[k][u] = nh[k];
             }
-            if ((GSA_KRKNOB & 16) == 0 && u == kBlk / 2)
+            if (u == kBlk / 2)
             {
                 rpin = raw_ld(f_in);
                 rpco = raw_ld(c_out);
                 rpxo = raw_ld(f_xo);
             }
         }
-        stamp(2);
         // the block's hand-off at its end (the next strip sees it a block earlier than when it is
         // written behind the next block's halo reads: measured 1 % faster at 100k, slightly slower
         // per block)
@@ -336,7 +316,6 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
                 }
             }
         }
-        stamp(3);
         return true;
     };
 

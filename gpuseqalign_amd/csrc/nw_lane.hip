@@ -48,91 +48,20 @@ namespace {
 __host__ __device__ constexpr int lane_lw(int ns) { return ns >= 5 ? 1024 : 512; }
 __host__ __device__ constexpr int lane_qrs(int ns) { return lane_lw(ns) + 32; }  // Q row stride in dwords: == 0 mod 32, 32 guard columns
 constexpr int kLRing = 512;        // hand-off ring elements per strip boundary (power of 2)
-// Output transposed across lanes before the stores (1) or one row per lane per store (0)
-#ifndef GSA_LXPOSE
-#define GSA_LXPOSE 1
-#endif
-#ifndef GSA_LBLK
-#define GSA_LBLK 16
-#endif
-constexpr int kLBlk = GSA_LBLK;    // steps per block (8 or 16)
-static_assert(kLBlk == 8 || kLBlk == 16, "block");
+constexpr int kLBlk = 16;          // steps per block
 constexpr int kLH = kLBlk / 4;     // halo registers (int4) per block
-static_assert(!GSA_LXPOSE || kLBlk == 16, "transposed stores: 4 chunks per block");
-// Halo read by all lanes (lanes >= 1 read a row of g from gfill: no exec mask or branch; 1,
-// default since the just-in-time halo: 10k 1.030 -> 1.020 ms) or by lane 0 alone (0).
-// Option: progress words read at block start (1) or in mid-block (0)
-#ifndef GSA_LHALO_ALL
-#define GSA_LHALO_ALL 1
-#endif
-#ifndef GSA_LFLAG_EARLY
-#define GSA_LFLAG_EARLY 0
-#endif
-// Lane 63's hand-off writes: all lanes write (the others into a per-strip sink), so the 4
-// ds_write_b128 need no exec mask (1), or lane 63 alone (0)
-#ifndef GSA_LHAND_ALL
-#define GSA_LHAND_ALL 1
-#endif
-#ifndef GSA_LSCHED_BARRIER
-#define GSA_LSCHED_BARRIER 0
-#endif
-// interior output stores as buffer stores (scalar base + 32-bit lane offsets) (1) or global
-// stores with 64-bit lane addresses (0, default: 1 measured 1-4 % slower on one 10k pair and
-// ~9 % slower on a 64-pair batch in same-box A/B runs, profiles/r01_lane_knobs_handoff.txt)
-#ifndef GSA_LBUFST
-#define GSA_LBUFST 0
-#endif
-// Halo (row above, lane 0) of block b read at the start of block b (1) or prefetched during
-// block b-1 (0).  The prefetch makes each strip wait one more block (16 steps) for the strip
-// above on every hop.
-#ifndef GSA_LHALO_JIT
-#define GSA_LHALO_JIT 1
-#endif
-constexpr int kLHaloAhead = GSA_LHALO_JIT ? 1 : 2;  // halo blocks needed at block start
-// Output path: 0 = every lane stores its own row (dwordx4 stores, 64 rows per store
-// instruction); 1 = rows staged in LDS and stored row-contiguously (8 lanes x 16 B per row),
-// one pair of blocks behind.  1 measured slower on one strip (114 vs 78 cycles/step) with no
-// change in the hand-off lags (profiles/r01_lane_probe.jsonl), so 0 is the default.
-#ifndef GSA_LSTAGE
-#define GSA_LSTAGE 0
-#endif
 constexpr int kLBig = 0x3fffffff;  // "everything published"
+// Variants measured and not kept (round 1, profiles/): lane-63-only halo reads and hand-off
+// writes behind an exec mask (slower by 10-15 cycles/step), the halo prefetched a block ahead
+// (one more block of lag per hop), output staged in LDS (114 vs 78 cycles/step), one row per
+// lane per store (the CU's requests delay the granule polls), buffer stores (1-4 % slower),
+// 8-step blocks.
 
 extern __shared__ __attribute__((aligned(16))) char lsm[];
-
-// Timing-experiment knobs (separate builds only; any set bit makes results WRONG):
-// 1 no global stores, 2 strips never wait, 4 no hand-off writes, 8 no halo reads, 16 no Q reads,
-// 32 no mid-block progress reads, 64 no progress stores by strips
-#ifndef GSA_LKNOB
-#define GSA_LKNOB 0
-#endif
-#ifndef GSA_STAMP
-#define GSA_STAMP 0
-#endif
-// Diagnostic stamps (separate build): s_memrealtime (100 MHz, one clock for all XCDs) at the start of every 8th block of the strip
-// waves of strips s = 0, S, .., 15S (S = GSA_STAMP_STRIDE), dbg[(s / S) * 160 + b / 8] (b < 1280).
-#ifndef GSA_STAMP_STRIDE
-#define GSA_STAMP_STRIDE 1
-#endif
-template <int NS>
-__device__ __forceinline__ void lstamp(const StripArgs& a, int tk, int w, int b, int k, int lane)
-{
-    if constexpr (GSA_STAMP)
-    {
-        const int s = tk * NS + w;
-        if (k == 0 && s % GSA_STAMP_STRIDE == 0 && s < 16 * GSA_STAMP_STRIDE && (b & 7) == 0 && b < 1280 && lane == 0 && a.dbg)
-        {
-            unsigned long long t;
-            asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-            a.dbg[(size_t)(s / GSA_STAMP_STRIDE) * 160 + (b >> 3)] = t;
-        }
-    }
-}
 
 
 typedef int int4v __attribute__((ext_vector_type(4)));
 typedef int int4a __attribute__((ext_vector_type(4), aligned(4)));
-typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 template <typename T>
 using gptr = __attribute__((address_space(1))) T*;
 template <typename T>
@@ -163,33 +92,14 @@ __device__ __forceinline__ bool err_set(const StripArgs& a)
 // lane l <- lane l-1, lane 0 <- 0 (DPP wave_shr:1, bound_ctrl zero)
 __device__ __forceinline__ int shr1z(int v) { return __builtin_amdgcn_update_dpp(0, v, 0x138, 0xF, 0xF, true); }
 
-// link stamps (stamp builds): s_memrealtime when the drain wave of ticket 0 has stored, and the
-// feed wave of ticket 1 has fed, the columns below 64k (dbg[2560 + k], dbg[2800 + k], k < 200)
-__device__ __forceinline__ void link_stamp(const StripArgs& a, int base, int oldc, int newc, int lane)
-{
-    if constexpr (GSA_STAMP)
-    {
-        if (lane == 0 && a.dbg && (oldc >> 6) != (newc >> 6) && (newc >> 6) < 200)
-        {
-            unsigned long long t;
-            asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-            for (int k = (oldc >> 6) + 1; k <= (newc >> 6) && k < 200; ++k) a.dbg[base + k] = t;
-        }
-    }
-}
-
 // LDS: Q profile, transposed substitution table subT[x][y] = s(y, x) - g (rows of kLSubRow
 // dwords, so one lane gathers 4 row letters per ds_read_b128), NS+1 hand-off rings, progress words.
 // flags: prog[i] @ 4i (ring i holds elements < prog[i]), cons[i] @ 64+4i (ring i's reader no
 // longer needs elements < cons[i]), xo @ 128 (Q holds columns < xo), ticket @ 132.
 struct LaneLds
 {
-    uint32_t q, stage, sub, ring, gfill, sink, flags;
+    uint32_t q, sub, ring, gfill, sink, flags;
 };
-// Output stage per strip: 2 buffers of [64 rows][32 steps] int32 (128-byte rows of 8 16-byte
-// chunks, chunk index XOR row & 7: conflict-free for the strip's row writes and its row-segment
-// read-back, 8 lanes per row)
-constexpr uint32_t kStageBytes = 64u * 128u;
 constexpr uint32_t kFCons = 64, kFXo = 128, kFTicket = 132;  // prog/cons: NS + 1 <= 16 words each
 constexpr int kLSubRow = 36;  // dwords per subT row: 32 letters + 4 (16-byte aligned rows)
 
@@ -197,12 +107,11 @@ __host__ __device__ inline LaneLds lane_layout(int ns, int substsz)
 {
     LaneLds L;
     L.q = 0;
-    L.stage = (uint32_t)substsz * lane_qrs(ns) * 4u;
-    L.sub = L.stage + (GSA_LSTAGE ? (uint32_t)ns * 2u * kStageBytes : 0u);
+    L.sub = (uint32_t)substsz * lane_qrs(ns) * 4u;
     L.ring = L.sub + (uint32_t)substsz * kLSubRow * 4u;
     L.gfill = L.ring + (uint32_t)(ns + 1) * kLRing * 4u;  // 16 x g: the "halo" of lanes >= 1
-    L.sink = L.gfill + 64u;                                // GSA_LHAND_ALL: lanes 0..62's hand-off writes
-    L.flags = L.sink + (GSA_LHAND_ALL ? (uint32_t)ns * 1024u : 0u);
+    L.sink = L.gfill + 64u;                                // lanes 0..62's hand-off writes
+    L.flags = L.sink + (uint32_t)ns * 1024u;
     return L;
 }
 
@@ -229,28 +138,15 @@ __device__ __forceinline__ void lane_strip(const StripArgs& a, const LaneLds& L,
     const uint32_t hsink = L.sink + (uint32_t)w * 1024u + 16u * (uint32_t)lane;
     const int NB = (C + 65 + kLBlk - 1) / kLBlk;  // lane 63 reaches step C+64 (element of column C)
     const int rg = r * g;
-    // output stage: this lane writes its row; for the read-back lane = 8 * srow + sq reads rows
-    // 8i + srow, chunk sq (steps 32p + 4sq ..) and stores them to columns 32p + 4sq - row
-    const uint32_t stg = L.stage + (uint32_t)w * (2u * kStageBytes);
-    const uint32_t stg_w = stg + 128u * (uint32_t)lane;
-    const int srow = lane >> 3, sq = lane & 7;
-    const uint32_t stg_r = stg + 128u * (uint32_t)srow + 16u * (uint32_t)(sq ^ srow);
-    const gptr<int> obase = G(a.score) + (size_t)(r0 + srow) * (size_t)a.ld;
-    const int rlim = a.R - r0 - srow;  // row 8i + srow of the strip is in the matrix iff 8i <= rlim
-    const gptr<int> orow = G(a.score) + (size_t)(live ? r : 0) * (size_t)a.ld;  // GSA_LSTAGE 0
-    // GSA_LXPOSE: column 16b of row r0 + (lane & 15), shifted by the lane's chunk 4 * (lane >> 4)
-    // and the row's skew; + 16k(ld-1) for row r0 + 16k + (lane & 15)
+    // transposed output: column 16b of row r0 + (lane & 15), shifted by the lane's chunk
+    // 4 * (lane >> 4) and the row's skew; + 16k(ld-1) for row r0 + 16k + (lane & 15)
     const gptr<int> xbase = G(a.score) + (ptrdiff_t)(r0 + (lane & 15)) * a.ld + 4 * (lane >> 4) - (lane & 15);
     const uint32_t xoff = (uint32_t)(lane & 15) * (uint32_t)(a.ld - 1) + 4u * (uint32_t)(lane >> 4);  // from row r0 + 16k
-    // GSA_LBUFST: the strip's 64 rows as one buffer resource (interior blocks only: r0 + 63 <= R)
-    const __amdgpu_buffer_rsrc_t srsrc = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(a.score + (size_t)r0 * (size_t)a.ld), 0, (int)min((long long)64 * a.ld * 4, 0x7fffffffll), 0x00020000);
 
     // block b prefetches block b+1's inputs (ring elements < B(b+1)+64+B, Q columns < B(b+1)+B,
     // B = kLBlk) and writes ring elements Bb .. Bb+B-1
     auto ok = [&](int pin, int pco, int pxo, int b) {
-        if constexpr ((GSA_LKNOB & 2) != 0) return true;
-        return pin >= kLBlk * b + 64 + kLHaloAhead * kLBlk && pco >= kLBlk * b + kLBlk - kLRing && (w != 0 || pxo >= kLBlk * b + 2 * kLBlk);
+        return pin >= kLBlk * b + 64 + kLBlk && pco >= kLBlk * b + kLBlk - kLRing && (w != 0 || pxo >= kLBlk * b + 2 * kLBlk);
     };
     auto spin = [&](int b) {
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
@@ -266,21 +162,13 @@ __device__ __forceinline__ void lane_strip(const StripArgs& a, const LaneLds& L,
             }
         }
     };
-    // halo of block bb: ring elements B*bb+64 .. +B-1 (lane 0; lanes >= 1 keep / read g)
-    const uint32_t halo_base = (GSA_LHALO_ALL && lane != 0) ? L.gfill : ring_in;
+    // halo of block bb, read at the start of block bb: ring elements B*bb+64 .. +B-1 (lane 0;
+    // lanes >= 1 read a row of g: no exec mask or branch)
+    const uint32_t halo_base = (lane != 0) ? L.gfill : ring_in;
     auto halo_load = [&](int bb, int4v (&h)[kLH]) {
-        if constexpr (GSA_LHALO_ALL)
-        {
-            const uint32_t hb = halo_base + (lane == 0 ? 4u * (uint32_t)((kLBlk * bb + 64) & (kLRing - 1)) : 0u);
+        const uint32_t hb = halo_base + (lane == 0 ? 4u * (uint32_t)((kLBlk * bb + 64) & (kLRing - 1)) : 0u);
 #pragma unroll
-            for (int j = 0; j < kLH; ++j) h[j] = lds_ld4(hb + 16u * (lane == 0 ? j : 0));
-        }
-        else if (lane == 0)
-        {
-            const uint32_t hb = ring_in + 4u * (uint32_t)((kLBlk * bb + 64) & (kLRing - 1));
-#pragma unroll
-            for (int j = 0; j < kLH; ++j) h[j] = lds_ld4(hb + 16u * j);
-        }
+        for (int j = 0; j < kLH; ++j) h[j] = lds_ld4(hb + 16u * (lane == 0 ? j : 0));
     };
 
     int qA[kLBlk], qB[kLBlk];
@@ -292,35 +180,25 @@ __device__ __forceinline__ void lane_strip(const StripArgs& a, const LaneLds& L,
         const uint32_t qb = qrow + 4u * (uint32_t)((-lane) & (kLW - 1));
 #pragma unroll
         for (int u = 0; u < kLBlk; ++u) qA[u] = lds_ld(qb + 4u * u);
-        if constexpr (!GSA_LHALO_JIT) halo_load(0, hA);
     }
     int H = rg, U = rg;
     int rpin = 0, rpco = 0, rpxo = 0;  // progress words read in the previous block, checked now
 
     auto block = [&](int b, int (&qc)[kLBlk], int (&qn)[kLBlk], int4v (&hc)[kLH], int4v (&hn)[kLH], auto rampT) {
         constexpr bool RAMP = decltype(rampT)::value;
-        lstamp<NS>(a, tk, w, b, 0, lane);
         {
             const int pin = __builtin_amdgcn_readfirstlane(rpin), pco = __builtin_amdgcn_readfirstlane(rpco);
             const int pxo = (w == 0) ? __builtin_amdgcn_readfirstlane(rpxo) : 0;
             if (!ok(pin, pco, pxo, b) && !spin(b)) return false;
         }
-        if (GSA_LFLAG_EARLY && !(GSA_LKNOB & 32))
-        {
-            rpin = raw_ld(f_in);
-            rpco = raw_ld(c_out);
-            rpxo = raw_ld(f_xo);
-        }
-        if constexpr (GSA_LHALO_JIT && !(GSA_LKNOB & 8)) halo_load(b, hc);
-        // prefetch block b+1: Q of columns B(b+1)-l .. +B-1 (and the halo unless GSA_LHALO_JIT)
+        halo_load(b, hc);
+        // prefetch block b+1: Q of columns B(b+1)-l .. +B-1
         {
             const uint32_t qb = qrow + 4u * (uint32_t)((kLBlk * b + kLBlk - lane) & (kLW - 1));
 #pragma unroll
-            for (int u = 0; u < kLBlk; ++u) qn[u] = (GSA_LKNOB & 16) ? qc[u] ^ 1 : lds_ld(qb + 4u * u);
-            if constexpr (!(GSA_LKNOB & 8) && !GSA_LHALO_JIT) halo_load(b + 1, hn);
-            if constexpr (!(GSA_LKNOB & 64)) flag_st(c_in, kLBlk * b + 64 + kLHaloAhead * kLBlk);
+            for (int u = 0; u < kLBlk; ++u) qn[u] = lds_ld(qb + 4u * u);
+            flag_st(c_in, kLBlk * b + 64 + kLBlk);
         }
-        lstamp<NS>(a, tk, w, b, 1, lane);
         int vals[kLBlk], lt[kLBlk];
 #pragma unroll
         for (int u = 0; u < kLBlk; ++u)
@@ -334,58 +212,23 @@ __device__ __forceinline__ void lane_strip(const StripArgs& a, const LaneLds& L,
             U = up;
             H = h;
             vals[u] = h;
-            if (!GSA_LFLAG_EARLY && !(GSA_LKNOB & 32) && u == kLBlk / 2 - 1)
+            if (u == kLBlk / 2 - 1)
             {
                 rpin = raw_ld(f_in);
                 rpco = raw_ld(c_out);
                 rpxo = raw_ld(f_xo);
             }
         }
-        lstamp<NS>(a, tk, w, b, 2, lane);
-#if GSA_LSCHED_BARRIER
-        __builtin_amdgcn_sched_barrier(0);  // keep the hand-off writes and swaps out of the step chain
-#endif
         // hand-off: lane 63's H + g of steps Bb-1 .. Bb+B-2 = ring elements Bb .. Bb+B-1 (columns
-        // Bb-64 ..); the last strip's ring is drained into granules by the drain wave
-        if constexpr (GSA_LHAND_ALL && !(GSA_LKNOB & 4))
+        // Bb-64 ..); the last strip's ring is drained into granules by the drain wave.  Every lane
+        // writes (no exec mask): lane 63 into the ring, the others into a sink
         {
-            // every lane writes (no exec mask): lane 63 into the ring, the others into a sink
             const uint32_t eb = (lane == 63) ? ring_out + 4u * (uint32_t)((kLBlk * b) & (kLRing - 1)) : hsink;
 #pragma unroll
             for (int j = 0; j < kLH; ++j)
                 lds_st4(eb + ((lane == 63) ? 16u * j : 0u), int4v {lt[4 * j], lt[4 * j + 1], lt[4 * j + 2], lt[4 * j + 3]});
         }
-        else if (!(GSA_LKNOB & 4) && lane == 63)
-        {
-            const uint32_t eb = ring_out + 4u * (uint32_t)((kLBlk * b) & (kLRing - 1));
-#pragma unroll
-            for (int j = 0; j < kLH; ++j) lds_st4(eb + 16u * j, int4v {lt[4 * j], lt[4 * j + 1], lt[4 * j + 2], lt[4 * j + 3]});
-        }
-        if constexpr (!(GSA_LKNOB & 64)) flag_st(f_out, b + 1 == NB ? kLBig : kLBlk * b + kLBlk);
-        if constexpr (GSA_LSTAGE && !(GSA_LKNOB & 1))
-        {
-            // output: this lane's row into the stage (steps Bb .. Bb+B-1 = chunks 4(b&1) ..)
-            const uint32_t sb = stg_w + (uint32_t)((b >> 1) & 1) * kStageBytes;
-#pragma unroll
-            for (int j = 0; j < kLH; ++j)
-                lds_st4(sb + 16u * (uint32_t)((kLH * (b & 1) + j) ^ (lane & 7)),
-                        int4v {vals[4 * j], vals[4 * j + 1], vals[4 * j + 2], vals[4 * j + 3]});
-        }
-        if constexpr ((GSA_LKNOB & 1024) != 0)
-        {
-            // timing knob: the same bytes as lane-contiguous stores into the strip's own rows
-            // (64 lanes x 16 B = 1 KB contiguous per instruction); values land in wrong places
-            if (r0 + 63 <= a.R)
-            {
-#pragma unroll
-                for (int j = 0; j < kLH; ++j)
-                {
-                    const size_t off = ((size_t)b * kLBlk * 64 + (size_t)j * 256 + 4u * (uint32_t)lane) % ((size_t)64 * a.ld - 4);
-                    *(gptr<int4a>)(G(a.score) + (size_t)r0 * a.ld + off) = int4a {vals[4 * j], vals[4 * j + 1], vals[4 * j + 2], vals[4 * j + 3]};
-                }
-            }
-        }
-        else if constexpr (GSA_LXPOSE && !GSA_LSTAGE && !(GSA_LKNOB & 1))
+        flag_st(f_out, b + 1 == NB ? kLBig : kLBlk * b + kLBlk);
         {
             // output, transposed in registers: the 4 chunks (4 columns each) of the block are
             // exchanged across lane bits 5 and 4 (permlane32/16 swaps, 16 per block), so that
@@ -419,18 +262,8 @@ __device__ __forceinline__ void lane_strip(const StripArgs& a, const LaneLds& L,
 #pragma unroll
                 for (int k = 0; k < 4; ++k)
                 {
-                    if constexpr (GSA_LBUFST)
-                    {
-                        // buffer store: per-lane 32-bit offset + scalar offset, no 64-bit VALU address
-                        const int so = 4 * (int)((long long)(16 * k) * a.ld - 16 * k + kLBlk * b);
-                        __builtin_amdgcn_raw_buffer_store_b128(u32x4 {(unsigned)t[4 * k], (unsigned)t[4 * k + 1], (unsigned)t[4 * k + 2], (unsigned)t[4 * k + 3]},
-                                                               srsrc, (int)(4u * xoff), so, 0);
-                    }
-                    else
-                    {
-                        const gptr<int> ub = G(a.score) + ((ptrdiff_t)(r0 + 16 * k) * a.ld - 16 * k + kLBlk * b);
-                        *(gptr<int4a>)(ub + xoff) = int4a {t[4 * k], t[4 * k + 1], t[4 * k + 2], t[4 * k + 3]};
-                    }
+                    const gptr<int> ub = G(a.score) + ((ptrdiff_t)(r0 + 16 * k) * a.ld - 16 * k + kLBlk * b);
+                    *(gptr<int4a>)(ub + xoff) = int4a {t[4 * k], t[4 * k + 1], t[4 * k + 2], t[4 * k + 3]};
                 }
             }
             else
@@ -453,61 +286,7 @@ __device__ __forceinline__ void lane_strip(const StripArgs& a, const LaneLds& L,
                 }
             }
         }
-        else if (!GSA_LSTAGE && !(GSA_LKNOB & 1) && live)
-        {
-            // output: this lane's row, columns Bb-l .. Bb-l+B-1 (column 0 is the header kernel's)
-            const int c0 = kLBlk * b - lane;
-            if (c0 >= 1 && c0 + kLBlk - 1 <= C)
-            {
-#pragma unroll
-                for (int j = 0; j < kLH; ++j)
-                    *(gptr<int4a>)(orow + c0 + 4 * j) = int4a {vals[4 * j], vals[4 * j + 1], vals[4 * j + 2], vals[4 * j + 3]};
-            }
-            else if (c0 + kLBlk - 1 >= 1 && c0 <= C)
-            {
-#pragma unroll
-                for (int e = 0; e < kLBlk; ++e)
-                    if (c0 + e >= 1 && c0 + e <= C) orow[c0 + e] = vals[e];
-            }
-        }
-        lstamp<NS>(a, tk, w, b, 3, lane);
         return true;
-    };
-
-    // GSA_LSTAGE: stage read-back (8 rows x 128 B per read) and row-contiguous stores, one pair of blocks
-    // (32 steps) behind the compute: the reads of pair p are issued after its last block and
-    // stored after the next pair, so neither waits
-    static_assert(kLBlk == 16, "stage pairs are 2 blocks of 16 steps");
-    int4v Rg[8];
-    auto stage_read = [&](int p) {
-        if constexpr (GSA_LSTAGE && !(GSA_LKNOB & 1))
-        {
-            const uint32_t rb = stg_r + (uint32_t)(p & 1) * kStageBytes;
-#pragma unroll
-            for (int i = 0; i < 8; ++i) Rg[i] = lds_ld4(rb + 1024u * i);
-        }
-    };
-    auto flush = [&](int p) {
-        if constexpr (GSA_LSTAGE && !(GSA_LKNOB & 1))
-        {
-#pragma unroll
-            for (int i = 0; i < 8; ++i)
-            {
-                const int c = 32 * p + 4 * sq - (8 * i + srow);  // column of Rg[i].x
-                if (8 * i <= rlim && c + 3 >= 1 && c <= C)
-                {
-                    const gptr<int> dst = obase + (size_t)(8 * i) * (size_t)a.ld + c;
-                    if (c >= 1 && c + 3 <= C)
-                        *(gptr<int4a>)dst = int4a {Rg[i].x, Rg[i].y, Rg[i].z, Rg[i].w};
-                    else
-                    {
-#pragma unroll
-                        for (int e = 0; e < 4; ++e)
-                            if (c + e >= 1 && c + e <= C) dst[e] = Rg[i][e];
-                    }
-                }
-            }
-        }
     };
 
     int b = 0;
@@ -516,17 +295,12 @@ __device__ __forceinline__ void lane_strip(const StripArgs& a, const LaneLds& L,
     {
         if (!block(b, qA, qB, hA, hB, std::integral_constant<bool, true>())) return;
         if (!block(b + 1, qB, qA, hB, hA, std::integral_constant<bool, true>())) return;
-        if (b > 0) flush((b >> 1) - 1);
-        stage_read(b >> 1);
     }
     for (; b < NB; b += 2)
     {
         if (!block(b, qA, qB, hA, hB, std::integral_constant<bool, false>())) return;
         if (b + 1 < NB && !block(b + 1, qB, qA, hB, hA, std::integral_constant<bool, false>())) return;
-        flush((b >> 1) - 1);
-        stage_read(b >> 1);
     }
-    flush((NB - 1) >> 1);
 }
 
 // ------------------------------------------------------------------------------------
@@ -550,8 +324,6 @@ __device__ __forceinline__ void lane_loader(const StripArgs& a, const LaneLds& L
     int xl = letter(lane);
     int pl = 0, c0 = 0;  // progress words, re-read only when their cached values block
     uint64_t last = __builtin_amdgcn_s_memrealtime();
-    int npoll = 0;       // stamp builds: polls of ticket 1 (issue / return times, dbg[4000 + 3k])
-    uint64_t tpoll = 0;
     while (qn <= C || hnext <= C)
     {
         bool moved = false;
@@ -564,8 +336,6 @@ __device__ __forceinline__ void lane_loader(const StripArgs& a, const LaneLds& L
         const int c = hnext + lane;
         const bool in = c <= C;
         unsigned long long q = 0ull;
-        if constexpr (GSA_STAMP)
-            if (feed && tk == 1) tpoll = __builtin_amdgcn_s_memrealtime();
         if (feed && tk > 0 && in) q = __hip_atomic_load(gprev + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         // (2) Q columns qn .. qn+63: the columns they replace (<= qn+63-kLW) are dead once the
         //     last strip has published elements pl (its next reads start at column pl-55).
@@ -610,22 +380,9 @@ __device__ __forceinline__ void lane_loader(const StripArgs& a, const LaneLds& L
             }
             const uint64_t badm = __ballot(!good);
             const int n = badm ? __builtin_ctzll(badm) : 64;
-            if constexpr (GSA_STAMP)
-            {
-                if (tk == 1 && npoll < 1000 && lane == 0 && a.dbg)
-                {
-                    unsigned long long t;
-                    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-                    a.dbg[4000 + 3 * npoll] = tpoll;
-                    a.dbg[4001 + 3 * npoll] = t;
-                    a.dbg[4002 + 3 * npoll] = (unsigned long long)(hnext + n);
-                }
-                ++npoll;
-            }
             if (n > 0)
             {
                 if (lane < n) lds_st(ring0 + 4u * (uint32_t)((c + 64) & (kLRing - 1)), v);
-                if (tk == 1) link_stamp(a, 2800, hnext, hnext + n, lane);
                 hnext += n;
                 flag_st(F, hnext > C ? kLBig : hnext + 64);
                 moved = true;
@@ -663,7 +420,6 @@ __device__ __forceinline__ void lane_drain(const StripArgs& a, const LaneLds& L,
     }
     const gptr<unsigned long long> gout = G(a.gran) + (size_t)tk * a.granStride;
     int dnext = 0;  // next column to drain
-    int ndr = 0;    // stamp builds: drain stores
     uint64_t last = __builtin_amdgcn_s_memrealtime();
     while (dnext <= C)
     {
@@ -676,19 +432,6 @@ __device__ __forceinline__ void lane_drain(const StripArgs& a, const LaneLds& L,
                 const int v = lds_ld(ringN + 4u * (uint32_t)((c + 64) & (kLRing - 1)));
                 __hip_atomic_store(gout + c, ((unsigned long long)a.epoch << 32) | (uint32_t)v, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
-            }
-            if (tk == 0) link_stamp(a, 2560, dnext, min(dnext + 64, avail), lane);
-            if constexpr (GSA_STAMP)
-            {
-                // stamp builds: drain stores of ticket 0 (time, columns < value), dbg[8000 + 2m]
-                if (tk == 0 && lane == 0 && a.dbg && ndr < 2000)
-                {
-                    unsigned long long t;
-                    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-                    a.dbg[8000 + 2 * ndr] = t;
-                    a.dbg[8001 + 2 * ndr] = (unsigned long long)min(dnext + 64, avail);
-                }
-                ++ndr;
             }
             dnext = min(dnext + 64, avail);
             flag_st(F + kFCons + 4u * NS, dnext > C ? kLBig : dnext + 64);
@@ -770,13 +513,6 @@ __global__ void __launch_bounds__(64 * (NS + 2)) nw_lane_kernel(StripArgs a)
         pa.gran = a.gran + d.granOff;
         pa.granStride = (long long)d.C + 1;
         const int tk = (tks >= 0) ? tks : tkg - d.ticketBase;
-        if constexpr (GSA_STAMP)
-        {
-            // stamp builds: the XCD (XCC id) each ticket runs on, dbg[3100 + ticket]
-            unsigned xcc;
-            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-            if (threadIdx.x == 0 && tkg < 100 && a.dbg) a.dbg[3100 + tkg] = xcc & 0xf;
-        }
         if (threadIdx.x < 32) lds_st(L.flags + 4u * threadIdx.x, 0);  // prog[], cons[]
         if (threadIdx.x < 16) lds_st(L.gfill + 4u * threadIdx.x, a.g);
         if (threadIdx.x == 0) lds_st(L.flags + kFXo, 0);

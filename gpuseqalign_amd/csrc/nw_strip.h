@@ -6,11 +6,8 @@
 
 namespace gsa {
 
-constexpr int kModeFull = 0;
+constexpr int kModeFull = 0;  // full matrix (nw_lane.hip; launch_headers)
 constexpr int kModeSparse = 1;
-// Full fill whose output leaves the strip's CU through an L2-resident ring: copy workgroups
-// on other CUs (same XCD) move it to the matrix (nw_strip.hip, "ring mode").
-constexpr int kModeFullRing = 2;
 // Score-only global alignment with affine gaps on the strip layout (gsa_score_dev, global):
 // shifted by (i+j)*gape, H', E', F' follow max recurrences with the constant d = gapo - gape.
 constexpr int kModeScoreAG = 3;
@@ -18,12 +15,9 @@ constexpr int kModeScoreAG = 3;
 // a per-row floor (i+j)*(-gape) in the shifted space; the best cell goes to a packed atomicMax.
 constexpr int kModeScoreSW = 4;
 __host__ __device__ constexpr bool is_score_mode(int mode) { return mode == kModeScoreAG || mode == kModeScoreSW; }
-constexpr int kRingBlocks = 16;  // ring slots (16-step blocks of 256 rows, 16 KB) per strip workgroup
-constexpr int kRingWaves = 4;    // waves per workgroup in ring mode (strip + loader + 2 idle / 4 copy)
 constexpr int kWaveRows = 256;                          // rows per strip (one wave, 4 rows per lane)
 constexpr int kSparseNS = 4;                            // strip waves per workgroup, sparse fills
 constexpr int kSparseTileBy = kWaveRows * kSparseNS;    // = tile height of the mlsp matrices
-constexpr int kFullNSDefault = 1;                       // strip waves per workgroup, full fills
 
 // One pair of a batched fill (device-resident array; tickets of pair p are
 // [ticketBase, ticketBase + nTickets), pair-major, so every ticket depends only on lower ones).
@@ -66,20 +60,9 @@ struct StripArgs
     unsigned* err;      // sticky: set by a spin that gave up, cleared by gsa_sync after reading
     unsigned long long spin;  // watchdog: s_memrealtime ticks (100 MHz) a wait may go without progress
     unsigned epoch;
-    unsigned long long* dbg;  // diagnostic builds only (GSA_STAMP): per-wave block time stamps
     // mlsppt: host-mapped per-ticket flags, set to `epoch` once a super-strip's outputs are
     // written back past L2 (null: no signalling)
     unsigned* done;
-    // ring mode (kModeFullRing): strip workgroups are blockIdx < nStrip, copy workgroup
-    // nStrip + s drains strip workgroup s's ring
-    int* ring;      // nStrip * kRingBlocks * 4096 ints (H', strip lane layout)
-    int* rdesc;     // nStrip * kRingBlocks * 2 ints: {global ticket, block}
-    int* rhead;     // nStrip: ring blocks published (agent release by the strip's loader)
-    int* rtail;     // nStrip * kRingWaves: ring blocks consumed, per copy wave
-    int* rfinal;    // nStrip: total blocks + 1 once the strip workgroup has no more tickets
-    int nStrip;
-    int ringBase;   // per ticket: ring blocks of this workgroup before this ticket
-    int ringTicket; // per ticket: its global ticket index (the copy workgroup maps it to rows)
     // kModeScoreAG: gap open / extend, the F' hand-off granules (same layout as gran), result H[R][C]
     int go, ge;
     unsigned long long* gran2;

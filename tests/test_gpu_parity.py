@@ -149,28 +149,13 @@ def test_mlsp_40k_related(engine, golden):
     assert rs.align_cost == cost
 
 
-@pytest.mark.parametrize("R", [1800, 2049, 4097])
-@pytest.mark.parametrize("C", [1, 2, 63, 64, 65, 1000, 3001])
-def test_full_ring_mode_shapes(engine, golden, R, C, monkeypatch):
-    """Opt-in ring mode (GSA_FULL_RING=1; >= 8 strips: output through L2-resident rings drained
-    by copy workgroups, nw_strip.hip): every word against cpu1, ragged row and column counts."""
-    monkeypatch.setenv("GSA_FULL_RING", "1")
-    monkeypatch.setenv("GSA_FULL_KERNEL", "strip")  # ring mode belongs to the 4-rows-per-lane kernel
-    Y, X = random_pair(R, C, R + 7 * C)
-    r = engine.align_full(Y, X, golden.blosum62, -11)
-    S, cost = oracle.fill_full(Y, X, golden.blosum62, -11)
-    assert np.array_equal(r.score, S) and r.align_cost == cost
-
-
-@pytest.mark.parametrize("kernel,ns", [("lane", "1"), ("lane", "2"), ("lane", "3"), ("lane", "4"), ("lane", "6"), ("lane", "8"),
-                                       ("strip", "1")])
+@pytest.mark.parametrize("ns", ["1", "2", "3", "4", "6", "8"])
 @pytest.mark.parametrize("R,C", [(1, 1), (1, 700), (63, 64), (64, 65), (127, 300), (128, 128), (129, 1029),
                                  (300, 1), (385, 1500), (1100, 2222), (2049, 777)])
-def test_full_kernels_shapes(engine, golden, kernel, ns, R, C, monkeypatch):
-    """Both full-fill kernels (GSA_FULL_KERNEL, read per launch): the one-row-per-lane kernel
-    (nw_lane.hip) with 1..4, 6, 8 strips per workgroup (GSA_LANE_NS: every super-strip boundary,
-    ragged last strips, rows beyond R) and the 4-rows-per-lane strip kernel, every word."""
-    monkeypatch.setenv("GSA_FULL_KERNEL", kernel)
+def test_full_kernel_shapes(engine, golden, ns, R, C, monkeypatch):
+    """The full-fill kernel (nw_lane.hip, one row per lane) with 1..4, 6, 8 strips per workgroup
+    (GSA_LANE_NS, read per launch): every super-strip boundary, ragged last strips, rows beyond
+    R, every word."""
     monkeypatch.setenv("GSA_LANE_NS", ns)
     Y, X = random_pair(R, C, 3 * R + C)
     r = engine.align_full(Y, X, golden.blosum62, -11)
@@ -182,7 +167,6 @@ def test_full_kernels_shapes(engine, golden, kernel, ns, R, C, monkeypatch):
 def test_lane_kernel_wide_pair(engine, golden, ns, monkeypatch):
     """Columns past the profile ring (512 columns, 1024 from NS = 5) and its guard copies,
     several super-strips."""
-    monkeypatch.setenv("GSA_FULL_KERNEL", "lane")
     monkeypatch.setenv("GSA_LANE_NS", ns)
     Y, X = related_pair(5000, 17)
     r = engine.align_full(Y, X, golden.blosum62, -11)

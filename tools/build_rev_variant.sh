@@ -1,16 +1,11 @@
 #!/bin/bash
-# Experiment build of the lane kernel + C ABI from a git revision: build_rev_variant.sh REV NAME
-# -> gpuseqalign_amd/libgsa_<NAME>.so (the other objects from the normal in-tree build).
+# A/B build of the whole library from a git revision: build_rev_variant.sh REV NAME
+# -> gpuseqalign_amd/libgsa_<NAME>.so (loaded by the timing tools with GSA_LIB=...).
 set -e
 REV=${1:-HEAD}
 NAME=${2:-head}
-cd "$(dirname "$0")/../gpuseqalign_amd/csrc"
-make -s -j8
-mkdir -p build/rev_$NAME
-git show $REV:gpuseqalign_amd/csrc/nw_lane.hip > build/rev_$NAME/nw_lane.hip
-git show $REV:gpuseqalign_amd/csrc/gsa_capi.hip > build/rev_$NAME/gsa_capi.hip
-hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -I. -c build/rev_$NAME/nw_lane.hip -o build/rev_$NAME/nw_lane.o &
-hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -I. -I../../include -c build/rev_$NAME/gsa_capi.hip -o build/rev_$NAME/gsa_capi.o &
-wait
-hipcc --offload-arch=gfx950 -shared -fPIC build/nw_strip.o build/rev_$NAME/nw_lane.o build/nw_check.o build/nw_trace_dev.o \
-  build/nw_scan.o build/rev_$NAME/gsa_capi.o build/nw_trace.o -o ../libgsa_$NAME.so
+ROOT=$(cd "$(dirname "$0")/.." && pwd)
+D=$ROOT/gpuseqalign_amd/csrc/build/rev_$NAME
+rm -rf $D && mkdir -p $D
+git -C $ROOT archive $REV gpuseqalign_amd/csrc include | tar -x -C $D
+make -s -C $D/gpuseqalign_amd/csrc -j8 OUT=$ROOT/gpuseqalign_amd/libgsa_$NAME.so

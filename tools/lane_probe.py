@@ -1,5 +1,5 @@
-"""Lane-kernel timing probe: full fills of R x C for a ladder of R (hop cost per strip) and both
-full-fill kernels (GSA_FULL_KERNEL / GSA_LANE_NS are read per launch)."""
+"""Lane-kernel timing probe: full fills of R x C for a ladder of R (hop cost per strip), per
+strips-per-workgroup count (GSA_LANE_NS is read per launch)."""
 import os, sys, json
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import gpuseqalign_amd as gsa
@@ -8,8 +8,7 @@ from tools.gpu_perf import run
 eng = gsa.Engine(0)
 C = int(sys.argv[1]) if len(sys.argv) > 1 else 10000
 rows = [int(x) for x in os.environ.get("ROWS", "64,128,256,512,1024,2048,4096,10000").split(",")]
-for kern, nss in (("lane", tuple(int(x) for x in os.environ.get("NSS", "1,2,3,4").split(","))),) + ((("strip", (1,)),) if os.environ.get("STRIP") else ()):
-    os.environ["GSA_FULL_KERNEL"] = kern
+for kern, nss in (("lane", tuple(int(x) for x in os.environ.get("NSS", "1,2,3,4").split(","))),):
     for ns in nss:
         os.environ["GSA_LANE_NS"] = str(ns)
         prev = None
