@@ -162,7 +162,8 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
     // header-column slots of this lane's rows: tile row iT, elements ea .. ea+K-1 (one tile)
     const int iT = (rl - 1) / tBy;
     const int ea = rl - iT * tBy;
-    const gptr<int> hcolT = G(a.hcol) + (size_t)iT * (size_t)tcols * (size_t)(tBy + 1) + ea;
+    // header column of the next boundary (tile column jb, starting at jb = 1), advanced per boundary
+    gptr<int> hcolP = G(a.hcol) + ((size_t)iT * (size_t)tcols + 1) * (size_t)(tBy + 1) + ea;
 
     // block b needs its halo (ring elements 16b+64 .. 16b+79), room in ring_out for elements
     // 16b .. 16b+15, and (strip 0; the others trail it) the profile of block b+1 (columns < 16b+32)
@@ -224,7 +225,11 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
         flag_st(f_out, bb + 1 == NB ? kBig : kBlk * bb + kBlk);
     };
     int rpin = 0, rpco = 0, rpxo = 0;  // progress words read in mid-block, checked at the next block
-    int nb0 = tBx, jb0 = 1;             // smallest tile boundary column >= 16b - 63 (uniform)
+    // Tile boundaries bc = jb*tBx are multiples of 16 columns, and lane l meets column bc at step
+    // bc + l: in block bc/16 + l/16, at step l & 15.  So the 4 blocks from bc/16 on capture it, 16
+    // lanes each, and every lane picks the block's step (lane & 15): the selection masks are
+    // constants.  nbb = bc/16 of the next boundary, jb its tile column (uniform).
+    int nbb = tBx / kBlk, jb = 1;
 
     // One body for blocks with and without a header-column capture (cap, uniform): separate
     // bodies get different register assignments and ~100 v_mov per block to reconcile them.
@@ -287,47 +292,42 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
         handoff(b);
         if (CAP && cap)
         {
-            // this lane's columns lo .. lo+15; boundaries nb0 (>= 16b-63) and nb0 + tBx
-            const int lo = kBlk * b - lane;
-            int bc = nb0, jT = jb0;
-            if (bc < lo)
+            // lanes 16m .. 16m+15 (m = b - nbb) hold column bc at step lane & 15: 16 -> 1 by its
+            // bits (v_cndmask tree with constant lane masks, 15 per row)
+            constexpr uint64_t m1 = 0xAAAAAAAAAAAAAAAAull, m2 = 0xCCCCCCCCCCCCCCCCull;
+            constexpr uint64_t m4 = 0xF0F0F0F0F0F0F0F0ull, m8 = 0xFF00FF00FF00FF00ull;
+            int v[K];
+#pragma unroll
+            for (int k = 0; k < K; ++k)
             {
-                bc += tBx;
-                ++jT;
+                int x[8];
+#pragma unroll
+                for (int i = 0; i < 8; ++i) x[i] = sel(m1, va[k][2 * i], va[k][2 * i + 1]);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) x[i] = sel(m2, x[2 * i], x[2 * i + 1]);
+#pragma unroll
+                for (int i = 0; i < 2; ++i) x[i] = sel(m4, x[2 * i], x[2 * i + 1]);
+                v[k] = sel(m8, x[0], x[1]);
             }
-            const int s = bc - lo;
-            if (s <= kBlk - 1 && jT < tcols)
+            const int gb = (rl + kBlk * nbb) * g;  // un-shift: + (row + bc) g
+            if ((lane >> 4) == b - nbb)
             {
-                // 16 -> 1 by the bits of s (v_cndmask tree, 15 per row)
-                const uint64_t m1 = __builtin_amdgcn_ballot_w64((s & 1) != 0), m2 = __builtin_amdgcn_ballot_w64((s & 2) != 0);
-                const uint64_t m4 = __builtin_amdgcn_ballot_w64((s & 4) != 0), m8 = __builtin_amdgcn_ballot_w64((s & 8) != 0);
-                const gptr<int> dst = hcolT + (size_t)jT * (size_t)(tBy + 1);
 #pragma unroll
-                for (int k = 0; k < K; ++k)
-                {
-                    int x[8];
-#pragma unroll
-                    for (int i = 0; i < 8; ++i) x[i] = sel(m1, va[k][2 * i], va[k][2 * i + 1]);
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) x[i] = sel(m2, x[2 * i], x[2 * i + 1]);
-#pragma unroll
-                    for (int i = 0; i < 2; ++i) x[i] = sel(m4, x[2 * i], x[2 * i + 1]);
-                    dst[k] = sel(m8, x[0], x[1]) + (rl + k + bc) * g;
-                }
+                for (int k = 0; k < K; ++k) hcolP[k] = v[k] + gb + k * g;
+            }
+            if (b == nbb + 3)
+            {
+                nbb += tBx / kBlk;
+                ++jb;
+                hcolP += (size_t)(tBy + 1);
             }
         }
         return true;
     };
 
-    // the window of block b holds a tile boundary iff nb0 <= 16b+15 (uniform)
-    auto advance = [&](int b) {
-        if (nb0 < kBlk * b - 63)  // the window moves 16 columns per block and tBx >= 64
-        {
-            nb0 += tBx;
-            ++jb0;
-        }
-        return nb0 <= kBlk * b + kBlk - 1 && jb0 < tcols;
-    };
+    // the block captures a header column iff it is one of the 4 blocks from the next boundary's
+    // (uniform; tBx >= 64 keeps the boundaries 4 blocks apart)
+    auto advance = [&](int b) { return b >= nbb && jb < tcols; };
     using T = std::integral_constant<bool, true>;
     using F = std::integral_constant<bool, false>;
     constexpr int kRampBlocks = 64 / kBlk;  // columns <= 0 occur only in the first 64 steps
