@@ -61,12 +61,21 @@ constexpr int kRing = 512;        // hand-off ring elements per strip boundary (
 constexpr int kBig = 0x3fffffff;  // "everything published"
 constexpr int kSubRow = 36;       // dwords per subT row (32 letters + 4)
 constexpr int kBatch = 128;       // profile columns the loader adds per pass (2 per lane)
-constexpr uint32_t kFCons = 64, kFXo = 128, kFTicket = 132;
+// Progress words in 8-byte slots, slot s (s = -1 .. NS) at byte 8(s+1) = {prog[s+1], cons[s]}:
+// prog[i] (ring i holds elements < prog[i]) is written by strip i-1 (the loader for i = 0),
+// cons[i] (ring i's reader no longer needs elements < cons[i]) by strip i (the drain wave for
+// i = NS), so a strip publishes both of its words with ONE 8-byte write, and reads the two it
+// waits on -- prog[w] in slot w-1 and cons[w+1] in slot w+1 -- with ONE ds_read2_b64.  Slot -1's
+// second word is xo (the profile holds columns < xo), which strip 0 reads in the same read.
+__host__ __device__ constexpr uint32_t kr_prog(int i) { return 8u * (uint32_t)i; }
+__host__ __device__ constexpr uint32_t kr_cons(int i) { return 8u * (uint32_t)(i + 1) + 4u; }
+constexpr uint32_t kFXo = 4, kFTicket = 132;
 
 extern __shared__ __attribute__((aligned(16))) char krsm[];
 
 
 typedef int int4v __attribute__((ext_vector_type(4)));
+typedef int int2v __attribute__((ext_vector_type(2)));
 template <typename T>
 using gptr = __attribute__((address_space(1))) T*;
 template <typename T>
@@ -89,6 +98,13 @@ __device__ __forceinline__ void flag_st(uint32_t a, int v)
 {
     asm volatile("" ::: "memory");  // data writes are issued before the word (LDS executes in order)
     __hip_atomic_store((int*)__builtin_assume_aligned(krsm + a, 4), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// two adjacent progress words with one 8-byte write, after the data writes it publishes
+__device__ __forceinline__ void flag_st2(uint32_t a, int v0, int v1)
+{
+    asm volatile("" ::: "memory");
+    *(int2v*)(krsm + a) = int2v {v0, v1};
+    asm volatile("" ::: "memory");
 }
 __device__ __forceinline__ bool err_set(const StripArgs& a)
 {
@@ -154,8 +170,8 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
     }
     const uint32_t ring_in = L.ring + (uint32_t)w * (kRing * 4u);
     const uint32_t ring_out = L.ring + (uint32_t)(w + 1) * (kRing * 4u);
-    const uint32_t f_in = L.flags + 4u * w, f_out = L.flags + 4u * (w + 1);
-    const uint32_t c_in = L.flags + kFCons + 4u * w, c_out = L.flags + kFCons + 4u * (w + 1);
+    const uint32_t f_in = L.flags + kr_prog(w), f_out = L.flags + kr_prog(w + 1);  // f_out: {prog[w+1], cons[w]}
+    const uint32_t c_out = L.flags + kr_cons(w + 1);
     const uint32_t f_xo = L.flags + kFXo;
     const uint32_t hsink = L.sink + (uint32_t)w * 1024u + 16u * (uint32_t)lane;
     const int NB = (Cp + 65 + kBlk - 1) / kBlk;  // lane 63 reaches step Cp+64 (element of column Cp)
@@ -222,7 +238,9 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
 #pragma unroll
         for (int j = 0; j < kHalo; ++j)
             lds_st4(eb + ((lane == 63) ? 16u * j : 0u), int4v {lt[4 * j], lt[4 * j + 1], lt[4 * j + 2], lt[4 * j + 3]});
-        flag_st(f_out, bb + 1 == NB ? kBig : kBlk * bb + kBlk);
+        // {prog[w+1], cons[w]}: block bb's 16 elements handed off; ring_in elements < 16bb+80
+        // (block bb's halo, read at its start) no longer needed
+        flag_st2(f_out, bb + 1 == NB ? kBig : kBlk * bb + kBlk, kBlk * bb + 64 + kBlk);
     };
     int rpin = 0, rpco = 0, rpxo = 0;  // progress words read in mid-block, checked at the next block
     // Tile boundaries bc = jb*tBx are multiples of 16 columns, and lane l meets column bc at step
@@ -242,7 +260,6 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
             if (!ok(pin, pco, pxo, b) && !spin(b)) return false;
         }
         halo_load(b);
-        flag_st(c_in, kBlk * b + 64 + kBlk);
         const uint32_t pn = q_off(b + 1);
         int va[CAP ? K : 1][CAP ? kBlk : 1];
 #pragma unroll
@@ -281,9 +298,14 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
             }
             if (u == kBlk / 2)
             {
-                rpin = raw_ld(f_in);
-                rpco = raw_ld(c_out);
-                rpxo = raw_ld(f_xo);
+                // slot w-1 {prog[w], cons[w-1] | xo} and slot w+1 {prog[w+2], cons[w+1]}: one
+                // ds_read2_b64 (plain loads, kept in place by the memory clobbers around them)
+                asm volatile("" ::: "memory");
+                const int2v lo = *(const int2v*)(krsm + f_in), hi = *(const int2v*)(krsm + f_in + 16u);
+                asm volatile("" ::: "memory");
+                rpin = lo.x;
+                rpxo = lo.y;
+                rpco = hi.y;
             }
         }
         // the block's hand-off at its end (the next strip sees it a block earlier than when it is
@@ -376,7 +398,7 @@ __device__ __forceinline__ void kr_loader(const StripArgs& a, const KrLds& L, in
         // (1) the row above strip 0 -> ring 0 elements c + 64, as far as granules of the previous
         //     super-strip are published (in column order) and ring 0 has room.  The poll is issued
         //     first and consumed after the profile work, which runs under its latency.
-        if (hnext <= Cp && hnext + 128 > c0 + kRing) c0 = flag_ld(F + kFCons);
+        if (hnext <= Cp && hnext + 128 > c0 + kRing) c0 = flag_ld(F + kr_cons(0));
         const bool feed = hnext <= Cp && hnext + 128 <= c0 + kRing;
         const int c = hnext + lane;
         const bool in = c <= Cp;
@@ -385,7 +407,7 @@ __device__ __forceinline__ void kr_loader(const StripArgs& a, const KrLds& L, in
         // (2) profile columns qn .. qn+127 (lane l: qn+2l-1 .. qn+2l+1): the ring slots they take
         //     held columns <= qn+127-kLW, dead once the last strip has published elements pl (it
         //     then reads columns >= pl-47)
-        if (qn <= Cp && qn + 192 > pl + kLW) pl = flag_ld(F + 4u * NS);
+        if (qn <= Cp && qn + 192 > pl + kLW) pl = flag_ld(F + kr_prog(NS));
         if (qn <= Cp && qn + 192 <= pl + kLW)
         {
             const int cl = qn + 2 * lane;
@@ -466,7 +488,7 @@ __device__ __forceinline__ void kr_drain(const StripArgs& a, const KrLds& L, int
     const uint32_t F = L.flags, ringN = L.ring + (uint32_t)NS * (kRing * 4u);
     if (tk + 1 >= a.nTickets)
     {
-        flag_st(F + kFCons + 4u * NS, kBig);  // nobody reads our last row
+        flag_st(F + kr_cons(NS), kBig);  // nobody reads our last row
         return;
     }
     const gptr<unsigned long long> gout = G(a.gran) + (size_t)tk * a.granStride;
@@ -477,7 +499,7 @@ __device__ __forceinline__ void kr_drain(const StripArgs& a, const KrLds& L, int
     uint64_t last = __builtin_amdgcn_s_memrealtime();
     while (dnext <= Cp)
     {
-        const int avail = min(flag_ld(F + 4u * NS) - 64, Cp + 1);  // columns < avail are in ring NS
+        const int avail = min(flag_ld(F + kr_prog(NS)) - 64, Cp + 1);  // columns < avail are in ring NS
         if (dnext < avail)
         {
             const int c = dnext + lane;
@@ -499,7 +521,7 @@ __device__ __forceinline__ void kr_drain(const StripArgs& a, const KrLds& L, int
                 }
             }
             dnext = min(dnext + 64, avail);
-            flag_st(F + kFCons + 4u * NS, dnext > Cp ? kBig : dnext + 64);
+            flag_st(F + kr_cons(NS), dnext > Cp ? kBig : dnext + 64);
             last = __builtin_amdgcn_s_memrealtime();
         }
         else
@@ -585,8 +607,7 @@ __global__ void __launch_bounds__(64 * (NS + 2)) nw_krow_kernel(StripArgs a)
         pa.gran = a.gran + d.granOff;
         pa.granStride = (long long)d.Cp + 1;
         const int tk = (tks >= 0) ? tks : tkg - d.ticketBase;
-        if (threadIdx.x < 32) lds_st(L.flags + 4u * threadIdx.x, 0);  // prog[], cons[]
-        if (threadIdx.x == 0) lds_st(L.flags + kFXo, 0);
+        if (threadIdx.x < 32) lds_st(L.flags + 4u * threadIdx.x, 0);  // prog[], cons[], xo
         __syncthreads();
         if (w == NS + 1)
             kr_drain<NS, K, LW>(pa, L, tk, lane);
