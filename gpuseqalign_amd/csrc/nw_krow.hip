@@ -60,6 +60,10 @@ constexpr int kHalo = kBlk / 4;   // halo registers (int4) per block
 constexpr int kRing = 512;        // hand-off ring elements per strip boundary (power of 2)
 constexpr int kBig = 0x3fffffff;  // "everything published"
 constexpr int kSubRow = 36;       // dwords per subT row (32 letters + 4)
+#ifndef GSA_KR_ASM_LDS
+#define GSA_KR_ASM_LDS 1
+#endif
+constexpr bool kAsmLds = GSA_KR_ASM_LDS;  // halo / hand-off by one lane under an exec mask set in asm
 constexpr int kBatch = 128;       // profile columns the loader adds per pass (2 per lane)
 // Progress words in 8-byte slots, slot s (s = -1 .. NS) at byte 8(s+1) = {prog[s+1], cons[s]}:
 // prog[i] (ring i holds elements < prog[i]) is written by strip i-1 (the loader for i = 0),
@@ -207,9 +211,32 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
 #pragma unroll
     for (int j = 0; j < kHalo; ++j) hc[j] = int4v {0, 0, 0, 0};
     auto halo_load = [&](int b) {
-        const uint32_t hb = (lane == 0) ? ring_in + 4u * (uint32_t)((kBlk * b + 64) & (kRing - 1)) : L.zfill;
+        if constexpr (kAsmLds)
+        {
+            // lane 0 alone (exec set and restored inside the asm: no divergent branch in the
+            // block); the other lanes' registers keep their 0; the reads are awaited here (the
+            // compiler cannot count them), as the first step needs them anyway
+            const uint32_t hb = ring_in + 4u * (uint32_t)((kBlk * b + 64) & (kRing - 1));
+            uint64_t sv;
+            asm volatile(
+                "s_mov_b64 %4, exec\n"
+                "s_mov_b64 exec, 1\n"
+                "ds_read_b128 %0, %5\n"
+                "ds_read_b128 %1, %5 offset:16\n"
+                "ds_read_b128 %2, %5 offset:32\n"
+                "ds_read_b128 %3, %5 offset:48\n"
+                "s_mov_b64 exec, %4\n"
+                "s_waitcnt lgkmcnt(0)"
+                : "+v"(hc[0]), "+v"(hc[1]), "+v"(hc[2]), "+v"(hc[3]), "=&s"(sv)
+                : "v"(hb)
+                : "memory");
+        }
+        else
+        {
+            const uint32_t hb = (lane == 0) ? ring_in + 4u * (uint32_t)((kBlk * b + 64) & (kRing - 1)) : L.zfill;
 #pragma unroll
-        for (int j = 0; j < kHalo; ++j) hc[j] = lds_ld4(hb + 16u * (lane == 0 ? j : 0));
+            for (int j = 0; j < kHalo; ++j) hc[j] = lds_ld4(hb + 16u * (lane == 0 ? j : 0));
+        }
     };
     // profile dwords of block b: columns 16b - lane .. +15 are dwords 8b - lane/2 .. +7 of copy
     // (lane & 1); reads past the ring's end hit the guard copy
@@ -234,10 +261,31 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
     // hand-off of block bb: every lane writes (lane 63 into the ring, the others into the sink,
     // no exec mask), then the progress word
     auto handoff = [&](int bb) {
-        const uint32_t eb = (lane == 63) ? ring_out + 4u * (uint32_t)((kBlk * bb) & (kRing - 1)) : hsink;
+        if constexpr (kAsmLds)
+        {
+            // lane 63 alone (exec set and restored inside the asm)
+            const uint32_t eb = ring_out + 4u * (uint32_t)((kBlk * bb) & (kRing - 1));
+            uint64_t sv;
+            asm volatile(
+                "s_mov_b64 %0, exec\n"
+                "s_mov_b64 exec, %1\n"
+                "ds_write_b128 %2, %3\n"
+                "ds_write_b128 %2, %4 offset:16\n"
+                "ds_write_b128 %2, %5 offset:32\n"
+                "ds_write_b128 %2, %6 offset:48\n"
+                "s_mov_b64 exec, %0"
+                : "=&s"(sv)
+                : "s"(1ull << 63), "v"(eb), "v"(int4v {lt[0], lt[1], lt[2], lt[3]}), "v"(int4v {lt[4], lt[5], lt[6], lt[7]}),
+                  "v"(int4v {lt[8], lt[9], lt[10], lt[11]}), "v"(int4v {lt[12], lt[13], lt[14], lt[15]})
+                : "memory");
+        }
+        else
+        {
+            const uint32_t eb = (lane == 63) ? ring_out + 4u * (uint32_t)((kBlk * bb) & (kRing - 1)) : hsink;
 #pragma unroll
-        for (int j = 0; j < kHalo; ++j)
-            lds_st4(eb + ((lane == 63) ? 16u * j : 0u), int4v {lt[4 * j], lt[4 * j + 1], lt[4 * j + 2], lt[4 * j + 3]});
+            for (int j = 0; j < kHalo; ++j)
+                lds_st4(eb + ((lane == 63) ? 16u * j : 0u), int4v {lt[4 * j], lt[4 * j + 1], lt[4 * j + 2], lt[4 * j + 3]});
+        }
         // {prog[w+1], cons[w]}: block bb's 16 elements handed off; ring_in elements < 16bb+80
         // (block bb's halo, read at its start) no longer needed
         flag_st2(f_out, bb + 1 == NB ? kBig : kBlk * bb + kBlk, kBlk * bb + 64 + kBlk);
