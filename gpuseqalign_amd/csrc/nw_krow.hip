@@ -440,6 +440,7 @@ __device__ __forceinline__ void kr_loader(const StripArgs& a, const KrLds& L, in
     int hnext = 0;  // next column of the row above to feed into ring 0
     int pl = 0, c0 = 0;  // progress words, re-read only when their cached values block
     uint64_t last = __builtin_amdgcn_s_memrealtime();
+    unsigned idle = 0;  // idle passes (error-word polls)
     while (qn <= Cp || hnext <= Cp)
     {
         bool moved = false;
@@ -512,7 +513,9 @@ __device__ __forceinline__ void kr_loader(const StripArgs& a, const KrLds& L, in
             last = now;
         else
         {
-            if (now - last > a.spin || err_set(a))
+            // the error word is a global load: it would wait for this wave's granule traffic and
+            // stretch the idle poll, so another wave's error is looked at every 64th idle pass
+            if (now - last > a.spin || ((++idle & 63) == 0 && err_set(a)))
             {
                 atomicOr(a.err, 1u);
                 return;
@@ -545,6 +548,7 @@ __device__ __forceinline__ void kr_drain(const StripArgs& a, const KrLds& L, int
     const size_t rowbase = (size_t)(rowEnd / tBy) * (size_t)tcols;  // tile index of (iT+1, 0)
     int dnext = 0;  // next column to drain
     uint64_t last = __builtin_amdgcn_s_memrealtime();
+    unsigned idle = 0;  // idle passes (error-word polls)
     while (dnext <= Cp)
     {
         const int avail = min(flag_ld(F + kr_prog(NS)) - 64, Cp + 1);  // columns < avail are in ring NS
@@ -574,7 +578,9 @@ __device__ __forceinline__ void kr_drain(const StripArgs& a, const KrLds& L, int
         }
         else
         {
-            if (__builtin_amdgcn_s_memrealtime() - last > a.spin || err_set(a))
+            // the error word is a global load, which waits for this wave's granule stores (vmcnt
+            // retires in order): looked at every 64th idle pass only
+            if (__builtin_amdgcn_s_memrealtime() - last > a.spin || ((++idle & 63) == 0 && err_set(a)))
             {
                 atomicOr(a.err, 1u);
                 return;

@@ -148,14 +148,16 @@ __device__ __forceinline__ void lane_strip(const StripArgs& a, const LaneLds& L,
     auto ok = [&](int pin, int pco, int pxo, int b) {
         return pin >= kLBlk * b + 64 + kLBlk && pco >= kLBlk * b + kLBlk - kLRing && (w != 0 || pxo >= kLBlk * b + 2 * kLBlk);
     };
+    // bounded spin; the error word is a global load, which waits for this wave's outstanding
+    // output stores (vmcnt retires in order), so it is polled once per 32 LDS polls
     auto spin = [&](int b) {
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        for (;;)
+        for (int it = 1;; ++it)
         {
             const int pin = flag_ld(f_in), pco = flag_ld(c_out), pxo = (w == 0) ? flag_ld(f_xo) : 0;
             if (ok(pin, pco, pxo, b)) return true;
             __builtin_amdgcn_s_sleep(1);
-            if (__builtin_amdgcn_s_memrealtime() - t0 > a.spin || err_set(a))
+            if (__builtin_amdgcn_s_memrealtime() - t0 > a.spin || ((it & 31) == 0 && err_set(a)))
             {
                 atomicOr(a.err, 1u);
                 return false;
@@ -324,6 +326,7 @@ __device__ __forceinline__ void lane_loader(const StripArgs& a, const LaneLds& L
     int xl = letter(lane);
     int pl = 0, c0 = 0;  // progress words, re-read only when their cached values block
     uint64_t last = __builtin_amdgcn_s_memrealtime();
+    unsigned idle = 0;  // idle passes (error-word polls)
     while (qn <= C || hnext <= C)
     {
         bool moved = false;
@@ -393,7 +396,9 @@ __device__ __forceinline__ void lane_loader(const StripArgs& a, const LaneLds& L
             last = now;
         else
         {
-            if (now - last > a.spin || err_set(a))
+            // the error word is a global load: it would wait for this wave's granule traffic and
+            // stretch the idle poll, so another wave's error is looked at every 64th idle pass
+            if (now - last > a.spin || ((++idle & 63) == 0 && err_set(a)))
             {
                 atomicOr(a.err, 1u);
                 return;
@@ -421,6 +426,7 @@ __device__ __forceinline__ void lane_drain(const StripArgs& a, const LaneLds& L,
     const gptr<unsigned long long> gout = G(a.gran) + (size_t)tk * a.granStride;
     int dnext = 0;  // next column to drain
     uint64_t last = __builtin_amdgcn_s_memrealtime();
+    unsigned idle = 0;  // idle passes (error-word polls)
     while (dnext <= C)
     {
         const int avail = min(flag_ld(F + 4u * NS) - 64, C + 1);  // columns < avail are in ring NS
@@ -439,7 +445,9 @@ __device__ __forceinline__ void lane_drain(const StripArgs& a, const LaneLds& L,
         }
         else
         {
-            if (__builtin_amdgcn_s_memrealtime() - last > a.spin || err_set(a))
+            // the error word is a global load, which waits for this wave's granule stores (vmcnt
+            // retires in order): looked at every 64th idle pass only
+            if (__builtin_amdgcn_s_memrealtime() - last > a.spin || ((++idle & 63) == 0 && err_set(a)))
             {
                 atomicOr(a.err, 1u);
                 return;
