@@ -438,6 +438,10 @@ __device__ __forceinline__ void kr_loader(const StripArgs& a, const KrLds& L, in
     };
     int qn = 0;     // the profile holds columns < qn
     int hnext = 0;  // next column of the row above to feed into ring 0
+    // letters of the next profile batch (lane l: columns qn+2l-1 .. qn+2l+1), loaded a batch
+    // ahead: waited for inside the batch, a global load would stall the granule feed for a
+    // round trip every 128 columns, and strip 0's lag ratchets to the worst feed delay
+    int xm = letter(2 * lane - 1), x0 = letter(2 * lane), x1 = letter(2 * lane + 1);
     int pl = 0, c0 = 0;  // progress words, re-read only when their cached values block
     uint64_t last = __builtin_amdgcn_s_memrealtime();
     unsigned idle = 0;  // idle passes (error-word polls)
@@ -459,11 +463,16 @@ __device__ __forceinline__ void kr_loader(const StripArgs& a, const KrLds& L, in
         if (qn <= Cp && qn + 192 > pl + kLW) pl = flag_ld(F + kr_prog(NS));
         if (qn <= Cp && qn + 192 <= pl + kLW)
         {
-            const int cl = qn + 2 * lane;
             int4v vm[8], v0[8], v1[8];
-            subrow(letter(cl - 1), vm);
-            subrow(letter(cl), v0);
-            subrow(letter(cl + 1), v1);
+            subrow(xm, vm);
+            subrow(x0, v0);
+            subrow(x1, v1);
+            {
+                const int cn = qn + kBatch + 2 * lane;
+                xm = letter(cn - 1);
+                x0 = letter(cn);
+                x1 = letter(cn + 1);
+            }
             const uint32_t d = (uint32_t)((qn / 2 + lane) & (kQW - 1));  // dword of columns (cl, cl+1) / (cl-1, cl)
             const bool guard = d < 8;                                     // ring head: also the guard copy at d + kQW
 #pragma unroll
