@@ -344,7 +344,10 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
                 H[k] = nh[k];
                 if constexpr (CAP) va[k][u] = nh[k];
             }
-            if (u == kBlk / 2)
+            // read late (step 14): the fresher the words, the rarer the spin at the next block
+            // start, where a strip that trails the one above at the minimum lag ends up each block
+            // (steps 8 / 12 / 14: 100k 5.95 / 5.97 / 5.87 ms)
+            if (u == kBlk - 2)
             {
                 // slot w-1 {prog[w], cons[w-1] | xo} and slot w+1 {prog[w+2], cons[w+1]}: one
                 // ds_read2_b64 (plain loads, kept in place by the memory clobbers around them)
