@@ -139,8 +139,8 @@ int check_inputs(int32_t adjrows, int32_t adjcols, int32_t substsz)
     return GSA_SUCCESS;
 }
 
-// Sparse fills run on the K-rows-per-lane kernel (nw_krow.hip, K = 4): 6.8 vs 8.0 ms for the
-// 100k pair and 5.2 vs 4.3 TCUPS for 512 pairs of 20k against the strip kernel (nw_strip.hip),
+// Sparse fills run on the K-rows-per-lane kernel (nw_krow.hip, K = 4): 5.9 vs 8.0 ms for the
+// 100k pair and 5.7 vs 4.3 TCUPS for 512 pairs of 20k against the strip kernel (nw_strip.hip),
 // which mlsppt keeps.  GSA_SPARSE_KERNEL=strip forces the strip kernel (read per launch, tested);
 // GSA_KROW_K (2, 4) and GSA_KROW_NS (2, 4) pick the K-rows geometry.
 enum SparseKern { kSpStrip, kSpKrow };

@@ -33,10 +33,11 @@
 // block whose 79-column window holds a tile boundary, each lane picks its (H[0..K-1]) at its
 // boundary step with a 4-level v_cndmask tree over the block's 16 steps and stores K ints.
 //
-// Hand-off between strips: lane 63 writes its old H[K-1] (column t-64) into the next strip's
-// ring (all lanes write, the others into a sink: no exec mask), behind the next block's halo
-// reads; lane 0 of the next strip reads block b's 16 halo values at the start of block b.  LDS
-// progress words keep the order (a wave's LDS operations execute in order).  Between
+// Hand-off between strips: at the end of block b lane 63 writes its old H[K-1] (columns t-64 of
+// the block's 16 steps) into the next strip's ring; lane 0 of the next strip reads block b's 16
+// halo values at the start of block b.  Both run under an exec mask set and restored inside one
+// asm block (no divergent branch splits the block).  LDS progress words keep the order (a wave's
+// LDS operations execute in order).  Between
 // super-strips (workgroups) the drain wave moves the last row through 8-byte {epoch, H'}
 // granules in HBM (sc1 atomics), polled by the next super-strip's loader wave
 // (MI355X_MICROARCH.md, handoff-1to1).  Every wait is bounded (StripArgs::spin, error word).
@@ -60,10 +61,6 @@ constexpr int kHalo = kBlk / 4;   // halo registers (int4) per block
 constexpr int kRing = 512;        // hand-off ring elements per strip boundary (power of 2)
 constexpr int kBig = 0x3fffffff;  // "everything published"
 constexpr int kSubRow = 36;       // dwords per subT row (32 letters + 4)
-#ifndef GSA_KR_ASM_LDS
-#define GSA_KR_ASM_LDS 1
-#endif
-constexpr bool kAsmLds = GSA_KR_ASM_LDS;  // halo / hand-off by one lane under an exec mask set in asm
 constexpr int kBatch = 128;       // profile columns the loader adds per pass (2 per lane)
 // Progress words in 8-byte slots, slot s (s = -1 .. NS) at byte 8(s+1) = {prog[s+1], cons[s]}:
 // prog[i] (ring i holds elements < prog[i]) is written by strip i-1 (the loader for i = 0),
@@ -91,7 +88,6 @@ __device__ __forceinline__ gptr<T> G(T* p)
 __device__ __forceinline__ int lds_ld(uint32_t a) { return *(const int*)(krsm + a); }
 __device__ __forceinline__ void lds_st(uint32_t a, int v) { *(int*)(krsm + a) = v; }
 __device__ __forceinline__ int4v lds_ld4(uint32_t a) { return *(const int4v*)(krsm + a); }
-__device__ __forceinline__ void lds_st4(uint32_t a, int4v v) { *(int4v*)(krsm + a) = v; }
 // progress words: relaxed workgroup-scope atomics (no vmcnt drains, unlike volatile accesses)
 __device__ __forceinline__ int raw_ld(uint32_t a)
 {
@@ -130,12 +126,10 @@ __device__ __forceinline__ int qlo(int v) { return (int)(short)v; }
 __device__ __forceinline__ int qhi(int v) { return v >> 16; }
 
 // LDS: profile (2 copies x substsz rows x kr_qrs dwords, copy 1 at kr_copy1), subT[x][y] = s(y, x) - 2g, NS+1
-// hand-off rings, 16 zeros (the halo of lanes >= 1), the hand-off sink, progress words:
-// prog[i] @ 4i (ring i holds elements < prog[i]), cons[i] @ 64+4i (ring i's reader no longer
-// needs elements < cons[i]), xo @ 128 (the profile holds columns < xo), ticket @ 132.
+// hand-off rings, progress words (slots kr_prog / kr_cons, xo at kFXo, the ticket at kFTicket).
 struct KrLds
 {
-    uint32_t q, sub, ring, zfill, sink, flags;
+    uint32_t q, sub, ring, flags;
 };
 
 __host__ __device__ inline KrLds kr_layout(int ns, int lw, int substsz)
@@ -144,9 +138,7 @@ __host__ __device__ inline KrLds kr_layout(int ns, int lw, int substsz)
     L.q = 0;
     L.sub = (kr_copy1(lw, substsz) + (uint32_t)substsz * kr_qrs(lw) + 16u) * 4u;
     L.ring = L.sub + (uint32_t)substsz * kSubRow * 4u;
-    L.zfill = L.ring + (uint32_t)(ns + 1) * kRing * 4u;
-    L.sink = L.zfill + 64u;
-    L.flags = L.sink + (uint32_t)ns * 1024u;
+    L.flags = L.ring + (uint32_t)(ns + 1) * kRing * 4u;
     return L;
 }
 
@@ -177,7 +169,6 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
     const uint32_t f_in = L.flags + kr_prog(w), f_out = L.flags + kr_prog(w + 1);  // f_out: {prog[w+1], cons[w]}
     const uint32_t c_out = L.flags + kr_cons(w + 1);
     const uint32_t f_xo = L.flags + kFXo;
-    const uint32_t hsink = L.sink + (uint32_t)w * 1024u + 16u * (uint32_t)lane;
     const int NB = (Cp + 65 + kBlk - 1) / kBlk;  // lane 63 reaches step Cp+64 (element of column Cp)
     // header-column slots of this lane's rows: tile row iT, elements ea .. ea+K-1 (one tile)
     const int iT = (rl - 1) / tBy;
@@ -211,32 +202,23 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
 #pragma unroll
     for (int j = 0; j < kHalo; ++j) hc[j] = int4v {0, 0, 0, 0};
     auto halo_load = [&](int b) {
-        if constexpr (kAsmLds)
-        {
-            // lane 0 alone (exec set and restored inside the asm: no divergent branch in the
-            // block); the other lanes' registers keep their 0; the reads are awaited here (the
-            // compiler cannot count them), as the first step needs them anyway
-            const uint32_t hb = ring_in + 4u * (uint32_t)((kBlk * b + 64) & (kRing - 1));
-            uint64_t sv;
-            asm volatile(
-                "s_mov_b64 %4, exec\n"
-                "s_mov_b64 exec, 1\n"
-                "ds_read_b128 %0, %5\n"
-                "ds_read_b128 %1, %5 offset:16\n"
-                "ds_read_b128 %2, %5 offset:32\n"
-                "ds_read_b128 %3, %5 offset:48\n"
-                "s_mov_b64 exec, %4\n"
-                "s_waitcnt lgkmcnt(0)"
-                : "+v"(hc[0]), "+v"(hc[1]), "+v"(hc[2]), "+v"(hc[3]), "=&s"(sv)
-                : "v"(hb)
-                : "memory");
-        }
-        else
-        {
-            const uint32_t hb = (lane == 0) ? ring_in + 4u * (uint32_t)((kBlk * b + 64) & (kRing - 1)) : L.zfill;
-#pragma unroll
-            for (int j = 0; j < kHalo; ++j) hc[j] = lds_ld4(hb + 16u * (lane == 0 ? j : 0));
-        }
+        // lane 0 alone (exec set and restored inside the asm: no divergent branch in the block);
+        // the other lanes' registers keep their 0; the reads are awaited here (the compiler cannot
+        // count them), as the first step needs them anyway
+        const uint32_t hb = ring_in + 4u * (uint32_t)((kBlk * b + 64) & (kRing - 1));
+        uint64_t sv;
+        asm volatile(
+            "s_mov_b64 %4, exec\n"
+            "s_mov_b64 exec, 1\n"
+            "ds_read_b128 %0, %5\n"
+            "ds_read_b128 %1, %5 offset:16\n"
+            "ds_read_b128 %2, %5 offset:32\n"
+            "ds_read_b128 %3, %5 offset:48\n"
+            "s_mov_b64 exec, %4\n"
+            "s_waitcnt lgkmcnt(0)"
+            : "+v"(hc[0]), "+v"(hc[1]), "+v"(hc[2]), "+v"(hc[3]), "=&s"(sv)
+            : "v"(hb)
+            : "memory");
     };
     // profile dwords of block b: columns 16b - lane .. +15 are dwords 8b - lane/2 .. +7 of copy
     // (lane & 1); reads past the ring's end hit the guard copy
@@ -258,34 +240,23 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
 #pragma unroll
     for (int k = 0; k < K; ++k) H[k] = 0;
     int lt[kBlk];  // lane 63's hand-off values of the last block (H[K-1] of columns t-64)
-    // hand-off of block bb: every lane writes (lane 63 into the ring, the others into the sink,
-    // no exec mask), then the progress word
+    // hand-off of block bb: lane 63's 16 values, then the progress word
     auto handoff = [&](int bb) {
-        if constexpr (kAsmLds)
-        {
-            // lane 63 alone (exec set and restored inside the asm)
-            const uint32_t eb = ring_out + 4u * (uint32_t)((kBlk * bb) & (kRing - 1));
-            uint64_t sv;
-            asm volatile(
-                "s_mov_b64 %0, exec\n"
-                "s_mov_b64 exec, %1\n"
-                "ds_write_b128 %2, %3\n"
-                "ds_write_b128 %2, %4 offset:16\n"
-                "ds_write_b128 %2, %5 offset:32\n"
-                "ds_write_b128 %2, %6 offset:48\n"
-                "s_mov_b64 exec, %0"
-                : "=&s"(sv)
-                : "s"(1ull << 63), "v"(eb), "v"(int4v {lt[0], lt[1], lt[2], lt[3]}), "v"(int4v {lt[4], lt[5], lt[6], lt[7]}),
-                  "v"(int4v {lt[8], lt[9], lt[10], lt[11]}), "v"(int4v {lt[12], lt[13], lt[14], lt[15]})
-                : "memory");
-        }
-        else
-        {
-            const uint32_t eb = (lane == 63) ? ring_out + 4u * (uint32_t)((kBlk * bb) & (kRing - 1)) : hsink;
-#pragma unroll
-            for (int j = 0; j < kHalo; ++j)
-                lds_st4(eb + ((lane == 63) ? 16u * j : 0u), int4v {lt[4 * j], lt[4 * j + 1], lt[4 * j + 2], lt[4 * j + 3]});
-        }
+        // lane 63 alone (exec set and restored inside the asm)
+        const uint32_t eb = ring_out + 4u * (uint32_t)((kBlk * bb) & (kRing - 1));
+        uint64_t sv;
+        asm volatile(
+            "s_mov_b64 %0, exec\n"
+            "s_mov_b64 exec, %1\n"
+            "ds_write_b128 %2, %3\n"
+            "ds_write_b128 %2, %4 offset:16\n"
+            "ds_write_b128 %2, %5 offset:32\n"
+            "ds_write_b128 %2, %6 offset:48\n"
+            "s_mov_b64 exec, %0"
+            : "=&s"(sv)
+            : "s"(1ull << 63), "v"(eb), "v"(int4v {lt[0], lt[1], lt[2], lt[3]}), "v"(int4v {lt[4], lt[5], lt[6], lt[7]}),
+              "v"(int4v {lt[8], lt[9], lt[10], lt[11]}), "v"(int4v {lt[12], lt[13], lt[14], lt[15]})
+            : "memory");
         // {prog[w+1], cons[w]}: block bb's 16 elements handed off; ring_in elements < 16bb+80
         // (block bb's halo, read at its start) no longer needed
         flag_st2(f_out, bb + 1 == NB ? kBig : kBlk * bb + kBlk, kBlk * bb + 64 + kBlk);
@@ -631,7 +602,6 @@ __global__ void __launch_bounds__(64 * (NS + 2)) nw_krow_kernel(StripArgs a)
         lds_st(L.sub + 4u * k, v);
     }
     if (bad) atomicOr(a.err, 2u);
-    if (threadIdx.x < 16) lds_st(L.zfill + 4u * threadIdx.x, 0);
     for (;;)
     {
         __syncthreads();
