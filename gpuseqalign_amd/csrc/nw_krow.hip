@@ -126,10 +126,13 @@ __device__ __forceinline__ int qlo(int v) { return (int)(short)v; }
 __device__ __forceinline__ int qhi(int v) { return v >> 16; }
 
 // LDS: profile (2 copies x substsz rows x kr_qrs dwords, copy 1 at kr_copy1), subT[x][y] = s(y, x) - 2g, NS+1
-// hand-off rings, progress words (slots kr_prog / kr_cons, xo at kFXo, the ticket at kFTicket).
+// hand-off rings, 16 zeros and a 1 KB slot per strip (unused since the halo and the hand-off run
+// under exec masks: kept, because dropping them and the zero row's initial stores changes the
+// register allocation of the strip loop, measured 2 % slower), progress words (slots kr_prog /
+// kr_cons, xo at kFXo, the ticket at kFTicket).
 struct KrLds
 {
-    uint32_t q, sub, ring, flags;
+    uint32_t q, sub, ring, zfill, sink, flags;
 };
 
 __host__ __device__ inline KrLds kr_layout(int ns, int lw, int substsz)
@@ -138,7 +141,9 @@ __host__ __device__ inline KrLds kr_layout(int ns, int lw, int substsz)
     L.q = 0;
     L.sub = (kr_copy1(lw, substsz) + (uint32_t)substsz * kr_qrs(lw) + 16u) * 4u;
     L.ring = L.sub + (uint32_t)substsz * kSubRow * 4u;
-    L.flags = L.ring + (uint32_t)(ns + 1) * kRing * 4u;
+    L.zfill = L.ring + (uint32_t)(ns + 1) * kRing * 4u;
+    L.sink = L.zfill + 64u;
+    L.flags = L.sink + (uint32_t)ns * 1024u;
     return L;
 }
 
@@ -202,23 +207,25 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
 #pragma unroll
     for (int j = 0; j < kHalo; ++j) hc[j] = int4v {0, 0, 0, 0};
     auto halo_load = [&](int b) {
-        // lane 0 alone (exec set and restored inside the asm: no divergent branch in the block);
-        // the other lanes' registers keep their 0; the reads are awaited here (the compiler cannot
-        // count them), as the first step needs them anyway
-        const uint32_t hb = ring_in + 4u * (uint32_t)((kBlk * b + 64) & (kRing - 1));
-        uint64_t sv;
-        asm volatile(
-            "s_mov_b64 %4, exec\n"
-            "s_mov_b64 exec, 1\n"
-            "ds_read_b128 %0, %5\n"
-            "ds_read_b128 %1, %5 offset:16\n"
-            "ds_read_b128 %2, %5 offset:32\n"
-            "ds_read_b128 %3, %5 offset:48\n"
-            "s_mov_b64 exec, %4\n"
-            "s_waitcnt lgkmcnt(0)"
-            : "+v"(hc[0]), "+v"(hc[1]), "+v"(hc[2]), "+v"(hc[3]), "=&s"(sv)
-            : "v"(hb)
-            : "memory");
+        {
+            // lane 0 alone (exec set and restored inside the asm: no divergent branch in the
+            // block); the other lanes' registers keep their 0; the reads are awaited here (the
+            // compiler cannot count them), as the first step needs them anyway
+            const uint32_t hb = ring_in + 4u * (uint32_t)((kBlk * b + 64) & (kRing - 1));
+            uint64_t sv;
+            asm volatile(
+                "s_mov_b64 %4, exec\n"
+                "s_mov_b64 exec, 1\n"
+                "ds_read_b128 %0, %5\n"
+                "ds_read_b128 %1, %5 offset:16\n"
+                "ds_read_b128 %2, %5 offset:32\n"
+                "ds_read_b128 %3, %5 offset:48\n"
+                "s_mov_b64 exec, %4\n"
+                "s_waitcnt lgkmcnt(0)"
+                : "+v"(hc[0]), "+v"(hc[1]), "+v"(hc[2]), "+v"(hc[3]), "=&s"(sv)
+                : "v"(hb)
+                : "memory");
+        }
     };
     // profile dwords of block b: columns 16b - lane .. +15 are dwords 8b - lane/2 .. +7 of copy
     // (lane & 1); reads past the ring's end hit the guard copy
@@ -242,21 +249,23 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
     int lt[kBlk];  // lane 63's hand-off values of the last block (H[K-1] of columns t-64)
     // hand-off of block bb: lane 63's 16 values, then the progress word
     auto handoff = [&](int bb) {
-        // lane 63 alone (exec set and restored inside the asm)
-        const uint32_t eb = ring_out + 4u * (uint32_t)((kBlk * bb) & (kRing - 1));
-        uint64_t sv;
-        asm volatile(
-            "s_mov_b64 %0, exec\n"
-            "s_mov_b64 exec, %1\n"
-            "ds_write_b128 %2, %3\n"
-            "ds_write_b128 %2, %4 offset:16\n"
-            "ds_write_b128 %2, %5 offset:32\n"
-            "ds_write_b128 %2, %6 offset:48\n"
-            "s_mov_b64 exec, %0"
-            : "=&s"(sv)
-            : "s"(1ull << 63), "v"(eb), "v"(int4v {lt[0], lt[1], lt[2], lt[3]}), "v"(int4v {lt[4], lt[5], lt[6], lt[7]}),
-              "v"(int4v {lt[8], lt[9], lt[10], lt[11]}), "v"(int4v {lt[12], lt[13], lt[14], lt[15]})
-            : "memory");
+        {
+            // lane 63 alone (exec set and restored inside the asm)
+            const uint32_t eb = ring_out + 4u * (uint32_t)((kBlk * bb) & (kRing - 1));
+            uint64_t sv;
+            asm volatile(
+                "s_mov_b64 %0, exec\n"
+                "s_mov_b64 exec, %1\n"
+                "ds_write_b128 %2, %3\n"
+                "ds_write_b128 %2, %4 offset:16\n"
+                "ds_write_b128 %2, %5 offset:32\n"
+                "ds_write_b128 %2, %6 offset:48\n"
+                "s_mov_b64 exec, %0"
+                : "=&s"(sv)
+                : "s"(1ull << 63), "v"(eb), "v"(int4v {lt[0], lt[1], lt[2], lt[3]}), "v"(int4v {lt[4], lt[5], lt[6], lt[7]}),
+                  "v"(int4v {lt[8], lt[9], lt[10], lt[11]}), "v"(int4v {lt[12], lt[13], lt[14], lt[15]})
+                : "memory");
+        }
         // {prog[w+1], cons[w]}: block bb's 16 elements handed off; ring_in elements < 16bb+80
         // (block bb's halo, read at its start) no longer needed
         flag_st2(f_out, bb + 1 == NB ? kBig : kBlk * bb + kBlk, kBlk * bb + 64 + kBlk);
@@ -602,6 +611,7 @@ __global__ void __launch_bounds__(64 * (NS + 2)) nw_krow_kernel(StripArgs a)
         lds_st(L.sub + 4u * k, v);
     }
     if (bad) atomicOr(a.err, 2u);
+    if (threadIdx.x < 16) lds_st(L.zfill + 4u * threadIdx.x, 0);
     for (;;)
     {
         __syncthreads();

@@ -1,0 +1,37 @@
+# Timing build of nw_krow.hip: per-block s_memtime stamps of the first 32 strips of a pair (tickets
+# 0..7): block entry (before the progress check), block start (check passed), hand-off published.
+# Read back with gsa_dbg_kst (tools/kr_stamps.py).  Diagnostics only; perturbs the kernel slightly.
+def rep(a, b, n=1):
+    global s
+    assert s.count(a) == n, a
+    s = s.replace(a, b)
+
+rep("extern __shared__ __attribute__((aligned(16))) char krsm[];",
+    "extern __shared__ __attribute__((aligned(16))) char krsm[];\n__device__ unsigned long long g_kst[32][6400][3];")
+rep("""        {
+            const int pin = __builtin_amdgcn_readfirstlane(rpin), pco = __builtin_amdgcn_readfirstlane(rpco);""",
+"""        const unsigned long long st0 = __builtin_amdgcn_s_memtime();
+        {
+            const int pin = __builtin_amdgcn_readfirstlane(rpin), pco = __builtin_amdgcn_readfirstlane(rpco);""")
+rep("""        halo_load(b);
+        const uint32_t pn = q_off(b + 1);""", """        const unsigned long long st1 = __builtin_amdgcn_s_memtime();
+        halo_load(b);
+        const uint32_t pn = q_off(b + 1);""")
+rep("""        handoff(b);
+        if (CAP && cap)""", """        handoff(b);
+        {
+            const unsigned long long st2 = __builtin_amdgcn_s_memtime();
+            if (tk < 8 && b < 6400 && lane == 0)
+            {
+                g_kst[tk * NS + w][b][0] = st0;
+                g_kst[tk * NS + w][b][1] = st1;
+                g_kst[tk * NS + w][b][2] = st2;
+            }
+        }
+        if (CAP && cap)""")
+s += """
+extern "C" int gsa_dbg_kst(void* dst, size_t n)
+{
+    return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(gsa::g_kst), n, 0, hipMemcpyDeviceToHost);
+}
+"""
