@@ -66,3 +66,24 @@ for w in range(1, ns):
     win = np.convolve(d, np.ones(5, dtype=np.int64), "valid")
     lag = np.median(t1[w, lo:hi] - t1[w - 1, lo:hi])
     print(f"strip {w:2d}: lag {lag:6.0f}  5-window of strip {w-1}: mean {win.mean():6.0f} p99 {np.percentile(win, 99):6.0f} max {win.max():6.0f}")
+
+# inter-workgroup hop, decomposed by column chunk (columns < 16c): strip 3 of ticket t publishes
+# its block c+3 (elements < 16(c+4) = columns < 16c), the drain stores the granules, the loader of
+# ticket t+1 feeds ring 0, strip 0 of ticket t+1 starts block c-1 (needs columns < 16c).
+if hasattr(L, "gsa_dbg_kld"):
+    d = np.zeros((8, 6400, 2), np.uint64)
+    assert L.gsa_dbg_kld(d.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(d.nbytes)) == 0
+    d = d.astype(np.int64)
+    cs = np.arange(16, NB - 8)
+    for t in range(min(7, ns // 4 - 1)):
+        p3 = t2[4 * t + 3, cs + 3]
+        dr = d[t, cs, 1]
+        ld = d[t + 1, cs, 0]
+        s0 = t1[4 * t + 4, cs - 1]
+        ok = (dr > 0) & (ld > 0)
+        print(f"ticket {t}->{t+1}: publish->drain med {np.median((dr - p3)[ok]):6.0f} | drain->loader med {np.median((ld - dr)[ok]):6.0f} "
+              f"p90 {np.percentile((ld - dr)[ok], 90):6.0f} | loader->strip0 start med {np.median((s0 - ld)[ok]):6.0f} | total med {np.median((s0 - p3)[ok]):6.0f}")
+    for t in range(min(8, ns // 4)):
+        # intra-workgroup equivalent: strip w's start of block c-1 vs strip w-1's publish of block c+3
+        w = 4 * t + 1
+        print(f"ticket {t} intra (strip {w}): publish->start med {np.median(t1[w, cs - 1] - t2[w - 1, cs + 3]):6.0f}")

@@ -35,3 +35,27 @@ extern "C" int gsa_dbg_kst(void* dst, size_t n)
     return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(gsa::g_kst), n, 0, hipMemcpyDeviceToHost);
 }
 """
+
+# loader / drain stamps: time at which the drain has stored, and the loader has fed into ring 0,
+# the columns < 16 c (c = 0 .. 6399), tickets 0..7
+rep("__device__ unsigned long long g_kst[32][6400][3];",
+    "__device__ unsigned long long g_kst[32][6400][3];\n__device__ unsigned long long g_kld[8][6400][2];")
+rep("""                hnext += n;""", """                {
+                    const unsigned long long tn = __builtin_amdgcn_s_memtime();
+                    if (tk < 8 && lane == 0)
+                        for (int c = hnext / 16 + 1; c <= (hnext + n) / 16 && c < 6400; ++c) g_kld[tk][c][0] = tn;
+                }
+                hnext += n;""")
+rep("""            dnext = min(dnext + 64, avail);""", """            {
+                const int dn = min(dnext + 64, avail);
+                const unsigned long long tn = __builtin_amdgcn_s_memtime();
+                if (tk < 8 && lane == 0)
+                    for (int c = dnext / 16 + 1; c <= dn / 16 && c < 6400; ++c) g_kld[tk][c][1] = tn;
+            }
+            dnext = min(dnext + 64, avail);""")
+s += """
+extern "C" int gsa_dbg_kld(void* dst, size_t n)
+{
+    return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(gsa::g_kld), n, 0, hipMemcpyDeviceToHost);
+}
+"""
