@@ -7,18 +7,28 @@
 
 namespace gsa {
 
-constexpr int kKrowKDefault = 4;   // rows per lane
-constexpr int kKrowNSDefault = 4;  // strip waves per workgroup
+constexpr int kKrowKDefault = 4;        // rows per lane
+constexpr int kKrowNSDefault = 4;       // strip waves per workgroup, single pairs
+constexpr int kKrowNSBatchDefault = 8;  // strip waves per workgroup, batches of pairs
 
-// (ns, k) pairs the library instantiates: a ticket = ns * 64 * k rows, which must divide the
-// sparse tile height kSparseTileBy (1024).
-__host__ __device__ constexpr bool krow_ok(int ns, int k) { return (k == 2 || k == 4) && (ns == 2 || ns == 4); }
+// (ns, k) pairs the library instantiates: a ticket = ns * 64 * k rows, which divides the sparse
+// tile height kSparseTileBy (1024) or, for (8, 4), spans two tile rows (the drain wave then also
+// writes the header row between strips 3 and 4).
+__host__ __device__ constexpr bool krow_ok(int ns, int k)
+{
+    return ((k == 2 || k == 4) && (ns == 2 || ns == 4)) || (k == 4 && ns == 8);
+}
 __host__ __device__ constexpr int krow_ticket_rows(int ns, int k) { return ns * 64 * k; }
+// tickets of a pair with trows tile rows (the last ticket of a two-row geometry may cover one)
+__host__ __device__ constexpr int krow_tickets(int trows, int ns, int k)
+{
+    return (trows * kSparseTileBy + krow_ticket_rows(ns, k) - 1) / krow_ticket_rows(ns, k);
+}
 size_t krow_lds_bytes(int ns, int lw, int substsz);
 // StripArgs / PairDesc / granule contract as launch_strip_fill (sparse mode, a.tBx, a.tBy,
-// per-pair hrow/hcol/trows/tcols/Cp); tickets of a pair = trows * tBy / krow_ticket_rows.
+// per-pair hrow/hcol/trows/tcols/Cp); tickets of a pair = krow_tickets(trows, ns, k).
 // Every |s - 2g| must fit int16 (the kernel sets error bit 2 otherwise).  grid <= 0: every resident slot.
-// The profile ring holds 1024 columns for (ns, k) = (4, 4), 512 otherwise (lw is reserved).
+// The profile ring holds 1024 columns for (ns, k) = (4, 4) and (8, 4), 512 otherwise (lw is reserved).
 hipError_t launch_krow_fill(const StripArgs& a, int ns, int k, int lw, int grid, hipStream_t stream);
 
 }  // namespace gsa

@@ -380,7 +380,9 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
 
     // the block captures a header column iff it is one of the 4 blocks from the next boundary's
     // (uniform; tBx >= 64 keeps the boundaries 4 blocks apart)
-    auto advance = [&](int b) { return b >= nbb && jb < tcols; };
+    // (a two-tile-row ticket's second half past the last tile row computes padding only)
+    const bool capRows = 64 * K * NS <= kSparseTileBy || (r0 - 1) / tBy < a.trows;
+    auto advance = [&](int b) { return b >= nbb && jb < tcols && capRows; };
     using T = std::integral_constant<bool, true>;
     using F = std::integral_constant<bool, false>;
     constexpr int kRampBlocks = 64 / kBlk;  // columns <= 0 occur only in the first 64 steps
@@ -538,62 +540,158 @@ __device__ __forceinline__ void kr_loader(const StripArgs& a, const KrLds& L, in
 // row closes a tile row, the header row of the tiles below (unshifted) with its duplicates: the
 // last element of the tile to the left and the corner of the header column
 // (nwalign_gpu9_mlsp_diagdiagdiag.cu:214-218, 253-257).  It issues no global loads, so its stores
-// never wait behind a poll.
+// never wait behind a poll.  A ticket of two tile rows (NS = 8, K = 4) also has a tile row
+// boundary after strip NS/2 - 1: the drain writes that header row from ring NS/2 as strip NS/2
+// reads it.  Strip NS/2 - 1 is throttled by strip NS/2's consumption only, so after each read the
+// drain checks that the slots it read could not have been rewritten yet (strip NS/2 - 1 rewrites
+// element e once it has published e - kRing + 16): it stays within a few columns of the strips, and
+// a lag of kRing - 96 elements would end the launch with the error word rather than a wrong header.
 // ------------------------------------------------------------------------------------
 template <int NS, int K, int LW>
 __device__ __forceinline__ void kr_drain(const StripArgs& a, const KrLds& L, int tk, int lane)
 {
     const int Cp = a.Cp, g = a.g, tBx = a.tBx, tBy = a.tBy, tcols = a.tcols;
     const uint32_t F = L.flags, ringN = L.ring + (uint32_t)NS * (kRing * 4u);
-    if (tk + 1 >= a.nTickets)
+    constexpr bool kTwoRows = 64 * K * NS == 2 * kSparseTileBy;
+    if constexpr (!kTwoRows)
     {
-        flag_st(F + kr_cons(NS), kBig);  // nobody reads our last row
-        return;
-    }
-    const gptr<unsigned long long> gout = G(a.gran) + (size_t)tk * a.granStride;
-    const int rowEnd = (tk + 1) * (64 * K * NS);  // the row this ticket hands down
-    const bool hdr = rowEnd % tBy == 0;
-    const size_t rowbase = (size_t)(rowEnd / tBy) * (size_t)tcols;  // tile index of (iT+1, 0)
-    int dnext = 0;  // next column to drain
-    uint64_t last = __builtin_amdgcn_s_memrealtime();
-    unsigned idle = 0;  // idle passes (error-word polls)
-    while (dnext <= Cp)
-    {
-        const int avail = min(flag_ld(F + kr_prog(NS)) - 64, Cp + 1);  // columns < avail are in ring NS
-        if (dnext < avail)
+        if (tk + 1 >= a.nTickets)
         {
-            const int c = dnext + lane;
-            if (c < avail)
+            flag_st(F + kr_cons(NS), kBig);  // nobody reads our last row
+            return;
+        }
+        const gptr<unsigned long long> gout = G(a.gran) + (size_t)tk * a.granStride;
+        const int rowEnd = (tk + 1) * (64 * K * NS);  // the row this ticket hands down
+        const bool hdr = rowEnd % tBy == 0;
+        const size_t rowbase = (size_t)(rowEnd / tBy) * (size_t)tcols;  // tile index of (iT+1, 0)
+        int dnext = 0;  // next column to drain
+        uint64_t last = __builtin_amdgcn_s_memrealtime();
+        unsigned idle = 0;  // idle passes (error-word polls)
+        while (dnext <= Cp)
+        {
+            const int avail = min(flag_ld(F + kr_prog(NS)) - 64, Cp + 1);  // columns < avail are in ring NS
+            if (dnext < avail)
             {
-                const int v = lds_ld(ringN + 4u * (uint32_t)((c + 64) & (kRing - 1)));
-                __hip_atomic_store(gout + c, ((unsigned long long)a.epoch << 32) | (uint32_t)v, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-                if (hdr)
+                const int c = dnext + lane;
+                if (c < avail)
                 {
-                    const int hv = v + (rowEnd + c) * g;
-                    const int jT = c / tBx, jj = c - jT * tBx;
-                    if (jT < tcols) G(a.hrow)[(rowbase + jT) * (size_t)(tBx + 1) + jj] = hv;
-                    if (jj == 0 && jT > 0)
+                    const int v = lds_ld(ringN + 4u * (uint32_t)((c + 64) & (kRing - 1)));
+                    __hip_atomic_store(gout + c, ((unsigned long long)a.epoch << 32) | (uint32_t)v, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+                    if (hdr)
                     {
-                        G(a.hrow)[(rowbase + jT - 1) * (size_t)(tBx + 1) + tBx] = hv;
-                        if (jT < tcols) G(a.hcol)[(rowbase + jT) * (size_t)(tBy + 1)] = hv;
+                        const int hv = v + (rowEnd + c) * g;
+                        const int jT = c / tBx, jj = c - jT * tBx;
+                        if (jT < tcols) G(a.hrow)[(rowbase + jT) * (size_t)(tBx + 1) + jj] = hv;
+                        if (jj == 0 && jT > 0)
+                        {
+                            G(a.hrow)[(rowbase + jT - 1) * (size_t)(tBx + 1) + tBx] = hv;
+                            if (jT < tcols) G(a.hcol)[(rowbase + jT) * (size_t)(tBy + 1)] = hv;
+                        }
+                    }
+                }
+                dnext = min(dnext + 64, avail);
+                flag_st(F + kr_cons(NS), dnext > Cp ? kBig : dnext + 64);
+                last = __builtin_amdgcn_s_memrealtime();
+            }
+            else
+            {
+                // the error word is a global load, which waits for this wave's granule stores (vmcnt
+                // retires in order): looked at every 64th idle pass only
+                if (__builtin_amdgcn_s_memrealtime() - last > a.spin || ((++idle & 63) == 0 && err_set(a)))
+                {
+                    atomicOr(a.err, 1u);
+                    return;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
+    }
+    else
+    {
+        constexpr int kTicketRows = 64 * K * NS;
+        constexpr int kMid = NS / 2;  // ring after the first tile row of a two-row ticket
+        const uint32_t ringM = L.ring + (uint32_t)kMid * (kRing * 4u);
+        // header row (row, columns c) of the tiles below a tile row boundary, with its duplicates
+        auto put_hdr = [&](int row, int c, int hv) {
+            const size_t rowbase = (size_t)(row / tBy) * (size_t)tcols;  // tile index of (row / tBy, 0)
+            const int jT = c / tBx, jj = c - jT * tBx;
+            if (jT < tcols) G(a.hrow)[(rowbase + jT) * (size_t)(tBx + 1) + jj] = hv;
+            if (jj == 0 && jT > 0)
+            {
+                G(a.hrow)[(rowbase + jT - 1) * (size_t)(tBx + 1) + tBx] = hv;
+                if (jT < tcols) G(a.hcol)[(rowbase + jT) * (size_t)(tBy + 1)] = hv;
+            }
+        };
+        const bool gr = tk + 1 < a.nTickets;  // a next super-strip reads our last row
+        if (!gr) flag_st(F + kr_cons(NS), kBig);  // nobody reads our last row
+        const gptr<unsigned long long> gout = G(a.gran) + (size_t)tk * a.granStride;
+        const int rowEnd = (tk + 1) * kTicketRows;  // the row this ticket hands down
+        const bool hdr = rowEnd % tBy == 0;
+        const int rowMid = tk * kTicketRows + kSparseTileBy;
+        const bool mid = kTwoRows && rowMid / tBy < a.trows;
+        int dnext = gr ? 0 : Cp + 1;   // next column to drain
+        int mnext = mid ? 0 : Cp + 1;  // next column of the mid header row
+    const int NBs = (Cp + 65 + kBlk - 1) / kBlk;  // blocks of a strip (kr_strip's NB)
+        uint64_t last = __builtin_amdgcn_s_memrealtime();
+        unsigned idle = 0;  // idle passes (error-word polls)
+        while (dnext <= Cp || mnext <= Cp)
+        {
+            bool moved = false;
+            if (dnext <= Cp)
+            {
+                const int avail = min(flag_ld(F + kr_prog(NS)) - 64, Cp + 1);  // columns < avail are in ring NS
+                if (dnext < avail)
+                {
+                    const int c = dnext + lane;
+                    if (c < avail)
+                    {
+                        const int v = lds_ld(ringN + 4u * (uint32_t)((c + 64) & (kRing - 1)));
+                        __hip_atomic_store(gout + c, ((unsigned long long)a.epoch << 32) | (uint32_t)v, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+                        if (hdr) put_hdr(rowEnd, c, v + (rowEnd + c) * g);
+                    }
+                    dnext = min(dnext + 64, avail);
+                    flag_st(F + kr_cons(NS), dnext > Cp ? kBig : dnext + 64);
+                    moved = true;
+                }
+            }
+            if constexpr (kTwoRows)
+            {
+                if (mnext <= Cp)
+                {
+                    const int availm = min(flag_ld(F + kr_prog(kMid)) - 64, Cp + 1);  // columns < availm in ring kMid
+                    if (mnext < availm)
+                    {
+                        const int c = mnext + lane;
+                        const int v = lds_ld(ringM + 4u * (uint32_t)((c + 64) & (kRing - 1)));
+                        asm volatile("" ::: "memory");  // the data reads before the check's read (LDS in order)
+                        // (kBig: the strip has finished, having written elements < 16 NBs)
+                    const int pm = flag_ld(F + kr_prog(kMid));
+                    if ((pm == kBig ? kBlk * NBs : pm) > mnext + 64 + kRing - 32)
+                        {
+                            atomicOr(a.err, 1u);
+                            return;
+                        }
+                        if (c < availm) put_hdr(rowMid, c, v + (rowMid + c) * g);
+                        mnext = min(mnext + 64, availm);
+                        moved = true;
                     }
                 }
             }
-            dnext = min(dnext + 64, avail);
-            flag_st(F + kr_cons(NS), dnext > Cp ? kBig : dnext + 64);
-            last = __builtin_amdgcn_s_memrealtime();
-        }
-        else
-        {
-            // the error word is a global load, which waits for this wave's granule stores (vmcnt
-            // retires in order): looked at every 64th idle pass only
-            if (__builtin_amdgcn_s_memrealtime() - last > a.spin || ((++idle & 63) == 0 && err_set(a)))
+            if (moved)
+                last = __builtin_amdgcn_s_memrealtime();
+            else
             {
-                atomicOr(a.err, 1u);
-                return;
+                // the error word is a global load, which waits for this wave's granule stores (vmcnt
+                // retires in order): looked at every 64th idle pass only
+                if (__builtin_amdgcn_s_memrealtime() - last > a.spin || ((++idle & 63) == 0 && err_set(a)))
+                {
+                    atomicOr(a.err, 1u);
+                    return;
+                }
+                __builtin_amdgcn_s_sleep(1);
             }
-            __builtin_amdgcn_s_sleep(1);
         }
     }
 }
@@ -714,6 +812,7 @@ hipError_t launch_krow_fill(const StripArgs& a, int ns, int k, int lw, int grid,
     if (k == 2) return ns == 2 ? launch_kr<2, 2, 512>(a, grid, stream) : launch_kr<4, 2, 1024>(a, grid, stream);
     (void)lw;  // 512 for (4, 4) measured slower for one pair and for batches (the first strip
                // is throttled by the window): 1024
+    if (ns == 8) return launch_kr<8, 4, 1024>(a, grid, stream);
     return ns == 2 ? launch_kr<2, 4, 512>(a, grid, stream) : launch_kr<4, 4, 1024>(a, grid, stream);
 }
 

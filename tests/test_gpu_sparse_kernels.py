@@ -12,7 +12,7 @@ from tests._data import random_pair, related_pair
 pytestmark = pytest.mark.gpu
 
 # (kernel, strips per workgroup, rows per lane)
-KERNELS = [("krow", 4, 4), ("krow", 4, 2), ("krow", 2, 4), ("krow", 2, 2), ("strip", 4, 4)]
+KERNELS = [("krow", 4, 4), ("krow", 8, 4), ("krow", 4, 2), ("krow", 2, 4), ("krow", 2, 2), ("strip", 4, 4)]
 
 
 def _select(monkeypatch, kern, ns, k):
