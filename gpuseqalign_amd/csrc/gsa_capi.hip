@@ -337,17 +337,17 @@ int enqueue_batch(gsa_ctx* ctx, int mode, int npairs, const gsa_pair_dev* pairs,
     a.substsz = substsz;
     a.g = gapo;
     const bool lane = mode == gsa::kModeFull;
-    // mlsppt (done flags per tile row) stays on the strip kernel
-    const bool krow = mode == gsa::kModeSparse && !done && sparse_kernel() == kSpKrow;
+    const bool krow = mode == gsa::kModeSparse && sparse_kernel() == kSpKrow;
     // single pairs: 4 strips per workgroup (each on its own SIMD: the pair's critical path);
     // batches: 8 (two strips per SIMD share the issue slots a single strip leaves idle, 512 x 20k
     // 5.7 -> 7.3 TCUPS; a single 100k pair 5.9 -> 8.4 ms)
     const int nsDefault = npairs > 1 ? gsa::kKrowNSBatchDefault : gsa::kKrowNSDefault;
     int krowK = env_int("GSA_KROW_K", gsa::kKrowKDefault), krowNS = env_int("GSA_KROW_NS", nsDefault);
-    if (!gsa::krow_ok(krowNS, krowK))
+    // mlsppt flags one ticket per tile row: only the geometry whose ticket is one tile row
+    if (!gsa::krow_ok(krowNS, krowK) || (done && gsa::krow_ticket_rows(krowNS, krowK) != gsa::kSparseTileBy))
     {
         krowK = gsa::kKrowKDefault;
-        krowNS = nsDefault;
+        krowNS = gsa::kKrowNSDefault;
     }
     a.ns = lane ? lane_ns() : krow ? krowNS : gsa::kSparseNS;
     const int fullRows = gsa::kLaneRows * a.ns;  // rows per ticket of a full fill

@@ -726,13 +726,21 @@ __global__ void __launch_bounds__(64 * (NS + 2)) nw_krow_kernel(StripArgs a)
     }
     if (bad) atomicOr(a.err, 2u);
     if (threadIdx.x < 16) lds_st(L.zfill + 4u * threadIdx.x, 0);
+    int prevTk = -1;  // ticket this workgroup finished last (mlsppt signalling)
     for (;;)
     {
+        // mlsppt (a.done: one host-mapped flag per ticket = tile row): every wave writes its stores
+        // of the finished ticket back past L2 (system-scope release), then one thread flags the
+        // ticket to the host, which copies that tile row while the fill goes on
+        if (a.done && prevTk >= 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
         __syncthreads();
+        if (a.done && prevTk >= 0 && threadIdx.x == 0)
+            __hip_atomic_store(a.done + prevTk, a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         if (threadIdx.x == 0) lds_st(L.flags + kFTicket, err_set(a) ? a.nTicketsTotal : (int)atomicAdd(a.ticket, 1u));
         __syncthreads();
         const int tkg = __builtin_amdgcn_readfirstlane(lds_ld(L.flags + kFTicket));
         if (tkg >= a.nTicketsTotal) break;
+        prevTk = tkg;
         // pair of this ticket: the batch schedule, or the last descriptor with ticketBase <= tkg
         int lo = 0, tks = -1;
         if (a.sched)
