@@ -62,6 +62,11 @@ struct gsa_ctx
     long long* tres = nullptr;
     unsigned* tdirs = nullptr;
     size_t tdirs_cap = 0;
+    // tiles precomputed around the diagonal (trace_band): codes, and [list | map] ints
+    unsigned* tband = nullptr;
+    size_t tband_cap = 0;
+    int* tlist = nullptr;
+    size_t tlist_cap = 0;
     // score-only fills (nw_scan.hip): boundary rows H/F, progress words, control words
     int* sbnd = nullptr;
     size_t sbnd_cap = 0;
@@ -174,7 +179,8 @@ hipStream_t pick_stream(gsa_ctx*, void* stream) { return (hipStream_t)stream; }
 long long held_bytes(const gsa_ctx* c)
 {
     long long b = 256 + 64 + (long long)c->gran_elems * 8 + (long long)c->desc_cap * (long long)sizeof(gsa::PairDesc) +
-                  (long long)c->tmoves_cap + (long long)c->tdirs_cap * 4 + (long long)c->sbnd_cap * 4;
+                  (long long)c->tmoves_cap + (long long)c->tdirs_cap * 4 + (long long)c->sbnd_cap * 4 +
+                  (long long)c->tband_cap + (long long)c->tlist_cap * 4;
     for (size_t k : c->dcap) b += (long long)k;
     return b;
 }
@@ -532,6 +538,8 @@ void gsa_ctx_destroy(gsa_ctx* ctx)
     if (ctx->tmoves) (void)hipFree(ctx->tmoves);
     if (ctx->tres) (void)hipFree(ctx->tres);
     if (ctx->tdirs) (void)hipFree(ctx->tdirs);
+    if (ctx->tband) (void)hipFree(ctx->tband);
+    if (ctx->tlist) (void)hipFree(ctx->tlist);
     if (ctx->sbnd) (void)hipFree(ctx->sbnd);
     if (ctx->sctl) (void)hipFree(ctx->sctl);
     if (ctx->ptflags) (void)hipHostFree(ctx->ptflags);
@@ -839,6 +847,62 @@ int gsa_trace_sparse_dev(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, con
     a.cap = (long long)nmax;
     a.res = ctx->tres;
     a.dirs_scratch = dirs_lds ? nullptr : ctx->tdirs;
+    // The walk enters tiles one after another, and recomputing one (a row scan over its rows) takes
+    // ~160 us at 1024 x 256.  The tiles are independent given their headers, so the ones within
+    // GSA_TRACE_BAND columns (default 2048) of the diagonal are recomputed first by many workgroups
+    // at once; the walk copies their codes and recomputes only the tiles it finds outside the band.
+    a.tmap = nullptr;
+    a.tcodes = nullptr;
+    if (dirs_lds)
+    {
+        const int band = env_int("GSA_TRACE_BAND", 2048);
+        const int trows = g.tileHdrMatRows, tcols = g.tileHdrMatCols;
+        const size_t words = gsa::trace_dir_words(g.tileBy, g.tileBx);
+        const size_t maxSlots = ((size_t)512 << 20) / (words * 4);  // 512 MB of codes at most
+        std::vector<int> list, map((size_t)trows * (size_t)tcols, -1);
+        const double slope = (double)std::max<int64_t>(1, adjcols - 1) / (double)std::max<int64_t>(1, adjrows - 1);
+        for (int r = 0; band > 0 && r < trows && list.size() / 2 < maxSlots; ++r)
+        {
+            const double c0 = (double)r * g.tileBy * slope - band, c1 = (double)(r + 1) * g.tileBy * slope + band;
+            const int j0 = std::max(0, (int)(c0 / g.tileBx)), j1 = std::min(tcols - 1, (int)(c1 / g.tileBx));
+            for (int c = j0; c <= j1 && list.size() / 2 < maxSlots; ++c)
+            {
+                if (r == iT && c == jT) continue;  // the start tile: recomputed by the walk (align cost)
+                map[(size_t)r * tcols + c] = (int)(list.size() / 2);
+                list.push_back(r);
+                list.push_back(c);
+            }
+        }
+        const int n = (int)(list.size() / 2);
+        if (n > 0)
+        {
+            const size_t ints = list.size() + map.size(), cbytes = (size_t)n * words * 4;
+            if (ctx->tlist_cap < ints)
+            {
+                if (ctx->tlist) (void)hipFree(ctx->tlist);
+                ctx->tlist = nullptr;
+                ctx->tlist_cap = 0;
+                if ((e = hipMalloc(&ctx->tlist, ints * 4)) != hipSuccess) return fail(ctx, e, GSA_ERROR_MEMORY_ALLOCATION);
+                ctx->tlist_cap = ints;
+            }
+            if (ctx->tband_cap < cbytes)
+            {
+                if (ctx->tband) (void)hipFree(ctx->tband);
+                ctx->tband = nullptr;
+                ctx->tband_cap = 0;
+                if ((e = hipMalloc(&ctx->tband, cbytes)) != hipSuccess) return fail(ctx, e, GSA_ERROR_MEMORY_ALLOCATION);
+                ctx->tband_cap = cbytes;
+            }
+            // pageable sources: the copies are complete when the calls return
+            if ((e = hipMemcpyAsync(ctx->tlist, list.data(), list.size() * 4, hipMemcpyHostToDevice, st)) != hipSuccess ||
+                (e = hipMemcpyAsync(ctx->tlist + list.size(), map.data(), map.size() * 4, hipMemcpyHostToDevice, st)) != hipSuccess)
+                return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
+            a.tmap = ctx->tlist + list.size();
+            a.tcodes = ctx->tband;
+            if ((e = gsa::launch_trace_band(a, ctx->tlist, n, 4 * ctx->cu_count, st)) != hipSuccess)
+                return fail(ctx, e, GSA_ERROR_KERNEL_FAILURE);
+        }
+    }
     if ((e = gsa::launch_trace_sparse(a, st)) != hipSuccess) return fail(ctx, e, GSA_ERROR_KERNEL_FAILURE);
     long long res[2] = {0, 0};
     if ((e = hipMemcpyAsync(res, ctx->tres, sizeof(res), hipMemcpyDeviceToHost, st)) != hipSuccess ||

@@ -22,10 +22,17 @@ struct TraceArgs
     long long cap;          // bytes available in edits
     long long* res;         // [0] moves, [1] align_cost
     unsigned* dirs_scratch; // move codes in global memory when the tile is too wide for LDS (else null)
+    // precomputed tiles (trace_band): tmap[iT * tcols + jT] = slot or -1, codes of slot s at
+    // tcodes + s * trace_dir_words(tBy, tBx); null: every tile is recomputed on entry
+    const int* tmap;
+    const unsigned* tcodes;
 };
 
 size_t trace_dir_words(int tBy, int tBx);
 size_t trace_lds_bytes(int tBy, int tBx, int substsz, bool dirs_lds);
 hipError_t launch_trace_sparse(const TraceArgs& a, hipStream_t st);
+// move codes of the n tiles list[2s], list[2s+1] (whole tiles) into a.tcodes, slot s; many
+// workgroups (the tiles are independent given their headers)
+hipError_t launch_trace_band(const TraceArgs& a, const int* list, int n, int grid, hipStream_t st);
 
 }  // namespace gsa

@@ -45,6 +45,12 @@ __device__ __forceinline__ int wave_prefix_max(int v)
     return v;
 }
 
+// lane l of v <- the uniform value x
+__device__ __forceinline__ void writelane(int& v, unsigned x, int l)
+{
+    v = ((int)(threadIdx.x & 63) == l) ? (int)x : v;
+}
+
 __device__ __forceinline__ int clamp_letter(int x, int substsz) { return ((unsigned)x < (unsigned)substsz) ? x : 0; }
 
 // move codes: diagonal with equal / different letters ('=' / 'X'), up ('I'), left ('D')
@@ -53,6 +59,11 @@ constexpr int kDiagEq = 0, kDiagX = 1, kUp = 2, kLeft = 3;
 }  // namespace
 
 extern __shared__ __attribute__((aligned(16))) int tsm[];
+
+__host__ __device__ inline size_t trace_dir_words_dev(int tBy, int tBx)
+{
+    return (size_t)((tBy + 15) / 16) * ((tBx + 63) / 64) * 64;
+}
 
 constexpr int kTW = 4;  // waves per workgroup: the panels of a tile are pipelined over them
 
@@ -179,6 +190,8 @@ __global__ void __launch_bounds__(64 * kTW) trace_sparse_kernel(TraceArgs a)
     int iT = a.iT0, jT = a.jT0, iE = a.iE0, jE = a.jE0;
     const int Wm = a.tBx, Hm = a.tBy;  // hrowLen-1, hcolLen-1
     long long n = 0;
+    unsigned acc = 0;  // edit bytes of the current dword (wave 0)
+    int ebuf = 0;      // packed edit dwords, lane k = moves 4k..4k+3 of the current 256
     bool first = true;
     if (tid == 0 && (iE == 0 || jE == 0))
     {
@@ -189,66 +202,105 @@ __global__ void __launch_bounds__(64 * kTW) trace_sparse_kernel(TraceArgs a)
     for (;;)
     {
         if (iE > 0 && jE > 0)
-            tile_moves<DIRS_LDS>(a, iT, jT, iE, jE, sub, bnd, yraw, xraw, bprog, dirs, w, lane, first);
+        {
+            // a tile trace_band precomputed (never the start tile, whose recompute yields the cost):
+            // its codes are copied into LDS; any other is recomputed here
+            int slot = -1;
+            if (DIRS_LDS && a.tmap && !first) slot = __builtin_amdgcn_readfirstlane(G(a.tmap)[(long long)iT * a.tcols + jT]);
+            if (slot >= 0)
+            {
+                const size_t words = trace_dir_words_dev(a.tBy, a.tBx);
+                typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+                const gptr<const u32x4> src = (gptr<const u32x4>)(a.tcodes + (size_t)slot * words);
+                __syncthreads();  // the previous walk has read its codes
+                // 8 loads in flight per thread per round (a loop of single loads pays a round
+                // trip per 16 bytes)
+                const size_t nq = words / 4;
+                for (size_t q0 = 0; q0 < nq; q0 += 8 * 64 * kTW)
+                {
+                    u32x4 v[8];
+#pragma unroll
+                    for (int r = 0; r < 8; ++r)
+                    {
+                        const size_t q = q0 + (size_t)r * 64 * kTW + tid;
+                        if (q < nq) v[r] = src[q];
+                    }
+#pragma unroll
+                    for (int r = 0; r < 8; ++r)
+                    {
+                        const size_t q = q0 + (size_t)r * 64 * kTW + tid;
+                        if (q < nq) ((u32x4*)dirs)[q] = v[r];
+                    }
+                }
+                __syncthreads();
+            }
+            else
+                tile_moves<DIRS_LDS>(a, iT, jT, iE, jE, sub, bnd, yraw, xraw, bprog, dirs, w, lane, first);
+        }
         first = false;
         int done = 0;
         if (w == 0)
         {
+            // The move codes of the current 16-row group x 64-column panel sit in one VGPR (lane =
+            // column), read with v_readlane: one LDS read per group / panel change, not per move.
+            // Edit bytes are packed 4 per dword into lane (n/4) % 64 of a VGPR and stored 256 at a
+            // time by the whole wave.
+            int cg = -1, cp = -1;  // row group / panel of the cached codes
+            int cw = 0;
+            // branch-free move: code -> (di, dj, edit byte) by arithmetic on uniform values;
+            // '=' 'X' 'I' 'D' packed in one word, indexed by the code
+            constexpr unsigned kEdits = (unsigned)'=' | ((unsigned)'X' << 8) | ((unsigned)'I' << 16) | ((unsigned)'D' << 24);
+            int ci = __builtin_amdgcn_readfirstlane(iE), cj = __builtin_amdgcn_readfirstlane(jE);
             for (;;)
             {
-                int di = 0, dj = 0, e = 0;
-                if (iE > 0 && jE > 0)
+                int code;
+                if (ci > 0 && cj > 0)
                 {
-                    const size_t wi = ((size_t)((iE - 1) >> 4) * nP + ((jE - 1) >> 6)) * 64 + ((jE - 1) & 63);
-                    const unsigned cw = __builtin_amdgcn_readfirstlane(dirs[wi]);
-                    const int code = (cw >> (2 * ((iE - 1) & 15))) & 3;
-                    if (code <= kDiagX)
+                    const int gi = (ci - 1) >> 4, pj = (cj - 1) >> 6;
+                    if (gi != cg || pj != cp)
                     {
-                        di = dj = -1;
-                        e = (code == kDiagEq) ? '=' : 'X';  // seqX[j] == seqY[i]
+                        cw = (int)dirs[((size_t)gi * nP + pj) * 64 + lane];
+                        cg = gi;
+                        cp = pj;
                     }
-                    else if (code == kUp)
-                    {
-                        di = -1;
-                        e = 'I';
-                    }
-                    else
-                    {
-                        dj = -1;
-                        e = 'D';
-                    }
+                    const unsigned word = (unsigned)__builtin_amdgcn_readlane(cw, (cj - 1) & 63);
+                    code = (int)((word >> (2 * ((ci - 1) & 15))) & 3u);
                 }
-                else if (iE > 0)
-                {
-                    di = -1;
-                    e = 'I';
-                }
-                else if (jE > 0)
-                {
-                    dj = -1;
-                    e = 'D';
-                }
-                if (di == 0 && dj == 0)
+                else
+                    code = ci > 0 ? kUp : kLeft;
+                if (ci == 0 && cj == 0)
                 {
                     done = 1;
                     break;
                 }
-                if (lane == 0 && n < a.cap) G(a.edits)[n] = (unsigned char)e;
-                ++n;
-                iE += di;
-                jE += dj;
-                // into the tile above / left / up-left on reaching its header (nwtrace2_sparse.cpp:195-214)
-                const int diT = (iE == 0 && iT > 0) ? 1 : 0;
-                const int djT = (jE == 0 && jT > 0) ? 1 : 0;
-                if (diT || djT)
+                const int di = code == kLeft ? 0 : -1, dj = code == kUp ? 0 : -1;
+                const unsigned e = (kEdits >> (8 * code)) & 0xffu;
+                const unsigned nn = (unsigned)n;
+                acc |= e << (8 * (nn & 3u));
+                writelane(ebuf, acc, (int)((nn >> 2) & 63u));
+                if ((nn & 255u) == 255u)
                 {
+                    const long long b0 = n - 255;  // first move of the 256 in ebuf
+                    if (b0 + 256 <= a.cap) G((unsigned*)(a.edits + b0))[lane] = (unsigned)ebuf;
+                }
+                acc = (nn & 3u) == 3u ? 0u : acc;
+                ++n;
+                ci += di;
+                cj += dj;
+                // into the tile above / left / up-left on reaching its header (nwtrace2_sparse.cpp:195-214)
+                if ((ci == 0 && iT > 0) || (cj == 0 && jT > 0))
+                {
+                    const int diT = (ci == 0 && iT > 0) ? 1 : 0;
+                    const int djT = (cj == 0 && jT > 0) ? 1 : 0;
                     iT -= diT;
                     jT -= djT;
-                    if (iE == 0 && di != 0) iE = Hm;
-                    if (jE == 0 && dj != 0) jE = Wm;
+                    if (ci == 0 && di != 0) ci = Hm;
+                    if (cj == 0 && dj != 0) cj = Wm;
                     break;
                 }
             }
+            iE = ci;
+            jE = cj;
             if (lane == 0)
             {
                 state[0] = iT;
@@ -266,7 +318,44 @@ __global__ void __launch_bounds__(64 * kTW) trace_sparse_kernel(TraceArgs a)
         done = state[4];
         if (done) break;
     }
+    if (w == 0)
+    {
+        // the last partial group of 256 moves: dwords of complete and the partial dword
+        if ((n & 3) != 0) writelane(ebuf, acc, (int)((n >> 2) & 63));
+        const long long b0 = n & ~255ll;
+        const int k = lane * 4;
+        if (b0 + k < n && b0 + k < a.cap)
+        {
+            for (int t = 0; t < 4 && b0 + k + t < n && b0 + k + t < a.cap; ++t)
+                a.edits[b0 + k + t] = (unsigned char)((unsigned)ebuf >> (8 * t));
+        }
+    }
     if (tid == 0) G(a.res)[0] = n;
+}
+
+// whole tiles, many workgroups: slot s = (list[2s], list[2s+1]), rows 1..min(tBy, rows left),
+// columns 1..min(tBx, columns left)
+__global__ void __launch_bounds__(64 * kTW) trace_band_kernel(TraceArgs a, const int* list, int n)
+{
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    const int tBy = a.tBy;
+    int* sub = tsm;
+    int* bnd = sub + 32 * 32;
+    int* yraw = bnd + (kTW + 1) * (tBy + 1);
+    int* xraw = yraw + (tBy + 1);
+    int* bprog = xraw + (a.tBx + 1);
+    for (int k = tid; k < a.substsz * a.substsz; k += 64 * kTW) sub[k] = G(a.subst)[k];
+    const size_t words = trace_dir_words_dev(a.tBy, a.tBx);
+    for (int s = blockIdx.x; s < n; s += gridDim.x)
+    {
+        const int iT = __builtin_amdgcn_readfirstlane(G(list)[2 * s]);
+        const int jT = __builtin_amdgcn_readfirstlane(G(list)[2 * s + 1]);
+        const int iE = (int)min((long long)a.tBy, a.adjrows - 1 - (long long)iT * a.tBy);
+        const int jE = (int)min((long long)a.tBx, a.adjcols - 1 - (long long)jT * a.tBx);
+        if (iE > 0 && jE > 0)
+            tile_moves<false>(a, iT, jT, iE, jE, sub, bnd, yraw, xraw, bprog, (unsigned*)a.tcodes + (size_t)s * words,
+                              w, lane, false);
+    }
 }
 
 size_t trace_lds_bytes(int tBy, int tBx, int substsz, bool dirs_lds)
@@ -276,7 +365,18 @@ size_t trace_lds_bytes(int tBy, int tBx, int substsz, bool dirs_lds)
     return base + (dirs_lds ? trace_dir_words(tBy, tBx) * 4 : 0);
 }
 
-size_t trace_dir_words(int tBy, int tBx) { return (size_t)((tBy + 15) / 16) * ((tBx + 63) / 64) * 64; }
+size_t trace_dir_words(int tBy, int tBx) { return trace_dir_words_dev(tBy, tBx); }
+
+hipError_t launch_trace_band(const TraceArgs& a, const int* list, int n, int grid, hipStream_t st)
+{
+    if (a.substsz > 32) return hipErrorInvalidValue;
+    if (n <= 0) return hipSuccess;
+    const size_t bytes = trace_lds_bytes(a.tBy, a.tBx, a.substsz, false);
+    hipError_t e = hipFuncSetAttribute((const void*)trace_band_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(trace_band_kernel, dim3(std::max(1, std::min(grid, n))), dim3(64 * kTW), bytes, st, a, list, n);
+    return hipGetLastError();
+}
 
 hipError_t launch_trace_sparse(const TraceArgs& a, hipStream_t st)
 {

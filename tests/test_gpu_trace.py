@@ -75,3 +75,19 @@ def test_device_trace_100k(engine, golden):
     dev, host = _both(engine, Y, X, golden.blosum62, -11, 256)
     assert dev == host
     assert len(dev[1]) > 1000  # a non-trivial edit path
+
+
+@pytest.mark.parametrize("band", ["0", "16", "300"])
+@pytest.mark.parametrize("R,C,tBx,related", [(3000, 3000, 64, False), (2500, 4100, 128, True), (4100, 1700, 64, False)])
+def test_device_trace_band(engine, golden, monkeypatch, band, R, C, tBx, related):
+    """Tiles precomputed around the diagonal (GSA_TRACE_BAND columns) and tiles the walk finds
+    outside the band (recomputed on entry) give the host walk: no band, a band narrower than a
+    tile (random pairs leave it), and a wider one."""
+    monkeypatch.setenv("GSA_TRACE_BAND", band)
+    if related:
+        Y, X = related_pair(R, R + C)
+        X = X[:C + 1] if len(X) > C + 1 else X
+    else:
+        Y, X = random_pair(R, C, 7 * R + C)
+    dev, host = _both(engine, Y, X, golden.blosum62, -11, tBx)
+    assert dev == host
