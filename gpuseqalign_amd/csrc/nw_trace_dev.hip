@@ -274,6 +274,21 @@ __global__ void __launch_bounds__(64 * kTW) trace_sparse_kernel(TraceArgs a)
                     const int gi = (ci - 1) >> 4, pj = (cj - 1) >> 6;
                     const int cw = (int)dirs[((size_t)gi * nP + pj) * 64 + lane];
                     const int ilo = 16 * gi + 1, jlo = 64 * pj + 1;
+                    auto step = [&]() {
+                        const unsigned word = (unsigned)__builtin_amdgcn_readlane(cw, (cj - 1) & 63);
+                        const int code = (int)((word >> (2 * ((ci - 1) & 15))) & 3u);
+                        di = code == kLeft ? 0 : -1;
+                        dj = code == kUp ? 0 : -1;
+                        emit(code);
+                        ci += di;
+                        cj += dj;
+                    };
+                    // 8 moves without a check while 8 cannot leave the window or cross a 256-move store
+                    while (ci - ilo >= 8 && cj - jlo >= 8 && (n & 255) <= 247)
+                    {
+#pragma unroll
+                        for (int u = 0; u < 8; ++u) step();
+                    }
                     do
                     {
                         const unsigned word = (unsigned)__builtin_amdgcn_readlane(cw, (cj - 1) & 63);
