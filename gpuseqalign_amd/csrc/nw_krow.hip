@@ -404,7 +404,8 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
 // loader wave: the column profile and the row above strip 0 (granules of the previous
 // super-strip, or row 0)
 // ------------------------------------------------------------------------------------
-template <int NS, int K, int LW>
+// ROLE 0: both jobs in one wave; 1: the feed only; 2: the profile only
+template <int NS, int K, int LW, int ROLE>
 __device__ __forceinline__ void kr_loader(const StripArgs& a, const KrLds& L, int tk, int lane)
 {
     const int Cp = a.Cp, C = a.C;
@@ -427,14 +428,14 @@ __device__ __forceinline__ void kr_loader(const StripArgs& a, const KrLds& L, in
     int pl = 0, c0 = 0;  // progress words, re-read only when their cached values block
     uint64_t last = __builtin_amdgcn_s_memrealtime();
     unsigned idle = 0;  // idle passes (error-word polls)
-    while (qn <= Cp || hnext <= Cp)
+    while ((ROLE != 1 && qn <= Cp) || (ROLE != 2 && hnext <= Cp))
     {
         bool moved = false;
         // (1) the row above strip 0 -> ring 0 elements c + 64, as far as granules of the previous
         //     super-strip are published (in column order) and ring 0 has room.  The poll is issued
         //     first and consumed after the profile work, which runs under its latency.
-        if (hnext <= Cp && hnext + 128 > c0 + kRing) c0 = flag_ld(F + kr_cons(0));
-        const bool feed = hnext <= Cp && hnext + 128 <= c0 + kRing;
+        if (ROLE != 2 && hnext <= Cp && hnext + 128 > c0 + kRing) c0 = flag_ld(F + kr_cons(0));
+        const bool feed = ROLE != 2 && hnext <= Cp && hnext + 128 <= c0 + kRing;
         const int c = hnext + lane;
         const bool in = c <= Cp;
         unsigned long long q = 0ull;
@@ -444,8 +445,8 @@ __device__ __forceinline__ void kr_loader(const StripArgs& a, const KrLds& L, in
         //     then reads columns >= pl-47).  Built in 4 passes of 8 letters, one per iteration,
         //     so the poll is consumed and re-issued between them: strip 0's lag ratchets to the
         //     feed delay's tail (one pass per iteration: 100k 5.88 -> 5.70 ms)
-        if (qsub == 0 && qn <= Cp && qn + 192 > pl + kLW) pl = flag_ld(F + kr_prog(NS));
-        if (qsub > 0 || (qn <= Cp && qn + 192 <= pl + kLW))
+        if (ROLE != 1 && qsub == 0 && qn <= Cp && qn + 192 > pl + kLW) pl = flag_ld(F + kr_prog(NS));
+        if (ROLE != 1 && (qsub > 0 || (qn <= Cp && qn + 192 <= pl + kLW)))
         {
             // letters yy = 8 qsub .. 8 qsub + 7: dwords 2 qsub, 2 qsub + 1 of the three subT rows
             int4v vm[2], v0[2], v1[2];
@@ -530,7 +531,7 @@ __device__ __forceinline__ void kr_loader(const StripArgs& a, const KrLds& L, in
                 atomicOr(a.err, 1u);
                 return;
             }
-            if (tk == 0 || hnext > Cp) __builtin_amdgcn_s_sleep(1);
+            if (ROLE == 2 || tk == 0 || hnext > Cp) __builtin_amdgcn_s_sleep(1);
         }
     }
 }
@@ -710,14 +711,21 @@ __device__ __forceinline__ PairDesc kr_desc(const PairDesc* p)
     return u.d;
 }
 
+// waves per workgroup: NS strips, the loader (split into a feeder and a profiler wave when the SIMDs
+// have room: NS <= 4), the drain
+template <int NS>
+constexpr bool kr_split() { return NS <= 4; }
+template <int NS>
+constexpr int kr_waves() { return NS + 2 + (kr_split<NS>() ? 1 : 0); }
+
 template <int NS, int K, int LW>
-__global__ void __launch_bounds__(64 * (NS + 2)) nw_krow_kernel(StripArgs a)
+__global__ void __launch_bounds__(64 * kr_waves<NS>()) nw_krow_kernel(StripArgs a)
 {
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     const KrLds L = kr_layout(NS, LW, a.substsz);
     bool bad = false;
-    for (int k = threadIdx.x; k < a.substsz * kSubRow; k += 64 * (NS + 2))
+    for (int k = threadIdx.x; k < a.substsz * kSubRow; k += 64 * kr_waves<NS>())
     {
         const int x = k / kSubRow, yy = k % kSubRow;
         const int v = yy < a.substsz ? G(a.subst)[yy * a.substsz + x] - 2 * a.g : 0;
@@ -780,7 +788,9 @@ __global__ void __launch_bounds__(64 * (NS + 2)) nw_krow_kernel(StripArgs a)
         if (w == NS + 1)
             kr_drain<NS, K, LW>(pa, L, tk, lane);
         else if (w == NS)
-            kr_loader<NS, K, LW>(pa, L, tk, lane);
+            kr_loader<NS, K, LW, kr_split<NS>() ? 1 : 0>(pa, L, tk, lane);
+        else if (kr_split<NS>() && w == NS + 2)
+            kr_loader<NS, K, LW, 2>(pa, L, tk, lane);
         else
         {
             __builtin_amdgcn_s_setprio(3);
@@ -800,14 +810,14 @@ hipError_t launch_kr(const StripArgs& a, int grid, hipStream_t stream)
     if (grid <= 0)
     {
         int per_cu = 0, dev = 0, cus = 0;
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)kern, 64 * (NS + 2), lds);
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)kern, 64 * kr_waves<NS>(), lds);
         if (e == hipSuccess) e = hipGetDevice(&dev);
         if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
         if (e != hipSuccess) return e;
         grid = std::max(1, std::min(a.nTicketsTotal, std::max(1, per_cu) * cus));
     }
-    if ((e = record_foot((const void*)kern, lds, 64 * (NS + 2), grid)) != hipSuccess) return e;
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * (NS + 2)), lds, stream, a);
+    if ((e = record_foot((const void*)kern, lds, 64 * kr_waves<NS>(), grid)) != hipSuccess) return e;
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * kr_waves<NS>()), lds, stream, a);
     return hipGetLastError();
 }
 
