@@ -46,13 +46,17 @@ rep("""                hnext += n;""", """                {
                         for (int c = hnext / 16 + 1; c <= (hnext + n) / 16 && c < 6400; ++c) g_kld[tk][c][0] = tn;
                 }
                 hnext += n;""")
-rep("""            dnext = min(dnext + 64, avail);""", """            {
-                const int dn = min(dnext + 64, avail);
-                const unsigned long long tn = __builtin_amdgcn_s_memtime();
-                if (tk < 8 && lane == 0)
-                    for (int c = dnext / 16 + 1; c <= dn / 16 && c < 6400; ++c) g_kld[tk][c][1] = tn;
-            }
-            dnext = min(dnext + 64, avail);""")
+rep("""                dnext = min(dnext + 64, avail);
+                flag_st(F + kr_cons(NS), dnext > Cp ? kBig : dnext + 64);
+                last = __builtin_amdgcn_s_memrealtime();""", """                {
+                    const int dn = min(dnext + 64, avail);
+                    const unsigned long long tn = __builtin_amdgcn_s_memtime();
+                    if (tk < 8 && lane == 0)
+                        for (int c = dnext / 16 + 1; c <= dn / 16 && c < 6400; ++c) g_kld[tk][c][1] = tn;
+                }
+                dnext = min(dnext + 64, avail);
+                flag_st(F + kr_cons(NS), dnext > Cp ? kBig : dnext + 64);
+                last = __builtin_amdgcn_s_memrealtime();""")
 s += """
 extern "C" int gsa_dbg_kld(void* dst, size_t n)
 {
