@@ -289,6 +289,11 @@ __global__ void __launch_bounds__(64 * kTW) trace_sparse_kernel(TraceArgs a)
 #pragma unroll
                         for (int u = 0; u < 8; ++u) step();
                     }
+                    while (ci - ilo >= 4 && cj - jlo >= 4 && (n & 255) <= 251)
+                    {
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) step();
+                    }
                     do
                     {
                         const unsigned word = (unsigned)__builtin_amdgcn_readlane(cw, (cj - 1) & 63);
