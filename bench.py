@@ -68,6 +68,12 @@ def load_golden(name):
         return json.load(f)
 
 
+def lane_ns():
+    """Lane strips per workgroup of full fills, as gsa_capi.hip's lane_ns() reads GSA_LANE_NS."""
+    v = os.environ.get("GSA_LANE_NS", "")
+    return int(v) if v in ("1", "2", "3", "4", "6", "8") else 4
+
+
 def sparse_kernel_name():
     return "gsa::nw_krow_kernel<4,4,1024> (sparse, K = 4 rows per lane)"
 
@@ -278,7 +284,7 @@ def main():
                                "(resrc/seq_generated.fa), full int32 score matrix in HBM",
                    "value": round(world * R2 * C2 * a.steps / el2 / 1e9, 2), "unit": "GCUPS",
                    "ms_per_step": round(el2 * 1e3 / a.steps, 4), "kernel_ms": round(km2, 4),
-                   "kernel": "gsa::nw_lane_kernel<4> (full, one row per lane)",
+                   "kernel": f"gsa::nw_lane_kernel<{lane_ns()}> (full, one row per lane)",
                    "hbm_write_GBps": round(b2 / (km2 * 1e-3) / 1e9, 1),
                    "hbm_frac": round(b2 / (km2 * 1e-3) / 1e9 / PEAK_HBM_GBPS, 4),
                    "align_cost": int(score[-1].item()), "golden_align_cost": -4922}
