@@ -76,11 +76,11 @@ def lane_ns():
 
 def sparse_kernel_name():
     """The K-rows instantiation a single-pair sparse fill runs (gsa_capi.hip: GSA_KROW_NS / GSA_KROW_K,
-    default (4, 4); the profile ring is 1024 columns for (4, 4) and (8, 4), 512 otherwise)."""
+    default (4, 4); the profile ring is 512 columns with 2 strips, 1024 otherwise)."""
     ns, k = os.environ.get("GSA_KROW_NS", "4"), os.environ.get("GSA_KROW_K", "4")
     ok = (k in ("2", "4") and ns in ("2", "4")) or (k == "4" and ns == "8")
     ns, k = (int(ns), int(k)) if ok else (4, 4)
-    lw = 1024 if k == 4 and ns in (4, 8) else 512
+    lw = 512 if ns == 2 else 1024
     return f"gsa::nw_krow_kernel<{ns},{k},{lw}> (sparse, K = {k} rows per lane)"
 
 
