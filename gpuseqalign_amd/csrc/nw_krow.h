@@ -28,7 +28,7 @@ size_t krow_lds_bytes(int ns, int lw, int substsz);
 // StripArgs / PairDesc / granule contract as launch_strip_fill (sparse mode, a.tBx, a.tBy,
 // per-pair hrow/hcol/trows/tcols/Cp); tickets of a pair = krow_tickets(trows, ns, k).
 // Every |s - 2g| must fit int16 (the kernel sets error bit 2 otherwise).  grid <= 0: every resident slot.
-// The profile ring holds 1024 columns for (ns, k) = (4, 4) and (8, 4), 512 otherwise (lw is reserved).
+// The profile ring holds 512 columns for ns = 2, 1024 otherwise (lw is reserved).
 hipError_t launch_krow_fill(const StripArgs& a, int ns, int k, int lw, int grid, hipStream_t stream);
 
 }  // namespace gsa
