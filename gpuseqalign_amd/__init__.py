@@ -1,8 +1,9 @@
 """gpuseqalign_amd -- MI355X-native NW-LG engine (drop-in for GpuSeqAlign's align path).
 
 Python host side over the C ABI of ``libgsa.so`` (include/gsa.h).  The compute path is the
-hand-written gfx950 HIP kernel in ``csrc/nw_strip.hip``; there is no CPU fallback: if the
-library is missing or no GPU is visible, GPU entry points raise.
+hand-written gfx950 HIP kernels in ``csrc/`` (``nw_krow.hip`` sparse fills, ``nw_lane.hip`` full
+fills, ``nw_strip.hip`` score-only fills); there is no CPU fallback: if the library is missing or
+no GPU is visible, GPU entry points raise.
 
 Mirrors the reference's registry (src/nw_algorithm.cpp:48-69): an ``NwAlgorithm`` is an
 {align, trace, hash} triple; the plain family pairs with Trace1/Hash1, the sparse (mlsp)
@@ -504,7 +505,7 @@ def _hash2(res: NwResult, seqY, seqX, subst, gapo):
 def get_nw_algorithm_map() -> Dict[str, NwAlgorithm]:
     """getNwAlgorithmMap (src/nw_algorithm.cpp:48-69) for this engine.
 
-    The reference's GPU family names resolve to the MI355X strip-wavefront kernels: the
+    The reference's GPU family names resolve to the MI355X wavefront kernels: the
     full-matrix names (gpu3..gpu6) to the plain fill with Trace1/Hash1, the mlsp names
     (gpu7..gpu9) to the tile-header fill with Trace2/Hash2."""
     plain = ["NwAlign_Amd_Strip_Full", "NwAlign_Gpu3_Ml_DiagDiag", "NwAlign_Gpu4_Ml_DiagDiag2Pass",

@@ -1,6 +1,7 @@
 // gsa_capi.hip -- extern "C" boundary of libgsa.so (declared in include/gsa.h).
 //
-// Device-resident entry points enqueue the strip-wavefront fill (nw_strip.hip); host-buffer
+// Device-resident entry points enqueue the wavefront fills (nw_krow.hip sparse, nw_lane.hip full,
+// nw_strip.hip score-only and the GSA_SPARSE_KERNEL=strip fallback); host-buffer
 // entry points reproduce what the reference's align functions do around their kernels
 // (allocate, copy in, fill, copy out, Stopwatch laps):
 //   NwAlign_Gpu3_Ml_DiagDiag        nwalign_gpu3_ml_diagdiag.cu:288-596     -> gsa_align_full
@@ -494,7 +495,7 @@ int enqueue_fill(gsa_ctx* ctx, int mode, const int32_t* seqY, int32_t adjrows, c
 
 extern "C" {
 
-const char* gsa_version(void) { return "gpuseqalign_amd 0.1 (gfx950 strip-wavefront)"; }
+const char* gsa_version(void) { return "gpuseqalign_amd 0.2 (gfx950 wavefront: K-rows sparse, lane full)"; }
 
 int32_t gsa_sparse_tile_by(void) { return gsa::kSparseTileBy; }
 

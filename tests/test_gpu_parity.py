@@ -1,4 +1,4 @@
-"""GPU parity: the HIP strip-wavefront fill (through the C ABI, libgsa.so) against the oracle.
+"""GPU parity: the HIP wavefront fills (through the C ABI, libgsa.so) against the oracle.
 
 Bar: bit-exact (integer DP).  Plain family: the whole (R+1)x(C+1) matrix equals
 cpu1-st-row's; mlsp family: the whole tileHrowMat/tileHcolMat buffers equal what the
