@@ -19,3 +19,19 @@ def test_overlap_equals_plain(engine, golden, R, C, tBx):
         assert np.array_equal(a.hrow, b.hrow) and np.array_equal(a.hcol, b.hcol)
         assert a.align_cost == b.align_cost
         assert (a.geom.tileHdrMatRows, a.geom.tileHdrMatCols) == (b.geom.tileHdrMatRows, b.geom.tileHdrMatCols)
+
+
+@pytest.mark.parametrize("kern,ns,k", [("krow", 2, 2), ("krow", 8, 4), ("strip", 4, 4)])
+def test_overlap_other_geometries(engine, golden, monkeypatch, kern, ns, k):
+    """mlsppt flags one ticket per tile row: a K-rows geometry whose ticket is not one tile row
+    (GSA_KROW_NS / GSA_KROW_K) falls back to the single-pair default, and the strip kernel
+    (GSA_SPARSE_KERNEL=strip) flags its own tickets; every word equals the plain path's."""
+    import oracle
+    Y, X = random_pair(3100, 2200, 41)
+    a = engine.align_sparse(Y, X, golden.blosum62, -11, tileBx=128)
+    monkeypatch.setenv("GSA_SPARSE_KERNEL", kern)
+    monkeypatch.setenv("GSA_KROW_NS", str(ns))
+    monkeypatch.setenv("GSA_KROW_K", str(k))
+    b = engine.align_sparse(Y, X, golden.blosum62, -11, tileBx=128, overlap=True)
+    assert np.array_equal(a.hrow, b.hrow) and np.array_equal(a.hcol, b.hcol)
+    assert a.align_cost == b.align_cost == oracle.fill_full(Y, X, golden.blosum62, -11)[1]
