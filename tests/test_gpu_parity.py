@@ -100,6 +100,20 @@ def test_other_substitution_and_gaps(engine, golden, name, gapo):
     assert np.array_equal(rs.hrow, hr) and np.array_equal(rs.hcol, hc)
 
 
+@pytest.mark.parametrize("ns", [4, 8])
+@pytest.mark.parametrize("name,gapo", [("blosum45", -4), ("blosum50", 3), ("blosum90", -30)])
+def test_other_substitution_and_gaps_multi_ticket(engine, golden, monkeypatch, ns, name, gapo):
+    """Same over several K-rows tickets (2.5 tile rows): the feed, drain and (ns = 8) mid header
+    row carry values of other tables and gap costs, positive included."""
+    monkeypatch.setenv("GSA_KROW_NS", str(ns))
+    sub = golden.subst_data.matrix(name)
+    Y, X = random_pair(2500, 2100, 41, alphabet=25)
+    rs = engine.align_sparse(Y, X, sub, gapo, tileBx=128)
+    hr, hc, _, _, cost = oracle.sparse_headers(Y, X, sub, gapo, gsa.sparse_tile_by(), 128)
+    assert np.array_equal(rs.hrow, hr) and np.array_equal(rs.hcol, hc)
+    assert rs.align_cost == cost
+
+
 def test_relaunch_is_deterministic(engine, golden):
     """Back-to-back launches reuse the hand-off buffer under a new epoch tag."""
     Y, X = related_pair(3000, 11)

@@ -91,3 +91,15 @@ def test_device_trace_band(engine, golden, monkeypatch, band, R, C, tBx, related
         Y, X = random_pair(R, C, 7 * R + C)
     dev, host = _both(engine, Y, X, golden.blosum62, -11, tBx)
     assert dev == host
+
+
+@pytest.mark.parametrize("name,gapo", [("blosum45", -4), ("blosum50", 3), ("blosum90", -30)])
+def test_device_trace_other_tables(engine, golden, name, gapo):
+    """Other substitution tables and gap costs (positive included): the band precompute and the
+    walk re-derive each move from the recurrence with the caller's table and gap."""
+    sub = golden.subst_data.matrix(name)
+    Y, X = random_pair(2300, 1900, 5, alphabet=25)
+    import oracle
+    dev, host = _both(engine, Y, X, sub, gapo, 128)
+    assert dev == host
+    assert dev[2] == oracle.fill_full(Y, X, sub, gapo)[1]
