@@ -45,12 +45,6 @@ __device__ __forceinline__ int wave_prefix_max(int v)
     return v;
 }
 
-// lane l of v <- the uniform value x
-__device__ __forceinline__ void writelane(int& v, unsigned x, int l)
-{
-    v = ((int)(threadIdx.x & 63) == l) ? (int)x : v;
-}
-
 __device__ __forceinline__ int clamp_letter(int x, int substsz) { return ((unsigned)x < (unsigned)substsz) ? x : 0; }
 
 // move codes: diagonal with equal / different letters ('=' / 'X'), up ('I'), left ('D')
@@ -189,10 +183,7 @@ __global__ void __launch_bounds__(64 * kTW) trace_sparse_kernel(TraceArgs a)
 
     int iT = a.iT0, jT = a.jT0, iE = a.iE0, jE = a.jE0;
     const int Wm = a.tBx, Hm = a.tBy;  // hrowLen-1, hcolLen-1
-    long long n = 0;
-    unsigned acc = 0;  // edit bytes of the current dword (wave 0)
-    int ebuf = 0;      // packed edit dwords, lane k = moves 4k..4k+3 of the current 256
-    long long flushed = 0;  // moves already stored (multiples of 256)
+    long long n = 0;  // moves emitted (wave 0)
     bool first = true;
     if (tid == 0 && (iE == 0 || jE == 0))
     {
@@ -242,22 +233,18 @@ __global__ void __launch_bounds__(64 * kTW) trace_sparse_kernel(TraceArgs a)
         int done = 0;
         if (w == 0)
         {
-            // The move codes of the current 16-row group x 64-column panel sit in one VGPR (lane =
-            // column), read with v_readlane: one LDS read per group / panel change, not per move.
-            // Edit bytes are packed 4 per dword into lane (n/4) % 64 of a VGPR and stored 256 at a
-            // time by the whole wave.
-            // branch-free move: code -> (di, dj, edit byte) by arithmetic on uniform values;
-            // '=' 'X' 'I' 'D' packed in one word, indexed by the code
+            // The walk goes by RUNS of equal moves: the move codes of the current 16-row group x
+            // 64-column panel sit in one VGPR (lane = column), and every lane l <= c evaluates move
+            // k = c - l of a run from (r, c) at once -- a diagonal run reads row r - k of its own
+            // column, an up run row r - k of column c, a left run row r of its own column.  One
+            // ballot gives the run length, and the run's lanes store its edit bytes in walk order
+            // ('=' 'X' 'I' 'D' packed in one word, indexed by the code).  A related pair's path
+            // is a few moves to tens of moves per run; the loop is branch-free per run.
             constexpr unsigned kEdits = (unsigned)'=' | ((unsigned)'X' << 8) | ((unsigned)'I' << 16) | ((unsigned)'D' << 24);
+            gptr<unsigned char> edits = G(a.edits);
+            const long long cap = a.cap;
             int ci = __builtin_amdgcn_readfirstlane(iE), cj = __builtin_amdgcn_readfirstlane(jE);
-            auto emit = [&](int code) {
-                const unsigned e = (kEdits >> (8 * code)) & 0xffu;
-                const unsigned nn = (unsigned)n;
-                acc |= e << (8 * (nn & 3u));
-                writelane(ebuf, acc, (int)((nn >> 2) & 63u));
-                acc = (nn & 3u) == 3u ? 0u : acc;
-                ++n;
-            };
+            int dI = 1, dJ = 1;  // row / column step of the last run
             for (;;)
             {
                 if (ci == 0 && cj == 0)
@@ -265,61 +252,48 @@ __global__ void __launch_bounds__(64 * kTW) trace_sparse_kernel(TraceArgs a)
                     done = 1;
                     break;
                 }
-                int di, dj;
                 if (ci > 0 && cj > 0)
                 {
-                    // the 16 x 64 window of codes holding (ci, cj), one register (lane = column); the
-                    // moves inside it run as one straight loop (a taken branch per move otherwise
-                    // costs an instruction fetch: ~450 cycles per move measured)
                     const int gi = (ci - 1) >> 4, pj = (cj - 1) >> 6;
-                    const int cw = (int)dirs[((size_t)gi * nP + pj) * 64 + lane];
+                    const unsigned cw = dirs[((size_t)gi * nP + pj) * 64 + lane];
                     const int ilo = 16 * gi + 1, jlo = 64 * pj + 1;
-                    auto step = [&]() {
-                        const unsigned word = (unsigned)__builtin_amdgcn_readlane(cw, (cj - 1) & 63);
-                        const int code = (int)((word >> (2 * ((ci - 1) & 15))) & 3u);
-                        di = code == kLeft ? 0 : -1;
-                        dj = code == kUp ? 0 : -1;
-                        emit(code);
-                        ci += di;
-                        cj += dj;
-                    };
-                    // 8 moves without a check while 8 cannot leave the window or cross a 256-move store
-                    while (ci - ilo >= 8 && cj - jlo >= 8 && (n & 255) <= 247)
-                    {
-#pragma unroll
-                        for (int u = 0; u < 8; ++u) step();
-                    }
-                    while (ci - ilo >= 4 && cj - jlo >= 4 && (n & 255) <= 251)
-                    {
-#pragma unroll
-                        for (int u = 0; u < 4; ++u) step();
-                    }
                     do
                     {
-                        const unsigned word = (unsigned)__builtin_amdgcn_readlane(cw, (cj - 1) & 63);
-                        const int code = (int)((word >> (2 * ((ci - 1) & 15))) & 3u);
-                        di = code == kLeft ? 0 : -1;
-                        dj = code == kUp ? 0 : -1;
-                        emit(code);
-                        ci += di;
-                        cj += dj;
-                    } while (ci >= ilo && cj >= jlo && (n & 255) != 0);
+                        const int r = ci - ilo, c = cj - jlo;
+                        const unsigned word = (unsigned)__builtin_amdgcn_readlane((int)cw, c);
+                        const int code = (int)((word >> (2 * r)) & 3u);
+                        const int cls = code <= kDiagX ? kDiagEq : code;  // diagonal runs mix '=' and 'X'
+                        const int sh = r - c + lane;                      // row of this lane's move
+                        const bool left = cls == kLeft;
+                        const unsigned src = cls == kUp ? word : cw;
+                        const int fs = left ? r : sh;
+                        const bool valid = lane <= c && fs >= 0;
+                        const int f = (int)((src >> ((2 * fs) & 31)) & 3u);
+                        const bool in = valid && (f <= kDiagX ? kDiagEq : f) == cls;
+                        const unsigned long long M = __builtin_amdgcn_ballot_w64(in);
+                        const unsigned long long below = c == 63 ? ~0ull : ((2ull << c) - 1ull);
+                        const unsigned long long stop = ~M & below;
+                        const int L = stop ? c - (63 - __builtin_clzll(stop)) : c + 1;
+                        const int k = c - lane;  // this lane's move in the run
+                        if (k >= 0 && k < L && n + k < cap) edits[n + k] = (unsigned char)(kEdits >> (8 * f));
+                        dI = left ? 0 : 1;
+                        dJ = cls == kUp ? 0 : 1;
+                        ci -= dI * L;
+                        cj -= dJ * L;
+                        n += L;
+                    } while (ci >= ilo && cj >= jlo);
                 }
                 else
                 {
-                    // on the matrix's top row or left column
-                    const int code = ci > 0 ? kUp : kLeft;
-                    di = code == kLeft ? 0 : -1;
-                    dj = code == kUp ? 0 : -1;
-                    emit(code);
-                    ci += di;
-                    cj += dj;
-                }
-                if ((n & 255) == 0 && n > flushed)
-                {
-                    const long long b0 = n - 256;  // the 256 moves in ebuf
-                    if (n <= a.cap) G((unsigned*)(a.edits + b0))[lane] = (unsigned)ebuf;
-                    flushed = n;
+                    // on the matrix's top row (left moves) or left column (up moves)
+                    const bool up = ci > 0;
+                    const int L = min(up ? ci : cj, 64);
+                    if (lane < L && n + lane < cap) edits[n + lane] = (unsigned char)(kEdits >> (8 * (up ? kUp : kLeft)));
+                    dI = up ? 1 : 0;
+                    dJ = up ? 0 : 1;
+                    ci -= dI * L;
+                    cj -= dJ * L;
+                    n += L;
                 }
                 // into the tile above / left / up-left on reaching its header (nwtrace2_sparse.cpp:195-214)
                 if ((ci == 0 && iT > 0) || (cj == 0 && jT > 0))
@@ -328,8 +302,8 @@ __global__ void __launch_bounds__(64 * kTW) trace_sparse_kernel(TraceArgs a)
                     const int djT = (cj == 0 && jT > 0) ? 1 : 0;
                     iT -= diT;
                     jT -= djT;
-                    if (ci == 0 && di != 0) ci = Hm;
-                    if (cj == 0 && dj != 0) cj = Wm;
+                    if (ci == 0 && dI != 0) ci = Hm;
+                    if (cj == 0 && dJ != 0) cj = Wm;
                     break;
                 }
             }
@@ -351,18 +325,6 @@ __global__ void __launch_bounds__(64 * kTW) trace_sparse_kernel(TraceArgs a)
         jE = state[3];
         done = state[4];
         if (done) break;
-    }
-    if (w == 0)
-    {
-        // the last partial group of 256 moves: dwords of complete and the partial dword
-        if ((n & 3) != 0) writelane(ebuf, acc, (int)((n >> 2) & 63));
-        const long long b0 = n & ~255ll;
-        const int k = lane * 4;
-        if (b0 + k < n && b0 + k < a.cap)
-        {
-            for (int t = 0; t < 4 && b0 + k + t < n && b0 + k + t < a.cap; ++t)
-                a.edits[b0 + k + t] = (unsigned char)((unsigned)ebuf >> (8 * t));
-        }
     }
     if (tid == 0) G(a.res)[0] = n;
 }
