@@ -166,7 +166,35 @@ __device__ void tile_moves(const TraceArgs& a, int iT, int jT, int iE, int jE, i
     (void)DIRS_LDS;
 }
 
-template <bool DIRS_LDS>
+// codes of band slot `slot` -> dst (LDS), by threads t0, t0 + nt, ...: 8 loads in flight per
+// thread per round (a loop of single loads pays a round trip per 16 bytes)
+__device__ __forceinline__ void copy_codes(const TraceArgs& a, int slot, unsigned* dst, int t, int nt)
+{
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    const size_t words = trace_dir_words_dev(a.tBy, a.tBx);
+    const gptr<const u32x4> src = (gptr<const u32x4>)(a.tcodes + (size_t)slot * words);
+    const size_t nq = words / 4;
+    for (size_t q0 = 0; q0 < nq; q0 += (size_t)8 * nt)
+    {
+        u32x4 v[8];
+#pragma unroll
+        for (int r = 0; r < 8; ++r)
+        {
+            const size_t q = q0 + (size_t)r * nt + t;
+            if (q < nq) v[r] = src[q];
+        }
+#pragma unroll
+        for (int r = 0; r < 8; ++r)
+        {
+            const size_t q = q0 + (size_t)r * nt + t;
+            if (q < nq) ((u32x4*)dst)[q] = v[r];
+        }
+    }
+}
+
+// DBUF: a second LDS code buffer; while wave 0 walks a tile, the other waves copy the band tile
+// the walk is predicted to enter next (the one a diagonal path from the entry cell would reach)
+template <bool DIRS_LDS, bool DBUF>
 __global__ void __launch_bounds__(64 * kTW) trace_sparse_kernel(TraceArgs a)
 {
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
@@ -179,6 +207,8 @@ __global__ void __launch_bounds__(64 * kTW) trace_sparse_kernel(TraceArgs a)
     int* bprog = xraw + (a.tBx + 1);
     int* state = bprog + 8;  // walk state handed from wave 0 to the others
     unsigned* dirs = DIRS_LDS ? (unsigned*)(state + 8) : a.dirs_scratch;
+    unsigned* dnext = dirs + (DBUF ? trace_dir_words_dev(a.tBy, a.tBx) : 0);
+    long long pre = -1;  // tile whose codes the other waves copied into dnext during the last walk
     for (int k = tid; k < a.substsz * a.substsz; k += 64 * kTW) sub[k] = G(a.subst)[k];
 
     int iT = a.iT0, jT = a.jT0, iE = a.iE0, jE = a.jE0;
@@ -197,33 +227,19 @@ __global__ void __launch_bounds__(64 * kTW) trace_sparse_kernel(TraceArgs a)
         {
             // a tile trace_band precomputed (never the start tile, whose recompute yields the cost):
             // its codes are copied into LDS; any other is recomputed here
+            const long long tile = (long long)iT * a.tcols + jT;
             int slot = -1;
-            if (DIRS_LDS && a.tmap && !first) slot = __builtin_amdgcn_readfirstlane(G(a.tmap)[(long long)iT * a.tcols + jT]);
-            if (slot >= 0)
+            if (DIRS_LDS && a.tmap && !first) slot = __builtin_amdgcn_readfirstlane(G(a.tmap)[tile]);
+            if (DBUF && slot >= 0 && tile == pre)
             {
-                const size_t words = trace_dir_words_dev(a.tBy, a.tBx);
-                typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-                const gptr<const u32x4> src = (gptr<const u32x4>)(a.tcodes + (size_t)slot * words);
+                unsigned* t = dirs;  // copied during the last walk (the barrier after it orders the copy)
+                dirs = dnext;
+                dnext = t;
+            }
+            else if (slot >= 0)
+            {
                 __syncthreads();  // the previous walk has read its codes
-                // 8 loads in flight per thread per round (a loop of single loads pays a round
-                // trip per 16 bytes)
-                const size_t nq = words / 4;
-                for (size_t q0 = 0; q0 < nq; q0 += 8 * 64 * kTW)
-                {
-                    u32x4 v[8];
-#pragma unroll
-                    for (int r = 0; r < 8; ++r)
-                    {
-                        const size_t q = q0 + (size_t)r * 64 * kTW + tid;
-                        if (q < nq) v[r] = src[q];
-                    }
-#pragma unroll
-                    for (int r = 0; r < 8; ++r)
-                    {
-                        const size_t q = q0 + (size_t)r * 64 * kTW + tid;
-                        if (q < nq) ((u32x4*)dirs)[q] = v[r];
-                    }
-                }
+                copy_codes(a, slot, dirs, tid, 64 * kTW);
                 __syncthreads();
             }
             else
@@ -231,6 +247,23 @@ __global__ void __launch_bounds__(64 * kTW) trace_sparse_kernel(TraceArgs a)
         }
         first = false;
         int done = 0;
+        if (DBUF)
+        {
+            // the tile a diagonal path from (iE, jE) reaches: left if it meets column 0 first, above
+            // if row 0, up-left if both
+            const int pi = iT - (iE <= jE ? 1 : 0), pj = jT - (jE <= iE ? 1 : 0);
+            pre = -1;
+            if (iE > 0 && jE > 0 && pi >= 0 && pj >= 0)
+            {
+                const long long t = (long long)pi * a.tcols + pj;
+                const int ps = __builtin_amdgcn_readfirstlane(G(a.tmap)[t]);
+                if (ps >= 0)
+                {
+                    pre = t;
+                    if (w > 0) copy_codes(a, ps, dnext, tid - 64, 64 * (kTW - 1));
+                }
+            }
+        }
         if (w == 0)
         {
             // The walk goes by RUNS of equal moves: the move codes of the current 16-row group x
@@ -374,26 +407,26 @@ hipError_t launch_trace_band(const TraceArgs& a, const int* list, int n, int gri
     return hipGetLastError();
 }
 
+template <bool DIRS_LDS, bool DBUF>
+static hipError_t launch_walk(const TraceArgs& a, size_t bytes, hipStream_t st)
+{
+    hipError_t e = hipFuncSetAttribute((const void*)trace_sparse_kernel<DIRS_LDS, DBUF>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((trace_sparse_kernel<DIRS_LDS, DBUF>), dim3(1), dim3(64 * kTW), bytes, st, a);
+    return hipGetLastError();
+}
+
 hipError_t launch_trace_sparse(const TraceArgs& a, hipStream_t st)
 {
     if (a.substsz > 32) return hipErrorInvalidValue;
     const bool lds = a.dirs_scratch == nullptr;
     const size_t bytes = trace_lds_bytes(a.tBy, a.tBx, a.substsz, lds);
-    if (lds)
-    {
-        hipError_t e = hipFuncSetAttribute((const void*)trace_sparse_kernel<true>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
-        if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(trace_sparse_kernel<true>, dim3(1), dim3(64 * kTW), bytes, st, a);
-    }
-    else
-    {
-        hipError_t e = hipFuncSetAttribute((const void*)trace_sparse_kernel<false>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
-        if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(trace_sparse_kernel<false>, dim3(1), dim3(64 * kTW), bytes, st, a);
-    }
-    return hipGetLastError();
+    if (!lds) return launch_walk<false, false>(a, bytes, st);
+    // a second code buffer for the band tile the walk enters next, when it fits
+    const size_t bytes2 = bytes + trace_dir_words(a.tBy, a.tBx) * 4;
+    if (a.tmap && a.tcodes && bytes2 <= 160 * 1024) return launch_walk<true, true>(a, bytes2, st);
+    return launch_walk<true, false>(a, bytes, st);
 }
 
 }  // namespace gsa
