@@ -166,6 +166,14 @@ __device__ void tile_moves(const TraceArgs& a, int iT, int jT, int iE, int jE, i
     (void)DIRS_LDS;
 }
 
+// band slot of tile t (uniform): a load through the scalar cache, so the wait for it counts
+// LDS/scalar traffic only, not the walk's outstanding edit-byte stores
+__device__ __forceinline__ int band_slot(const TraceArgs& a, long long t)
+{
+    typedef const __attribute__((address_space(4))) int* cptr;
+    return ((cptr)a.tmap)[t];
+}
+
 // codes of band slot `slot` -> dst (LDS), by threads t0, t0 + nt, ...: 8 loads in flight per
 // thread per round (a loop of single loads pays a round trip per 16 bytes)
 __device__ __forceinline__ void copy_codes(const TraceArgs& a, int slot, unsigned* dst, int t, int nt)
@@ -229,7 +237,10 @@ __global__ void __launch_bounds__(64 * kTW) trace_sparse_kernel(TraceArgs a)
             // its codes are copied into LDS; any other is recomputed here
             const long long tile = (long long)iT * a.tcols + jT;
             int slot = -1;
-            if (DIRS_LDS && a.tmap && !first) slot = __builtin_amdgcn_readfirstlane(G(a.tmap)[tile]);
+            if (DBUF && tile == pre)
+                slot = state[5];  // looked up by the copying waves
+            else if (DIRS_LDS && a.tmap && !first)
+                slot = band_slot(a, tile);
             if (DBUF && slot >= 0 && tile == pre)
             {
                 unsigned* t = dirs;  // copied during the last walk (the barrier after it orders the copy)
@@ -255,12 +266,13 @@ __global__ void __launch_bounds__(64 * kTW) trace_sparse_kernel(TraceArgs a)
             pre = -1;
             if (iE > 0 && jE > 0 && pi >= 0 && pj >= 0)
             {
-                const long long t = (long long)pi * a.tcols + pj;
-                const int ps = __builtin_amdgcn_readfirstlane(G(a.tmap)[t]);
-                if (ps >= 0)
+                pre = (long long)pi * a.tcols + pj;
+                if (w > 0)
                 {
-                    pre = t;
-                    if (w > 0) copy_codes(a, ps, dnext, tid - 64, 64 * (kTW - 1));
+                    // wave 0 walks without waiting for this lookup; the slot reaches it in state[5]
+                    const int ps = band_slot(a, pre);
+                    if (tid == 64) state[5] = ps;
+                    if (ps >= 0) copy_codes(a, ps, dnext, tid - 64, 64 * (kTW - 1));
                 }
             }
         }
