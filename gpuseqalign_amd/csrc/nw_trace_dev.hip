@@ -278,8 +278,8 @@ __global__ void __launch_bounds__(64 * kTW) trace_sparse_kernel(TraceArgs a)
         }
         if (w == 0)
         {
-            // The walk goes by RUNS of equal moves: the move codes of the current 16-row group x
-            // 64-column panel sit in one VGPR (lane = column), and every lane l <= c evaluates move
+            // The walk goes by RUNS of equal moves: the move codes of the current 32-row x 64-column
+            // window sit in one 64-bit value per lane (lane = column), and every lane l <= c evaluates move
             // k = c - l of a run from (r, c) at once -- a diagonal run reads row r - k of its own
             // column, an up run row r - k of column c, a left run row r of its own column.  One
             // ballot gives the run length, and the run's lanes store its edit bytes in walk order
@@ -290,6 +290,7 @@ __global__ void __launch_bounds__(64 * kTW) trace_sparse_kernel(TraceArgs a)
             const long long cap = a.cap;
             int ci = __builtin_amdgcn_readfirstlane(iE), cj = __builtin_amdgcn_readfirstlane(jE);
             int dI = 1, dJ = 1;  // row / column step of the last run
+            const int nG = (a.tBy + 15) / 16;  // 16-row code groups of a tile
             for (;;)
             {
                 if (ci == 0 && cj == 0)
@@ -299,21 +300,27 @@ __global__ void __launch_bounds__(64 * kTW) trace_sparse_kernel(TraceArgs a)
                 }
                 if (ci > 0 && cj > 0)
                 {
-                    const int gi = (ci - 1) >> 4, pj = (cj - 1) >> 6;
-                    const unsigned cw = dirs[((size_t)gi * nP + pj) * 64 + lane];
-                    const int ilo = 16 * gi + 1, jlo = 64 * pj + 1;
+                    // a window of 32 rows (two 16-row code groups, one 64-bit value per lane)
+                    const int gh = (ci - 1) >> 5, pj = (cj - 1) >> 6;
+                    const size_t at = ((size_t)(2 * gh) * nP + pj) * 64 + lane;
+                    const unsigned lo = dirs[at];
+                    const unsigned hi = 2 * gh + 1 < nG ? dirs[at + (size_t)nP * 64] : 0u;
+                    const unsigned long long cw = ((unsigned long long)hi << 32) | lo;
+                    const int ilo = 32 * gh + 1, jlo = 64 * pj + 1;
                     do
                     {
                         const int r = ci - ilo, c = cj - jlo;
-                        const unsigned word = (unsigned)__builtin_amdgcn_readlane((int)cw, c);
+                        const unsigned long long word =
+                            ((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)hi, c) << 32) |
+                            (unsigned)__builtin_amdgcn_readlane((int)lo, c);
                         const int code = (int)((word >> (2 * r)) & 3u);
                         const int cls = code <= kDiagX ? kDiagEq : code;  // diagonal runs mix '=' and 'X'
                         const int sh = r - c + lane;                      // row of this lane's move
                         const bool left = cls == kLeft;
-                        const unsigned src = cls == kUp ? word : cw;
+                        const unsigned long long src = cls == kUp ? word : cw;
                         const int fs = left ? r : sh;
                         const bool valid = lane <= c && fs >= 0;
-                        const int f = (int)((src >> ((2 * fs) & 31)) & 3u);
+                        const int f = (int)((src >> ((2 * fs) & 63)) & 3u);
                         const bool in = valid && (f <= kDiagX ? kDiagEq : f) == cls;
                         const unsigned long long M = __builtin_amdgcn_ballot_w64(in);
                         const unsigned long long below = c == 63 ? ~0ull : ((2ull << c) - 1ull);
