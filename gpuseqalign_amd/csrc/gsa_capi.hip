@@ -850,13 +850,13 @@ int gsa_trace_sparse_dev(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, con
     a.dirs_scratch = dirs_lds ? nullptr : ctx->tdirs;
     // The walk enters tiles one after another, and recomputing one (a row scan over its rows) takes
     // ~160 us at 1024 x 256.  The tiles are independent given their headers, so the ones within
-    // GSA_TRACE_BAND columns (default 2048) of the diagonal are recomputed first by many workgroups
+    // GSA_TRACE_BAND columns (default 1024) of the diagonal are recomputed first by many workgroups
     // at once; the walk copies their codes and recomputes only the tiles it finds outside the band.
     a.tmap = nullptr;
     a.tcodes = nullptr;
     if (dirs_lds)
     {
-        const int band = env_int("GSA_TRACE_BAND", 2048);
+        const int band = env_int("GSA_TRACE_BAND", 1024);
         const int trows = g.tileHdrMatRows, tcols = g.tileHdrMatCols;
         const size_t words = gsa::trace_dir_words(g.tileBy, g.tileBx);
         const size_t maxSlots = ((size_t)512 << 20) / (words * 4);  // 512 MB of codes at most

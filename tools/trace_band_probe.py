@@ -10,7 +10,7 @@ eng = gsa.Engine(0)
 dev = torch.device("cuda:0")
 d = lambda a: torch.from_numpy(np.ascontiguousarray(a, dtype=np.int32)).to(dev)
 X = F.synthetic_seq(100000, 100); Y = F.mutate_seq(X, 101)
-for band in ["0", "2048", "4096"]:
+for band in (sys.argv[1:] or ["0", "2048", "4096"]):
     os.environ["GSA_TRACE_BAND"] = band
     geom = gsa.sparse_geometry(len(Y), len(X), 256)
     y, x, s = d(Y), d(X), d(sub)
