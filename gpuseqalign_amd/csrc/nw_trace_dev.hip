@@ -286,11 +286,12 @@ __global__ void __launch_bounds__(64 * kTW) trace_sparse_kernel(TraceArgs a)
             // ('=' 'X' 'I' 'D' packed in one word, indexed by the code).  A related pair's path
             // is a few moves to tens of moves per run; the loop is branch-free per run.
             constexpr unsigned kEdits = (unsigned)'=' | ((unsigned)'X' << 8) | ((unsigned)'I' << 16) | ((unsigned)'D' << 24);
+            // a.cap >= adjrows + adjcols - 1 >= the moves of any path (the host sizes it so)
             gptr<unsigned char> edits = G(a.edits);
-            const long long cap = a.cap;
             int ci = __builtin_amdgcn_readfirstlane(iE), cj = __builtin_amdgcn_readfirstlane(jE);
             int dI = 1, dJ = 1;  // row / column step of the last run
             const int nG = (a.tBy + 15) / 16;  // 16-row code groups of a tile
+            const int lane2 = 2 * lane;
             for (;;)
             {
                 if (ci == 0 && cj == 0)
@@ -315,21 +316,23 @@ __global__ void __launch_bounds__(64 * kTW) trace_sparse_kernel(TraceArgs a)
                             (unsigned)__builtin_amdgcn_readlane((int)lo, c);
                         const int code = (int)((word >> (2 * r)) & 3u);
                         const int cls = code <= kDiagX ? kDiagEq : code;  // diagonal runs mix '=' and 'X'
-                        const int sh = r - c + lane;                      // row of this lane's move
-                        const bool left = cls == kLeft;
-                        const unsigned long long src = cls == kUp ? word : cw;
-                        const int fs = left ? r : sh;
-                        const bool valid = lane <= c && fs >= 0;
-                        const int f = (int)((src >> ((2 * fs) & 63)) & 3u);
-                        const bool in = valid && (f <= kDiagX ? kDiagEq : f) == cls;
-                        const unsigned long long M = __builtin_amdgcn_ballot_w64(in);
-                        const unsigned long long below = c == 63 ? ~0ull : ((2ull << c) - 1ull);
-                        const unsigned long long stop = ~M & below;
-                        const int L = stop ? c - (63 - __builtin_clzll(stop)) : c + 1;
-                        const int k = c - lane;  // this lane's move in the run
-                        if (k >= 0 && k < L && n + k < cap) edits[n + k] = (unsigned char)(kEdits >> (8 * f));
+                        const bool left = cls == kLeft, up = cls == kUp;
+                        const unsigned m = cls == kDiagEq ? 1u : 0u;
+                        // this lane's move k = c - lane: row r - k of its own column (diagonal), of
+                        // column c (up), row r of its own column (left); the shift wraps mod 64 and
+                        // lanes past the window's top are cut by the row limit below
+                        const unsigned long long src = up ? word : cw;
+                        const int sft = (left ? 0 : lane2) + 2 * (left ? r : r - c);
+                        const unsigned f = (unsigned)(src >> (sft & 63)) & 3u;
+                        const bool in = (f | m) == ((unsigned)cls | m);
+                        // run length: the ones from lane c down (lanes above c shift out)
+                        const unsigned long long M = __builtin_amdgcn_ballot_w64(in) << (63 - c);
+                        const int lim = min(c + 1, left ? 64 : r + 1);
+                        const int L = min((unsigned)__builtin_clzll(~M | 1ull), (unsigned)lim);
+                        const unsigned k = (unsigned)(c - lane);  // this lane's move in the run
+                        if (k < (unsigned)L) ((gptr<unsigned char>)(edits + n))[k] = (unsigned char)(kEdits >> (8 * f));
                         dI = left ? 0 : 1;
-                        dJ = cls == kUp ? 0 : 1;
+                        dJ = up ? 0 : 1;
                         ci -= dI * L;
                         cj -= dJ * L;
                         n += L;
@@ -340,7 +343,7 @@ __global__ void __launch_bounds__(64 * kTW) trace_sparse_kernel(TraceArgs a)
                     // on the matrix's top row (left moves) or left column (up moves)
                     const bool up = ci > 0;
                     const int L = min(up ? ci : cj, 64);
-                    if (lane < L && n + lane < cap) edits[n + lane] = (unsigned char)(kEdits >> (8 * (up ? kUp : kLeft)));
+                    if (lane < L) edits[n + lane] = (unsigned char)(kEdits >> (8 * (up ? kUp : kLeft)));
                     dI = up ? 1 : 0;
                     dJ = up ? 0 : 1;
                     ci -= dI * L;
