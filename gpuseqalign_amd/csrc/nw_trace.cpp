@@ -6,6 +6,8 @@
 //
 // Tie-break, RLE edit-string format and djb2-xor hashing follow the reference exactly;
 // indices are 64-bit.
+#include <emmintrin.h>
+
 #include <algorithm>
 #include <climits>
 #include <cstring>
@@ -122,11 +124,48 @@ namespace gsa {
 // traces fold theirs (the final '\0' push flushes the last run).
 int fold_moves(const unsigned char* moves, int64_t n, char* edit, int64_t cap, int64_t* edit_len, uint32_t* trace_hash)
 {
-    EditTrace t;
-    for (int64_t k = 0; k < n; k++) t.push((char)moves[k]);
-    t.push('\0');
-    *trace_hash = t.finish();
-    return emit(t, edit, cap, edit_len);
+    // EditTrace's result without a string per run: each run in walk order as its letter and its
+    // count's digits least significant first, then the whole read backwards (hash on the way).
+    // Run ends are found 16 moves at a time (byte compare of the moves with their predecessors).
+    std::vector<char> buf((size_t)(2 * n + 32));
+    char* o = buf.data();
+    auto run = [&](unsigned char c, int64_t cnt) {
+        *o++ = (char)c;
+        if (cnt < 10)
+            *o++ = (char)('0' + cnt);
+        else
+            for (; cnt > 0; cnt /= 10) *o++ = (char)('0' + cnt % 10);
+    };
+    int64_t start = 0, b = 1;
+    for (; b + 16 <= n; b += 16)
+    {
+        const __m128i x = _mm_loadu_si128((const __m128i*)(moves + b));
+        const __m128i y = _mm_loadu_si128((const __m128i*)(moves + b - 1));
+        unsigned m = ~(unsigned)_mm_movemask_epi8(_mm_cmpeq_epi8(x, y)) & 0xffffu;
+        while (m)
+        {
+            const int64_t k = b + __builtin_ctz(m);
+            m &= m - 1;
+            run(moves[start], k - start);
+            start = k;
+        }
+    }
+    for (; b < n; b++)
+        if (moves[b] != moves[b - 1])
+        {
+            run(moves[start], b - start);
+            start = b;
+        }
+    if (n > 0) run(moves[start], n - start);
+    const int64_t len = (int64_t)(o - buf.data());
+    uint32_t h = 5381;
+    for (int64_t k = len - 1; k >= 0; k--) h = djb2x(h, (uint32_t)(int32_t)buf[(size_t)k]);
+    *trace_hash = h;
+    if (len > cap) return GSA_ERROR_MEMORY_ALLOCATION;
+    for (int64_t k = 0; k < len; k++) edit[k] = buf[(size_t)(len - 1 - k)];
+    if (len < cap) edit[len] = '\0';
+    *edit_len = len;
+    return GSA_SUCCESS;
 }
 
 }  // namespace gsa
