@@ -851,10 +851,10 @@ int gsa_trace_sparse_dev(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, con
     // The walk enters tiles one after another, and recomputing one (a row scan over its rows) takes
     // ~160 us at 1024 x 256.  The tiles are independent given their headers, so the ones within
     // GSA_TRACE_BAND columns (default 1024) of the diagonal are recomputed first by many workgroups
-    // at once; the walk copies their codes and recomputes only the tiles it finds outside the band.
+    // at once; the walk copies their codes (or reads them in place when a tile is too wide for
+    // LDS) and recomputes only the tiles it finds outside the band.
     a.tmap = nullptr;
     a.tcodes = nullptr;
-    if (dirs_lds)
     {
         const int band = env_int("GSA_TRACE_BAND", 1024);
         const int trows = g.tileHdrMatRows, tcols = g.tileHdrMatCols;

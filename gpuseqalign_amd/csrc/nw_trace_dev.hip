@@ -239,7 +239,7 @@ __global__ void __launch_bounds__(64 * kTW) trace_sparse_kernel(TraceArgs a)
             int slot = -1;
             if (DBUF && tile == pre)
                 slot = state[5];  // looked up by the copying waves
-            else if (DIRS_LDS && a.tmap && !first)
+            else if (a.tmap && !first)
                 slot = band_slot(a, tile);
             if (DBUF && slot >= 0 && tile == pre)
             {
@@ -247,14 +247,20 @@ __global__ void __launch_bounds__(64 * kTW) trace_sparse_kernel(TraceArgs a)
                 dirs = dnext;
                 dnext = t;
             }
-            else if (slot >= 0)
+            else if (slot >= 0 && DIRS_LDS)
             {
                 __syncthreads();  // the previous walk has read its codes
                 copy_codes(a, slot, dirs, tid, 64 * kTW);
                 __syncthreads();
             }
+            else if (slot >= 0)
+                // codes too large for LDS: the walk reads the band tile where trace_band left it
+                dirs = const_cast<unsigned*>(a.tcodes) + (size_t)slot * trace_dir_words_dev(a.tBy, a.tBx);
             else
+            {
+                if (!DIRS_LDS) dirs = a.dirs_scratch;
                 tile_moves<DIRS_LDS>(a, iT, jT, iE, jE, sub, bnd, yraw, xraw, bprog, dirs, w, lane, first);
+            }
         }
         first = false;
         int done = 0;
