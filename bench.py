@@ -92,14 +92,12 @@ def cpu_topology():
         cpus = list(range(os.cpu_count() or 1))
     phys = set()
     try:
-        cur = {}
         with open("/proc/cpuinfo") as f:
             for line in f.read().split("\n\n"):
                 d = dict(kv.split(":", 1) for kv in line.split("\n") if ":" in kv)
                 d = {k.strip(): v.strip() for k, v in d.items()}
                 if "processor" in d and int(d["processor"]) in cpus:
                     phys.add((d.get("physical id", "0"), d.get("core id", d["processor"])))
-        del cur
     except Exception:
         phys = set()
     quota = None
@@ -187,7 +185,8 @@ def bench_config4(world, rank, local, n_pairs):
     from gpuseqalign_amd import shard
     pairs = shard.synthetic_batch(n_pairs, 18000, 22000, seed0=1000)
     sub = subst_blosum62()
-    rep = shard.shard_align(pairs, sub, -11, shard.gpu_batch_align(device=local, mode="sparse", tileBx=TILE_BX),
+    rep = shard.shard_align(pairs, sub, -11, shard.gpu_batch_align(device=local, mode="sparse", tileBx=TILE_BX,
+                                                                warmup=1, repeats=3),
                             device=f"cuda:{local}" if world > 1 else None)
     gold = load_golden("config4_pairs.json")
     costs = [r.align_cost for r in rep.results]
@@ -196,7 +195,7 @@ def bench_config4(world, rank, local, n_pairs):
         match = sum(int(a == b) for a, b in zip(costs, gold["align_cost"][:n_pairs]))
     return {"workload": f"BASELINE configs[3]: {n_pairs} NW-LG pairs, lengths uniform in [18000, 22000] "
                         f"(seeds 1000+k), sparse tile headers (tileBx {TILE_BX}), LPT-sharded over {world} rank(s), "
-                        "one persistent batched launch per rank",
+                        "one persistent batched launch per rank (1 untimed + 3 timed launches; seconds per launch)",
             "value": round(rep.gcups, 2), "unit": "GCUPS", "scaling": "strong", "cells": rep.cells,
             "seconds": round(rep.elapsed_s, 4), "pairs": n_pairs,
             "pairs_matching_golden": match, "golden_pairs": None if gold is None else gold.get("n_pairs")}

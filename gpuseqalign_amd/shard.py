@@ -166,11 +166,15 @@ def gpu_batch_align(device: int = 0, mode: str = "sparse", tileBx: int = 256, re
             cur_sz += sz
         chunks.append(cur)
         flat = torch.empty(max(sum(sizes[j] for j in c) for c in chunks), dtype=torch.int32, device=dev)
-        keep = [torch.empty((g.tileHrowLen + g.tileHcolLen) if g is not None else 1, dtype=torch.int32, device=dev)
-                for g in geoms]
-        descs = []
+        # result slices (last cell / last tile's header row and column) of every pair: positions in
+        # `flat`, gathered by one index_select per chunk behind its fill, not one copy per pair
+        klen = [(g.tileHrowLen + g.tileHcolLen) if g is not None else 1 for g in geoms]
+        kbase = np.concatenate([[0], np.cumsum(klen)]).astype(np.int64)
+        keepflat = torch.empty(int(kbase[-1]), dtype=torch.int32, device=dev)
+        keep = [keepflat[kbase[j]:kbase[j + 1]] for j in range(len(geoms))]
+        descs, gathers = [], []
         for c in chunks:
-            off, d = 0, []
+            off, d, gi = 0, [], []
             for j in c:
                 y, x = ins[j]
                 g = geoms[j]
@@ -178,11 +182,17 @@ def gpu_batch_align(device: int = 0, mode: str = "sparse", tileBx: int = 256, re
                     hr = flat[off:off + g.hrowElems]
                     hc = flat[off + g.hrowElems:off + g.hrowElems + g.hcolElems]
                     d.append((y.data_ptr(), len(y), x.data_ptr(), len(x), (hr.data_ptr(), hc.data_ptr()), hr, hc))
+                    last = g.tileHdrMatRows * g.tileHdrMatCols - 1
+                    gi.append(np.arange(g.tileHrowLen, dtype=np.int64) + off + last * g.tileHrowLen)
+                    gi.append(np.arange(g.tileHcolLen, dtype=np.int64) + off + g.hrowElems + last * g.tileHcolLen)
                 else:
                     sc = flat[off:off + sizes[j]]
                     d.append((y.data_ptr(), len(y), x.data_ptr(), len(x), sc.data_ptr(), sc, None))
+                    gi.append(np.array([off + sizes[j] - 1], dtype=np.int64))
                 off += sizes[j]
             descs.append(d)
+            # chunk c's pairs are consecutive, so their slices of keepflat are one range
+            gathers.append((torch.from_numpy(np.concatenate(gi)).to(dev), keepflat[kbase[c[0]]:kbase[c[-1] + 1]]))
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
         for it in range(max(0, warmup) + max(1, repeats)):
@@ -191,19 +201,12 @@ def gpu_batch_align(device: int = 0, mode: str = "sparse", tileBx: int = 256, re
                 eng.sync(stream.cuda_stream)
                 torch.cuda.synchronize(dev)
                 t0 = time.perf_counter()
-            for c, d in zip(chunks, descs):
+            for d, (gidx, gout) in zip(descs, gathers):
                 eng.fill_batch_dev([e[:5] for e in d], ts.data_ptr(), substsz, gapo, mode=mode, tileBx=tileBx,
                                    stream=stream.cuda_stream)
-                # result slices, in stream order behind the fill: last cell / last tile's headers
+                # result slices, in stream order behind the fill (before the next chunk reuses flat)
                 with torch.cuda.stream(stream):
-                    for j, e in zip(c, d):
-                        g = geoms[j]
-                        if g is None:
-                            keep[j].copy_(e[5][-1:])
-                        else:
-                            last = g.tileHdrMatRows * g.tileHdrMatCols - 1
-                            keep[j][:g.tileHrowLen].copy_(e[5][last * g.tileHrowLen:(last + 1) * g.tileHrowLen])
-                            keep[j][g.tileHrowLen:].copy_(e[6][last * g.tileHcolLen:(last + 1) * g.tileHcolLen])
+                    torch.index_select(flat, 0, gidx, out=gout)
         eng.sync(stream.cuda_stream)
         torch.cuda.synchronize(dev)
         secs = (time.perf_counter() - t0) / max(1, repeats)
