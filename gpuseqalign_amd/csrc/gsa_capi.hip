@@ -347,8 +347,13 @@ int enqueue_batch(gsa_ctx* ctx, int mode, int npairs, const gsa_pair_dev* pairs,
     const bool krow = mode == gsa::kModeSparse && sparse_kernel() == kSpKrow;
     // single pairs: 4 strips per workgroup (each on its own SIMD: the pair's critical path);
     // batches: 8 (two strips per SIMD share the issue slots a single strip leaves idle, 512 x 20k
-    // 5.7 -> 7.3 TCUPS; a single 100k pair 5.9 -> 8.4 ms)
-    const int nsDefault = npairs > 1 ? gsa::kKrowNSBatchDefault : gsa::kKrowNSDefault;
+    // 5.7 -> 7.3 TCUPS; a single 100k pair 5.9 -> 8.4 ms), unless the batch's 4-strip tickets
+    // (one tile row each) all fit the chip at once: then every pair runs on its critical path
+    long long tileRows = 0;
+    for (int p = 0; p < npairs; ++p)
+        tileRows += std::max<long long>(1, ((long long)pairs[p].adjrows - 1 + gsa::kSparseTileBy - 1) / gsa::kSparseTileBy);
+    const bool fitsChip = tileRows <= (long long)std::max(1, ctx->cu_count);
+    const int nsDefault = (npairs > 1 && !fitsChip) ? gsa::kKrowNSBatchDefault : gsa::kKrowNSDefault;
     int krowK = env_int("GSA_KROW_K", gsa::kKrowKDefault), krowNS = env_int("GSA_KROW_NS", nsDefault);
     // mlsppt flags one ticket per tile row: only the geometry whose ticket is one tile row
     if (!gsa::krow_ok(krowNS, krowK) || (done && gsa::krow_ticket_rows(krowNS, krowK) != gsa::kSparseTileBy))
