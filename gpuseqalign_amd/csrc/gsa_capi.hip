@@ -71,15 +71,14 @@ struct gsa_ctx
     // score-only fills (nw_scan.hip): boundary rows H/F, progress words, control words
     int* sbnd = nullptr;
     size_t sbnd_cap = 0;
-    // mlsppt: host-mapped per-ticket completion flags and the copy-back stream
+    // mlsppt: host-mapped per-ticket completion flags
     unsigned* ptflags = nullptr;
     size_t ptflags_cap = 0;
-    hipStream_t cstream = nullptr;
     unsigned long long* sctl = nullptr;  // [0] ticket|err, [1] best key, [2] result
     // copy-back of the host-buffer entry points into pageable caller memory: per copy thread a
     // stream and two pinned chunks (DMA of chunk k+1 overlaps the host copy of chunk k)
     static constexpr int kCopyThreads = 4;
-    static constexpr size_t kCopyChunk = 8u << 20;
+    static constexpr size_t kCopyChunk = 4u << 20;
     hipStream_t xstream[kCopyThreads] = {};
     void* xstage[kCopyThreads][2] = {};
     hipEvent_t xev[kCopyThreads][2] = {};
@@ -556,7 +555,6 @@ void gsa_ctx_destroy(gsa_ctx* ctx)
     if (ctx->sbnd) (void)hipFree(ctx->sbnd);
     if (ctx->sctl) (void)hipFree(ctx->sctl);
     if (ctx->ptflags) (void)hipHostFree(ctx->ptflags);
-    if (ctx->cstream) (void)hipStreamDestroy(ctx->cstream);
     for (int k = 0; k < gsa_ctx::kStage; ++k)
     {
         if (ctx->stage[k]) (void)hipHostFree(ctx->stage[k]);
@@ -684,11 +682,18 @@ hipError_t copy_d2h(gsa_ctx* ctx, void* dst, const void* src, size_t bytes)
 {
     constexpr int T = gsa_ctx::kCopyThreads;
     constexpr size_t kC = gsa_ctx::kCopyChunk;
-    if (bytes < 4 * kC) return hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost);
     hipError_t e = hipSuccess;
+    // non-blocking streams: mlsppt copies finished tile rows while the fill still runs
+    for (int k = 0; k < T && e == hipSuccess; ++k)
+        if (!ctx->xstream[k]) e = hipStreamCreateWithFlags(&ctx->xstream[k], hipStreamNonBlocking);
+    if (e != hipSuccess) return e;
+    if (bytes < 2 * kC)
+    {
+        e = hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->xstream[0]);
+        return e == hipSuccess ? hipStreamSynchronize(ctx->xstream[0]) : e;
+    }
     for (int k = 0; k < T && e == hipSuccess; ++k)
     {
-        if (!ctx->xstream[k]) e = hipStreamCreateWithFlags(&ctx->xstream[k], hipStreamNonBlocking);
         for (int j = 0; j < 2 && e == hipSuccess; ++j)
         {
             if (!ctx->xstage[k][j]) e = hipHostMalloc(&ctx->xstage[k][j], kC, hipHostMallocDefault);
@@ -1163,8 +1168,6 @@ int gsa_align_sparse_pt(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, cons
         std::memset(ctx->ptflags, 0, trows * sizeof(unsigned));
         ctx->ptflags_cap = trows;
     }
-    if (!ctx->cstream && (e = hipStreamCreateWithFlags(&ctx->cstream, hipStreamNonBlocking)) != hipSuccess)
-        return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
     unsigned* dflags = nullptr;
     if ((e = hipHostGetDevicePointer((void**)&dflags, ctx->ptflags, 0)) != hipSuccess)
         return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
@@ -1193,12 +1196,9 @@ int gsa_align_sparse_pt(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, cons
     auto copy_rows = [&](size_t hrUpTo, size_t hcUpTo) -> hipError_t {
         hipError_t err = hipSuccess;
         if (hrUpTo > hrowCopied)
-            err = hipMemcpyAsync(hrow_out + hrowCopied * W, dhr + hrowCopied * W, (hrUpTo - hrowCopied) * W * 4,
-                                 hipMemcpyDeviceToHost, ctx->cstream);
+            err = copy_d2h(ctx, hrow_out + hrowCopied * W, dhr + hrowCopied * W, (hrUpTo - hrowCopied) * W * 4);
         if (err == hipSuccess && hcUpTo > hcolCopied)
-            err = hipMemcpyAsync(hcol_out + hcolCopied * H, dhc + hcolCopied * H, (hcUpTo - hcolCopied) * H * 4,
-                                 hipMemcpyDeviceToHost, ctx->cstream);
-        if (err == hipSuccess) err = hipStreamSynchronize(ctx->cstream);
+            err = copy_d2h(ctx, hcol_out + hcolCopied * H, dhc + hcolCopied * H, (hcUpTo - hcolCopied) * H * 4);
         hrowCopied = std::max(hrowCopied, hrUpTo);
         hcolCopied = std::max(hcolCopied, hcUpTo);
         return err;
