@@ -77,7 +77,7 @@ struct gsa_ctx
     unsigned long long* sctl = nullptr;  // [0] ticket|err, [1] best key, [2] result
     // copy-back of the host-buffer entry points into pageable caller memory: per copy thread a
     // stream and two pinned chunks (DMA of chunk k+1 overlaps the host copy of chunk k)
-    static constexpr int kCopyThreads = 4;
+    static constexpr int kCopyThreads = 8;
     static constexpr size_t kCopyChunk = 4u << 20;
     hipStream_t xstream[kCopyThreads] = {};
     void* xstage[kCopyThreads][2] = {};
