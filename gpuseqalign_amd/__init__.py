@@ -14,13 +14,12 @@ from __future__ import annotations
 import ctypes
 import dataclasses
 import os
-import subprocess
 from typing import Callable, Dict, Optional, Tuple
 
 import numpy as np
 
 __all__ = [
-    "NwStat", "NwError", "lib", "build_library", "Engine", "AlignResult", "SparseResult", "PairDev",
+    "NwStat", "NwError", "lib", "Engine", "AlignResult", "SparseResult", "PairDev",
     "NwAlgorithm", "get_nw_algorithm_map", "hash_full", "trace_full", "trace_sparse", "hash_sparse",
     "sparse_align_cost", "sparse_tile_by",
 ]
@@ -52,14 +51,6 @@ class NwError(RuntimeError):
         self.stat = stat
         self.hip_error = hip_error
         super().__init__(f"{where}: {NwStat.names.get(stat, stat)} (hipError {hip_error})")
-
-
-def build_library(force: bool = False) -> str:
-    """Compile libgsa.so in-tree (hipcc --offload-arch=gfx950)."""
-    csrc = os.path.join(_PKG, "csrc")
-    if force or not os.path.exists(_SO):
-        subprocess.check_call(["make", "-s", "-C", csrc, "-j4"])
-    return _SO
 
 
 class _Laps(ctypes.Structure):
@@ -107,6 +98,7 @@ class ScoreResult(ctypes.Structure):
                 ("calc_kernel_ms", ctypes.c_float)]
 
 
+_LAPFN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_char_p)  # gsa_lap_fn
 _i32p = ctypes.POINTER(ctypes.c_int32)
 _vp = ctypes.c_void_p
 _i32 = ctypes.c_int32
@@ -119,6 +111,7 @@ SIGNATURES = {
     "gsa_last_hip_error": (ctypes.c_int, [_vp]),
     "gsa_device_cu_count": (ctypes.c_int, [_vp]),
     "gsa_version": (ctypes.c_char_p, []),
+    "gsa_set_lap_callback": (ctypes.c_int, [_vp, _vp, _vp]),
     "gsa_sparse_tile_by": (_i32, []),
     "gsa_sparse_geometry": (ctypes.c_int, [_i32, _i32, _i32, ctypes.POINTER(SparseGeom)]),
     "gsa_fill_full_dev": (ctypes.c_int, [_vp, _vp, _i32, _vp, _i32, _vp, _i32, _i32, _vp, _vp]),
@@ -321,6 +314,18 @@ class Engine:
         """Wait for `stream`; raises NwError if a hand-off of ANY fill enqueued since the last
         sync gave up (the error word is sticky until this call clears it)."""
         self._check(lib().gsa_sync(self._h, stream), "gsa_sync")
+
+    def set_lap_callback(self, fn: Optional[Callable[[str], None]]):
+        """fn(lap_name) at every phase boundary of the host-buffer entry points (align_full,
+        align_sparse, score): gsa_set_lap_callback, the hook an adapter uses to drive the
+        reference's Stopwatch::lap (src/stopwatch.hpp:19).  None removes it."""
+        if fn is None:
+            self._lapcb = None
+            self._check(lib().gsa_set_lap_callback(self._h, None, None), "gsa_set_lap_callback")
+            return
+        cb = _LAPFN(lambda _user, name: fn(name.decode()))
+        self._check(lib().gsa_set_lap_callback(self._h, ctypes.cast(cb, _vp), None), "gsa_set_lap_callback")
+        self._lapcb = cb  # keep the thunk alive while the library holds it
 
     def set_watchdog(self, microseconds: int):
         """No-progress limit of every wait inside later fills (default 1 s)."""

@@ -62,19 +62,21 @@ struct gsa_ctx
     size_t tmoves_cap = 0;
     long long* tres = nullptr;
     unsigned* tdirs = nullptr;
-    size_t tdirs_cap = 0;
+    size_t tdirs_cap = 0;  // bytes
     // tiles precomputed around the diagonal (trace_band): codes, and [list | map] ints
     unsigned* tband = nullptr;
-    size_t tband_cap = 0;
+    size_t tband_cap = 0;  // bytes
     int* tlist = nullptr;
-    size_t tlist_cap = 0;
+    size_t tlist_cap = 0;  // ints
     // score-only fills (nw_scan.hip): boundary rows H/F, progress words, control words
     int* sbnd = nullptr;
-    size_t sbnd_cap = 0;
+    size_t sbnd_cap = 0;  // ints
     // mlsppt: host-mapped per-ticket completion flags
     unsigned* ptflags = nullptr;
     size_t ptflags_cap = 0;
-    unsigned long long* sctl = nullptr;  // [0] ticket|err, [1] best key, [2] result
+    // score-only control words: row scan [0] ticket|err, [1] best key, [2] result; AG/SW strip
+    // [0] result, [1] best key, [3] its own error word (the fills' sticky word is not touched)
+    unsigned long long* sctl = nullptr;
     // copy-back of the host-buffer entry points into pageable caller memory: per copy thread a
     // stream and two pinned chunks (DMA of chunk k+1 overlaps the host copy of chunk k)
     static constexpr int kCopyThreads = 8;
@@ -83,6 +85,9 @@ struct gsa_ctx
     void* xstage[kCopyThreads][2] = {};
     hipEvent_t xev[kCopyThreads][2] = {};
     gsa_mem_stats mem {};  // peak resource use of the fills since creation / gsa_mem_stats_reset
+    // phase-boundary callback of the host-buffer entry points (gsa_set_lap_callback)
+    gsa_lap_fn lap_fn = nullptr;
+    void* lap_user = nullptr;
 };
 
 namespace {
@@ -95,6 +100,14 @@ inline float ms_since(Clock::time_point& t)
     float ms = std::chrono::duration<float, std::milli>(now - t).count();
     t = now;
     return ms;
+}
+
+// Phase boundary of a host-buffer entry point: the caller's Stopwatch::lap(name)
+// (stopwatch.cpp:43-50) through the registered callback, at the points the reference's align
+// functions lap (nwalign_gpu9_mlsp_diagdiagdiag.cu:459-719)
+inline void lap(gsa_ctx* ctx, const char* name)
+{
+    if (ctx->lap_fn) ctx->lap_fn(ctx->lap_user, name);
 }
 
 inline int fail(gsa_ctx* ctx, hipError_t e, int stat)
@@ -152,9 +165,10 @@ int check_inputs(int32_t adjrows, int32_t adjcols, int32_t substsz)
 }
 
 // Sparse fills run on the K-rows-per-lane kernel (nw_krow.hip, K = 4): 5.9 vs 8.0 ms for the
-// 100k pair and 5.7 vs 4.3 TCUPS for 512 pairs of 20k against the strip kernel (nw_strip.hip),
-// which mlsppt keeps.  GSA_SPARSE_KERNEL=strip forces the strip kernel (read per launch, tested);
-// GSA_KROW_K (2, 4) and GSA_KROW_NS (2, 4) pick the K-rows geometry.
+// 100k pair and 5.7 vs 4.3 TCUPS for 512 pairs of 20k against the strip kernel (nw_strip.hip).
+// mlsppt runs on the K-rows kernel too, in its (NS 4, K 4) geometry (one tile row per ticket,
+// enqueue_batch).  GSA_SPARSE_KERNEL=strip forces the strip kernel (read per launch, tested);
+// GSA_KROW_K (2, 4) and GSA_KROW_NS (2, 4, 8) pick the K-rows geometry.
 enum SparseKern { kSpStrip, kSpKrow };
 SparseKern sparse_kernel()
 {
@@ -183,10 +197,11 @@ int lane_ns()
 hipStream_t pick_stream(gsa_ctx*, void* stream) { return (hipStream_t)stream; }
 
 // Device bytes this context holds (scratch, hand-off granules, the host entry points' I/O buffers).
+// Units of the *_cap fields: bytes for tmoves, tdirs, tband and dcap; ints for sbnd and tlist.
 long long held_bytes(const gsa_ctx* c)
 {
     long long b = 256 + 64 + (long long)c->gran_elems * 8 + (long long)c->desc_cap * (long long)sizeof(gsa::PairDesc) +
-                  (long long)c->tmoves_cap + (long long)c->tdirs_cap * 4 + (long long)c->sbnd_cap * 4 +
+                  (long long)c->tmoves_cap + (long long)c->tdirs_cap + (long long)c->sbnd_cap * 4 +
                   (long long)c->tband_cap + (long long)c->tlist_cap * 4;
     for (size_t k : c->dcap) b += (long long)k;
     return b;
@@ -294,14 +309,16 @@ int score_ag_strip(gsa_ctx* ctx, const int32_t* seqY, int64_t R, const int32_t* 
     a.gran = ctx->gran;
     a.gran2 = ctx->gran + gran;
     a.ticket = ctx->ctl;
-    a.err = ctx->ctl + 1;
+    // an error word of its own: a fill enqueued earlier on this stream keeps its sticky error for
+    // the caller's gsa_sync, and its error does not read as this launch's
+    a.err = (unsigned*)(ctx->sctl + 3);
     a.spin = ctx->spin_ticks;
     a.agResult = (int*)ctx->sctl;
     a.swBest = ctx->sctl + 1;
     a.idxBits = sw_idx_bits(R, C);
     a.epoch = ++ctx->epoch;
     if (a.epoch == 0) a.epoch = ++ctx->epoch;
-    if ((e = hipMemsetAsync(ctx->ctl, 0, 4, st)) != hipSuccess || (e = hipMemsetAsync(ctx->sctl, 0, 16, st)) != hipSuccess)
+    if ((e = hipMemsetAsync(ctx->ctl, 0, 4, st)) != hipSuccess || (e = hipMemsetAsync(ctx->sctl, 0, 32, st)) != hipSuccess)
         return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
     (void)hipEventRecord(ctx->ev0, st);
     const int grid = std::max(1, std::min((int)tickets, ctx->cu_count));
@@ -309,12 +326,11 @@ int score_ag_strip(gsa_ctx* ctx, const int32_t* seqY, int64_t R, const int32_t* 
         return fail(ctx, e, GSA_ERROR_KERNEL_FAILURE);
     note_launch(ctx);
     (void)hipEventRecord(ctx->ev1, st);
-    unsigned long long res[2] = {0, 0};
-    unsigned err = 0;
+    unsigned long long res[4] = {0, 0, 0, 0};
     if ((e = hipMemcpyAsync(res, ctx->sctl, sizeof(res), hipMemcpyDeviceToHost, st)) != hipSuccess ||
         (e = hipStreamSynchronize(st)) != hipSuccess)
         return fail(ctx, e, GSA_ERROR_KERNEL_FAILURE);
-    if ((e = take_err(ctx, st, &err)) != hipSuccess) return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
+    const unsigned err = (unsigned)res[3];
     (void)hipEventElapsedTime(&out->calc_kernel_ms, ctx->ev0, ctx->ev1);
     // a substitution value outside int16 after the shift: the int32 row scan computes it
     if (err == 2u) return kScoreTooLarge;
@@ -665,6 +681,14 @@ int gsa_mem_stats_reset(gsa_ctx* ctx)
     return GSA_SUCCESS;
 }
 
+int gsa_set_lap_callback(gsa_ctx* ctx, gsa_lap_fn fn, void* user)
+{
+    if (!ctx) return GSA_ERROR_INVALID_VALUE;
+    ctx->lap_fn = fn;
+    ctx->lap_user = fn ? user : nullptr;
+    return GSA_SUCCESS;
+}
+
 int gsa_set_watchdog(gsa_ctx* ctx, int64_t microseconds)
 {
     if (!ctx || microseconds < 0 || microseconds > 3600ll * 1000000ll) return GSA_ERROR_INVALID_VALUE;
@@ -752,6 +776,7 @@ int gsa_align_full(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, const int
         (s = ensure_dev(ctx, 2, (size_t)substsz * substsz * 4)) || (s = ensure_dev(ctx, 3, cells * 4)))
         return s;
     L.alloc = ms_since(t);
+    lap(ctx, "align.alloc");
     hipError_t e;
     if ((e = hipMemcpyAsync(ctx->dbuf[0], seqY, (size_t)adjrows * 4, hipMemcpyHostToDevice, ctx->stream)) ||
         (e = hipMemcpyAsync(ctx->dbuf[1], seqX, (size_t)adjcols * 4, hipMemcpyHostToDevice, ctx->stream)) ||
@@ -759,7 +784,9 @@ int gsa_align_full(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, const int
         (e = hipStreamSynchronize(ctx->stream)))
         return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
     L.cpy_dev = ms_since(t);
+    lap(ctx, "align.cpy_dev");
     L.init_hdr = 0.f;  // headers are written by the fill launch itself
+    lap(ctx, "align.init_hdr");
     (void)hipEventRecord(ctx->ev0, ctx->stream);
     s = gsa_fill_full_dev(ctx, (const int32_t*)ctx->dbuf[0], adjrows, (const int32_t*)ctx->dbuf[1], adjcols,
                           (const int32_t*)ctx->dbuf[2], substsz, gapo, (int32_t*)ctx->dbuf[3], ctx->stream);
@@ -767,10 +794,12 @@ int gsa_align_full(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, const int
     (void)hipEventRecord(ctx->ev1, ctx->stream);
     if ((s = gsa_sync(ctx, ctx->stream)) != GSA_SUCCESS) return s;
     L.calc = ms_since(t);
+    lap(ctx, "align.calc");
     (void)hipEventElapsedTime(&L.calc_kernel_ms, ctx->ev0, ctx->ev1);
     if ((e = copy_d2h(ctx, score_out, ctx->dbuf[3], cells * 4)))
         return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
     L.cpy_host = ms_since(t);
+    lap(ctx, "align.cpy_host");
     if (align_cost) *align_cost = score_out[cells - 1];
     if (laps) *laps = L;
     return GSA_SUCCESS;
@@ -792,6 +821,7 @@ int gsa_align_sparse(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, const i
         (s = ensure_dev(ctx, 4, (size_t)geom.hcolElems * 4)))
         return s;
     L.alloc = ms_since(t);
+    lap(ctx, "align.alloc");
     hipError_t e;
     if ((e = hipMemcpyAsync(ctx->dbuf[0], seqY, (size_t)adjrows * 4, hipMemcpyHostToDevice, ctx->stream)) ||
         (e = hipMemcpyAsync(ctx->dbuf[1], seqX, (size_t)adjcols * 4, hipMemcpyHostToDevice, ctx->stream)) ||
@@ -799,6 +829,8 @@ int gsa_align_sparse(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, const i
         (e = hipStreamSynchronize(ctx->stream)))
         return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
     L.cpy_dev = ms_since(t);
+    lap(ctx, "align.cpy_dev");
+    lap(ctx, "align.init_hdr");  // headers are written by the fill launch itself
     (void)hipEventRecord(ctx->ev0, ctx->stream);
     s = gsa_fill_sparse_dev(ctx, (const int32_t*)ctx->dbuf[0], adjrows, (const int32_t*)ctx->dbuf[1], adjcols,
                             (const int32_t*)ctx->dbuf[2], substsz, gapo, tileBx, (int32_t*)ctx->dbuf[3],
@@ -807,15 +839,18 @@ int gsa_align_sparse(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, const i
     (void)hipEventRecord(ctx->ev1, ctx->stream);
     if ((s = gsa_sync(ctx, ctx->stream)) != GSA_SUCCESS) return s;
     L.calc = ms_since(t);
+    lap(ctx, "align.calc");
     (void)hipEventElapsedTime(&L.calc_kernel_ms, ctx->ev0, ctx->ev1);
     if ((e = copy_d2h(ctx, hrow_out, ctx->dbuf[3], (size_t)geom.hrowElems * 4)) ||
         (e = copy_d2h(ctx, hcol_out, ctx->dbuf[4], (size_t)geom.hcolElems * 4)))
         return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
     L.cpy_host = ms_since(t);
+    lap(ctx, "align.cpy_host");
     // align_cost from the last tile, as the reference does after its copy-back (:713-716);
     // the reference adds this to the align.calc lap.
     int32_t cost = gsa_sparse_align_cost(hrow_out, hcol_out, &geom, seqY, adjrows, seqX, adjcols, subst, substsz, gapo);
     L.calc += ms_since(t);
+    lap(ctx, "align.calc");
     if (align_cost) *align_cost = cost;
     if (geom_out) *geom_out = geom;
     if (laps) *laps = L;
@@ -940,11 +975,21 @@ int gsa_trace_sparse_dev(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, con
     // LDS) and recomputes only the tiles it finds outside the band.
     a.tmap = nullptr;
     a.tcodes = nullptr;
+    // The band is only a speed-up: its codes take at most 512 MB and half the free device memory
+    // (GSA_TRACE_BAND_BUDGET, bytes, lowers the cap), and if its buffers cannot be had the walk
+    // runs alone and recomputes every tile it enters.
     {
         const int band = env_int("GSA_TRACE_BAND", 1024);
         const int trows = g.tileHdrMatRows, tcols = g.tileHdrMatCols;
         const size_t words = gsa::trace_dir_words(g.tileBy, g.tileBx);
-        const size_t maxSlots = ((size_t)512 << 20) / (words * 4);  // 512 MB of codes at most
+        size_t budget = (size_t)512 << 20;
+        {
+            size_t freeB = 0, totalB = 0;
+            if (hipMemGetInfo(&freeB, &totalB) == hipSuccess) budget = std::min(budget, freeB / 2);
+            const char* eb = std::getenv("GSA_TRACE_BAND_BUDGET");
+            if (eb) budget = std::min(budget, (size_t)std::strtoull(eb, nullptr, 10));
+        }
+        const size_t maxSlots = budget / (words * 4);
         std::vector<int> list, map((size_t)trows * (size_t)tcols, -1);
         const double slope = (double)std::max<int64_t>(1, adjcols - 1) / (double)std::max<int64_t>(1, adjrows - 1);
         for (int r = 0; band > 0 && r < trows && list.size() / 2 < maxSlots; ++r)
@@ -960,25 +1005,31 @@ int gsa_trace_sparse_dev(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, con
             }
         }
         const int n = (int)(list.size() / 2);
-        if (n > 0)
+        bool have = n > 0;
+        const size_t ints = list.size() + map.size(), cbytes = (size_t)n * words * 4;
+        if (have && ctx->tlist_cap < ints)
         {
-            const size_t ints = list.size() + map.size(), cbytes = (size_t)n * words * 4;
-            if (ctx->tlist_cap < ints)
-            {
-                if (ctx->tlist) (void)hipFree(ctx->tlist);
-                ctx->tlist = nullptr;
-                ctx->tlist_cap = 0;
-                if ((e = hipMalloc(&ctx->tlist, ints * 4)) != hipSuccess) return fail(ctx, e, GSA_ERROR_MEMORY_ALLOCATION);
+            if (ctx->tlist) (void)hipFree(ctx->tlist);
+            ctx->tlist = nullptr;
+            ctx->tlist_cap = 0;
+            if (hipMalloc(&ctx->tlist, ints * 4) == hipSuccess)
                 ctx->tlist_cap = ints;
-            }
-            if (ctx->tband_cap < cbytes)
-            {
-                if (ctx->tband) (void)hipFree(ctx->tband);
-                ctx->tband = nullptr;
-                ctx->tband_cap = 0;
-                if ((e = hipMalloc(&ctx->tband, cbytes)) != hipSuccess) return fail(ctx, e, GSA_ERROR_MEMORY_ALLOCATION);
+            else
+                have = false;
+        }
+        if (have && ctx->tband_cap < cbytes)
+        {
+            if (ctx->tband) (void)hipFree(ctx->tband);
+            ctx->tband = nullptr;
+            ctx->tband_cap = 0;
+            if (hipMalloc(&ctx->tband, cbytes) == hipSuccess)
                 ctx->tband_cap = cbytes;
-            }
+            else
+                have = false;
+        }
+        if (!have) (void)hipGetLastError();  // a failed band allocation: the walk runs alone
+        if (have)
+        {
             // pageable sources: the copies are complete when the calls return
             if ((e = hipMemcpyAsync(ctx->tlist, list.data(), list.size() * 4, hipMemcpyHostToDevice, st)) != hipSuccess ||
                 (e = hipMemcpyAsync(ctx->tlist + list.size(), map.data(), map.size() * 4, hipMemcpyHostToDevice, st)) != hipSuccess)
@@ -1002,9 +1053,24 @@ int gsa_trace_sparse_dev(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, con
     return gsa::fold_moves(moves.data(), (int64_t)res[0], edit, cap, edit_len, trace_hash);
 }
 
-int gsa_score_dev(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, const int32_t* seqX, int32_t adjcols,
-                  const int32_t* subst, int32_t substsz, int32_t gapo, int32_t gape, int32_t local,
-                  gsa_score_result* out, void* stream)
+}  // extern "C"
+
+namespace {
+
+// Largest |substitution value| (>= 1) of a host table.
+long long subst_absmax(const int32_t* sub, int32_t substsz)
+{
+    long long smax = 1;
+    for (size_t k = 0; k < (size_t)substsz * (size_t)substsz; ++k)
+        smax = std::max<long long>(smax, sub[k] < 0 ? -(long long)sub[k] : (long long)sub[k]);
+    return smax;
+}
+
+// gsa_score_dev; smax < 0: read the table back from the device (in stream order, so the caller's
+// writes to it are seen) to find the largest |value|; gsa_score passes it from its host copy.
+int score_dev_impl(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, const int32_t* seqX, int32_t adjcols,
+                   const int32_t* subst, int32_t substsz, int32_t gapo, int32_t gape, int32_t local,
+                   gsa_score_result* out, hipStream_t st, long long smax)
 {
     if (!ctx || !seqY || !seqX || !subst || !out) return GSA_ERROR_INVALID_VALUE;
     int s = check_inputs(adjrows, adjcols, substsz);
@@ -1023,14 +1089,15 @@ int gsa_score_dev(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, const int3
     }
     hipError_t e = hipSetDevice(ctx->device);
     if (e != hipSuccess) return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
-    hipStream_t st = pick_stream(ctx, stream);
     // value ranges: the largest |substitution value| bounds every score and shifted value
-    std::vector<int32_t> sub((size_t)substsz * (size_t)substsz);
-    if ((e = hipMemcpyAsync(sub.data(), subst, sub.size() * 4, hipMemcpyDeviceToHost, st)) != hipSuccess ||
-        (e = hipStreamSynchronize(st)) != hipSuccess)
-        return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
-    long long smax = 1;
-    for (int32_t v : sub) smax = std::max<long long>(smax, v < 0 ? -(long long)v : (long long)v);
+    if (smax < 0)
+    {
+        std::vector<int32_t> sub((size_t)substsz * (size_t)substsz);
+        if ((e = hipMemcpyAsync(sub.data(), subst, sub.size() * 4, hipMemcpyDeviceToHost, st)) != hipSuccess ||
+            (e = hipStreamSynchronize(st)) != hipSuccess)
+            return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
+        smax = subst_absmax(sub.data(), substsz);
+    }
     const long long span = (R + C) * (long long)(-gape) + (long long)(gape - gapo) + smax;
     // unshifted int32 (row scan): |H| <= smax*min(R,C) + |go| + (R+C)|ge|
     if (smax * std::min(R, C) + (long long)(-gapo) + (R + C) * (long long)(-gape) >= (1ll << 30))
@@ -1112,6 +1179,18 @@ int gsa_score_dev(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, const int3
     return GSA_SUCCESS;
 }
 
+}  // namespace
+
+extern "C" {
+
+int gsa_score_dev(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, const int32_t* seqX, int32_t adjcols,
+                  const int32_t* subst, int32_t substsz, int32_t gapo, int32_t gape, int32_t local,
+                  gsa_score_result* out, void* stream)
+{
+    return score_dev_impl(ctx, seqY, adjrows, seqX, adjcols, subst, substsz, gapo, gape, local, out,
+                          pick_stream(ctx, stream), -1);
+}
+
 int gsa_score(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, const int32_t* seqX, int32_t adjcols,
               const int32_t* subst, int32_t substsz, int32_t gapo, int32_t gape, int32_t local,
               gsa_score_result* out, gsa_laps* laps)
@@ -1125,6 +1204,7 @@ int gsa_score(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, const int32_t*
         (s = ensure_dev(ctx, 2, (size_t)substsz * substsz * 4)))
         return s;
     L.alloc = ms_since(t);
+    lap(ctx, "align.alloc");
     hipError_t e;
     if ((e = hipMemcpyAsync(ctx->dbuf[0], seqY, (size_t)adjrows * 4, hipMemcpyHostToDevice, ctx->stream)) ||
         (e = hipMemcpyAsync(ctx->dbuf[1], seqX, (size_t)adjcols * 4, hipMemcpyHostToDevice, ctx->stream)) ||
@@ -1132,10 +1212,13 @@ int gsa_score(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, const int32_t*
         (e = hipStreamSynchronize(ctx->stream)))
         return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
     L.cpy_dev = ms_since(t);
-    s = gsa_score_dev(ctx, (const int32_t*)ctx->dbuf[0], adjrows, (const int32_t*)ctx->dbuf[1], adjcols,
-                      (const int32_t*)ctx->dbuf[2], substsz, gapo, gape, local, out, ctx->stream);
+    lap(ctx, "align.cpy_dev");
+    s = score_dev_impl(ctx, (const int32_t*)ctx->dbuf[0], adjrows, (const int32_t*)ctx->dbuf[1], adjcols,
+                       (const int32_t*)ctx->dbuf[2], substsz, gapo, gape, local, out, ctx->stream,
+                       subst_absmax(subst, substsz));
     if (s != GSA_SUCCESS) return s;
     L.calc = ms_since(t);
+    lap(ctx, "align.calc");
     L.calc_kernel_ms = out->calc_kernel_ms;
     if (laps) *laps = L;
     return GSA_SUCCESS;
@@ -1172,12 +1255,15 @@ int gsa_align_sparse_pt(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, cons
     if ((e = hipHostGetDevicePointer((void**)&dflags, ctx->ptflags, 0)) != hipSuccess)
         return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
     L.alloc = ms_since(t);
+    lap(ctx, "align.alloc");
     if ((e = hipMemcpyAsync(ctx->dbuf[0], seqY, (size_t)adjrows * 4, hipMemcpyHostToDevice, ctx->stream)) ||
         (e = hipMemcpyAsync(ctx->dbuf[1], seqX, (size_t)adjcols * 4, hipMemcpyHostToDevice, ctx->stream)) ||
         (e = hipMemcpyAsync(ctx->dbuf[2], subst, (size_t)substsz * substsz * 4, hipMemcpyHostToDevice, ctx->stream)) ||
         (e = hipStreamSynchronize(ctx->stream)))
         return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
     L.cpy_dev = ms_since(t);
+    lap(ctx, "align.cpy_dev");
+    lap(ctx, "align.init_hdr");  // headers are written by the fill launch itself
     int32_t* dhr = (int32_t*)ctx->dbuf[3];
     int32_t* dhc = (int32_t*)ctx->dbuf[4];
     (void)hipEventRecord(ctx->ev0, ctx->stream);
@@ -1219,11 +1305,14 @@ int gsa_align_sparse_pt(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, cons
     }
     if ((s = gsa_sync(ctx, ctx->stream)) != GSA_SUCCESS) return s;
     L.calc = ms_since(t);
+    lap(ctx, "align.calc");
     (void)hipEventElapsedTime(&L.calc_kernel_ms, ctx->ev0, ctx->ev1);
     if ((e = copy_rows(trows, trows)) != hipSuccess) return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
     L.cpy_host = ms_since(t);
+    lap(ctx, "align.cpy_host");
     int32_t cost = gsa_sparse_align_cost(hrow_out, hcol_out, &geom, seqY, adjrows, seqX, adjcols, subst, substsz, gapo);
     L.calc += ms_since(t);
+    lap(ctx, "align.calc");
     if (align_cost) *align_cost = cost;
     if (geom_out) *geom_out = geom;
     if (laps) *laps = L;

@@ -89,6 +89,13 @@ void Laps::add(const std::string& name, float ms)
     laps.emplace_back(name, ms);
 }
 
+void Laps::lap(const std::string& name)
+{
+    const auto now = std::chrono::steady_clock::now();
+    add(name, std::chrono::duration<float, std::milli>(now - mark).count());
+    mark = now;
+}
+
 float Laps::get_or_default(const std::string& name) const
 {
     for (auto& l : laps)
@@ -124,127 +131,12 @@ void NwAlgInput::resetAllocsBenchmarkCycle()
     tileHcolMat.shrink_to_fit();
 }
 
-// ---- align adapters --------------------------------------------------------------------------
 namespace {
-
 using Clock = std::chrono::steady_clock;
 float ms_since(Clock::time_point t0) { return std::chrono::duration<float, std::milli>(Clock::now() - t0).count(); }
-
-void copy_laps(const gsa_laps& l, Laps& out)
-{
-    out.add("align.alloc", l.alloc);
-    out.add("align.cpy_dev", l.cpy_dev);
-    out.add("align.init_hdr", l.init_hdr);
-    out.add("align.calc", l.calc);
-    out.add("align.cpy_host", l.cpy_host);
-}
-
-NwStat check_input(const NwAlgInput& nw)
-{
-    if (!nw.ctx || nw.adjrows < 1 || nw.adjcols < 1 || (int)nw.seqY.size() != nw.adjrows ||
-        (int)nw.seqX.size() != nw.adjcols || (int)nw.subst.size() != nw.substsz * nw.substsz)
-        return NwStat::errorInvalidValue;
-    return NwStat::success;
-}
-
 }  // namespace
 
-// Peak-alloc columns from the context's launch footprints (updateNwAlgPeakMemUsage,
-// nwalign_shared.cpp:5-25): kernel attributes x resident workgroups of every fill so far.
-static void update_peak_mem(const NwAlgInput& nw, NwAlgResult& res)
-{
-    gsa_mem_stats m {};
-    if (gsa_mem_stats_get(nw.ctx, &m) != GSA_SUCCESS) return;
-    res.globalMemPeakAllocs = std::max(res.globalMemPeakAllocs, (size_t)m.glmem_peak_allocs);
-    res.sharedMemPeakAllocs = std::max(res.sharedMemPeakAllocs, (size_t)m.shmem_peak_allocs);
-    res.localMemPeakAllocs = std::max(res.localMemPeakAllocs, (size_t)m.locmem_peak_allocs);
-    res.regMemPeakAllocs = std::max(res.regMemPeakAllocs, (size_t)m.regmem_peak_allocs);
-}
-
-// Plain family (NwAlign_Gpu1..6 slots): the full (adjrows x adjcols) matrix in nw.score.
-// No tunables: the strip geometry is fixed by the hardware; parameters the
-// reference's files list for these slots are accepted and ignored.
-NwStat NwAlign_Amd_Strip_Full(const NwAlgParams&, NwAlgInput& nw, NwAlgResult& res)
-{
-    if (NwStat s = check_input(nw); s != NwStat::success) return s;
-    try
-    {
-        nw.score.resize((size_t)nw.adjrows * (size_t)nw.adjcols);
-    }
-    catch (const std::exception&)
-    {
-        return NwStat::errorMemoryAllocation;
-    }
-    gsa_laps laps {};
-    int cost = 0;
-    gsa_mem_stats_reset(nw.ctx);  // peaks of this call only (res keeps the max over runs)
-    int st = gsa_align_full(nw.ctx, nw.seqY.data(), nw.adjrows, nw.seqX.data(), nw.adjcols, nw.subst.data(), nw.substsz,
-                            nw.gapoCost, nw.score.data(), &cost, &laps);
-    res.hipStat = gsa_last_hip_error(nw.ctx);
-    if (st != GSA_SUCCESS) return (NwStat)st;
-    copy_laps(laps, res.sw_align);
-    res.align_cost = cost;
-    res.globalMemPeakAllocs = std::max(res.globalMemPeakAllocs, nw.score.size() * sizeof(int));
-    update_peak_mem(nw, res);
-    return NwStat::success;
-}
-
-// Sparse family (NwAlign_Gpu7..9 slots): tile header matrices.  Parameter "tileBx" (a
-// multiple of 16, >= 64) selects the tile width; default 256.  The tile height is the
-// engine's super-strip height (gsa_sparse_tile_by()).
-static NwStat align_mlsp(const NwAlgParams& pr, NwAlgInput& nw, NwAlgResult& res, bool overlap)
-{
-    if (NwStat s = check_input(nw); s != NwStat::success) return s;
-    int tileBx = 256;
-    if (pr.has("tileBx"))
-    {
-        int v = pr.at("tileBx").curr();
-        if (v >= 64 && v % 16 == 0) tileBx = v;
-    }
-    gsa_sparse_geom g {};
-    if (int st = gsa_sparse_geometry(nw.adjrows, nw.adjcols, tileBx, &g); st != GSA_SUCCESS) return (NwStat)st;
-    try
-    {
-        nw.tileHrowMat.resize((size_t)g.hrowElems);
-        nw.tileHcolMat.resize((size_t)g.hcolElems);
-    }
-    catch (const std::exception&)
-    {
-        return NwStat::errorMemoryAllocation;
-    }
-    gsa_laps laps {};
-    int cost = 0;
-    gsa_mem_stats_reset(nw.ctx);
-    int st = (overlap ? gsa_align_sparse_pt : gsa_align_sparse)(nw.ctx, nw.seqY.data(), nw.adjrows, nw.seqX.data(),
-                                                                nw.adjcols, nw.subst.data(), nw.substsz, nw.gapoCost,
-                                                                tileBx, nw.tileHrowMat.data(), nw.tileHcolMat.data(),
-                                                                &g, &cost, &laps);
-    res.hipStat = gsa_last_hip_error(nw.ctx);
-    if (st != GSA_SUCCESS) return (NwStat)st;
-    nw.geom = g;
-    nw.tileHdrMatRows = g.tileHdrMatRows;
-    nw.tileHdrMatCols = g.tileHdrMatCols;
-    nw.tileHrowLen = g.tileHrowLen;
-    nw.tileHcolLen = g.tileHcolLen;
-    copy_laps(laps, res.sw_align);
-    res.align_cost = cost;
-    res.globalMemPeakAllocs =
-        std::max(res.globalMemPeakAllocs, (nw.tileHrowMat.size() + nw.tileHcolMat.size()) * sizeof(int));
-    update_peak_mem(nw, res);
-    return NwStat::success;
-}
-
-NwStat NwAlign_Amd_Strip_Mlsp(const NwAlgParams& pr, NwAlgInput& nw, NwAlgResult& res)
-{
-    return align_mlsp(pr, nw, res, false);
-}
-
-// mlsppt ("multi-launch sparse with parallel transfer", README.md:39 of the reference, never
-// implemented there): the same outputs, the header copy-back overlapped with the fill.
-NwStat NwAlign_Amd_Strip_Mlsppt(const NwAlgParams& pr, NwAlgInput& nw, NwAlgResult& res)
-{
-    return align_mlsp(pr, nw, res, true);
-}
+// The align adapters (NwAlign_Amd_Strip_*) are in nwalign_amd.cpp.
 
 // ---- trace / hash adapters (the reference's L4 consumers, host C++ in libgsa) -------------
 NwStat NwHash1_Plain(NwAlgInput& nw, NwAlgResult& res)

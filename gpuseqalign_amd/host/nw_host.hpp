@@ -9,6 +9,7 @@
 // holds host buffers, parameters, timings and the benchmark bookkeeping only.
 #pragma once
 
+#include <chrono>
 #include <cstdint>
 #include <map>
 #include <ostream>
@@ -75,14 +76,19 @@ struct NwAlgParams
     std::string toJson() const;  // {"name":value,...} as the TSV alg_params column
 };
 
-// Stopwatch laps in ms, accumulated per name (src/stopwatch.cpp:43-50).
+// Stopwatch laps in ms, accumulated per name (src/stopwatch.hpp:10-33, stopwatch.cpp:4-50):
+// start() sets the mark, lap(name) adds the time since the mark to `name` and moves the mark.
 struct Laps
 {
     std::vector<std::pair<std::string, float>> laps;
+    std::chrono::steady_clock::time_point mark {};
+    void start() { mark = std::chrono::steady_clock::now(); }
+    void lap(const std::string& name);
     void add(const std::string& name, float ms);
     float get_or_default(const std::string& name) const;
     static Laps combine(const std::vector<Laps>& runs);  // per-name average
 };
+using Stopwatch = Laps;  // the reference's name
 
 struct NwAlgInput
 {

@@ -65,6 +65,17 @@ typedef struct gsa_laps
     float calc_kernel_ms;
 } gsa_laps;
 
+/* Phase-boundary callback of the host-buffer entry points (gsa_align_full, gsa_align_sparse,
+ * gsa_align_sparse_pt, gsa_score): called with "align.alloc", "align.cpy_dev", "align.init_hdr",
+ * "align.calc", "align.cpy_host" (and "align.calc" again after the last-tile recompute of the
+ * sparse forms) at the points where the reference's align functions call Stopwatch::lap
+ * (nwalign_gpu9_mlsp_diagdiagdiag.cu:435-719, nwalign_gpu3_ml_diagdiag.cu:329-593;
+ * src/stopwatch.hpp:19), so an adapter drives the reference's own stopwatch:
+ *     static void onLap(void* sw, const char* name) { ((Stopwatch*)sw)->lap(name); }
+ *     res.sw_align.start(); gsa_set_lap_callback(ctx, onLap, &res.sw_align);
+ * Called on the calling thread, before the entry point returns.  fn = NULL removes it. */
+typedef void (*gsa_lap_fn)(void* user, const char* lap_name);
+
 /* ---- context --------------------------------------------------------------------- */
 /* One context per device and host thread (the reference's initNwInput, src/benchmark.cpp:175-223). */
 int gsa_ctx_create(int device, gsa_ctx** out);
@@ -72,6 +83,7 @@ void gsa_ctx_destroy(gsa_ctx* ctx);
 int gsa_last_hip_error(const gsa_ctx* ctx);
 int gsa_device_cu_count(const gsa_ctx* ctx);
 const char* gsa_version(void);
+int gsa_set_lap_callback(gsa_ctx* ctx, gsa_lap_fn fn, void* user);
 
 /* Tile height of the sparse representation this build produces (63 * strips per workgroup). */
 int32_t gsa_sparse_tile_by(void);
@@ -210,6 +222,9 @@ int gsa_trace_sparse_dev(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, con
  *   global: score = H[R][C], boundaries gapo + (k-1)*gape; local: max over H, end = first
  *   cell in row-major order.  gapo == gape == g is the reference's NW-LG.  Requires
  *   gapo <= gape <= 0.  Synchronous. */
+/* gsa_score_dev reads the substitution table back in stream order (it sizes the value range
+ * from it) before its launch; the score kernels report errors in a control word of their own, so
+ * the fills' sticky error word is left for the caller's gsa_sync. */
 typedef struct gsa_score_result
 {
     int32_t score;

@@ -6,7 +6,11 @@ the build container, so the GPU box needs neither the oracle nor the reference):
     tileHrowMat + tileHcolMat), and the device Trace2 walk (nwtrace2_sparse.cpp:102-257): trace
     hash and edit string (sha256);
   * BASELINE configs[3] -- all 512 pairs of 18-22k (shard.synthetic_batch, seeds 1000+k) in one
-    batched launch: every align_cost against the cpu1 streaming restatement.
+    batched launch: every align_cost against the cpu1 streaming restatement; every header word
+    of all 512 pairs by the device checker (tile consistency, gsa_check_sparse_dev), and the
+    headers of 16 of them (sha256) against the oracle's, on the batch's 8-strip geometry and on
+    the 4-strip one.  The reference itself compares headers only along the trace path
+    (nwtrace2_sparse.cpp:263-340, the constant-index quirk at :293).
 """
 import hashlib
 import json
@@ -85,3 +89,50 @@ def test_config4_512_pairs_match_golden(golden, tBx):
     bad = [k for k in range(n) if costs[k] != gold["align_cost"][k]]
     assert not bad, ("pairs differing from the oracle", bad[:10], len(bad))
     assert secs > 0
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("ns", ["batch-default", "4"])
+def test_config4_headers_at_size(engine, golden, monkeypatch, ns):
+    """configs[3] at full size, header by header: one persistent launch over all 512 pairs (the
+    batch default is 8 strips per workgroup, two tile rows per ticket), then every pair's
+    tile headers through the device checker, and 16 pairs' headers against the oracle."""
+    import torch
+    from gpuseqalign_amd import shard
+    if ns != "batch-default":
+        monkeypatch.setenv("GSA_KROW_NS", ns)
+    gold = _load("config4_pairs.json")
+    hd = gold["headers"]
+    tBx = hd["tileBx"]
+    assert hd["tileBy"] == gsa.sparse_tile_by()
+    n = gold["n_pairs"]
+    pairs = shard.synthetic_batch(n, 18000, 22000, seed0=1000)
+    dev = torch.device("cuda:0")
+    sub = golden.blosum62
+    ts = torch.from_numpy(sub).to(dev)
+    ins, outs, geoms = [], [], []
+    for Y, X in pairs:
+        g = gsa.sparse_geometry(len(Y), len(X), tBx)
+        y, x = torch.from_numpy(Y).to(dev), torch.from_numpy(X).to(dev)
+        hr = torch.full((g.hrowElems,), -7, dtype=torch.int32, device=dev)  # poison: every word must be written
+        hc = torch.full((g.hcolElems,), -7, dtype=torch.int32, device=dev)
+        ins.append((y, x))
+        outs.append((hr, hc))
+        geoms.append(g)
+    engine.fill_batch_dev([(y.data_ptr(), len(y), x.data_ptr(), len(x), (hr.data_ptr(), hc.data_ptr()))
+                           for (y, x), (hr, hc) in zip(ins, outs)], ts.data_ptr(), 25, -11, mode="sparse", tileBx=tBx)
+    engine.sync()
+    bad = []
+    for k in range(n):
+        (y, x), (hr, hc), g = ins[k], outs[k], geoms[k]
+        r = engine.check_sparse_dev(y.data_ptr(), len(y), x.data_ptr(), len(x), ts.data_ptr(), 25, -11, g,
+                                    hr.data_ptr(), hc.data_ptr())
+        # every header word is compared at least once (nw_check.hip), corners twice
+        if r["mismatches"] != 0 or r["checked"] < g.hrowElems + g.hcolElems:
+            bad.append((k, r))
+    assert not bad, ("pairs whose headers fail the device check", bad[:5], len(bad))
+    for k, want in zip(hd["pairs"], hd["sha256"]):
+        h = hashlib.sha256()
+        h.update(outs[k][0].cpu().numpy().tobytes())
+        h.update(outs[k][1].cpu().numpy().tobytes())
+        assert h.hexdigest() == want, ("headers differ from the oracle's", k)

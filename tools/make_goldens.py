@@ -11,7 +11,10 @@
       [18000, 22000] (shard.synthetic_batch, seeds 1000+k); align_cost and score hash of
       each pair from the streaming cpu1 restatement (orc_hash_stream).
 
-Test infrastructure: the oracle is the checker.  Run:  python tools/make_goldens.py [config3|config4]
+      Plus sha256 digests of the tile headers of 16 of the pairs (tileBx 256).
+
+Test infrastructure: the oracle is the checker.
+Run:  python tools/make_goldens.py [config3|config4|config4_headers]
 """
 import hashlib
 import json
@@ -83,6 +86,37 @@ def _cfg4_one(k):
     return k, len(Y) - 1, len(X) - 1, cost, sh
 
 
+CFG4_HDR_PAIRS = list(range(0, 512, 32))  # 16 pairs spread over the batch
+CFG4_HDR_TBX = 256
+
+
+def _cfg4_hdr(k):
+    import oracle
+    from gpuseqalign_amd import shard
+    Y, X = shard.synthetic_batch(1, 18000, 22000, seed0=1000 + k)[0]
+    hr, hc, tr, tc, cost = oracle.sparse_headers(Y, X, _subst(), -11, 1024, CFG4_HDR_TBX)
+    return k, cost, header_digest(hr, hc)
+
+
+def make_config4_headers(procs=8):
+    """Tile-header digests of 16 config-4 pairs (tileBy 1024, tileBx 256) added to
+    config4_pairs.json: the batch's header words at full size, on whatever strip geometry
+    the batch runs."""
+    path = os.path.join(GOLDEN, "config4_pairs.json")
+    with open(path) as f:
+        out = json.load(f)
+    t0 = time.time()
+    with Pool(procs) as p:
+        res = sorted(p.map(_cfg4_hdr, CFG4_HDR_PAIRS))
+    for k, cost, _ in res:
+        assert cost == out["align_cost"][k]
+    out["headers"] = {"tileBy": 1024, "tileBx": CFG4_HDR_TBX, "pairs": [r[0] for r in res],
+                      "sha256": [r[2] for r in res]}
+    with open(path, "w") as f:
+        json.dump(out, f)
+    print("config4 headers: %d pairs, %.1fs" % (len(res), time.time() - t0))
+
+
 def make_config4(n=512, procs=8):
     t0 = time.time()
     with Pool(procs) as p:
@@ -102,3 +136,5 @@ if __name__ == "__main__":
         make_config3()
     if "config4" in what:
         make_config4()
+    if "config4" in what or "config4_headers" in what:
+        make_config4_headers()
