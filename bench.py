@@ -201,6 +201,99 @@ def bench_config4(world, rank, local, n_pairs):
             "pairs_matching_golden": match, "golden_pairs": None if gold is None else gold.get("n_pairs")}
 
 
+CLOCK_GHZ = 2.4          # MI355X_MICROARCH.md chip table (max clock)
+VALU_ISSUE_CYC = 4       # one wave alone issues one VALU per 4 cycles (MI355X_MICROARCH.md constants table)
+
+
+def critical_path(C, nStrips, valu_per_step, kern_ms, rows_per_strip):
+    """Design bound of one pair's wavefront fill: the last strip cannot finish before C steps
+    after it starts, and it starts nStrips x 64 steps after the first (each strip trails the one
+    above by at least the 64-lane skew); a step is at least its VALU at one wave's issue rate."""
+    step_cyc = valu_per_step * VALU_ISSUE_CYC
+    steps = C + nStrips * 64
+    bound_ms = steps * step_cyc / (CLOCK_GHZ * 1e9) * 1e3
+    return {"model": f"(C + strips x 64) steps x {valu_per_step} VALU x {VALU_ISSUE_CYC} cycles / {CLOCK_GHZ} GHz",
+            "strips": nStrips, "rows_per_strip": rows_per_strip, "steps": steps, "step_cycles_bound": step_cyc,
+            "bound_ms": round(bound_ms, 4), "frac": round(bound_ms / kern_ms, 4),
+            "step_cycles_achieved": round(kern_ms * 1e-3 * CLOCK_GHZ * 1e9 / steps, 1)}
+
+
+def bench_full_batch(world, rank, local, n_pairs):
+    """Full-matrix family at throughput (the plain gpu3-gpu6 slots, nwalign_gpu3_ml_diagdiag.cu:
+    288-596): n_pairs of the configs[3] pairs (18-22k, seeds 1000+k) as full int32 matrices in ONE
+    persistent launch; the bound is HBM writes (4 B per cell).  Every align_cost (the last cell)
+    is checked against the oracle goldens of tests/golden/config4_pairs.json."""
+    from gpuseqalign_amd import shard
+    pairs = shard.synthetic_batch(n_pairs, 18000, 22000, seed0=1000)
+    sub = subst_blosum62()
+    rep = shard.shard_align(pairs, sub, -11, shard.gpu_batch_align(device=local, mode="full", warmup=1, repeats=3,
+                                                                out_budget_bytes=int(0.9 * 140e9)),
+                            device=f"cuda:{local}" if world > 1 else None)
+    gold = load_golden("config4_pairs.json")
+    costs = [r.align_cost for r in rep.results]
+    match = None if gold is None else sum(int(a == b) for a, b in zip(costs, gold["align_cost"][:n_pairs]))
+    out_bytes = 4.0 * sum(len(y) * len(x) for y, x in pairs)
+    gbps = out_bytes / rep.elapsed_s / 1e9
+    return {"workload": f"{n_pairs} NW-LG pairs of BASELINE configs[3] (18-22k, seeds 1000+k) as FULL int32 score "
+                        f"matrices ({out_bytes / 1e9:.1f} GB), one persistent launch, LPT-sharded over {world} rank(s) "
+                        "(1 untimed + 3 timed launches; seconds per launch)",
+            "value": round(rep.gcups, 2), "unit": "GCUPS", "scaling": "strong", "seconds": round(rep.elapsed_s, 4),
+            "kernel": f"gsa::nw_lane_kernel<{lane_ns()}> (full, one row per lane)",
+            "hbm_write_GBps": round(gbps * world, 1), "hbm_frac": round(gbps / PEAK_HBM_GBPS, 4),
+            "bound": "hbm (4 B written per cell; MI355X 8 TB/s spec)",
+            "pairs": n_pairs, "pairs_matching_golden": match}
+
+
+CFG5 = [("SW-LG", -11, -11, True), ("NW-AG", -11, -1, False)]
+
+
+def bench_config5(dev, eng, steps, warmup, cpu_sample, rank, world):
+    """BASELINE configs[4]: score-only SW-LG and NW-AG (gapo -11, gape -1) on the 50k x 50k random
+    pair (seeds 200/201), inputs resident in HBM; kernel time from HIP events around each launch
+    (gsa_score_dev is synchronous).  Scores and end cells checked against the oracle goldens
+    (tests/golden/config5_50k.json, oracle/score_oracle.c).  cpu_baseline: the oracle's tiled
+    OpenMP score wavefront (cpu4-mt-diagrow shape) on a bounded prefix sample, rank 0 at N = 1."""
+    import torch
+    from gpuseqalign_amd import formats as F
+    Y, X = F.synthetic_seq(50000, 200), F.synthetic_seq(50000, 201)
+    sub = subst_blosum62()
+    y, x, s = (torch.from_numpy(np.ascontiguousarray(a, dtype=np.int32)).to(dev) for a in (Y, X, sub))
+    gold = load_golden("config5_50k.json")
+    R, C = len(Y) - 1, len(X) - 1
+    out = {}
+    for name, go, ge, local in CFG5:
+        run = lambda: eng.score_dev(y.data_ptr(), len(Y), x.data_ptr(), len(X), s.data_ptr(), 25, go, ge, local)
+        for _ in range(warmup):
+            run()
+        ks = []
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            r = run()
+            ks.append(r["kernel_ms"])
+        wall = (time.perf_counter() - t0) / steps
+        g = None if gold is None else gold["modes"][name]
+        ok = None if g is None else (r["score"], r["i_end"], r["j_end"]) == (g["score"], g["i_end"], g["j_end"])
+        kms = float(np.mean(ks))
+        out[name] = {"value": round(R * C / kms / 1e6, 2), "unit": "GCUPS", "kernel_ms": round(kms, 4),
+                     "ms_per_call": round(wall * 1e3, 4), "score": r["score"], "end": [r["i_end"], r["j_end"]],
+                     "golden_match": ok, "gapo": go, "gape": ge, "local": local,
+                     "kernel": "gsa::nw_strip_kernel score mode (%s)" % ("kModeScoreSW" if local else "kModeScoreAG")}
+        if cpu_sample > 0 and rank == 0 and world == 1:
+            import oracle
+            ncpu, phys, quota, nproc = cpu_topology()
+            th = max(1, min(phys, int(quota) if quota else phys))
+            m = cpu_sample
+            t1 = time.perf_counter()
+            oracle.score_ag(Y[:m + 1], X[:m + 1], sub, go, ge, local, mt=True, blocksz=256, nthreads=th)
+            cs = time.perf_counter() - t1
+            out[name]["cpu_baseline"] = {"value": round(m * m / cs / 1e9, 3), "unit": "GCUPS", "cores": th,
+                                         "kind": "port",
+                                         "sample": f"oracle score_oracle.c tiled OpenMP wavefront (blocksz 256) on the "
+                                                   f"{m}x{m} prefix of the same pair, {cs:.1f} s at {th} threads"}
+    return {"workload": "BASELINE configs[4]: score-only 50000x50000 random pair (synthetic seeds 200/201), blosum62",
+            "modes": out}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -210,6 +303,9 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--config4-pairs", type=int, default=512, help="0 = skip the configs[3] batch field")
     ap.add_argument("--no-10k", action="store_true", help="skip the configs[1] full-matrix field")
+    ap.add_argument("--full-batch-pairs", type=int, default=64, help="0 = skip the full-matrix batch field")
+    ap.add_argument("--no-config5", action="store_true", help="skip the configs[4] score-only field")
+    ap.add_argument("--config5-cpu-sample", type=int, default=16000, help="n x n prefix for the config-5 CPU leg")
     a = ap.parse_args()
 
     import torch
@@ -292,11 +388,21 @@ def main():
                    "kernel": f"gsa::nw_lane_kernel<{lane_ns()}> (full, one row per lane)",
                    "hbm_write_GBps": round(b2 / (km2 * 1e-3) / 1e9, 1),
                    "hbm_frac": round(b2 / (km2 * 1e-3) / 1e9 / PEAK_HBM_GBPS, 4),
-                   "align_cost": int(score[-1].item()), "golden_align_cost": -4922}
+                   "align_cost": int(score[-1].item()), "golden_align_cost": -4922,
+                   "critical_path": critical_path(C2, -(-R2 // (64 * lane_ns())) * lane_ns(), 4, km2, 64)}
         del score
         torch.cuda.empty_cache()
+    cfg5 = None
+    if not a.no_config5:
+        cfg5 = bench_config5(dev, eng, max(3, a.steps // 4), 2, 0 if a.no_cpu_baseline else a.config5_cpu_sample,
+                             rank, world)
     eng.sync(sh)
     eng.close()
+    torch.cuda.empty_cache()
+
+    # ---- full-matrix family at throughput (HBM-write bound) ------------------------------
+    fullb = bench_full_batch(world, rank, local, a.full_batch_pairs) if a.full_batch_pairs > 0 else None
+    torch.cuda.empty_cache()
 
     # ---- configs[3]: 512 pairs, LPT-sharded (strong scaling field) ------------------------
     cfg4 = bench_config4(world, rank, local, a.config4_pairs) if a.config4_pairs > 0 else None
@@ -318,10 +424,11 @@ def main():
                          "algorithmic_ops_per_launch": OPS_PER_CELL * cells,
                          "header_bytes_per_launch": hdr_bytes,
                          "header_GBps": round(hdr_bytes / (kern_ms * 1e-3) / 1e9, 1),
-                         "hbm_frac": round(hdr_bytes / (kern_ms * 1e-3) / 1e9 / PEAK_HBM_GBPS, 5)},
+                         "hbm_frac": round(hdr_bytes / (kern_ms * 1e-3) / 1e9 / PEAK_HBM_GBPS, 5),
+                         "critical_path": critical_path(C, -(-R // 256), 9, kern_ms, 256)},
             "align_costs": costs[:8], "golden_align_cost": gold_cost,
             "golden_match": None if gold_cost is None else all(c == gold_cost for c in costs),
-            "fill_10k_full": full10k, "config4": cfg4,
+            "fill_10k_full": full10k, "config4": cfg4, "full_batch": fullb, "config5": cfg5,
         }
         if not a.no_cpu_baseline and world == 1:  # the CPU leg runs on rank 0 at N = 1 only
             out["cpu_baseline"] = cpu_baseline(Y, X, sub, budget_s=a.cpu_budget)

@@ -71,8 +71,8 @@ struct gsa_ctx
     // score-only fills (nw_scan.hip): boundary rows H/F, progress words, control words
     int* sbnd = nullptr;
     size_t sbnd_cap = 0;  // ints
-    // mlsppt: host-mapped per-ticket completion flags
-    unsigned* ptflags = nullptr;
+    // mlsppt: host-mapped per-tile-row words (epoch << 32 | column chunks in memory)
+    unsigned long long* ptflags = nullptr;
     size_t ptflags_cap = 0;
     // score-only control words: row scan [0] ticket|err, [1] best key, [2] result; AG/SW strip
     // [0] result, [1] best key, [3] its own error word (the fills' sticky word is not touched)
@@ -300,7 +300,7 @@ int score_ag_strip(gsa_ctx* ctx, const int32_t* seqY, int64_t R, const int32_t* 
     if (s != GSA_SUCCESS) return s;
     hipError_t e = hipMemcpyAsync(ctx->desc, &d, sizeof(d), hipMemcpyHostToDevice, st);
     if (e != hipSuccess) return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
-    const size_t gran = (size_t)tickets * (size_t)(C + 1);
+    const size_t gran = (size_t)tickets * (size_t)gsa::gran_stride((int)C);
     if ((s = ensure_gran(ctx, 2 * gran, st)) != GSA_SUCCESS) return s;
     if (!ctx->sctl && (e = hipMalloc(&ctx->sctl, 64)) != hipSuccess) return fail(ctx, e, GSA_ERROR_MEMORY_ALLOCATION);
     a.pairs = ctx->desc;
@@ -356,7 +356,7 @@ int score_ag_strip(gsa_ctx* ctx, const int32_t* seqY, int64_t R, const int32_t* 
 // One batched launch: headers of every pair, then the persistent strip kernel over the
 // tickets of all pairs (pair-major).  `pairs` holds device pointers.
 int enqueue_batch(gsa_ctx* ctx, int mode, int npairs, const gsa_pair_dev* pairs, const int32_t* subst, int32_t substsz,
-                  int32_t gapo, int32_t tileBx, hipStream_t st, unsigned* done = nullptr)
+                  int32_t gapo, int32_t tileBx, hipStream_t st, unsigned long long* done = nullptr, int ptChunk = 0)
 {
     if (npairs < 1 || !pairs || !subst) return GSA_ERROR_INVALID_VALUE;
     if (substsz < 1 || substsz > 32) return GSA_ERROR_INVALID_VALUE;  // LDS profile holds <= 32 letters
@@ -366,7 +366,8 @@ int enqueue_batch(gsa_ctx* ctx, int mode, int npairs, const gsa_pair_dev* pairs,
     a.substsz = substsz;
     a.g = gapo;
     const bool lane = mode == gsa::kModeFull;
-    const bool krow = mode == gsa::kModeSparse && sparse_kernel() == kSpKrow;
+    // mlsppt publishes column chunks from the K-rows kernel only
+    const bool krow = mode == gsa::kModeSparse && (sparse_kernel() == kSpKrow || done);
     // single pairs: 4 strips per workgroup (each on its own SIMD: the pair's critical path);
     // batches: 8 (two strips per SIMD share the issue slots a single strip leaves idle, 512 x 20k
     // 5.7 -> 7.3 TCUPS; a single 100k pair 5.9 -> 8.4 ms), unless the batch's 4-strip tickets
@@ -431,7 +432,7 @@ int enqueue_batch(gsa_ctx* ctx, int mode, int npairs, const gsa_pair_dev* pairs,
         d.ticketBase = (int)tickets;
         d.granOff = gran;
         tickets += d.nTickets;
-        gran += (long long)d.nTickets * ((long long)d.Cp + 1);
+        gran += (long long)d.nTickets * gsa::gran_stride(d.Cp);
         if (tickets > (1ll << 30)) return GSA_ERROR_INVALID_VALUE;
     }
     // batch schedule (more than one pair): round-robin over the pairs, longest first, so the
@@ -496,6 +497,7 @@ int enqueue_batch(gsa_ctx* ctx, int mode, int npairs, const gsa_pair_dev* pairs,
     a.err = ctx->ctl + 1;
     a.spin = ctx->spin_ticks;
     a.done = done;
+    a.ptChunk = std::max(1, ptChunk);
     a.epoch = ++ctx->epoch;
     if (a.epoch == 0) a.epoch = ++ctx->epoch;  // 0 is the cleared-tag value
     e = hipMemsetAsync(ctx->ctl, 0, 4, st);  // the ticket; the error word stays sticky
@@ -512,10 +514,10 @@ int enqueue_batch(gsa_ctx* ctx, int mode, int npairs, const gsa_pair_dev* pairs,
 
 int enqueue_fill(gsa_ctx* ctx, int mode, const int32_t* seqY, int32_t adjrows, const int32_t* seqX, int32_t adjcols,
                  const int32_t* subst, int32_t substsz, int32_t gapo, int32_t* score, int32_t tileBx, int32_t* hrow,
-                 int32_t* hcol, hipStream_t st, unsigned* done = nullptr)
+                 int32_t* hcol, hipStream_t st, unsigned long long* done = nullptr, int ptChunk = 0)
 {
     gsa_pair_dev p {seqY, adjrows, seqX, adjcols, score, hrow, hcol};
-    return enqueue_batch(ctx, mode, 1, &p, subst, substsz, gapo, tileBx, st, done);
+    return enqueue_batch(ctx, mode, 1, &p, subst, substsz, gapo, tileBx, st, done, ptChunk);
 }
 
 }  // namespace
@@ -756,6 +758,63 @@ hipError_t copy_d2h(gsa_ctx* ctx, void* dst, const void* src, size_t bytes)
     work(0);
     for (auto& x : th) x.join();
     for (int k = 0; k < T; ++k)
+        if (errs[k] != hipSuccess) return errs[k];
+    return hipSuccess;
+}
+
+// Device -> pageable host copy of `height` rows of `width` bytes, source rows `spitch` apart,
+// destination rows `dpitch` apart (a column chunk of a tile-major header matrix): the rows are split
+// over the copy threads, each moving groups of rows by one 2-D DMA into a pinned chunk and copying
+// them into place while the next group's DMA runs.  width <= kCopyChunk.
+hipError_t copy_d2h_2d(gsa_ctx* ctx, char* dst, size_t dpitch, const char* src, size_t spitch, size_t width,
+                       size_t height)
+{
+    constexpr int T = gsa_ctx::kCopyThreads;
+    constexpr size_t kC = gsa_ctx::kCopyChunk;
+    if (width == 0 || height == 0) return hipSuccess;
+    if (width > kC) return hipErrorInvalidValue;
+    hipError_t e = hipSuccess;
+    for (int k = 0; k < T && e == hipSuccess; ++k)
+    {
+        if (!ctx->xstream[k]) e = hipStreamCreateWithFlags(&ctx->xstream[k], hipStreamNonBlocking);
+        for (int j = 0; j < 2 && e == hipSuccess; ++j)
+        {
+            if (!ctx->xstage[k][j]) e = hipHostMalloc(&ctx->xstage[k][j], kC, hipHostMallocDefault);
+            if (e == hipSuccess && !ctx->xev[k][j]) e = hipEventCreateWithFlags(&ctx->xev[k][j], hipEventDisableTiming);
+        }
+    }
+    if (e != hipSuccess) return e;
+    const size_t perGroup = std::max<size_t>(1, kC / width);
+    const int nT = (int)std::min<size_t>(T, (height + perGroup - 1) / perGroup);
+    const size_t perT = (height + nT - 1) / nT;
+    hipError_t errs[T];
+    auto work = [&](int k) {
+        hipError_t r = hipSetDevice(ctx->device);
+        const size_t lo = std::min(height, (size_t)k * perT), hi = std::min(height, (size_t)(k + 1) * perT);
+        const size_t n = (hi - lo + perGroup - 1) / perGroup;
+        auto issue = [&](size_t i) {
+            const size_t r0 = lo + i * perGroup, rows = std::min(perGroup, hi - r0);
+            hipError_t q = hipMemcpy2DAsync(ctx->xstage[k][i & 1], width, src + r0 * spitch, spitch, width, rows,
+                                            hipMemcpyDeviceToHost, ctx->xstream[k]);
+            return q == hipSuccess ? hipEventRecord(ctx->xev[k][i & 1], ctx->xstream[k]) : q;
+        };
+        if (r == hipSuccess && n > 0) r = issue(0);
+        for (size_t i = 0; r == hipSuccess && i < n; ++i)
+        {
+            if (i + 1 < n && (r = issue(i + 1)) != hipSuccess) break;
+            if ((r = hipEventSynchronize(ctx->xev[k][i & 1])) != hipSuccess) break;
+            const size_t r0 = lo + i * perGroup, rows = std::min(perGroup, hi - r0);
+            for (size_t j = 0; j < rows; ++j)
+                std::memcpy(dst + (r0 + j) * dpitch, (const char*)ctx->xstage[k][i & 1] + j * width, width);
+        }
+        if (r != hipSuccess) (void)hipStreamSynchronize(ctx->xstream[k]);
+        errs[k] = r;
+    };
+    std::vector<std::thread> th;
+    for (int k = 1; k < nT; ++k) th.emplace_back(work, k);
+    work(0);
+    for (auto& x : th) x.join();
+    for (int k = 0; k < nT; ++k)
         if (errs[k] != hipSuccess) return errs[k];
     return hipSuccess;
 }
@@ -1246,12 +1305,13 @@ int gsa_align_sparse_pt(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, cons
         if (ctx->ptflags) (void)hipHostFree(ctx->ptflags);
         ctx->ptflags = nullptr;
         ctx->ptflags_cap = 0;
-        if ((e = hipHostMalloc((void**)&ctx->ptflags, trows * sizeof(unsigned), hipHostMallocMapped)) != hipSuccess)
+        if ((e = hipHostMalloc((void**)&ctx->ptflags, trows * sizeof(unsigned long long), hipHostMallocMapped)) !=
+            hipSuccess)
             return fail(ctx, e, GSA_ERROR_MEMORY_ALLOCATION);
-        std::memset(ctx->ptflags, 0, trows * sizeof(unsigned));
+        std::memset(ctx->ptflags, 0, trows * sizeof(unsigned long long));
         ctx->ptflags_cap = trows;
     }
-    unsigned* dflags = nullptr;
+    unsigned long long* dflags = nullptr;
     if ((e = hipHostGetDevicePointer((void**)&dflags, ctx->ptflags, 0)) != hipSuccess)
         return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
     L.alloc = ms_since(t);
@@ -1266,39 +1326,46 @@ int gsa_align_sparse_pt(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, cons
     lap(ctx, "align.init_hdr");  // headers are written by the fill launch itself
     int32_t* dhr = (int32_t*)ctx->dbuf[3];
     int32_t* dhc = (int32_t*)ctx->dbuf[4];
+    // Column chunks of ptChunk tile columns: a chunk's headers (header rows and columns of every
+    // tile row) are final once every tile row's word counts it; the fill reaches a column in every
+    // super-strip within the wavefront's fill-in, so chunks complete left to right while the fill
+    // runs, and each is copied back (one strided copy per matrix) as soon as it is complete.
+    const int tcols = geom.tileHdrMatCols;
+    const int cw = std::max(1, std::min(tcols, (4096 + tileBx - 1) / tileBx));
+    const int nCh = (tcols + cw - 1) / cw;
     (void)hipEventRecord(ctx->ev0, ctx->stream);
     s = enqueue_fill(ctx, gsa::kModeSparse, (const int32_t*)ctx->dbuf[0], adjrows, (const int32_t*)ctx->dbuf[1],
                      adjcols, (const int32_t*)ctx->dbuf[2], substsz, gapo, nullptr, tileBx, dhr, dhc, ctx->stream,
-                     dflags);
+                     dflags, cw);
     if (s != GSA_SUCCESS) return s;
     (void)hipEventRecord(ctx->ev1, ctx->stream);
-    const unsigned epoch = ctx->epoch;
-    const size_t W = (size_t)geom.tileHrowLen * (size_t)geom.tileHdrMatCols;  // ints per tile row of hrow
-    const size_t H = (size_t)geom.tileHcolLen * (size_t)geom.tileHdrMatCols;  // ints per tile row of hcol
-    // tile rows whose headers are final: hrow row k+1 and hcol row k once super-strip k is done;
-    // hrow row 0 comes from the headers kernel before any super-strip starts
-    size_t done = 0, hrowCopied = 0, hcolCopied = 0;
-    const size_t chunk = std::max<size_t>(1, trows / 16);
-    auto copy_rows = [&](size_t hrUpTo, size_t hcUpTo) -> hipError_t {
-        hipError_t err = hipSuccess;
-        if (hrUpTo > hrowCopied)
-            err = copy_d2h(ctx, hrow_out + hrowCopied * W, dhr + hrowCopied * W, (hrUpTo - hrowCopied) * W * 4);
-        if (err == hipSuccess && hcUpTo > hcolCopied)
-            err = copy_d2h(ctx, hcol_out + hcolCopied * H, dhc + hcolCopied * H, (hcUpTo - hcolCopied) * H * 4);
-        hrowCopied = std::max(hrowCopied, hrUpTo);
-        hcolCopied = std::max(hcolCopied, hcUpTo);
+    const unsigned long long epoch = ctx->epoch;
+    const size_t rowW = (size_t)geom.tileHrowLen * 4, rowH = (size_t)geom.tileHcolLen * 4;  // bytes per tile
+    int copied = 0;  // chunks copied back
+    auto copy_chunks = [&](int upTo) -> hipError_t {
+        const size_t j0 = (size_t)copied * cw, j1 = std::min((size_t)tcols, (size_t)upTo * cw);
+        hipError_t err = copy_d2h_2d(ctx, (char*)hrow_out + j0 * rowW, tcols * rowW, (const char*)dhr + j0 * rowW,
+                                     tcols * rowW, (j1 - j0) * rowW, trows);
+        if (err == hipSuccess)
+            err = copy_d2h_2d(ctx, (char*)hcol_out + j0 * rowH, tcols * rowH, (const char*)dhc + j0 * rowH,
+                              tcols * rowH, (j1 - j0) * rowH, trows);
+        copied = upTo;
         return err;
     };
     for (;;)
     {
         const hipError_t q = hipStreamQuery(ctx->stream);  // the fill (and its headers kernel) finished?
         if (q != hipSuccess && q != hipErrorNotReady) return fail(ctx, q, GSA_ERROR_KERNEL_FAILURE);
-        while (done < trows && __atomic_load_n(ctx->ptflags + done, __ATOMIC_ACQUIRE) == epoch) ++done;
         if (q == hipSuccess) break;
-        if (done >= hcolCopied + chunk)
+        int ready = nCh;
+        for (size_t r = 0; r < trows && ready > copied; ++r)
         {
-            if ((e = copy_rows(std::min(done + 1, trows), done)) != hipSuccess)
-                return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
+            const unsigned long long v = __atomic_load_n(ctx->ptflags + r, __ATOMIC_ACQUIRE);
+            ready = std::min(ready, (v >> 32) == epoch ? (int)(v & 0xffffffffu) : 0);
+        }
+        if (ready > copied)
+        {
+            if ((e = copy_chunks(ready)) != hipSuccess) return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
         }
         else
             std::this_thread::sleep_for(std::chrono::microseconds(20));
@@ -1307,7 +1374,7 @@ int gsa_align_sparse_pt(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, cons
     L.calc = ms_since(t);
     lap(ctx, "align.calc");
     (void)hipEventElapsedTime(&L.calc_kernel_ms, ctx->ev0, ctx->ev1);
-    if ((e = copy_rows(trows, trows)) != hipSuccess) return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
+    if (copied < nCh && (e = copy_chunks(nCh)) != hipSuccess) return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
     L.cpy_host = ms_since(t);
     lap(ctx, "align.cpy_host");
     int32_t cost = gsa_sparse_align_cost(hrow_out, hcol_out, &geom, seqY, adjrows, seqX, adjcols, subst, substsz, gapo);

@@ -71,6 +71,8 @@ constexpr int kBatch = 128;       // profile columns the loader adds per pass (2
 __host__ __device__ constexpr uint32_t kr_prog(int i) { return 8u * (uint32_t)i; }
 __host__ __device__ constexpr uint32_t kr_cons(int i) { return 8u * (uint32_t)(i + 1) + 4u; }
 constexpr uint32_t kFXo = 4, kFTicket = 132;
+// mlsppt: strip w's header columns of tile columns < word are in memory (kBig: all), at kFCap + 4w
+constexpr uint32_t kFCap = 160;
 
 extern __shared__ __attribute__((aligned(16))) char krsm[];
 
@@ -126,13 +128,10 @@ __device__ __forceinline__ int qlo(int v) { return (int)(short)v; }
 __device__ __forceinline__ int qhi(int v) { return v >> 16; }
 
 // LDS: profile (2 copies x substsz rows x kr_qrs dwords, copy 1 at kr_copy1), subT[x][y] = s(y, x) - 2g, NS+1
-// hand-off rings, 16 zeros and a 1 KB slot per strip (unused since the halo and the hand-off run
-// under exec masks: kept, because dropping them and the zero row's initial stores changes the
-// register allocation of the strip loop, measured 2 % slower), progress words (slots kr_prog /
-// kr_cons, xo at kFXo, the ticket at kFTicket).
+// hand-off rings, progress words (slots kr_prog / kr_cons, xo at kFXo, the ticket at kFTicket).
 struct KrLds
 {
-    uint32_t q, sub, ring, zfill, sink, flags;
+    uint32_t q, sub, ring, flags;
 };
 
 __host__ __device__ inline KrLds kr_layout(int ns, int lw, int substsz)
@@ -141,9 +140,7 @@ __host__ __device__ inline KrLds kr_layout(int ns, int lw, int substsz)
     L.q = 0;
     L.sub = (kr_copy1(lw, substsz) + (uint32_t)substsz * kr_qrs(lw) + 16u) * 4u;
     L.ring = L.sub + (uint32_t)substsz * kSubRow * 4u;
-    L.zfill = L.ring + (uint32_t)(ns + 1) * kRing * 4u;
-    L.sink = L.zfill + 64u;
-    L.flags = L.sink + (uint32_t)ns * 1024u;
+    L.flags = L.ring + (uint32_t)(ns + 1) * kRing * 4u;
     return L;
 }
 
@@ -276,6 +273,10 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
     // lanes each, and every lane picks the block's step (lane & 15): the selection masks are
     // constants.  nbb = bc/16 of the next boundary, jb its tile column (uniform).
     int nbb = tBx / kBlk, jb = 1;
+    // mlsppt: tile columns [0, ptPend) captured, to be published once their stores are acknowledged
+    // (at the next capture block, or at the strip's end); header stores are then system-scope
+    const bool pt = a.done != nullptr;
+    int ptPend = 0;
 
     // One body for blocks with and without a header-column capture (cap, uniform): separate
     // bodies get different register assignments and ~100 v_mov per block to reconcile them.
@@ -345,6 +346,13 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
         handoff(b);
         if (CAP && cap)
         {
+            if (ptPend)
+            {
+                // the previous boundary's stores, issued blocks ago, are acknowledged: publish them
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                flag_st(L.flags + kFCap + 4u * (uint32_t)w, ptPend);
+                ptPend = 0;
+            }
             // lanes 16m .. 16m+15 (m = b - nbb) hold column bc at step lane & 15: 16 -> 1 by its
             // bits (v_cndmask tree with constant lane masks, 15 per row)
             constexpr uint64_t m1 = 0xAAAAAAAAAAAAAAAAull, m2 = 0xCCCCCCCCCCCCCCCCull;
@@ -365,14 +373,24 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
             const int gb = (rl + kBlk * nbb) * g;  // un-shift: + (row + bc) g
             if ((lane >> 4) == b - nbb)
             {
+                if (pt)
+                {
 #pragma unroll
-                for (int k = 0; k < K; ++k) hcolP[k] = v[k] + gb + k * g;
+                    for (int k = 0; k < K; ++k)
+                        __hip_atomic_store(&hcolP[k], v[k] + gb + k * g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                }
+                else
+                {
+#pragma unroll
+                    for (int k = 0; k < K; ++k) hcolP[k] = v[k] + gb + k * g;
+                }
             }
             if (b == nbb + 3)
             {
                 nbb += tBx / kBlk;
                 ++jb;
                 hcolP += (size_t)(tBy + 1);
+                if (pt && (jb % a.ptChunk == 0 || jb == tcols)) ptPend = jb;
             }
         }
         return true;
@@ -397,6 +415,11 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
         if (!block(b, qA, qB, F(), advance(b))) return;
         if (b + 1 >= NB) break;
         if (!block(b + 1, qB, qA, F(), advance(b + 1))) return;
+    }
+    if (pt)
+    {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        flag_st(L.flags + kFCap + 4u * (uint32_t)w, kBig);
     }
 }
 
@@ -426,6 +449,11 @@ __device__ __forceinline__ void kr_loader(const StripArgs& a, const KrLds& L, in
     int nxm = 0, nx0 = 0, nx1 = 0;  // the batch after (loaded in pass 0)
     int qsub = 0;                   // next pass (8 letters each) of the batch at qn
     int pl = 0, c0 = 0;  // progress words, re-read only when their cached values block
+    // lanes of the next granule poll: the drain stores whole aligned 16-granule lines (gran_stride),
+    // so a poll reads one line more than the last one found complete (2 to 4 lines): a 64-lane poll
+    // on the producer's edge re-read ~3 unfinished lines per line it found (PMC: reads 1.5x the
+    // granule bytes)
+    int pw = 64;
     uint64_t last = __builtin_amdgcn_s_memrealtime();
     unsigned idle = 0;  // idle passes (error-word polls)
     while ((ROLE != 1 && qn <= Cp) || (ROLE != 2 && hnext <= Cp))
@@ -437,7 +465,7 @@ __device__ __forceinline__ void kr_loader(const StripArgs& a, const KrLds& L, in
         if (ROLE != 2 && hnext <= Cp && hnext + 128 > c0 + kRing) c0 = flag_ld(F + kr_cons(0));
         const bool feed = ROLE != 2 && hnext <= Cp && hnext + 128 <= c0 + kRing;
         const int c = hnext + lane;
-        const bool in = c <= Cp;
+        const bool in = c <= Cp && lane < pw;
         unsigned long long q = 0ull;
         if (feed && tk > 0 && in) q = __hip_atomic_load(gprev + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         // (2) profile columns qn .. qn+127 (lane l: qn+2l-1 .. qn+2l+1): the ring slots they take
@@ -511,6 +539,7 @@ __device__ __forceinline__ void kr_loader(const StripArgs& a, const KrLds& L, in
             }
             const uint64_t badm = __ballot(!good);
             const int n = badm ? __builtin_ctzll(badm) : 64;
+            if (tk > 0) pw = max(32, min(64, (n & ~15) + 16));
             if (n > 0)
             {
                 if (lane < n) lds_st(ring0 + 4u * (uint32_t)((c + 64) & (kRing - 1)), v);
@@ -556,9 +585,53 @@ __device__ __forceinline__ void kr_drain(const StripArgs& a, const KrLds& L, int
     constexpr bool kTwoRows = 64 * K * NS == 2 * kSparseTileBy;
     if constexpr (!kTwoRows)
     {
+        // mlsppt (one tile row per ticket): publish to the host the column chunks of this tile row
+        // whose headers are in memory -- header columns captured by every strip (their words in
+        // LDS follow their acknowledged stores) and the header row below written by this wave
+        const bool pt = a.done != nullptr;
+        const int cw = pt ? a.ptChunk : 1;
+        const int nCh = (tcols + cw - 1) / cw;
+        int pub = 0;
+        auto publish = [&](int hrowTiles) {
+            int t = hrowTiles;
+#pragma unroll
+            for (int s = 0; s < NS; ++s)
+            {
+                const int v = flag_ld(F + kFCap + 4u * (uint32_t)s);
+                t = min(t, v == kBig ? tcols : v);
+            }
+            const int n = t >= tcols ? nCh : t / cw;
+            if (n > pub)
+            {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's header-row stores
+                if (lane == 0)
+                    __hip_atomic_store(a.done + tk, ((unsigned long long)a.epoch << 32) | (unsigned)n, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_SYSTEM);
+                pub = n;
+            }
+        };
+        // after the last column: wait for the strips' last captures
+        auto publish_rest = [&]() {
+            uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            unsigned spins = 0;
+            while (pt && pub < nCh)
+            {
+                const int before = pub;
+                publish(tcols);
+                if (pub > before) t0 = __builtin_amdgcn_s_memrealtime();
+                if (pub >= nCh) break;
+                __builtin_amdgcn_s_sleep(1);
+                if (__builtin_amdgcn_s_memrealtime() - t0 > a.spin || ((++spins & 63) == 0 && err_set(a)))
+                {
+                    atomicOr(a.err, 1u);
+                    return;
+                }
+            }
+        };
         if (tk + 1 >= a.nTickets)
         {
             flag_st(F + kr_cons(NS), kBig);  // nobody reads our last row
+            publish_rest();                   // (the last tile row has no header row below)
             return;
         }
         const gptr<unsigned long long> gout = G(a.gran) + (size_t)tk * a.granStride;
@@ -583,11 +656,17 @@ __device__ __forceinline__ void kr_drain(const StripArgs& a, const KrLds& L, int
                     {
                         const int hv = v + (rowEnd + c) * g;
                         const int jT = c / tBx, jj = c - jT * tBx;
-                        if (jT < tcols) G(a.hrow)[(rowbase + jT) * (size_t)(tBx + 1) + jj] = hv;
+                        auto put = [&](int* p) {
+                            if (pt)
+                                __hip_atomic_store(p, hv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                            else
+                                *G(p) = hv;
+                        };
+                        if (jT < tcols) put(a.hrow + (rowbase + jT) * (size_t)(tBx + 1) + jj);
                         if (jj == 0 && jT > 0)
                         {
-                            G(a.hrow)[(rowbase + jT - 1) * (size_t)(tBx + 1) + tBx] = hv;
-                            if (jT < tcols) G(a.hcol)[(rowbase + jT) * (size_t)(tBy + 1)] = hv;
+                            put(a.hrow + (rowbase + jT - 1) * (size_t)(tBx + 1) + tBx);
+                            if (jT < tcols) put(a.hcol + (rowbase + jT) * (size_t)(tBy + 1));
                         }
                     }
                 }
@@ -597,6 +676,8 @@ __device__ __forceinline__ void kr_drain(const StripArgs& a, const KrLds& L, int
             }
             else
             {
+                // idle: chunks whose header rows and columns are complete go to the host
+                if (pt && pub < nCh) publish(dnext > 0 ? min(tcols, (dnext - 1) / tBx) : 0);
                 // the error word is a global load, which waits for this wave's granule stores (vmcnt
                 // retires in order): looked at every 64th idle pass only
                 if (__builtin_amdgcn_s_memrealtime() - last > a.spin || ((++idle & 63) == 0 && err_set(a)))
@@ -607,6 +688,7 @@ __device__ __forceinline__ void kr_drain(const StripArgs& a, const KrLds& L, int
                 __builtin_amdgcn_s_sleep(1);
             }
         }
+        publish_rest();
     }
     else
     {
@@ -733,22 +815,13 @@ __global__ void __launch_bounds__(64 * kr_waves<NS>()) nw_krow_kernel(StripArgs 
         lds_st(L.sub + 4u * k, v);
     }
     if (bad) atomicOr(a.err, 2u);
-    if (threadIdx.x < 16) lds_st(L.zfill + 4u * threadIdx.x, 0);
-    int prevTk = -1;  // ticket this workgroup finished last (mlsppt signalling)
     for (;;)
     {
-        // mlsppt (a.done: one host-mapped flag per ticket = tile row): every wave writes its stores
-        // of the finished ticket back past L2 (system-scope release), then one thread flags the
-        // ticket to the host, which copies that tile row while the fill goes on
-        if (a.done && prevTk >= 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
         __syncthreads();
-        if (a.done && prevTk >= 0 && threadIdx.x == 0)
-            __hip_atomic_store(a.done + prevTk, a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         if (threadIdx.x == 0) lds_st(L.flags + kFTicket, err_set(a) ? a.nTicketsTotal : (int)atomicAdd(a.ticket, 1u));
         __syncthreads();
         const int tkg = __builtin_amdgcn_readfirstlane(lds_ld(L.flags + kFTicket));
         if (tkg >= a.nTicketsTotal) break;
-        prevTk = tkg;
         // pair of this ticket: the batch schedule, or the last descriptor with ticketBase <= tkg
         int lo = 0, tks = -1;
         if (a.sched)
@@ -781,9 +854,10 @@ __global__ void __launch_bounds__(64 * kr_waves<NS>()) nw_krow_kernel(StripArgs 
         pa.trows = d.trows;
         pa.tcols = d.tcols;
         pa.gran = a.gran + d.granOff;
-        pa.granStride = (long long)d.Cp + 1;
+        pa.granStride = gran_stride(d.Cp);
         const int tk = (tks >= 0) ? tks : tkg - d.ticketBase;
         if (threadIdx.x < 32) lds_st(L.flags + 4u * threadIdx.x, 0);  // prog[], cons[], xo
+        if (threadIdx.x >= kFCap / 4 && threadIdx.x < kFCap / 4 + 8) lds_st(L.flags + 4u * threadIdx.x, 0);
         __syncthreads();
         if (w == NS + 1)
             kr_drain<NS, K, LW>(pa, L, tk, lane);

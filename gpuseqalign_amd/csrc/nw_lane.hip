@@ -519,7 +519,7 @@ __global__ void __launch_bounds__(64 * (NS + 2)) nw_lane_kernel(StripArgs a)
         pa.score = d.score;
         pa.ld = d.ld;
         pa.gran = a.gran + d.granOff;
-        pa.granStride = (long long)d.C + 1;
+        pa.granStride = gran_stride(d.C);
         const int tk = (tks >= 0) ? tks : tkg - d.ticketBase;
         if (threadIdx.x < 32) lds_st(L.flags + 4u * threadIdx.x, 0);  // prog[], cons[]
         if (threadIdx.x < 16) lds_st(L.gfill + 4u * threadIdx.x, a.g);

@@ -34,6 +34,10 @@ struct PairDesc
     long long granOff;  // first granule of this pair in the hand-off buffer
 };
 
+// Granules per super-strip boundary of a pair whose last computed column is Cp: Cp + 1 rounded up
+// to 16, so every 16-column chunk a drain stores with one instruction is one aligned 128-B line
+__host__ __device__ inline long long gran_stride(int Cp) { return ((long long)Cp + 16) & ~15ll; }
+
 struct StripArgs
 {
     const int* seqY;  // adjrows ints, element 0 = header (unused)
@@ -60,9 +64,11 @@ struct StripArgs
     unsigned* err;      // sticky: set by a spin that gave up, cleared by gsa_sync after reading
     unsigned long long spin;  // watchdog: s_memrealtime ticks (100 MHz) a wait may go without progress
     unsigned epoch;
-    // mlsppt: host-mapped per-ticket flags, set to `epoch` once a super-strip's outputs are
-    // written back past L2 (null: no signalling)
-    unsigned* done;
+    // mlsppt (K-rows kernel, one tile row per ticket): host-mapped word per ticket, set to
+    // (epoch << 32 | n) once the headers of that tile row's first n column chunks (ptChunk tile
+    // columns each) are in memory (system-scope stores, acknowledged); null: no signalling
+    unsigned long long* done;
+    int ptChunk;
     // kModeScoreAG: gap open / extend, the F' hand-off granules (same layout as gran), result H[R][C]
     int go, ge;
     unsigned long long* gran2;

@@ -36,8 +36,8 @@
 //  * SPARSE : tileHrowMat / tileHcolMat exactly as gpu7/8/9 leave them, for tile height
 //             tBy = 256*NS and a tile width tBx (multiple of 16, >= 64); padded cells use
 //             letter 0 as the reference does (nwalign_gpu9_mlsp_diagdiagdiag.cu:469-478).
-//             mlsppt uses this mode (per-ticket done flags); single pairs and batches run on the
-//             K-rows kernel (nw_krow.hip).
+//             Single pairs, batches and mlsppt run on the K-rows kernel (nw_krow.hip);
+//             this mode is reached with GSA_SPARSE_KERNEL=strip.
 //  * SCORE  : score-only NW / SW with affine gaps (kModeScoreAG / kModeScoreSW, below).
 // Full matrices run on the one-row-per-lane kernel (nw_lane.hip).  This kernel's full-matrix
 // modes (LDS staging + store waves; L2 output rings drained by copy workgroups) were measured
@@ -759,20 +759,13 @@ __global__ void __launch_bounds__(64 * (NS + 1)) nw_strip_kernel(StripArgs a)
     const int lane = threadIdx.x & 63;
     const Lds L = lds_layout<NS, MODE>(a.substsz);
     const uint32_t F = L.flags;
-    int prevTk = -1;  // global ticket this workgroup finished last (mlsppt signalling)
     for (;;)
     {
-        // mlsppt: every wave writes its stores of the finished ticket back past L2 (system-scope
-        // release), then one thread flags the ticket to the host, which copies it meanwhile
-        if (a.done && prevTk >= 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
         __syncthreads();
-        if (a.done && prevTk >= 0 && threadIdx.x == 0)
-            __hip_atomic_store(a.done + prevTk, a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         if (threadIdx.x == 0) lds_st(F + kFTicket, (err_set(a) ? a.nTicketsTotal : (int)atomicAdd(a.ticket, 1u)));
         __syncthreads();
         const int tkg = __builtin_amdgcn_readfirstlane(lds_ld(F + kFTicket));
         if (tkg >= a.nTicketsTotal) break;
-        prevTk = tkg;
         // pair of this ticket: the batch schedule, or the last descriptor with ticketBase <= tkg
         // (binary search, uniform)
         int lo = 0, tks = -1;
@@ -807,7 +800,7 @@ __global__ void __launch_bounds__(64 * (NS + 1)) nw_strip_kernel(StripArgs a)
         pa.tcols = d.tcols;
         pa.gran = a.gran + d.granOff;
         pa.gran2 = a.gran2 + d.granOff;
-        pa.granStride = (long long)d.Cp + 1;
+        pa.granStride = gran_stride(d.Cp);
         const int tk = (tks >= 0) ? tks : tkg - d.ticketBase;
         // per-super-strip state: letter ring = NEG, ring 0 = row 0 (H' = 0), progress words
         for (int k = threadIdx.x; k < kXCopy; k += 64 * kWaves<NS>) lds_st(L.xo + 4 * k, pa.substsz * 512);

@@ -1,6 +1,8 @@
 """mlsppt -- sparse fill with the header copy-back overlapped with the fill (gsa_align_sparse_pt;
-named in the reference's README.md:39, never implemented there): every word
-of both header matrices, the geometry and align_cost equal the plain mlsp path's."""
+named in the reference's README.md:39, never implemented there): the kernel
+publishes column chunks of the headers (every tile row's header rows and columns of ~4096 columns)
+as they become final, and the host copies each while the fill runs.  Every word of both header
+matrices and align_cost equal the oracle's (tests below) and the plain mlsp path's."""
 import numpy as np
 import pytest
 
@@ -21,11 +23,28 @@ def test_overlap_equals_plain(engine, golden, R, C, tBx):
         assert (a.geom.tileHdrMatRows, a.geom.tileHdrMatCols) == (b.geom.tileHdrMatRows, b.geom.tileHdrMatCols)
 
 
+@pytest.mark.parametrize("R,C,tBx", [(1, 1, 64), (700, 900, 64), (3000, 20000, 64), (5000, 3000, 256),
+                                     (9000, 33000, 512), (2100, 70000, 4096)])
+def test_overlap_equals_oracle(engine, golden, R, C, tBx):
+    """Every header word against the oracle's streaming extractor, on shapes of one to many
+    column chunks (the last chunk partial) and one to several tile rows, run twice (the words
+    of the previous launch carry an older epoch and must not count)."""
+    import oracle
+    import gpuseqalign_amd as gsa
+    Y, X = random_pair(R, C, 3 * R + C)
+    hr, hc, tr, tc, cost = oracle.sparse_headers(Y, X, golden.blosum62, -11, gsa.sparse_tile_by(), tBx)
+    for _ in range(2):
+        b = engine.align_sparse(Y, X, golden.blosum62, -11, tileBx=tBx, overlap=True)
+        assert (b.geom.tileHdrMatRows, b.geom.tileHdrMatCols) == (tr, tc)
+        assert np.array_equal(b.hrow, hr) and np.array_equal(b.hcol, hc)
+        assert b.align_cost == cost
+
+
 @pytest.mark.parametrize("kern,ns,k", [("krow", 2, 2), ("krow", 8, 4), ("strip", 4, 4)])
 def test_overlap_other_geometries(engine, golden, monkeypatch, kern, ns, k):
-    """mlsppt flags one ticket per tile row: a K-rows geometry whose ticket is not one tile row
-    (GSA_KROW_NS / GSA_KROW_K) falls back to the single-pair default, and the strip kernel
-    (GSA_SPARSE_KERNEL=strip) flags its own tickets; every word equals the plain path's."""
+    """mlsppt publishes one word per tile row from the K-rows kernel: a geometry whose ticket is
+    not one tile row (GSA_KROW_NS / GSA_KROW_K), or GSA_SPARSE_KERNEL=strip, falls back to the
+    single-pair default geometry; every word equals the plain path's."""
     import oracle
     Y, X = random_pair(3100, 2200, 41)
     a = engine.align_sparse(Y, X, golden.blosum62, -11, tileBx=128)
