@@ -81,7 +81,7 @@ def sparse_kernel_name():
     ok = (k in ("2", "4") and ns in ("2", "4")) or (k == "4" and ns == "8")
     ns, k = (int(ns), int(k)) if ok else (4, 4)
     lw = 512 if ns == 2 else 1024
-    return f"gsa::nw_krow_kernel<{ns},{k},{lw}> (sparse, K = {k} rows per lane)"
+    return f"gsa::nw_krow_kernel<{ns},{k},{lw},false> (sparse, K = {k} rows per lane)"
 
 
 def cpu_topology():
@@ -305,7 +305,7 @@ def main():
     ap.add_argument("--no-10k", action="store_true", help="skip the configs[1] full-matrix field")
     ap.add_argument("--full-batch-pairs", type=int, default=64, help="0 = skip the full-matrix batch field")
     ap.add_argument("--no-config5", action="store_true", help="skip the configs[4] score-only field")
-    ap.add_argument("--config5-cpu-sample", type=int, default=16000, help="n x n prefix for the config-5 CPU leg")
+    ap.add_argument("--config5-cpu-sample", type=int, default=50000, help="n x n prefix for the config-5 CPU leg")
     a = ap.parse_args()
 
     import torch

@@ -147,7 +147,8 @@ __host__ __device__ inline KrLds kr_layout(int ns, int lw, int substsz)
 // ------------------------------------------------------------------------------------
 // strip wave: 64K rows, K per lane
 // ------------------------------------------------------------------------------------
-template <int NS, int K, int LW>
+// PT: mlsppt (a.done set; a kernel instance of its own, so the plain fill's strip loop is unchanged)
+template <int NS, int K, int LW, bool PT>
 __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int tk, int w, int lane)
 {
     const int g = a.g;
@@ -275,7 +276,7 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
     int nbb = tBx / kBlk, jb = 1;
     // mlsppt: tile columns [0, ptPend) captured, to be published once their stores are acknowledged
     // (at the next capture block, or at the strip's end); header stores are then system-scope
-    const bool pt = a.done != nullptr;
+    constexpr bool pt = PT;
     int ptPend = 0;
 
     // One body for blocks with and without a header-column capture (cap, uniform): separate
@@ -346,7 +347,7 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
         handoff(b);
         if (CAP && cap)
         {
-            if (ptPend)
+            if (pt && ptPend)
             {
                 // the previous boundary's stores, issued blocks ago, are acknowledged: publish them
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -577,7 +578,7 @@ __device__ __forceinline__ void kr_loader(const StripArgs& a, const KrLds& L, in
 // element e once it has published e - kRing + 16): it stays within a few columns of the strips, and
 // a lag of kRing - 96 elements would end the launch with the error word rather than a wrong header.
 // ------------------------------------------------------------------------------------
-template <int NS, int K, int LW>
+template <int NS, int K, int LW, bool PT>
 __device__ __forceinline__ void kr_drain(const StripArgs& a, const KrLds& L, int tk, int lane)
 {
     const int Cp = a.Cp, g = a.g, tBx = a.tBx, tBy = a.tBy, tcols = a.tcols;
@@ -588,7 +589,7 @@ __device__ __forceinline__ void kr_drain(const StripArgs& a, const KrLds& L, int
         // mlsppt (one tile row per ticket): publish to the host the column chunks of this tile row
         // whose headers are in memory -- header columns captured by every strip (their words in
         // LDS follow their acknowledged stores) and the header row below written by this wave
-        const bool pt = a.done != nullptr;
+        constexpr bool pt = PT;
         const int cw = pt ? a.ptChunk : 1;
         const int nCh = (tcols + cw - 1) / cw;
         int pub = 0;
@@ -800,7 +801,7 @@ constexpr bool kr_split() { return NS <= 4; }
 template <int NS>
 constexpr int kr_waves() { return NS + 2 + (kr_split<NS>() ? 1 : 0); }
 
-template <int NS, int K, int LW>
+template <int NS, int K, int LW, bool PT>
 __global__ void __launch_bounds__(64 * kr_waves<NS>()) nw_krow_kernel(StripArgs a)
 {
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -860,7 +861,7 @@ __global__ void __launch_bounds__(64 * kr_waves<NS>()) nw_krow_kernel(StripArgs 
         if (threadIdx.x >= kFCap / 4 && threadIdx.x < kFCap / 4 + 8) lds_st(L.flags + 4u * threadIdx.x, 0);
         __syncthreads();
         if (w == NS + 1)
-            kr_drain<NS, K, LW>(pa, L, tk, lane);
+            kr_drain<NS, K, LW, PT>(pa, L, tk, lane);
         else if (w == NS)
             kr_loader<NS, K, LW, kr_split<NS>() ? 1 : 0>(pa, L, tk, lane);
         else if (kr_split<NS>() && w == NS + 2)
@@ -868,17 +869,17 @@ __global__ void __launch_bounds__(64 * kr_waves<NS>()) nw_krow_kernel(StripArgs 
         else
         {
             __builtin_amdgcn_s_setprio(3);
-            kr_strip<NS, K, LW>(pa, L, tk, w, lane);
+            kr_strip<NS, K, LW, PT>(pa, L, tk, w, lane);
             __builtin_amdgcn_s_setprio(0);
         }
     }
 }
 
-template <int NS, int K, int LW>
+template <int NS, int K, int LW, bool PT = false>
 hipError_t launch_kr(const StripArgs& a, int grid, hipStream_t stream)
 {
     const size_t lds = krow_lds_bytes(NS, LW, a.substsz);
-    auto kern = nw_krow_kernel<NS, K, LW>;
+    auto kern = nw_krow_kernel<NS, K, LW, PT>;
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     if (grid <= 0)
@@ -905,6 +906,7 @@ hipError_t launch_krow_fill(const StripArgs& a, int ns, int k, int lw, int grid,
     (void)lw;  // 512 for (4, 4) measured slower for one pair and for batches (the first strip
                // is throttled by the window): 1024
     if (ns == 8) return launch_kr<8, 4, 1024>(a, grid, stream);
+    if (a.done) return launch_kr<4, 4, 1024, true>(a, grid, stream);  // mlsppt: (4, 4) only (enqueue_batch)
     return ns == 2 ? launch_kr<2, 4, 512>(a, grid, stream) : launch_kr<4, 4, 1024>(a, grid, stream);
 }
 
