@@ -71,8 +71,14 @@ struct gsa_ctx
     // score-only fills (nw_scan.hip): boundary rows H/F, progress words, control words
     int* sbnd = nullptr;
     size_t sbnd_cap = 0;  // ints
-    // mlsppt: host-mapped per-tile-row words (epoch << 32 | column chunks in memory)
+    // mlsppt: host-mapped per-tile-row words (epoch << 32 | column chunks in memory); a pinned
+    // host buffer the strided column chunks are packed into by a kernel on ptstream
     unsigned long long* ptflags = nullptr;
+    void* ptpin = nullptr;  // pinned, device-mapped, ptpin_cap bytes (>= kPtPin)
+    size_t ptpin_cap = 0;
+    hipEvent_t ptev[2] = {nullptr, nullptr};
+    static constexpr size_t kPtPin = 64u << 20;  // two slots
+    hipStream_t ptstream = nullptr;
     size_t ptflags_cap = 0;
     // score-only control words: row scan [0] ticket|err, [1] best key, [2] result; AG/SW strip
     // [0] result, [1] best key, [3] its own error word (the fills' sticky word is not touched)
@@ -538,12 +544,15 @@ int gsa_ctx_create(int device, gsa_ctx** out)
     hipError_t e = hipSetDevice(device);
     if (e == hipSuccess) e = hipDeviceGetAttribute(&ctx->cu_count, hipDeviceAttributeMultiprocessorCount, device);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
+    // mlsppt's copy-back stream, created next so that it gets a hardware queue of its own
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->ptstream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipMalloc(&ctx->ctl, 256);
     if (e == hipSuccess) e = hipMemset(ctx->ctl, 0, 256);
     if (e == hipSuccess) e = hipEventCreate(&ctx->ev0);
     if (e == hipSuccess) e = hipEventCreate(&ctx->ev1);
     for (int k = 0; k < gsa_ctx::kStage && e == hipSuccess; ++k)
         e = hipEventCreateWithFlags(&ctx->stage_ev[k], hipEventDisableTiming);
+    for (int k = 0; k < 2 && e == hipSuccess; ++k) e = hipEventCreateWithFlags(&ctx->ptev[k], hipEventDisableTiming);
     if (e != hipSuccess)
     {
         int code = (int)e;
@@ -573,6 +582,10 @@ void gsa_ctx_destroy(gsa_ctx* ctx)
     if (ctx->sbnd) (void)hipFree(ctx->sbnd);
     if (ctx->sctl) (void)hipFree(ctx->sctl);
     if (ctx->ptflags) (void)hipHostFree(ctx->ptflags);
+    if (ctx->ptpin) (void)hipHostFree(ctx->ptpin);
+    for (hipEvent_t ev : ctx->ptev)
+        if (ev) (void)hipEventDestroy(ev);
+    if (ctx->ptstream) (void)hipStreamDestroy(ctx->ptstream);
     for (int k = 0; k < gsa_ctx::kStage; ++k)
     {
         if (ctx->stage[k]) (void)hipHostFree(ctx->stage[k]);
@@ -764,8 +777,10 @@ hipError_t copy_d2h(gsa_ctx* ctx, void* dst, const void* src, size_t bytes)
 
 // Device -> pageable host copy of `height` rows of `width` bytes, source rows `spitch` apart,
 // destination rows `dpitch` apart (a column chunk of a tile-major header matrix): the rows are split
-// over the copy threads, each moving groups of rows by one 2-D DMA into a pinned chunk and copying
-// them into place while the next group's DMA runs.  width <= kCopyChunk.
+// over the copy threads, each moving groups of rows by one DMA into a pinned chunk and copying them
+// into place while the next group's DMA runs.  width <= kCopyChunk.  A packed source (spitch ==
+// width) moves by plain copies: the runtime splits a strided device-to-host copy into one DMA per
+// row (~4 us each, measured: 25 column chunks of 98 tile rows took 20 ms).
 hipError_t copy_d2h_2d(gsa_ctx* ctx, char* dst, size_t dpitch, const char* src, size_t spitch, size_t width,
                        size_t height)
 {
@@ -794,8 +809,11 @@ hipError_t copy_d2h_2d(gsa_ctx* ctx, char* dst, size_t dpitch, const char* src, 
         const size_t n = (hi - lo + perGroup - 1) / perGroup;
         auto issue = [&](size_t i) {
             const size_t r0 = lo + i * perGroup, rows = std::min(perGroup, hi - r0);
-            hipError_t q = hipMemcpy2DAsync(ctx->xstage[k][i & 1], width, src + r0 * spitch, spitch, width, rows,
-                                            hipMemcpyDeviceToHost, ctx->xstream[k]);
+            hipError_t q = spitch == width
+                               ? hipMemcpyAsync(ctx->xstage[k][i & 1], src + r0 * spitch, rows * width,
+                                                hipMemcpyDeviceToHost, ctx->xstream[k])
+                               : hipMemcpy2DAsync(ctx->xstage[k][i & 1], width, src + r0 * spitch, spitch, width, rows,
+                                                  hipMemcpyDeviceToHost, ctx->xstream[k]);
             return q == hipSuccess ? hipEventRecord(ctx->xev[k][i & 1], ctx->xstream[k]) : q;
         };
         if (r == hipSuccess && n > 0) r = issue(0);
@@ -1333,6 +1351,19 @@ int gsa_align_sparse_pt(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, cons
     const int tcols = geom.tileHdrMatCols;
     const int cw = std::max(1, std::min(tcols, (4096 + tileBx - 1) / tileBx));
     const int nCh = (tcols + cw - 1) / cw;
+    {
+        // room for a batch of at least one chunk
+        const size_t need = std::max(gsa_ctx::kPtPin, 2 * trows * (size_t)cw * (geom.tileHrowLen + geom.tileHcolLen) * 4);
+        if (ctx->ptpin_cap < need)
+        {
+            if (ctx->ptpin) (void)hipHostFree(ctx->ptpin);
+            ctx->ptpin = nullptr;
+            ctx->ptpin_cap = 0;
+            if ((e = hipHostMalloc(&ctx->ptpin, need, hipHostMallocDefault)) != hipSuccess)
+                return fail(ctx, e, GSA_ERROR_MEMORY_ALLOCATION);
+            ctx->ptpin_cap = need;
+        }
+    }
     (void)hipEventRecord(ctx->ev0, ctx->stream);
     s = enqueue_fill(ctx, gsa::kModeSparse, (const int32_t*)ctx->dbuf[0], adjrows, (const int32_t*)ctx->dbuf[1],
                      adjcols, (const int32_t*)ctx->dbuf[2], substsz, gapo, nullptr, tileBx, dhr, dhc, ctx->stream,
@@ -1341,15 +1372,120 @@ int gsa_align_sparse_pt(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, cons
     (void)hipEventRecord(ctx->ev1, ctx->stream);
     const unsigned long long epoch = ctx->epoch;
     const size_t rowW = (size_t)geom.tileHrowLen * 4, rowH = (size_t)geom.tileHcolLen * 4;  // bytes per tile
+    // The caller's result buffers are usually fresh pages: fault them in (the kernel zero-fills each
+    // page on first touch) on the copy threads while the fill runs, before the first chunk arrives,
+    // instead of inside the first chunk's scatter (measured: 2-4.6 ms for an 8 MB chunk at 100k)
+    std::vector<std::thread> prefault;
+    {
+        constexpr int T = gsa_ctx::kCopyThreads;
+        const size_t nb[2] = {(size_t)geom.hrowElems * 4, (size_t)geom.hcolElems * 4};
+        char* base[2] = {(char*)hrow_out, (char*)hcol_out};
+        for (int k = 0; k < T; ++k)
+            prefault.emplace_back([=]() {
+                for (int m = 0; m < 2; ++m)
+                {
+                    const size_t lo = nb[m] * k / T, hi = nb[m] * (k + 1) / T;
+                    for (size_t o = lo & ~(size_t)4095; o < hi; o += 4096)
+                        if (o >= lo) ((volatile char*)base[m])[o] = 0;
+                }
+            });
+    }
+    auto join_prefault = [&]() {
+        for (auto& x : prefault) x.join();
+        prefault.clear();
+    };
+    struct JoinAtExit  // every return path joins the prefault threads
+    {
+        std::vector<std::thread>& v;
+        ~JoinAtExit()
+        {
+            for (auto& x : v)
+                if (x.joinable()) x.join();
+        }
+    } joinAtExit {prefault};
     int copied = 0;  // chunks copied back
-    auto copy_chunks = [&](int upTo) -> hipError_t {
-        const size_t j0 = (size_t)copied * cw, j1 = std::min((size_t)tcols, (size_t)upTo * cw);
-        hipError_t err = copy_d2h_2d(ctx, (char*)hrow_out + j0 * rowW, tcols * rowW, (const char*)dhr + j0 * rowW,
-                                     tcols * rowW, (j1 - j0) * rowW, trows);
+    const bool ptdbg = std::getenv("GSA_PT_DEBUG") != nullptr;  // diagnostics: when chunks become ready
+    auto t0dbg = Clock::now();
+    // Two pinned slots: the strided DMA of one batch of chunks (ptstream) runs while the copy
+    // threads scatter the previous batch into the tile-major host matrices.
+    const size_t chunkBytes = trows * (size_t)cw * (rowW + rowH);
+    const size_t slotBytes = ctx->ptpin_cap / 2;
+    const int perBatch = (int)std::max<size_t>(1, slotBytes / chunkBytes);
+    struct Batch
+    {
+        int c0, c1, slot;
+    };
+    Batch inflight[2];
+    int nInflight = 0, issued = 0, nextSlot = 0;
+    auto dbg = [&](const char* what, int c0, int c1) {
+        if (ptdbg)
+            std::fprintf(stderr, "mlsppt %.3f ms: %s %d..%d (fill %s)\n",
+                         std::chrono::duration<float, std::milli>(Clock::now() - t0dbg).count(), what, c0, c1,
+                         hipStreamQuery(ctx->stream) == hipSuccess ? "done" : "running");
+    };
+    auto batch_geom = [&](const Batch& bt, size_t& j0, size_t& wr, size_t& wc, char*& hh, char*& hc) {
+        j0 = (size_t)bt.c0 * cw;
+        const size_t j1 = std::min((size_t)tcols, (size_t)bt.c1 * cw);
+        wr = (j1 - j0) * rowW;  // bytes per tile row
+        wc = (j1 - j0) * rowH;
+        hh = (char*)ctx->ptpin + (size_t)bt.slot * slotBytes;
+        hc = hh + trows * wr;
+    };
+    // the DMA engine reads HBM (the fill's header stores are system-scope and acknowledged before
+    // their chunk is published); ptstream is the context's second stream, created right after the
+    // fill's, so it has a hardware queue of its own and its copies run beside the fill (copies on
+    // streams that share the fill's queue wait for it: measured)
+    auto issue = [&](int upTo) -> hipError_t {
+        Batch bt {issued, std::min(upTo, issued + perBatch), nextSlot};
+        size_t j0, wr, wc;
+        char *hh, *hc;
+        batch_geom(bt, j0, wr, wc, hh, hc);
+        hipError_t err = hipMemcpy2DAsync(hh, wr, (const char*)dhr + j0 * rowW, tcols * rowW, wr, trows,
+                                          hipMemcpyDeviceToHost, ctx->ptstream);
         if (err == hipSuccess)
-            err = copy_d2h_2d(ctx, (char*)hcol_out + j0 * rowH, tcols * rowH, (const char*)dhc + j0 * rowH,
-                              tcols * rowH, (j1 - j0) * rowH, trows);
-        copied = upTo;
+            err = hipMemcpy2DAsync(hc, wc, (const char*)dhc + j0 * rowH, tcols * rowH, wc, trows, hipMemcpyDeviceToHost,
+                                   ctx->ptstream);
+        if (err == hipSuccess) err = hipEventRecord(ctx->ptev[bt.slot], ctx->ptstream);
+        if (err != hipSuccess) return err;
+        inflight[nInflight++] = bt;
+        issued = bt.c1;
+        nextSlot ^= 1;
+        dbg("dma issued", bt.c0, bt.c1);
+        return hipSuccess;
+    };
+    // scatter the oldest batch once its DMA is done (wait: block until it is)
+    auto scatter = [&](bool wait) -> hipError_t {
+        const Batch bt = inflight[0];
+        hipError_t err = wait ? hipEventSynchronize(ctx->ptev[bt.slot]) : hipEventQuery(ctx->ptev[bt.slot]);
+        if (err == hipErrorNotReady) return hipSuccess;
+        if (err != hipSuccess) return err;
+        join_prefault();
+        size_t j0, wr, wc;
+        char *hh, *hc;
+        batch_geom(bt, j0, wr, wc, hh, hc);
+        constexpr int T = gsa_ctx::kCopyThreads;
+        auto work = [&](int k) {
+            for (size_t r = (size_t)k; r < trows; r += T)
+            {
+                std::memcpy((char*)hrow_out + r * tcols * rowW + j0 * rowW, hh + r * wr, wr);
+                std::memcpy((char*)hcol_out + r * tcols * rowH + j0 * rowH, hc + r * wc, wc);
+            }
+        };
+        std::vector<std::thread> th;
+        for (int k = 1; k < T; ++k) th.emplace_back(work, k);
+        work(0);
+        for (auto& x : th) x.join();
+        copied = bt.c1;
+        inflight[0] = inflight[1];
+        --nInflight;
+        dbg("scattered", bt.c0, bt.c1);
+        return hipSuccess;
+    };
+    // one pipeline step: issue a DMA for ready chunks if a slot is free, scatter a finished batch
+    auto pump = [&](int ready, bool wait) -> hipError_t {
+        hipError_t err = hipSuccess;
+        if (ready > issued && nInflight < 2) err = issue(ready);
+        if (err == hipSuccess && nInflight > 0) err = scatter(wait || nInflight == 2);
         return err;
     };
     for (;;)
@@ -1358,14 +1494,14 @@ int gsa_align_sparse_pt(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, cons
         if (q != hipSuccess && q != hipErrorNotReady) return fail(ctx, q, GSA_ERROR_KERNEL_FAILURE);
         if (q == hipSuccess) break;
         int ready = nCh;
-        for (size_t r = 0; r < trows && ready > copied; ++r)
+        for (size_t r = 0; r < trows && ready > issued; ++r)
         {
             const unsigned long long v = __atomic_load_n(ctx->ptflags + r, __ATOMIC_ACQUIRE);
             ready = std::min(ready, (v >> 32) == epoch ? (int)(v & 0xffffffffu) : 0);
         }
-        if (ready > copied)
+        if (ready > issued || nInflight > 0)
         {
-            if ((e = copy_chunks(ready)) != hipSuccess) return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
+            if ((e = pump(ready, false)) != hipSuccess) return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
         }
         else
             std::this_thread::sleep_for(std::chrono::microseconds(20));
@@ -1374,7 +1510,8 @@ int gsa_align_sparse_pt(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, cons
     L.calc = ms_since(t);
     lap(ctx, "align.calc");
     (void)hipEventElapsedTime(&L.calc_kernel_ms, ctx->ev0, ctx->ev1);
-    if (copied < nCh && (e = copy_chunks(nCh)) != hipSuccess) return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
+    while (copied < nCh)
+        if ((e = pump(nCh, true)) != hipSuccess) return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
     L.cpy_host = ms_since(t);
     lap(ctx, "align.cpy_host");
     int32_t cost = gsa_sparse_align_cost(hrow_out, hcol_out, &geom, seqY, adjrows, seqX, adjcols, subst, substsz, gapo);

@@ -269,6 +269,7 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
         flag_st2(f_out, bb + 1 == NB ? kBig : kBlk * bb + kBlk, kBlk * bb + 64 + kBlk);
     };
     int rpin = 0, rpco = 0, rpxo = 0;  // progress words read in mid-block, checked at the next block
+    int rsink = 0;                     // the read's 4th dword (unused)
     // Tile boundaries bc = jb*tBx are multiples of 16 columns, and lane l meets column bc at step
     // bc + l: in block bc/16 + l/16, at step l & 15.  So the 4 blocks from bc/16 on capture it, 16
     // lanes each, and every lane picks the block's step (lane & 15): the selection masks are
@@ -287,6 +288,11 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
         {
             const int pin = __builtin_amdgcn_readfirstlane(rpin), pco = __builtin_amdgcn_readfirstlane(rpco);
             const int pxo = (w == 0) ? __builtin_amdgcn_readfirstlane(rpxo) : 0;
+            // every destination register of the progress read stays allocated until here: a dead
+            // one reused by the block's last steps is a write-after-write on an LDS load, which
+            // the compiler resolves with lgkmcnt(1) there -- a wait for the whole LDS queue (the
+            // profile reads and the hand-off writes) on the critical path of every block
+            asm volatile("" ::"v"(rpin), "v"(rpco), "v"(rpxo), "v"(rsink));
             if (!ok(pin, pco, pxo, b) && !spin(b)) return false;
         }
         halo_load(b);
@@ -339,6 +345,7 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
                 rpin = lo.x;
                 rpxo = lo.y;
                 rpco = hi.y;
+                rsink = hi.x;
             }
         }
         // the block's hand-off at its end (the next strip sees it a block earlier than when it is
@@ -593,6 +600,8 @@ __device__ __forceinline__ void kr_drain(const StripArgs& a, const KrLds& L, int
         const int cw = pt ? a.ptChunk : 1;
         const int nCh = (tcols + cw - 1) / cw;
         int pub = 0;
+        // hrowTiles: tile columns whose header-row stores are complete -- after s_waitcnt vmcnt(0),
+        // or vmcnt(60) for stores issued before the wave's last 60 vector-memory instructions
         auto publish = [&](int hrowTiles) {
             int t = hrowTiles;
 #pragma unroll
@@ -604,7 +613,6 @@ __device__ __forceinline__ void kr_drain(const StripArgs& a, const KrLds& L, int
             const int n = t >= tcols ? nCh : t / cw;
             if (n > pub)
             {
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's header-row stores
                 if (lane == 0)
                     __hip_atomic_store(a.done + tk, ((unsigned long long)a.epoch << 32) | (unsigned)n, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_SYSTEM);
@@ -615,6 +623,7 @@ __device__ __forceinline__ void kr_drain(const StripArgs& a, const KrLds& L, int
         auto publish_rest = [&]() {
             uint64_t t0 = __builtin_amdgcn_s_memrealtime();
             unsigned spins = 0;
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's header-row stores
             while (pt && pub < nCh)
             {
                 const int before = pub;
@@ -640,6 +649,10 @@ __device__ __forceinline__ void kr_drain(const StripArgs& a, const KrLds& L, int
         const bool hdr = rowEnd % tBy == 0;
         const size_t rowbase = (size_t)(rowEnd / tBy) * (size_t)tcols;  // tile index of (iT+1, 0)
         int dnext = 0;  // next column to drain
+        // mlsppt: publication lags the header-row stores by >= 64 loop passes (each issues >= 1
+        // vector-memory instruction, the granule store), so vmcnt(60) finds them complete without
+        // waiting on the fresh granule stores the next super-strip is polling for
+        int passes = 0, markPass = 0, markTiles = 0;
         uint64_t last = __builtin_amdgcn_s_memrealtime();
         unsigned idle = 0;  // idle passes (error-word polls)
         while (dnext <= Cp)
@@ -674,11 +687,16 @@ __device__ __forceinline__ void kr_drain(const StripArgs& a, const KrLds& L, int
                 dnext = min(dnext + 64, avail);
                 flag_st(F + kr_cons(NS), dnext > Cp ? kBig : dnext + 64);
                 last = __builtin_amdgcn_s_memrealtime();
+                if (pt && ++passes - markPass >= 64)
+                {
+                    asm volatile("s_waitcnt vmcnt(60)" ::: "memory");
+                    publish(markTiles);
+                    markPass = passes;
+                    markTiles = min(tcols, (dnext - 1) / tBx);
+                }
             }
             else
             {
-                // idle: chunks whose header rows and columns are complete go to the host
-                if (pt && pub < nCh) publish(dnext > 0 ? min(tcols, (dnext - 1) / tBx) : 0);
                 // the error word is a global load, which waits for this wave's granule stores (vmcnt
                 // retires in order): looked at every 64th idle pass only
                 if (__builtin_amdgcn_s_memrealtime() - last > a.spin || ((++idle & 63) == 0 && err_set(a)))
