@@ -177,6 +177,10 @@ template <int NS, int MODE>
 __device__ __forceinline__ void strip_wave(const StripArgs& a, const Lds& L, int tk, int w, int lane)
 {
     constexpr int TR = kWaveRows * NS;  // rows per super-strip
+    // the lane index made opaque per ticket: otherwise the compiler hoists this wave's per-lane
+    // LDS addresses out of the ticket loop into the kernel prologue, where the score modes'
+    // register budget (256) cannot hold them all and 3 of them went to scratch
+    asm volatile("" : "+v"(lane));
     const int g = a.g;
     const int Cp = a.Cp;
     const int r0 = tk * TR + kWaveRows * w + 1;  // first row of the strip

@@ -186,3 +186,25 @@ def test_lane_kernel_wide_pair(engine, golden, ns, monkeypatch):
     r = engine.align_full(Y, X, golden.blosum62, -11)
     S, cost = oracle.fill_full(Y, X, golden.blosum62, -11)
     assert np.array_equal(r.score, S) and r.align_cost == cost
+
+
+
+@pytest.mark.parametrize("R,C,off", [(1, 1, 0), (2, 3, 1), (63, 64, 3), (64, 65, 0), (129, 1029, 7), (300, 1, 5),
+                                     (385, 1500, 13), (1100, 2222, 1), (2049, 777, 15), (700, 4099, 9)])
+def test_full_fill_at_unaligned_base(engine, golden, R, C, off):
+    """The full fill into a device buffer that starts 0..15 ints past a 64-byte boundary: every
+    matrix word equals the oracle and the words around the matrix stay untouched (the transposed
+    stores address rows by a scalar base plus lane offsets; edge blocks store per element)."""
+    import torch
+    Y, X = random_pair(R, C, 7 * R + C + off)
+    dev = torch.device("cuda:0")
+    y, x = torch.from_numpy(Y).to(dev), torch.from_numpy(X).to(dev)
+    s = torch.from_numpy(golden.blosum62).to(dev)
+    n = len(Y) * len(X)
+    buf = torch.full((n + 16 + off,), -7, dtype=torch.int32, device=dev)
+    engine.fill_full_dev(y.data_ptr(), len(Y), x.data_ptr(), len(X), s.data_ptr(), 25, -11, buf.data_ptr() + 4 * off)
+    engine.sync()
+    out = buf.cpu().numpy()
+    S, _ = oracle.fill_full(Y, X, golden.blosum62, -11)
+    assert (out[:off] == -7).all() and (out[off + n:] == -7).all()
+    assert np.array_equal(out[off:off + n].reshape(len(Y), len(X)), S)

@@ -27,7 +27,7 @@ for n in [int(x) for x in (sys.argv[1:] or ["50000"])]:
         kms = float(np.median(ks[1:]))
         line = {"config": name, "R": n, "C": n, "gapo": go, "gape": ge, "score": r["score"],
                 "end": [r["i_end"], r["j_end"]], "kernel_ms": round(kms, 3), "gcups": round(n * n / kms / 1e6, 1)}
-        if n <= 50000 and name in ("SW-LG", "NW-AG"):
+        if n <= 50000 and name in ("SW-LG", "NW-AG") and not os.environ.get("NO_CPU"):
             import oracle
             m = 12000  # bounded CPU sample: a 12k x 12k prefix of the same pair
             t = time.perf_counter()

@@ -36,6 +36,39 @@ __global__ void kern(int* out, long long ld, long long off, int iters)
     }
 }
 
+// Lane-fill shaped stores: every instruction writes 16 rows x 64 B (4 lanes per row), aligned.
+// PAIR: consecutive instructions write the two 64-B halves of the same 128-B lines (a row's two
+// blocks stored together); MASK: only half of the rows (alternating per pair of blocks) store,
+// the other half idle (the parity scheme: a row emits its two aligned halves every other block).
+template <bool PAIR, bool MASK>
+__global__ void kernL(int* out, long long ld, long long off, int iters)
+{
+    const int lane = threadIdx.x & 63;
+    const long long wave = (long long)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const long long row0 = wave * 64;
+    int4a v = {lane, lane + 1, lane + 2, lane + 3};
+    // one "block" = 16 columns per row of all 64 rows = 4 instructions (16 rows each)
+    for (int it = 0; it < iters; ++it)
+    {
+        int blk, k;  // block (64-B column chunk) and row group
+        if (!PAIR)
+        {
+            blk = it / 4, k = it % 4;
+        }
+        else
+        {
+            // blocks 2q, 2q+1 issued as: k0 b0, k0 b1, k1 b0, k1 b1, ...
+            const int q = it / 8, r = it % 8;
+            k = r / 2, blk = 2 * q + (r & 1);
+        }
+        const long long rr = row0 + 16 * k + (lane & 15);
+        const long long c = (long long)blk * 16 + 4 * (lane >> 4) + off;
+        if (MASK && ((rr + blk / 2) & 1)) continue;
+        *(int4a*)(out + rr * ld + c) = v;
+        v += 1;
+    }
+}
+
 int main()
 {
     int* out = nullptr;
@@ -59,6 +92,24 @@ int main()
         const double bytes = (double)wgs * waves_per_wg * iters * 1024;
         printf("%-3s W %5d B  ld %5lld off %lld: %8.3f ms  %8.1f GB/s\n", name, W, ld, off, ms, bytes / ms / 1e6);
     };
+    {
+        auto runL = [&](auto k, const char* name, int mult) {
+            const long long ld = 20032;
+            hipLaunchKernelGGL(k, wgs, 64 * waves_per_wg, 0, 0, out, ld, 0LL, iters * mult);
+            hipEventRecord(e0);
+            hipLaunchKernelGGL(k, wgs, 64 * waves_per_wg, 0, 0, out, ld, 0LL, iters * mult);
+            hipEventRecord(e1);
+            hipEventSynchronize(e1);
+            float ms;
+            hipEventElapsedTime(&ms, e0, e1);
+            const double bytes = (double)wgs * waves_per_wg * iters * 1024;  // MASK: half the lanes over 2x iters
+            printf("lane-shaped %-12s: %8.3f ms  %8.1f GB/s\n", name, ms, bytes / ms / 1e6);
+        };
+        runL(kernL<false, false>, "plain", 1);
+        runL(kernL<true, false>, "pair", 1);
+        runL(kernL<true, true>, "pair+mask", 2);
+        runL(kernL<false, true>, "mask", 2);
+    }
     for (long long ld : {20001LL, 20032LL})
     {
         const long long off = ld == 20001 ? 1 : 0;
