@@ -241,7 +241,22 @@ def bench_full_batch(world, rank, local, n_pairs):
             "kernel": f"gsa::nw_lane_kernel<{lane_ns()}> (full, one row per lane)",
             "hbm_write_GBps": round(gbps * world, 1), "hbm_frac": round(gbps / PEAK_HBM_GBPS, 4),
             "bound": "hbm (4 B written per cell; MI355X 8 TB/s spec)",
+            "pmc_write_over_algorithmic": pmc_write_ratio(n_pairs, f"gsa::nw_lane_kernel<{lane_ns()}>"),
             "pairs": n_pairs, "pairs_matching_golden": match}
+
+
+def pmc_write_ratio(n_pairs, kernel):
+    """HBM bytes written (PMC WRITE_SIZE, profiles/r03_pmc_full_batch.json, collected by
+    tools/r03_pmc.sh on the same batch) over the matrix bytes, or None for another shape/kernel:
+    the physical write rate is hbm_write_GBps times this."""
+    p = os.path.join(ROOT, "profiles", "r03_pmc_full_batch.json")
+    try:
+        j = json.load(open(p))
+        if n_pairs == 64 and j.get("kernel", "").startswith(kernel):
+            return round(j["write_over_algorithmic"], 4)
+    except Exception:
+        return None
+    return None
 
 
 CFG5 = [("SW-LG", -11, -11, True), ("NW-AG", -11, -1, False)]
