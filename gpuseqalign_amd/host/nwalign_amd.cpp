@@ -16,7 +16,8 @@
 // Differences against the reference's types, the only edits when this file moves into the
 // reference's src/ (INTEGRATION.md lists them): the include below becomes "run_types.hpp" +
 // "gsa.h"; the result buffers are HostArray<int> (init(n) in place of resize(n)); res.hipStat
-// is res.cudaStat; update_peak_mem is the reference's updateNwAlgPeakMemUsage.
+// is res.cudaStat; update_peak_mem is the reference's updateNwAlgPeakMemUsage; nw.ctx (the
+// mirror's device context) is a per-process gsa_ctx created where initNwInput sets the device up.
 #include <algorithm>
 #include <exception>
 
