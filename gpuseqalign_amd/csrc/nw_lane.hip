@@ -37,6 +37,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "nw_lane.h"
 
@@ -309,7 +310,10 @@ __device__ __forceinline__ void lane_strip(const StripArgs& a, const LaneLds& L,
 // loader wave: Q profile, the row above strip 0 (granules of the previous super-strip, or
 // row 0), the drain of the last strip's row into granules for the next super-strip
 // ------------------------------------------------------------------------------------
-template <int NS>
+// ROLE 0: both jobs in one wave; 1: the feed only; 2: the profile only.  Single pairs run the
+// feed in a wave of its own (FD instance), so a poll is never behind a profile batch: the row
+// above strip 0 arrives as soon as its granules are stored
+template <int NS, int ROLE>
 __device__ __forceinline__ void lane_loader(const StripArgs& a, const LaneLds& L, int tk, int lane)
 {
     const int C = a.C, g = a.g;
@@ -327,15 +331,15 @@ __device__ __forceinline__ void lane_loader(const StripArgs& a, const LaneLds& L
     int pl = 0, c0 = 0;  // progress words, re-read only when their cached values block
     uint64_t last = __builtin_amdgcn_s_memrealtime();
     unsigned idle = 0;  // idle passes (error-word polls)
-    while (qn <= C || hnext <= C)
+    while ((ROLE != 1 && qn <= C) || (ROLE != 2 && hnext <= C))
     {
         bool moved = false;
         // (1) the row above strip 0 (H + g) -> ring 0 elements c + 64, as far as granules of the
         //     previous super-strip are published (in column order) and ring 0 has room.  The poll
         //     is issued first and consumed after the Q work below, which runs under its latency;
         //     that latency paces this loop (no sleep while granules are awaited).
-        if (hnext <= C && hnext + 128 > c0 + kLRing) c0 = flag_ld(F + kFCons);  // ring 0 consumed
-        const bool feed = hnext <= C && hnext + 128 <= c0 + kLRing;
+        if (ROLE != 2 && hnext <= C && hnext + 128 > c0 + kLRing) c0 = flag_ld(F + kFCons);  // ring 0 consumed
+        const bool feed = ROLE != 2 && hnext <= C && hnext + 128 <= c0 + kLRing;
         const int c = hnext + lane;
         const bool in = c <= C;
         unsigned long long q = 0ull;
@@ -343,8 +347,8 @@ __device__ __forceinline__ void lane_loader(const StripArgs& a, const LaneLds& L
         // (2) Q columns qn .. qn+63: the columns they replace (<= qn+63-kLW) are dead once the
         //     last strip has published elements pl (its next reads start at column pl-55).
         //     Gather the lane's letter column of subT (8 x b128), then 32 straight-line writes.
-        if (qn <= C && qn > pl + kLW - 128) pl = flag_ld(F + 4u * NS);  // last strip's elements
-        if (qn <= C && qn <= pl + kLW - 128)
+        if (ROLE != 1 && qn <= C && qn > pl + kLW - 128) pl = flag_ld(F + 4u * NS);  // last strip's elements
+        if (ROLE != 1 && qn <= C && qn <= pl + kLW - 128)
         {
             const uint32_t p = (uint32_t)((qn + lane) & (kLW - 1));
             const uint32_t sb = L.sub + 4u * kLSubRow * (uint32_t)xl;
@@ -403,7 +407,7 @@ __device__ __forceinline__ void lane_loader(const StripArgs& a, const LaneLds& L
                 atomicOr(a.err, 1u);
                 return;
             }
-            if (tk == 0 || hnext > C) __builtin_amdgcn_s_sleep(1);
+            if (ROLE == 2 || tk == 0 || hnext > C) __builtin_amdgcn_s_sleep(1);
         }
     }
 }
@@ -471,13 +475,13 @@ __device__ __forceinline__ PairDesc lane_desc(const PairDesc* p)
     return u.d;
 }
 
-template <int NS>
-__global__ void __launch_bounds__(64 * (NS + 2)) nw_lane_kernel(StripArgs a)
+template <int NS, bool FD>
+__global__ void __launch_bounds__(64 * (NS + 2 + FD)) nw_lane_kernel(StripArgs a)
 {
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     const LaneLds L = lane_layout(NS, a.substsz);
-    for (int k = threadIdx.x; k < a.substsz * kLSubRow; k += 64 * (NS + 2))
+    for (int k = threadIdx.x; k < a.substsz * kLSubRow; k += 64 * (NS + 2 + FD))
     {
         const int x = k / kLSubRow, yy = k % kLSubRow;
         lds_st(L.sub + 4u * k, yy < a.substsz ? G(a.subst)[yy * a.substsz + x] - a.g : 0);
@@ -528,7 +532,9 @@ __global__ void __launch_bounds__(64 * (NS + 2)) nw_lane_kernel(StripArgs a)
         if (w == NS + 1)
             lane_drain<NS>(pa, L, tk, lane);
         else if (w == NS)
-            lane_loader<NS>(pa, L, tk, lane);
+            lane_loader<NS, FD ? 2 : 0>(pa, L, tk, lane);
+        else if (FD && w == NS + 2)
+            lane_loader<NS, 1>(pa, L, tk, lane);
         else
         {
             __builtin_amdgcn_s_setprio(3);
@@ -538,24 +544,25 @@ __global__ void __launch_bounds__(64 * (NS + 2)) nw_lane_kernel(StripArgs a)
     }
 }
 
-template <int NS>
+template <int NS, bool FD = false>
 hipError_t launch_lane(const StripArgs& a, int grid, hipStream_t stream)
 {
     const size_t lds = lane_lds_bytes(NS, a.substsz);
-    auto kern = nw_lane_kernel<NS>;
+    auto kern = nw_lane_kernel<NS, FD>;
+    constexpr int kThreads = 64 * (NS + 2 + FD);
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     if (grid <= 0)
     {
         int per_cu = 0, dev = 0, cus = 0;
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)kern, 64 * (NS + 2), lds);
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)kern, kThreads, lds);
         if (e == hipSuccess) e = hipGetDevice(&dev);
         if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
         if (e != hipSuccess) return e;
         grid = std::max(1, std::min(a.nTicketsTotal, std::max(1, per_cu) * cus));
     }
-    if ((e = record_foot((const void*)kern, lds, 64 * (NS + 2), grid)) != hipSuccess) return e;
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * (NS + 2)), lds, stream, a);
+    if ((e = record_foot((const void*)kern, lds, kThreads, grid)) != hipSuccess) return e;
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreads), lds, stream, a);
     return hipGetLastError();
 }
 
@@ -570,7 +577,11 @@ hipError_t launch_lane_fill(const StripArgs& a, int ns, int grid, hipStream_t st
 {
     if (ns == 1) return launch_lane<1>(a, grid, stream);
     if (ns == 3) return launch_lane<3>(a, grid, stream);
-    if (ns == 4) return launch_lane<4>(a, grid, stream);
+    // a single pair: the feed in a wave of its own (a 7th wave would cost a batch its second
+    // workgroup per CU); GSA_LANE_FEED=0/1 overrides
+    const char* fe = getenv("GSA_LANE_FEED");
+    const bool fd = fe && *fe ? atoi(fe) != 0 : a.nPairs == 1;
+    if (ns == 4) return fd ? launch_lane<4, true>(a, grid, stream) : launch_lane<4>(a, grid, stream);
     if (ns == 6) return launch_lane<6>(a, grid, stream);
     if (ns == 8) return launch_lane<8>(a, grid, stream);
     return launch_lane<2>(a, grid, stream);
