@@ -916,6 +916,16 @@ hipError_t launch_kr(const StripArgs& a, int grid, hipStream_t stream)
 
 }  // namespace
 
+#ifdef GSA_KROW_BATCH8
+// nw_krow8.hip: the 8-strip batch instance in a translation unit of its own, so it can be built
+// with another instruction scheduler than the single-pair instances (Makefile)
+hipError_t launch_krow_fill_b8(const StripArgs& a, int grid, hipStream_t stream)
+{
+    return launch_kr<8, 4, 1024>(a, grid, stream);
+}
+#else
+hipError_t launch_krow_fill_b8(const StripArgs& a, int grid, hipStream_t stream);
+
 size_t krow_lds_bytes(int ns, int lw, int substsz) { return (size_t)kr_layout(ns, lw, substsz).flags + 256; }
 
 hipError_t launch_krow_fill(const StripArgs& a, int ns, int k, int lw, int grid, hipStream_t stream)
@@ -923,9 +933,10 @@ hipError_t launch_krow_fill(const StripArgs& a, int ns, int k, int lw, int grid,
     if (k == 2) return ns == 2 ? launch_kr<2, 2, 512>(a, grid, stream) : launch_kr<4, 2, 1024>(a, grid, stream);
     (void)lw;  // 512 for (4, 4) measured slower for one pair and for batches (the first strip
                // is throttled by the window): 1024
-    if (ns == 8) return launch_kr<8, 4, 1024>(a, grid, stream);
+    if (ns == 8) return launch_krow_fill_b8(a, grid, stream);
     if (a.done) return launch_kr<4, 4, 1024, true>(a, grid, stream);  // mlsppt: (4, 4) only (enqueue_batch)
     return ns == 2 ? launch_kr<2, 4, 512>(a, grid, stream) : launch_kr<4, 4, 1024>(a, grid, stream);
 }
+#endif
 
 }  // namespace gsa
