@@ -1,0 +1,11 @@
+# scheduling-group barriers over the block's steps: (4 VALU, 1 DS read) x 16, then the rest
+# (guides the compiler's interleaving of the profile reads with the step chain)
+a = """        // the block's hand-off at its end (the next strip sees it a block earlier than when it is"""
+assert s.count(a) == 1
+s = s.replace(a, """#pragma unroll
+        for (int i = 0; i < 16; ++i)
+        {
+            __builtin_amdgcn_sched_group_barrier(0x2, 4, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        }
+""" + a)
