@@ -138,6 +138,17 @@ def cpu_baseline(Y, X, sub, budget_s=20.0, n=20000):
                        + ", ".join(f"{t}: {runs[t][0]:.3f} GCUPS" for t in sorted(runs)))}
 
 
+# GSA_BENCH_REHEARSE=1 (test only): N ranks share cuda:0 and talk over gloo with CPU tensors, to
+# exercise the N > 1 code path on a one-GPU box; its numbers mean nothing (the GPU is shared)
+REHEARSE = os.environ.get("GSA_BENCH_REHEARSE") == "1"
+
+
+def coll_dev(dev):
+    """Where collective tensors live: the rank's GPU (RCCL), or the CPU in a gloo rehearsal."""
+    import torch
+    return torch.device("cpu") if REHEARSE else dev
+
+
 def timed_steps(step, stream, dev, steps, warmup, world, eng):
     import torch
     import torch.distributed as dist
@@ -161,7 +172,7 @@ def timed_steps(step, stream, dev, steps, warmup, world, eng):
         elapsed = time.perf_counter() - t0
     kern_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs]))
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev(dev))
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     return elapsed, kern_ms
@@ -187,7 +198,7 @@ def bench_config4(world, rank, local, n_pairs):
     sub = subst_blosum62()
     rep = shard.shard_align(pairs, sub, -11, shard.gpu_batch_align(device=local, mode="sparse", tileBx=TILE_BX,
                                                                 warmup=1, repeats=3),
-                            device=f"cuda:{local}" if world > 1 else None)
+                            device=f"cuda:{local}" if world > 1 and not REHEARSE else None)
     gold = load_golden("config4_pairs.json")
     costs = [r.align_cost for r in rep.results]
     match = None
@@ -228,7 +239,7 @@ def bench_full_batch(world, rank, local, n_pairs):
     sub = subst_blosum62()
     rep = shard.shard_align(pairs, sub, -11, shard.gpu_batch_align(device=local, mode="full", warmup=1, repeats=3,
                                                                 out_budget_bytes=int(0.9 * 140e9)),
-                            device=f"cuda:{local}" if world > 1 else None)
+                            device=f"cuda:{local}" if world > 1 and not REHEARSE else None)
     gold = load_golden("config4_pairs.json")
     costs = [r.align_cost for r in rep.results]
     match = None if gold is None else sum(int(a == b) for a, b in zip(costs, gold["align_cost"][:n_pairs]))
@@ -330,15 +341,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if REHEARSE:
+        local = 0
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        dist.init_process_group("gloo" if REHEARSE else "nccl")
     dev = torch.device("cuda", local if world > 1 else 0)
 
     sub = subst_blosum62()
-    tS = torch.from_numpy(sub).to(dev)
+    tS = torch.from_numpy(sub).to(coll_dev(dev))
     if world > 1:
         dist.broadcast(tS, src=0)  # substitution table from rank 0 (RCCL over xGMI)
+    tS = tS.to(dev)
     eng = gsa.Engine(dev.index)
     stream = torch.cuda.Stream(device=dev)
     sh = stream.cuda_stream
@@ -367,7 +381,7 @@ def main():
     del hr, hc
     costs = [cost]
     if world > 1:
-        t = torch.tensor([cost], dtype=torch.int64, device=dev)
+        t = torch.tensor([cost], dtype=torch.int64, device=coll_dev(dev))
         lst = [torch.zeros_like(t) for _ in range(world)]
         dist.all_gather(lst, t)
         costs = [int(v.item()) for v in lst]
