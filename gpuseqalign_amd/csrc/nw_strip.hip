@@ -133,11 +133,13 @@ __device__ __forceinline__ Lds lds_layout(int substsz)
     return L;
 }
 
+#ifndef GSA_STRIP_SW
 size_t strip_lds_bytes(int ns, int substsz, int mode)
 {
     return (size_t)4 * kXCopy + (size_t)(ns + 1) * kRing * 16 * (is_score_mode(mode) ? 2 : 1) + 16 + 128 +
            (size_t)ns * (substsz + 1) * 512;
 }
+#endif
 
 __device__ __forceinline__ bool err_set(const StripArgs& a)
 {
@@ -838,6 +840,7 @@ __global__ void __launch_bounds__(64 * (NS + 1)) nw_strip_kernel(StripArgs a)
 // tile row 0 (Kernel A of nwalign_gpu9_mlsp_diagdiagdiag.cu:15-63), the header column of
 // tile column 0 and entry 0 of tile row 0's header columns (all plain multiples of g).
 // grid.y = pair of the batch.
+#ifndef GSA_STRIP_SW
 __global__ void nw_headers_kernel(StripArgs a, int mode)
 {
     const PairDesc& d = a.pairs[blockIdx.y];
@@ -867,6 +870,7 @@ __global__ void nw_headers_kernel(StripArgs a, int mode)
         }
     }
 }
+#endif
 
 template <int NS, int MODE>
 static hipError_t launch_strip(const StripArgs& a, int grid, hipStream_t stream)
@@ -890,6 +894,7 @@ static hipError_t launch_strip(const StripArgs& a, int grid, hipStream_t stream)
     return hipGetLastError();
 }
 
+#ifndef GSA_STRIP_SW
 thread_local LaunchFoot g_last_foot {};
 
 hipError_t record_foot(const void* kern, size_t lds, int threads, int grid)
@@ -916,12 +921,21 @@ hipError_t launch_headers(const StripArgs& a, int mode, long long maxWork, hipSt
     return hipGetLastError();
 }
 
+hipError_t launch_strip_sw(const StripArgs& a, int grid, hipStream_t stream);
+
 hipError_t launch_strip_fill(const StripArgs& a, int mode, int grid, hipStream_t stream)
 {
     if (mode == kModeScoreAG) return launch_strip<kSparseNS, kModeScoreAG>(a, grid, stream);
-    if (mode == kModeScoreSW) return launch_strip<kSparseNS, kModeScoreSW>(a, grid, stream);
+    if (mode == kModeScoreSW) return launch_strip_sw(a, grid, stream);
     if (mode == kModeSparse) return launch_strip<kSparseNS, kModeSparse>(a, grid, stream);
     return hipErrorInvalidValue;  // full matrices: launch_lane_fill (nw_lane.hip)
 }
+#else
+// nw_strip_sw.hip: the SW score instance in a translation unit of its own (its own scheduler flags)
+hipError_t launch_strip_sw(const StripArgs& a, int grid, hipStream_t stream)
+{
+    return launch_strip<kSparseNS, kModeScoreSW>(a, grid, stream);
+}
+#endif
 
 }  // namespace gsa
