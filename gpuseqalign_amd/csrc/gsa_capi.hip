@@ -1417,6 +1417,15 @@ int gsa_align_sparse_pt(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, cons
     };
     Batch inflight[2];
     int nInflight = 0, issued = 0, nextSlot = 0;
+    struct DrainAtExit  // an error return waits for DMAs still writing the pinned slots
+    {
+        gsa_ctx* c;
+        const int& n;
+        ~DrainAtExit()
+        {
+            if (n > 0) (void)hipStreamSynchronize(c->ptstream);
+        }
+    } drainAtExit {ctx, nInflight};
     auto dbg = [&](const char* what, int c0, int c1) {
         if (ptdbg)
             std::fprintf(stderr, "mlsppt %.3f ms: %s %d..%d (fill %s)\n",

@@ -54,3 +54,22 @@ def test_overlap_other_geometries(engine, golden, monkeypatch, kern, ns, k):
     b = engine.align_sparse(Y, X, golden.blosum62, -11, tileBx=128, overlap=True)
     assert np.array_equal(a.hrow, b.hrow) and np.array_equal(a.hcol, b.hcol)
     assert a.align_cost == b.align_cost == oracle.fill_full(Y, X, golden.blosum62, -11)[1]
+
+
+def test_overlap_error_then_recovers(golden):
+    """A fill that fails while its chunks are being copied (watchdog 0: every wait gives up at once)
+    makes mlsppt report errorKernelFailure, with the copies it had issued drained before it
+    returns; the next mlsppt call on the same context is exact."""
+    import gpuseqalign_amd as gsa
+    import oracle
+    Y, X = related_pair(20000, 7)
+    sub = golden.blosum62
+    with gsa.Engine(0) as eng:
+        eng.set_watchdog(0)
+        with pytest.raises(gsa.NwError) as ei:
+            eng.align_sparse(Y, X, sub, -11, tileBx=256, overlap=True)
+        assert ei.value.stat == gsa.NwStat.errorKernelFailure
+        eng.set_watchdog(1000000)
+        r = eng.align_sparse(Y, X, sub, -11, tileBx=256, overlap=True)
+    hr, hc, _, _, cost = oracle.sparse_headers(Y, X, sub, -11, gsa.sparse_tile_by(), 256)
+    assert np.array_equal(r.hrow, hr) and np.array_equal(r.hcol, hc) and r.align_cost == cost
