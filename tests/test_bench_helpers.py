@@ -1,0 +1,41 @@
+"""bench.py's CPU-side helpers: the critical-path bound it reports beside the VALU roofline, and
+the PMC files it reads (`roofline.traffic`, the full batch's write ratio), which must match the
+kernel the bench times or be reported as absent."""
+import json
+import os
+
+import pytest
+
+import bench
+
+
+def test_critical_path_model():
+    # the headline: 100k columns, 391 strips of 256 rows, 9 VALU per step at 4 cycles, 2.4 GHz
+    cp = bench.critical_path(100000, 391, 9, 5.5, 256)
+    assert cp["steps"] == 100000 + 391 * 64
+    assert cp["step_cycles_bound"] == 36
+    assert cp["bound_ms"] == pytest.approx(125024 * 36 / 2.4e9 * 1e3, rel=1e-4)
+    assert cp["frac"] == pytest.approx(cp["bound_ms"] / 5.5, rel=1e-3)
+    assert cp["step_cycles_achieved"] == pytest.approx(5.5e-3 * 2.4e9 / 125024, rel=1e-3)
+
+
+def test_traffic_file_matches_the_bench_kernel():
+    """profiles/traffic_config3.json is read into roofline.traffic only for the kernel, R and C the
+    bench runs: the committed file must name the current headline kernel."""
+    p = os.path.join(bench.ROOT, "profiles", "traffic_config3.json")
+    tj = json.load(open(p))
+    kname = bench.sparse_kernel_name()
+    assert tj["kernel"] == kname
+    assert bench.traffic_for("traffic_config3.json", tj["R"], tj["C"], kname) == tj["hbm_bytes_per_launch"]
+    assert bench.traffic_for("traffic_config3.json", tj["R"], tj["C"], "another kernel") is None
+    assert bench.traffic_for("no_such_file.json", tj["R"], tj["C"], kname) is None
+    # the PMC bytes are the headers written plus the granules written and read once
+    alg = tj["algorithmic_bytes"]
+    assert tj["hbm_bytes_per_launch"] == pytest.approx(sum(alg.values()), rel=0.05)
+
+
+def test_full_batch_write_ratio():
+    r = bench.pmc_write_ratio(64, "gsa::nw_lane_kernel<4>")
+    assert r is not None and 1.0 <= r < 1.5
+    assert bench.pmc_write_ratio(32, "gsa::nw_lane_kernel<4>") is None
+    assert bench.pmc_write_ratio(64, "gsa::nw_krow_kernel<4>") is None
