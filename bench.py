@@ -249,10 +249,10 @@ def bench_full_batch(world, rank, local, n_pairs):
                         f"matrices ({out_bytes / 1e9:.1f} GB), one persistent launch, LPT-sharded over {world} rank(s) "
                         "(1 untimed + 3 timed launches; seconds per launch)",
             "value": round(rep.gcups, 2), "unit": "GCUPS", "scaling": "strong", "seconds": round(rep.elapsed_s, 4),
-            "kernel": f"gsa::nw_lane_kernel<{lane_ns()}> (full, one row per lane)",
+            "kernel": f"gsa::nw_lane_kernel<{lane_ns()},false> (full, one row per lane)",
             "hbm_write_GBps": round(gbps * world, 1), "hbm_frac": round(gbps / PEAK_HBM_GBPS, 4),
             "bound": "hbm (4 B written per cell; MI355X 8 TB/s spec)",
-            "pmc_write_over_algorithmic": pmc_write_ratio(n_pairs, f"gsa::nw_lane_kernel<{lane_ns()}>"),
+            "pmc_write_over_algorithmic": pmc_write_ratio(n_pairs, f"gsa::nw_lane_kernel<{lane_ns()},false>"),
             "pairs": n_pairs, "pairs_matching_golden": match}
 
 
@@ -414,7 +414,8 @@ def main():
                                "(resrc/seq_generated.fa), full int32 score matrix in HBM",
                    "value": round(world * R2 * C2 * a.steps / el2 / 1e9, 2), "unit": "GCUPS",
                    "ms_per_step": round(el2 * 1e3 / a.steps, 4), "kernel_ms": round(km2, 4),
-                   "kernel": f"gsa::nw_lane_kernel<{lane_ns()}> (full, one row per lane)",
+                   "kernel": (f"gsa::nw_lane_kernel<{lane_ns()},{'true' if lane_ns() == 4 else 'false'}> "
+                              "(full, one row per lane" + (", feeder wave)" if lane_ns() == 4 else ")")),
                    "hbm_write_GBps": round(b2 / (km2 * 1e-3) / 1e9, 1),
                    "hbm_frac": round(b2 / (km2 * 1e-3) / 1e9 / PEAK_HBM_GBPS, 4),
                    "align_cost": int(score[-1].item()), "golden_align_cost": -4922,

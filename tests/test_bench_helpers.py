@@ -35,7 +35,7 @@ def test_traffic_file_matches_the_bench_kernel():
 
 
 def test_full_batch_write_ratio():
-    r = bench.pmc_write_ratio(64, "gsa::nw_lane_kernel<4>")
+    r = bench.pmc_write_ratio(64, "gsa::nw_lane_kernel<4,false>")
     assert r is not None and 1.0 <= r < 1.5
-    assert bench.pmc_write_ratio(32, "gsa::nw_lane_kernel<4>") is None
+    assert bench.pmc_write_ratio(32, "gsa::nw_lane_kernel<4,false>") is None
     assert bench.pmc_write_ratio(64, "gsa::nw_krow_kernel<4>") is None
