@@ -328,7 +328,10 @@ int score_ag_strip(gsa_ctx* ctx, const int32_t* seqY, int64_t R, const int32_t* 
         return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
     (void)hipEventRecord(ctx->ev0, st);
     const int grid = std::max(1, std::min((int)tickets, ctx->cu_count));
-    if ((e = gsa::launch_strip_fill(a, local ? gsa::kModeScoreSW : gsa::kModeScoreAG, grid, st)) != hipSuccess)
+    // a linear gap (gapo == gape) runs the step without E' and F' (d = 0)
+    const int mode = local ? (gapo == gape ? gsa::kModeScoreSWL : gsa::kModeScoreSW)
+                           : (gapo == gape ? gsa::kModeScoreAGL : gsa::kModeScoreAG);
+    if ((e = gsa::launch_strip_fill(a, mode, grid, st)) != hipSuccess)
         return fail(ctx, e, GSA_ERROR_KERNEL_FAILURE);
     note_launch(ctx);
     (void)hipEventRecord(ctx->ev1, st);

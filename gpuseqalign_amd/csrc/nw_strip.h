@@ -14,7 +14,15 @@ constexpr int kModeScoreAG = 3;
 // Score-only local alignment (Smith-Waterman) with affine gaps, same layout: the clamp at 0 is
 // a per-row floor (i+j)*(-gape) in the shifted space; the best cell goes to a packed atomicMax.
 constexpr int kModeScoreSW = 4;
-__host__ __device__ constexpr bool is_score_mode(int mode) { return mode == kModeScoreAG || mode == kModeScoreSW; }
+// The same with a linear gap (gapo == gape, so d = 0): E' and F' never exceed H' and drop out, and
+// only H' is handed between strips (BASELINE configs[4]'s SW-LG)
+constexpr int kModeScoreSWL = 5;
+// NW (global) with a linear gap: the AG step without E' and F' (d = 0)
+constexpr int kModeScoreAGL = 6;
+__host__ __device__ constexpr bool is_sw_mode(int mode) { return mode == kModeScoreSW || mode == kModeScoreSWL; }
+__host__ __device__ constexpr bool is_ag_mode(int mode) { return mode == kModeScoreAG || mode == kModeScoreAGL; }
+__host__ __device__ constexpr bool is_lin_mode(int mode) { return mode == kModeScoreSWL || mode == kModeScoreAGL; }
+__host__ __device__ constexpr bool is_score_mode(int mode) { return is_ag_mode(mode) || is_sw_mode(mode); }
 constexpr int kWaveRows = 256;                          // rows per strip (one wave, 4 rows per lane)
 constexpr int kSparseNS = 4;                            // strip waves per workgroup, sparse fills
 constexpr int kSparseTileBy = kWaveRows * kSparseNS;    // = tile height of the mlsp matrices

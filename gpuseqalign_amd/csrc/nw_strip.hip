@@ -38,7 +38,8 @@
 //             letter 0 as the reference does (nwalign_gpu9_mlsp_diagdiagdiag.cu:469-478).
 //             Single pairs, batches and mlsppt run on the K-rows kernel (nw_krow.hip);
 //             this mode is reached with GSA_SPARSE_KERNEL=strip.
-//  * SCORE  : score-only NW / SW with affine gaps (kModeScoreAG / kModeScoreSW, below).
+//  * SCORE  : score-only NW / SW with affine gaps (kModeScoreAG / kModeScoreSW, below; with a
+//             linear gap: kModeScoreAGL / kModeScoreSWL, the same step without E' and F').
 // Full matrices run on the one-row-per-lane kernel (nw_lane.hip).  This kernel's full-matrix
 // modes (LDS staging + store waves; L2 output rings drained by copy workgroups) were measured
 // slower and removed.
@@ -250,7 +251,7 @@ __device__ __forceinline__ void strip_wave(const StripArgs& a, const Lds& L, int
         for (int u = 0; u < kBLK; ++u) hv[u] = win[(u + 3) >> 2][(u + 3) & 3];
     };
     auto hvf_load = [&](int b, int (&hv)[kBLK]) {
-        if constexpr (is_score_mode(MODE))
+        if constexpr (is_score_mode(MODE) && !is_lin_mode(MODE))  // F' (linear gaps: unused)
         {
             int4v win[5];
 #pragma unroll
@@ -338,10 +339,10 @@ __device__ __forceinline__ void strip_wave(const StripArgs& a, const Lds& L, int
     constexpr int i0v = is_score_mode(MODE) ? kNegAG : 0;
     int A = i0v, B = i0v, Cc = i0v, D = i0v, dA = i0v;
     int EA = kNegAG, EB = kNegAG, EC = kNegAG, ED = kNegAG, FD = kNegAG;
-    const int dd = is_score_mode(MODE) ? a.go - a.ge : 0;
+    const int dd = (is_score_mode(MODE) && !is_lin_mode(MODE)) ? a.go - a.ge : 0;  // linear: d = 0
     // AG: the cell (R, C) lies in this strip iff r0 <= R < r0 + 256: lane, row, step of it
     const int rR = a.R - r0;
-    const bool hasR = (MODE == kModeScoreAG) && rR >= 0 && rR < kWaveRows;
+    const bool hasR = is_ag_mode(MODE) && rR >= 0 && rR < kWaveRows;
     const int laneR = rR >> 2, kR = rR & 3, tStar = a.C + laneR;
     // SW: floor of row k at the current step, H' >= -(i+j)ge (H >= 0).  Per row, the block's best
     // as H << 4 | (15 - step in block) (one max per step: the larger H, then the earlier step) and,
@@ -349,7 +350,7 @@ __device__ __forceinline__ void strip_wave(const StripArgs& a, const Lds& L, int
     // a best nothing beats.  Columns past C are never the maximum: their E/F chains pay go < 0.
     int zA = 0, zB = 0, zC = 0, zD = 0, pA = 0, pB = 0, pC = 0, pD = 0;
     int bA = 0, bB = 0, bC = 0, bD = 0, tA = 0, tB = 0, tC = 0, tD = 0;
-    if constexpr (MODE == kModeScoreSW)
+    if constexpr (is_sw_mode(MODE))
     {
         const int rb = r0 + kK * lane;  // row of k = A; i + j = rb + k + (t - lane)
         constexpr int kOff = 0x7fffffff;
@@ -389,21 +390,25 @@ __device__ __forceinline__ void strip_wave(const StripArgs& a, const Lds& L, int
                     // F'(k,c) = max(F'(k-1,c), Hgo'(k-1,c)), H' = max3(Hgo'diag + s'', E', F'),
                     // Hgo' = H' + d; the row above comes from lane l-1 (DPP) or the halo
                     const int upH = shr1z(D) + hvcur[4 * q + u];
-                    const int upF = shr1z(FD) + hfcur[4 * q + u];
-                    const int eA = max(EA, A), eB = max(EB, B), eC = max(EC, Cc), eD = max(ED, D);
+                    constexpr bool LIN = is_lin_mode(MODE);  // d = 0: E' = H' of the left cell, F' <= Hgo' above
+                    const int upF = LIN ? 0 : shr1z(FD) + hfcur[4 * q + u];
+                    const int eA = LIN ? A : max(EA, A), eB = LIN ? B : max(EB, B);
+                    const int eC = LIN ? Cc : max(EC, Cc), eD = LIN ? D : max(ED, D);
                     // SW: H >= 0 enters as F' >= floor (the max3 that forms F'): H = max(0, diag,
                     // E, F) exactly, and a clamped F passes on at most ge <= 0, below the next floor
-                    constexpr bool SW = MODE == kModeScoreSW;
-                    const int fA = SW ? max(max(upF, upH), zA) : max(upF, upH);
+                    // linear gaps (d = 0): E' <= H' and F' <= H' hold by induction, so E' is the left
+                    // H', F' of a row the H' above it, and only the SW floor stays
+                    constexpr bool SW = is_sw_mode(MODE);
+                    const int fA = LIN ? (SW ? max(upH, zA) : upH) : SW ? max(max(upF, upH), zA) : max(upF, upH);
                     const int hA = max(max(dA + (int)(short)sv.x, eA), fA);
                     const int nA = hA + dd;
-                    const int fB = SW ? max(max(fA, nA), zB) : max(fA, nA);
+                    const int fB = LIN ? (SW ? max(nA, zB) : nA) : SW ? max(max(fA, nA), zB) : max(fA, nA);
                     const int hB = max(max(A + (sv.x >> 16), eB), fB);
                     const int nB = hB + dd;
-                    const int fC = SW ? max(max(fB, nB), zC) : max(fB, nB);
+                    const int fC = LIN ? (SW ? max(nB, zC) : nB) : SW ? max(max(fB, nB), zC) : max(fB, nB);
                     const int hC = max(max(B + (int)(short)sv.y, eC), fC);
                     const int nC = hC + dd;
-                    const int fD = SW ? max(max(fC, nC), zD) : max(fC, nC);
+                    const int fD = LIN ? (SW ? max(nC, zD) : nC) : SW ? max(max(fC, nC), zD) : max(fC, nC);
                     const int hD = max(max(Cc + (sv.y >> 16), eD), fD);
                     const int nD = hD + dd;
                     if constexpr (SW)
@@ -459,12 +464,12 @@ __device__ __forceinline__ void strip_wave(const StripArgs& a, const Lds& L, int
             }
             // hand-off: row D of 4 steps, slot (group - lane)
             lds_st4(ring_out + 16u * (uint32_t)(((t0 >> 2) - lane) & (kRing - 1)), int4v {Xd[0], Xd[1], Xd[2], Xd[3]});
-            if constexpr (is_score_mode(MODE))
+            if constexpr (is_score_mode(MODE) && !is_lin_mode(MODE))
                 lds_st4(ring2_out + 16u * (uint32_t)(((t0 >> 2) - lane) & (kRing - 1)), int4v {Fd[0], Fd[1], Fd[2], Fd[3]});
             if (q == kHopQ - 1) rpin = raw_ld(fin);
             // SW reads its halo at block start (one halo buffer live: no spills, 50k 7.64 ->
             // 7.01 ms); NW-AG keeps the prefetch (5.13 vs 5.46 ms; profiles/r01_score_jit.txt)
-            if (q == kHopQ && MODE != kModeScoreSW)
+            if (q == kHopQ && !is_sw_mode(MODE))
             {
                 // halo of the next block, once the row above covers it
                 int pn = __builtin_amdgcn_readfirstlane(rpin);
@@ -492,7 +497,7 @@ __device__ __forceinline__ void strip_wave(const StripArgs& a, const Lds& L, int
                 if (w == 0) rpxo = raw_ld(F + kFXo);
             }
         }
-        if constexpr (MODE == kModeScoreSW)
+        if constexpr (is_sw_mode(MODE))
         {
             auto fold = [&](int& p, int& best, int& tb) {
                 const int v = p >> 4;
@@ -529,7 +534,7 @@ __device__ __forceinline__ void strip_wave(const StripArgs& a, const Lds& L, int
         {
             if (!wait_start(pco, pxo, b)) return false;
         }
-        if constexpr (MODE == kModeScoreSW)
+        if constexpr (is_sw_mode(MODE))
         {
             // halo of this block (block 0's came with the prologue), once the row above covers it
             if (b > 0)
@@ -561,7 +566,7 @@ __device__ __forceinline__ void strip_wave(const StripArgs& a, const Lds& L, int
             const int jT = (16 * b) / a.tBx;
             capblk = jT >= 1 && jT < a.tcols && 16 * b - jT * a.tBx < 64;
         }
-        if constexpr (MODE == kModeScoreAG) capblk = hasR && (tStar >> 4) == b;
+        if constexpr (is_ag_mode(MODE)) capblk = hasR && (tStar >> 4) == b;
         if (capblk)
             block(b, scur, snext, lnext, lfree, hvcur, hvnext, hfcur, hfnext, std::integral_constant<bool, true>());
         else
@@ -574,7 +579,7 @@ __device__ __forceinline__ void strip_wave(const StripArgs& a, const Lds& L, int
         if (!run_block(b, sA, sB, lxB, lxA, hvA, hvB, hfA, hfB)) return;
         if (b + 1 < NB && !run_block(b + 1, sB, sA, lxA, lxB, hvB, hvA, hfB, hfA)) return;
     }
-    if constexpr (MODE == kModeScoreSW)
+    if constexpr (is_sw_mode(MODE))
     {
         // this lane's best cell, first in row-major order: rows in order, first step per row
         const unsigned long long W = (unsigned long long)a.C + 1, mask = (1ull << a.idxBits) - 1;
@@ -659,7 +664,7 @@ __device__ __forceinline__ void loader_wave(const StripArgs& a, const Lds& L, in
                 // row 0 in the shifted space: global H'(0,c) = d for c >= 1 (0 at c = 0), local
                 // H'(0,c) = -c*ge (H = 0); carried as Hgo' = H' + d
                 const int dd = a.go - a.ge;
-                q = (uint32_t)(MODE == kModeScoreSW ? dd - c * a.ge : (c == 0 ? dd : 2 * dd));
+                q = (uint32_t)(is_sw_mode(MODE) ? dd - c * a.ge : (c == 0 ? dd : 2 * dd));
                 q2 = (uint32_t)(-(1 << 29));
                 good = in;
             }
@@ -667,7 +672,7 @@ __device__ __forceinline__ void loader_wave(const StripArgs& a, const Lds& L, in
             {
                 q = in ? __hip_atomic_load(gprev + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
                 good = in && (uint32_t)(q >> 32) == a.epoch;
-                if constexpr (is_score_mode(MODE))
+                if constexpr (is_score_mode(MODE) && !is_lin_mode(MODE))
                 {
                     q2 = in ? __hip_atomic_load(gprev2 + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
                     good = good && (uint32_t)(q2 >> 32) == a.epoch;
@@ -678,7 +683,7 @@ __device__ __forceinline__ void loader_wave(const StripArgs& a, const Lds& L, in
             if (n > 0)
             {
                 if (lane < n) lds_st(ring0 + ring_elem(c), (int)(uint32_t)q);
-                if (is_score_mode(MODE) && lane < n) lds_st(ring20 + ring_elem(c), (int)(uint32_t)q2);
+                if (is_score_mode(MODE) && !is_lin_mode(MODE) && lane < n) lds_st(ring20 + ring_elem(c), (int)(uint32_t)q2);
                 hnext += n;
                 flag_st(F + kFProg + 0, hnext > Cp ? kBig : hnext);
                 moved = true;
@@ -696,7 +701,7 @@ __device__ __forceinline__ void loader_wave(const StripArgs& a, const Lds& L, in
                 if (pub)
                     __hip_atomic_store(gout + c, ((unsigned long long)a.epoch << 32) | (uint32_t)v, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
-                if constexpr (is_score_mode(MODE))
+                if constexpr (is_score_mode(MODE) && !is_lin_mode(MODE))
                 {
                     const int v2 = lds_ld(ringN2 + ring_elem(c));
                     if (pub)
@@ -921,20 +926,22 @@ hipError_t launch_headers(const StripArgs& a, int mode, long long maxWork, hipSt
     return hipGetLastError();
 }
 
-hipError_t launch_strip_sw(const StripArgs& a, int grid, hipStream_t stream);
+hipError_t launch_strip_sw(const StripArgs& a, int mode, int grid, hipStream_t stream);
 
 hipError_t launch_strip_fill(const StripArgs& a, int mode, int grid, hipStream_t stream)
 {
     if (mode == kModeScoreAG) return launch_strip<kSparseNS, kModeScoreAG>(a, grid, stream);
-    if (mode == kModeScoreSW) return launch_strip_sw(a, grid, stream);
+    if (mode == kModeScoreAGL) return launch_strip<kSparseNS, kModeScoreAGL>(a, grid, stream);
+    if (is_sw_mode(mode)) return launch_strip_sw(a, mode, grid, stream);
     if (mode == kModeSparse) return launch_strip<kSparseNS, kModeSparse>(a, grid, stream);
     return hipErrorInvalidValue;  // full matrices: launch_lane_fill (nw_lane.hip)
 }
 #else
 // nw_strip_sw.hip: the SW score instance in a translation unit of its own (its own scheduler flags)
-hipError_t launch_strip_sw(const StripArgs& a, int grid, hipStream_t stream)
+hipError_t launch_strip_sw(const StripArgs& a, int mode, int grid, hipStream_t stream)
 {
-    return launch_strip<kSparseNS, kModeScoreSW>(a, grid, stream);
+    return mode == kModeScoreSWL ? launch_strip<kSparseNS, kModeScoreSWL>(a, grid, stream)
+                                 : launch_strip<kSparseNS, kModeScoreSW>(a, grid, stream);
 }
 #endif
 
