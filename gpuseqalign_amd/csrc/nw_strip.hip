@@ -926,22 +926,22 @@ hipError_t launch_headers(const StripArgs& a, int mode, long long maxWork, hipSt
     return hipGetLastError();
 }
 
-hipError_t launch_strip_sw(const StripArgs& a, int mode, int grid, hipStream_t stream);
+hipError_t launch_strip_sw(const StripArgs& a, int grid, hipStream_t stream);
 
 hipError_t launch_strip_fill(const StripArgs& a, int mode, int grid, hipStream_t stream)
 {
     if (mode == kModeScoreAG) return launch_strip<kSparseNS, kModeScoreAG>(a, grid, stream);
     if (mode == kModeScoreAGL) return launch_strip<kSparseNS, kModeScoreAGL>(a, grid, stream);
-    if (is_sw_mode(mode)) return launch_strip_sw(a, mode, grid, stream);
+    if (mode == kModeScoreSWL) return launch_strip<kSparseNS, kModeScoreSWL>(a, grid, stream);
+    if (mode == kModeScoreSW) return launch_strip_sw(a, grid, stream);
     if (mode == kModeSparse) return launch_strip<kSparseNS, kModeSparse>(a, grid, stream);
     return hipErrorInvalidValue;  // full matrices: launch_lane_fill (nw_lane.hip)
 }
 #else
 // nw_strip_sw.hip: the SW score instance in a translation unit of its own (its own scheduler flags)
-hipError_t launch_strip_sw(const StripArgs& a, int mode, int grid, hipStream_t stream)
+hipError_t launch_strip_sw(const StripArgs& a, int grid, hipStream_t stream)
 {
-    return mode == kModeScoreSWL ? launch_strip<kSparseNS, kModeScoreSWL>(a, grid, stream)
-                                 : launch_strip<kSparseNS, kModeScoreSW>(a, grid, stream);
+    return launch_strip<kSparseNS, kModeScoreSW>(a, grid, stream);
 }
 #endif
 
