@@ -33,6 +33,7 @@ struct gsa_ctx
 {
     int device = 0;
     int cu_count = 0;
+    long long lds_max = 65536;  // dynamic LDS a workgroup may opt into (bytes)
     hipStream_t stream = nullptr;
     // [0] ticket (zeroed per launch), [1] error flags: sticky across launches, read and cleared
     // by gsa_sync (or by the synchronous call that reports them)
@@ -272,6 +273,13 @@ bool score_scan_forced()
 
 constexpr int kScoreTooLarge = 1000;  // internal: score_ag_strip -> row scan
 
+// score-only fills on the K-rows layout (default) or, with GSA_SCORE_KERNEL=strip, the strip kernel
+bool score_kernel_krow()
+{
+    const char* e = std::getenv("GSA_SCORE_KERNEL");
+    return !(e && std::strcmp(e, "strip") == 0);
+}
+
 // SW end-cell keys: score << bits | (2^bits-1 - row-major index), bits = ceil(log2((R+1)(C+1)));
 // scores (< 2^31) keep 63 - bits >= 29 bits up to (R+1)(C+1) = 2^34
 int sw_idx_bits(int64_t R, int64_t C)
@@ -331,7 +339,10 @@ int score_ag_strip(gsa_ctx* ctx, const int32_t* seqY, int64_t R, const int32_t* 
     // a linear gap (gapo == gape) runs the step without E' and F' (d = 0)
     const int mode = local ? (gapo == gape ? gsa::kModeScoreSWL : gsa::kModeScoreSW)
                            : (gapo == gape ? gsa::kModeScoreAGL : gsa::kModeScoreAG);
-    if ((e = gsa::launch_strip_fill(a, mode, grid, st)) != hipSuccess)
+    // the K-rows score kernel (nw_kscore.hip) unless GSA_SCORE_KERNEL=strip, or its LDS (a profile of
+    // substsz rows) does not fit, or SW with ge > 0 (its per-row key offsets assume z grows along j)
+    const bool krow = score_kernel_krow() && (!local || gape <= 0) && gsa::krow_score_lds_bytes(substsz) <= ctx->lds_max;
+    if ((e = krow ? gsa::launch_krow_score(a, mode, grid, st) : gsa::launch_strip_fill(a, mode, grid, st)) != hipSuccess)
         return fail(ctx, e, GSA_ERROR_KERNEL_FAILURE);
     note_launch(ctx);
     (void)hipEventRecord(ctx->ev1, st);
@@ -546,6 +557,14 @@ int gsa_ctx_create(int device, gsa_ctx** out)
     ctx->device = device;
     hipError_t e = hipSetDevice(device);
     if (e == hipSuccess) e = hipDeviceGetAttribute(&ctx->cu_count, hipDeviceAttributeMultiprocessorCount, device);
+    if (e == hipSuccess)
+    {
+        int lm = 0;
+        if (hipDeviceGetAttribute(&lm, hipDeviceAttributeSharedMemPerBlockOptin, device) == hipSuccess && lm > 0)
+            ctx->lds_max = lm;
+        else if (hipDeviceGetAttribute(&lm, hipDeviceAttributeMaxSharedMemoryPerBlock, device) == hipSuccess && lm > 0)
+            ctx->lds_max = lm;
+    }
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
     // mlsppt's copy-back stream, created next so that it gets a hardware queue of its own
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->ptstream, hipStreamNonBlocking);
@@ -1190,7 +1209,8 @@ int score_dev_impl(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, const int
     // the strip kernel's SW mode needs go < 0 (cells past C then never tie the maximum) and scores
     // below 2^26 packed with bits index bits (it reports larger ones); both modes keep shifted
     // values (i+j)*ge apart within int32 with margin; otherwise the row scan
-    const bool stripOk = (!local || (gapo < 0 && bits + 27 <= 63)) && span < (1ll << 28);
+    // (and scores below 2^26 by construction, so that no shifted key can wrap before the kernel flags it)
+    const bool stripOk = (!local || (gapo < 0 && bits + 27 <= 63 && smax * std::min(R, C) < (1ll << 26))) && span < (1ll << 28);
     if (!score_scan_forced() && stripOk)
     {
         s = score_ag_strip(ctx, seqY, R, seqX, C, subst, substsz, gapo, gape, local, out, st);

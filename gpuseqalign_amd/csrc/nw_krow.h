@@ -31,4 +31,11 @@ size_t krow_lds_bytes(int ns, int lw, int substsz);
 // The profile ring holds 512 columns for ns = 2, 1024 otherwise (lw is reserved).
 hipError_t launch_krow_fill(const StripArgs& a, int ns, int k, int lw, int grid, hipStream_t stream);
 
+// Score-only NW / SW (modes kModeScoreAG/AGL/SW/SWL of nw_strip.h, same StripArgs contract as
+// launch_strip_fill for one pair: go, ge, gran + gran2, agResult, swBest, idxBits) on the K-rows
+// layout (nw_kscore.hip): 1024-row tickets, grid > 0 workgroups.  Every s - go - ge must lie in
+// (-32768, 32767] (error bit 2 otherwise); SW needs go < 0 and ge <= 0.
+size_t krow_score_lds_bytes(int substsz);
+hipError_t launch_krow_score(const StripArgs& a, int mode, int grid, hipStream_t stream);
+
 }  // namespace gsa

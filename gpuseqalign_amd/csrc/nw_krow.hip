@@ -914,9 +914,681 @@ hipError_t launch_kr(const StripArgs& a, int grid, hipStream_t stream)
     return hipGetLastError();
 }
 
+#ifdef GSA_KROW_SCORE
+// ====================================================================================
+// Score-only NW / SW, linear or affine gaps, on the K-rows layout (nw_kscore.hip; BASELINE
+// configs[4]).  The same workgroup as the sparse fill -- 4 strip waves of K = 4 rows per lane, a
+// feeder, a profiler and a drain wave, one 1024-row ticket per workgroup -- with the shifted Gotoh
+// recurrence of the strip kernel's score modes (nw_strip.hip kModeScoreAG/SW/AGL/SWL):
+//   X' = X - (i+j) ge, d = go - ge, Hgo' = H' + d carried (H' alone when d = 0),
+//   E'(k,c) = max(E'(k,c-1), Hgo'(k,c-1)),  F'(k,c) = max(F'(k-1,c), Hgo'(k-1,c)),
+//   H'      = max3(Hgo'(k-1,c-1) + s - go - ge, E', F'),
+// the SW clamp H >= 0 folded into F' as the floor z = -(i+j) ge, the first maximal cell tracked
+// per row.  Two values cross strip boundaries (Hgo' and F' of the last row: two LDS rings, two
+// granule arrays between tickets); a linear gap carries H' only.  Column letters past C (and at
+// columns <= 0) are a NEG letter whose profile value is -32768: those cells are reached only
+// through a gap and never tie a real cell's score.
+// ====================================================================================
+constexpr int kNegS = -(1 << 29);  // "before the matrix": far from overflow, never the maximum
+constexpr int kNegQ = -32768;      // profile value of the NEG column letter
+constexpr uint32_t kRing2Off = (uint32_t)(kKrowNSDefault + 1) * kRing * 4u;  // ring2 = ring + this
+
+// LDS: profile as kr_layout, subT with one more row (the NEG letter), NS+1 rings of Hgo' and NS+1
+// of F', progress words
+struct KsLds
+{
+    uint32_t q, sub, ring, ring2, flags;
+};
+
+__host__ __device__ inline KsLds ks_layout(int substsz)
+{
+    constexpr int LW = 1024;
+    KsLds L;
+    L.q = 0;
+    L.sub = (kr_copy1(LW, substsz) + (uint32_t)substsz * kr_qrs(LW) + 16u) * 4u;
+    L.ring = L.sub + (uint32_t)(substsz + 1) * kSubRow * 4u;
+    L.ring2 = L.ring + kRing2Off;
+    L.flags = L.ring2 + kRing2Off;
+    return L;
+}
+
+// strip wave (NS = 4, K = 4): 256 rows, 4 per lane
+template <int MODE>
+__device__ __forceinline__ void ks_strip(const StripArgs& a, const KsLds& L, int tk, int w, int lane)
+{
+    constexpr int NS = kKrowNSDefault, K = 4, LW = 1024;
+    constexpr bool AG = !is_lin_mode(MODE);  // E' and F' carried
+    constexpr bool SW = is_sw_mode(MODE);
+    const int Cp = a.Cp;
+    const int ge = a.ge;
+    const int dd = AG ? a.go - a.ge : 0;
+    const int r0 = tk * (64 * K * NS) + 64 * K * w + 1;
+    const int rl = r0 + K * lane;
+    constexpr int kQRS = kr_qrs(LW), kQW = LW / 2;
+    uint32_t qrow[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+    {
+        const int r = rl + k;
+        int y = (r <= a.R) ? G(a.seqY)[r] : 0;
+        y = ((unsigned)y < (unsigned)a.substsz) ? y : 0;
+        qrow[k] = L.q + 4u * ((lane & 1) * kr_copy1(LW, a.substsz) + (uint32_t)y * kQRS);
+    }
+    const uint32_t ring_in = L.ring + (uint32_t)w * (kRing * 4u);
+    const uint32_t ring_out = L.ring + (uint32_t)(w + 1) * (kRing * 4u);
+    const uint32_t f_in = L.flags + kr_prog(w), f_out = L.flags + kr_prog(w + 1);
+    const uint32_t c_out = L.flags + kr_cons(w + 1);
+    const uint32_t f_xo = L.flags + kFXo;
+    const int NB = (Cp + 65 + kBlk - 1) / kBlk;
+    auto ok = [&](int pin, int pco, int pxo, int b) {
+        return pin >= kBlk * b + 64 + kBlk && pco >= kBlk * b + kBlk - kRing && (w != 0 || pxo >= kBlk * b + 2 * kBlk);
+    };
+    auto spin = [&](int b) {
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        for (int it = 1;; ++it)
+        {
+            const int pin = flag_ld(f_in), pco = flag_ld(c_out), pxo = (w == 0) ? flag_ld(f_xo) : 0;
+            if (ok(pin, pco, pxo, b)) return true;
+            __builtin_amdgcn_s_sleep(1);
+            if (__builtin_amdgcn_s_memrealtime() - t0 > a.spin || ((it & 31) == 0 && err_set(a)))
+            {
+                atomicOr(a.err, 1u);
+                return false;
+            }
+        }
+    };
+    // halo of block b (Hgo' and, affine, F' of the row above): lane 0 reads ring elements
+    // 16b+64 .. +15 of both rings, the other lanes keep 0 (exec set and restored in the asm)
+    int4v hc[kHalo], hf[kHalo];
+#pragma unroll
+    for (int j = 0; j < kHalo; ++j)
+    {
+        hc[j] = int4v {0, 0, 0, 0};
+        hf[j] = int4v {0, 0, 0, 0};
+    }
+    auto halo_load = [&](int b) {
+        const uint32_t hb = ring_in + 4u * (uint32_t)((kBlk * b + 64) & (kRing - 1));
+        uint64_t sv;
+        if constexpr (AG)
+            asm volatile(
+                "s_mov_b64 %8, exec\n"
+                "s_mov_b64 exec, 1\n"
+                "ds_read_b128 %0, %9\n"
+                "ds_read_b128 %1, %9 offset:16\n"
+                "ds_read_b128 %2, %9 offset:32\n"
+                "ds_read_b128 %3, %9 offset:48\n"
+                "ds_read_b128 %4, %9 offset:%10\n"
+                "ds_read_b128 %5, %9 offset:%11\n"
+                "ds_read_b128 %6, %9 offset:%12\n"
+                "ds_read_b128 %7, %9 offset:%13\n"
+                "s_mov_b64 exec, %8\n"
+                "s_waitcnt lgkmcnt(0)"
+                : "+v"(hc[0]), "+v"(hc[1]), "+v"(hc[2]), "+v"(hc[3]), "+v"(hf[0]), "+v"(hf[1]), "+v"(hf[2]), "+v"(hf[3]),
+                  "=&s"(sv)
+                : "v"(hb), "n"(kRing2Off), "n"(kRing2Off + 16), "n"(kRing2Off + 32), "n"(kRing2Off + 48)
+                : "memory");
+        else
+            asm volatile(
+                "s_mov_b64 %4, exec\n"
+                "s_mov_b64 exec, 1\n"
+                "ds_read_b128 %0, %5\n"
+                "ds_read_b128 %1, %5 offset:16\n"
+                "ds_read_b128 %2, %5 offset:32\n"
+                "ds_read_b128 %3, %5 offset:48\n"
+                "s_mov_b64 exec, %4\n"
+                "s_waitcnt lgkmcnt(0)"
+                : "+v"(hc[0]), "+v"(hc[1]), "+v"(hc[2]), "+v"(hc[3]), "=&s"(sv)
+                : "v"(hb)
+                : "memory");
+    };
+    auto q_off = [&](int b) { return 4u * (uint32_t)((8 * b - (lane >> 1)) & (kQW - 1)); };
+    int qA[K][8], qB[K][8];
+    {
+        const uint32_t p = q_off(0);
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) qA[k][j] = 0;
+        if (!spin(-1)) return;
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) qA[k][j] = lds_ld(qrow[k] + p + 4u * j);
+    }
+    // Hgo' (H' when linear), E' of the K rows, F' of the last row, the diagonal of row 0
+    int H[K], E[K], FD = kNegS, D = kNegS;
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+    {
+        H[k] = kNegS;
+        E[k] = kNegS;
+    }
+    // SW: floors z_k = -(i+j) ge of the lane's rows at the current column (column t - lane) and the
+    // first maximum per row.  One key per cell, ((h_k - z_0) << 4) + 15 - u = (h_k << 4) + wv with
+    // wv = 15 - u - 16 z_0 shared by the rows: h_k - z_0 = H + k |ge| >= 0 is the score of row k
+    // plus a per-row constant, so the maximum per row and its first step are those of H; the
+    // block's best is folded (score - k |ge|, step) at the block end.  Rows past R never win.
+    int z[K], p[K], best[K], tb[K];
+    uint32_t wv = 0;  // (mod 2^32: the keys themselves stay below 2^31 while scores stay below 2^26)
+    if constexpr (SW)
+    {
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+        {
+            z[k] = -(rl + k - lane) * ge;
+            p[k] = 0;
+            best[k] = (rl + k <= a.R) ? 0 : 0x7fffffff;
+            tb[k] = 0;
+        }
+    }
+    // NW: the cell (R, C) lies in this strip iff r0 <= R < r0 + 256; lane laneR reaches column C
+    // at step tStar, in block tStar / 16, row kR
+    const int rR = a.R - r0;
+    const bool hasR = !SW && rR >= 0 && rR < 64 * K;
+    const int laneR = rR >> 2, kR = rR & 3, tStar = a.C + laneR;
+    int lt[kBlk], lf[kBlk];  // lane 63's hand-off values of the last block (Hgo', F' of columns t-64)
+    auto handoff = [&](int bb) {
+        const uint32_t eb = ring_out + 4u * (uint32_t)((kBlk * bb) & (kRing - 1));
+        uint64_t sv;
+        if constexpr (AG)
+            asm volatile(
+                "s_mov_b64 %0, exec\n"
+                "s_mov_b64 exec, %1\n"
+                "ds_write_b128 %2, %3\n"
+                "ds_write_b128 %2, %4 offset:16\n"
+                "ds_write_b128 %2, %5 offset:32\n"
+                "ds_write_b128 %2, %6 offset:48\n"
+                "ds_write_b128 %2, %7 offset:%11\n"
+                "ds_write_b128 %2, %8 offset:%12\n"
+                "ds_write_b128 %2, %9 offset:%13\n"
+                "ds_write_b128 %2, %10 offset:%14\n"
+                "s_mov_b64 exec, %0"
+                : "=&s"(sv)
+                : "s"(1ull << 63), "v"(eb), "v"(int4v {lt[0], lt[1], lt[2], lt[3]}), "v"(int4v {lt[4], lt[5], lt[6], lt[7]}),
+                  "v"(int4v {lt[8], lt[9], lt[10], lt[11]}), "v"(int4v {lt[12], lt[13], lt[14], lt[15]}),
+                  "v"(int4v {lf[0], lf[1], lf[2], lf[3]}), "v"(int4v {lf[4], lf[5], lf[6], lf[7]}),
+                  "v"(int4v {lf[8], lf[9], lf[10], lf[11]}), "v"(int4v {lf[12], lf[13], lf[14], lf[15]}), "n"(kRing2Off),
+                  "n"(kRing2Off + 16), "n"(kRing2Off + 32), "n"(kRing2Off + 48)
+                : "memory");
+        else
+            asm volatile(
+                "s_mov_b64 %0, exec\n"
+                "s_mov_b64 exec, %1\n"
+                "ds_write_b128 %2, %3\n"
+                "ds_write_b128 %2, %4 offset:16\n"
+                "ds_write_b128 %2, %5 offset:32\n"
+                "ds_write_b128 %2, %6 offset:48\n"
+                "s_mov_b64 exec, %0"
+                : "=&s"(sv)
+                : "s"(1ull << 63), "v"(eb), "v"(int4v {lt[0], lt[1], lt[2], lt[3]}), "v"(int4v {lt[4], lt[5], lt[6], lt[7]}),
+                  "v"(int4v {lt[8], lt[9], lt[10], lt[11]}), "v"(int4v {lt[12], lt[13], lt[14], lt[15]})
+                : "memory");
+        flag_st2(f_out, bb + 1 == NB ? kBig : kBlk * bb + kBlk, kBlk * bb + 64 + kBlk);
+    };
+    int rpin = 0, rpco = 0, rpxo = 0, rsink = 0;
+
+    auto block = [&](int b, int (&qc)[K][8], int (&qn)[K][8]) {
+        {
+            const int pin = __builtin_amdgcn_readfirstlane(rpin), pco = __builtin_amdgcn_readfirstlane(rpco);
+            const int pxo = (w == 0) ? __builtin_amdgcn_readfirstlane(rpxo) : 0;
+            asm volatile("" ::"v"(rpin), "v"(rpco), "v"(rpxo), "v"(rsink));  // (kr_strip: WAW on the read)
+            if (!ok(pin, pco, pxo, b) && !spin(b)) return false;
+        }
+        halo_load(b);
+        const uint32_t pn = q_off(b + 1);
+        int va[SW ? 1 : K][SW ? 1 : kBlk];  // NW: the block's Hgo' (result cell)
+#pragma unroll
+        for (int u = 0; u < kBlk; ++u)
+        {
+            const int upH = shr1z(H[K - 1]) + hc[u >> 2][u & 3];
+            const int upF = AG ? shr1z(FD) + hf[u >> 2][u & 3] : 0;
+            int nh[K], ne[K], h[K];
+            int f = 0;
+#pragma unroll
+            for (int k = 0; k < K; ++k)
+            {
+                const int q = (u & 1) ? qhi(qc[k][u >> 1]) : qlo(qc[k][u >> 1]);
+                const int dg = (k == 0 ? D : H[k - 1]) + q;
+                const int vup = (k == 0) ? upH : nh[k - 1];
+                if constexpr (AG)
+                {
+                    const int fprev = (k == 0) ? upF : f;
+                    f = SW ? max3i(fprev, vup, z[k]) : max(fprev, vup);
+                    ne[k] = max(E[k], H[k]);
+                    h[k] = max3i(dg, ne[k], f);
+                    nh[k] = h[k] + dd;
+                }
+                else
+                {
+                    f = SW ? max(vup, z[k]) : vup;
+                    h[k] = max3i(dg, H[k], f);
+                    nh[k] = h[k];
+                }
+            }
+            if constexpr (SW)
+            {
+#pragma unroll
+                for (int k = 0; k < K; ++k)
+                {
+                    p[k] = max(p[k], (int)(((uint32_t)h[k] << 4) + wv));
+                    z[k] -= ge;
+                }
+                wv += 16u * (uint32_t)ge - 1u;
+            }
+            if (u < 8)
+#pragma unroll
+                for (int k = 0; k < K; ++k) qn[k][u] = lds_ld(qrow[k] + pn + 4u * u);
+            lt[u] = H[K - 1];
+            if constexpr (AG) lf[u] = FD;
+            D = upH;
+#pragma unroll
+            for (int k = 0; k < K; ++k)
+            {
+                H[k] = nh[k];
+                if constexpr (AG) E[k] = ne[k];
+                if constexpr (!SW) va[k][u] = nh[k];
+            }
+            if constexpr (AG) FD = f;
+            if (u == kBlk - 2)
+            {
+                asm volatile("" ::: "memory");
+                const int2v lo = *(const int2v*)(krsm + f_in), hi = *(const int2v*)(krsm + f_in + 16u);
+                asm volatile("" ::: "memory");
+                rpin = lo.x;
+                rpxo = lo.y;
+                rpco = hi.y;
+                rsink = hi.x;
+            }
+        }
+        handoff(b);
+        if constexpr (SW)
+        {
+            // fold the block's best per row: score = key >> 4 - k |ge|, first step 15 - key & 15
+#pragma unroll
+            for (int k = 0; k < K; ++k)
+            {
+                const int v = (p[k] >> 4) + k * ge;
+                const bool up = v > best[k];
+                best[k] = up ? v : best[k];
+                tb[k] = up ? kBlk * b + 15 - (p[k] & 15) : tb[k];
+                p[k] = 0;
+            }
+            wv = 15u - 16u * (uint32_t)z[0];
+        }
+        else
+        {
+            if (hasR && (tStar >> 4) == b)
+            {
+                // (uniform) the result cell: lane laneR, row kR, step tStar & 15 of this block;
+                // that lane parks the block's values in LDS and reads the one back
+                const uint32_t scr = L.flags + 256u;
+                if (lane == laneR)
+                {
+#pragma unroll
+                    for (int k = 0; k < K; ++k)
+#pragma unroll
+                        for (int u = 0; u < kBlk; ++u) lds_st(scr + 4u * (uint32_t)(kBlk * k + u), va[k][u]);
+                    const int v = lds_ld(scr + 4u * (uint32_t)(kBlk * kR + (tStar & 15)));
+                    G(a.agResult)[0] = v - dd + (a.R + a.C) * ge;
+                }
+            }
+        }
+        return true;
+    };
+
+    if constexpr (SW) wv = 15u - 16u * (uint32_t)z[0];
+    for (int b = 0; b < NB; b += 2)
+    {
+        if (!block(b, qA, qB)) return;
+        if (b + 1 >= NB) break;
+        if (!block(b + 1, qB, qA)) return;
+    }
+    if constexpr (SW)
+    {
+        // this lane's best cell, first in row-major order (rows in order, first step per row):
+        // key score << idxBits | (2^idxBits - 1 - row-major index); one 64-bit atomicMax per lane
+        const unsigned long long W = (unsigned long long)a.C + 1, mask = (1ull << a.idxBits) - 1;
+        unsigned long long key = 0;
+        bool big = false;
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+        {
+            const bool in = rl + k <= a.R;
+            // a score >= 2^26 (before the packing could wrap): the host's row scan
+            big |= in && best[k] >= (1 << 26);
+            if (in && best[k] > 0)
+            {
+                const unsigned long long idx = (unsigned long long)(rl + k) * W + (unsigned long long)(tb[k] - lane);
+                const unsigned long long kk = ((unsigned long long)best[k] << a.idxBits) | (mask - idx);
+                key = kk > key ? kk : key;
+            }
+        }
+        if (key) atomicMax(a.swBest, key);
+        if (big) atomicOr((unsigned*)a.agResult, 1u);
+    }
+}
+
+// feeder wave: the row above strip 0 (Hgo' and F') into ring 0 -- ticket 0 from the border
+// generator, later tickets from the previous ticket's granules (both arrays, in column order)
+template <int MODE>
+__device__ __forceinline__ void ks_feed(const StripArgs& a, const KsLds& L, int tk, int lane)
+{
+    constexpr bool AG = !is_lin_mode(MODE);
+    const int Cp = a.Cp;
+    const int dd = AG ? a.go - a.ge : 0;
+    const uint32_t F = L.flags;
+    const size_t prev = (size_t)(tk > 0 ? tk - 1 : 0) * a.granStride;
+    const gptr<const unsigned long long> gp = G((const unsigned long long*)a.gran) + prev;
+    const gptr<const unsigned long long> gp2 = G((const unsigned long long*)a.gran2) + prev;
+    int hnext = 0, c0 = 0, pw = 64;
+    uint64_t last = __builtin_amdgcn_s_memrealtime();
+    unsigned idle = 0;
+    while (hnext <= Cp)
+    {
+        bool moved = false;
+        if (hnext + 128 > c0 + kRing) c0 = flag_ld(F + kr_cons(0));
+        const bool feed = hnext + 128 <= c0 + kRing;
+        const int c = hnext + lane;
+        const bool in = c <= Cp && lane < pw;
+        unsigned long long q = 0ull, q2 = 0ull;
+        if (feed && tk > 0 && in)
+        {
+            q = __hip_atomic_load(gp + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if constexpr (AG) q2 = __hip_atomic_load(gp2 + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (feed)
+        {
+            int v, v2 = kNegS;
+            bool good;
+            if (tk == 0)
+            {
+                // row 0 shifted: global H'(0,c) = d for c >= 1 (0 at c = 0), local -c ge (H = 0);
+                // carried as Hgo' = H' + d; F' = -inf
+                v = is_sw_mode(MODE) ? dd - c * a.ge : (c == 0 ? dd : 2 * dd);
+                good = in;
+            }
+            else
+            {
+                good = in && (uint32_t)(q >> 32) == a.epoch && (!AG || (uint32_t)(q2 >> 32) == a.epoch);
+                v = (int)(uint32_t)q;
+                v2 = (int)(uint32_t)q2;
+            }
+            const uint64_t badm = __ballot(!good);
+            const int n = badm ? __builtin_ctzll(badm) : 64;
+            if (tk > 0) pw = max(32, min(64, (n & ~15) + 16));
+            if (n > 0)
+            {
+                if (lane < n)
+                {
+                    const uint32_t o = 4u * (uint32_t)((c + 64) & (kRing - 1));
+                    lds_st(L.ring + o, v);
+                    if constexpr (AG) lds_st(L.ring2 + o, v2);
+                }
+                hnext += n;
+                flag_st(F, hnext > Cp ? kBig : hnext + 64);
+                moved = true;
+            }
+        }
+        const uint64_t now = __builtin_amdgcn_s_memrealtime();
+        if (moved)
+            last = now;
+        else
+        {
+            if (now - last > a.spin || ((++idle & 63) == 0 && err_set(a)))
+            {
+                atomicOr(a.err, 1u);
+                return;
+            }
+            if (tk == 0) __builtin_amdgcn_s_sleep(1);
+        }
+    }
+}
+
+// profiler wave: kr_loader's profile job (ROLE 2) with the NEG letter for columns <= 0 and > C
+__device__ __forceinline__ void ks_profile(const StripArgs& a, const KsLds& L, int lane)
+{
+    constexpr int NS = kKrowNSDefault, LW = 1024;
+    const int Cp = a.Cp, C = a.C;
+    constexpr int kQRS = kr_qrs(LW), kQW = LW / 2;
+    const uint32_t F = L.flags;
+    auto letter = [&](int c) {
+        if (c < 1 || c > C) return a.substsz;  // NEG
+        const int x = G(a.seqX)[c];
+        return ((unsigned)x < (unsigned)a.substsz) ? x : 0;
+    };
+    // columns -64 .. -1 (the ring's last 32 dwords of both copies, read by lanes still left of
+    // column 0 in the first 4 blocks): NEG, or a stale profile there would lift the SW floor's
+    // values at negative columns and flow into column 0 through E'.  The first batch that
+    // overwrites them (columns 960..) waits until every strip is past them.
+    for (int i = lane; i < 2 * 32 * a.substsz; i += 64)
+    {
+        const int yy = i >> 6, cp = (i >> 5) & 1, dw = kQW - 32 + (i & 31);
+        lds_st(L.q + 4u * ((cp ? kr_copy1(LW, a.substsz) : 0u) + kQRS * (uint32_t)yy + (uint32_t)dw), (int)0x80008000u);
+    }
+    int qn = 0;
+    int xm = letter(2 * lane - 1), x0 = letter(2 * lane), x1 = letter(2 * lane + 1);
+    int nxm = 0, nx0 = 0, nx1 = 0;
+    int qsub = 0, pl = 0;
+    uint64_t last = __builtin_amdgcn_s_memrealtime();
+    unsigned idle = 0;
+    while (qn <= Cp)
+    {
+        bool moved = false;
+        if (qsub == 0 && qn + 192 > pl + LW) pl = flag_ld(F + kr_prog(NS));
+        if (qsub > 0 || qn + 192 <= pl + LW)
+        {
+            int4v vm[2], v0[2], v1[2];
+            {
+                const uint32_t o = 32u * (uint32_t)qsub;
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+                {
+                    vm[j] = lds_ld4(L.sub + 4u * kSubRow * (uint32_t)xm + o + 16u * j);
+                    v0[j] = lds_ld4(L.sub + 4u * kSubRow * (uint32_t)x0 + o + 16u * j);
+                    v1[j] = lds_ld4(L.sub + 4u * kSubRow * (uint32_t)x1 + o + 16u * j);
+                }
+            }
+            if (qsub == 0)
+            {
+                const int cn = qn + kBatch + 2 * lane;
+                nxm = letter(cn - 1);
+                nx0 = letter(cn);
+                nx1 = letter(cn + 1);
+            }
+            const uint32_t d = (uint32_t)((qn / 2 + lane) & (kQW - 1));
+            const bool guard = d < 8;
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+            {
+                const int yy = 8 * qsub + i;
+                if (yy < a.substsz)
+                {
+                    const int s0 = v0[i >> 2][i & 3];
+                    const int p0 = (s0 & 0xffff) | (v1[i >> 2][i & 3] << 16);
+                    const int p1 = (vm[i >> 2][i & 3] & 0xffff) | (s0 << 16);
+                    const uint32_t r0a = L.q + 4u * (kQRS * (uint32_t)yy + d);
+                    const uint32_t r1a = L.q + 4u * (kr_copy1(LW, a.substsz) + kQRS * (uint32_t)yy + d);
+                    lds_st(r0a, p0);
+                    lds_st(r1a, p1);
+                    if (guard)
+                    {
+                        lds_st(r0a + 4u * kQW, p0);
+                        lds_st(r1a + 4u * kQW, p1);
+                    }
+                }
+            }
+            if (++qsub == 4 || 8 * qsub >= a.substsz)
+            {
+                qsub = 0;
+                xm = nxm;
+                x0 = nx0;
+                x1 = nx1;
+                qn += kBatch;
+                flag_st(F + kFXo, qn > Cp ? kBig : qn);
+            }
+            moved = true;
+        }
+        const uint64_t now = __builtin_amdgcn_s_memrealtime();
+        if (moved)
+            last = now;
+        else
+        {
+            if (now - last > a.spin || ((++idle & 63) == 0 && err_set(a)))
+            {
+                atomicOr(a.err, 1u);
+                return;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+}
+
+// drain wave: the last strip's Hgo' (and F') -> granules for the next ticket
+template <int MODE>
+__device__ __forceinline__ void ks_drain(const StripArgs& a, const KsLds& L, int tk, int lane)
+{
+    constexpr int NS = kKrowNSDefault;
+    constexpr bool AG = !is_lin_mode(MODE);
+    const int Cp = a.Cp;
+    const uint32_t F = L.flags, ringN = L.ring + (uint32_t)NS * (kRing * 4u);
+    if (tk + 1 >= a.nTickets)
+    {
+        flag_st(F + kr_cons(NS), kBig);  // nobody reads our last row
+        return;
+    }
+    const size_t off = (size_t)tk * a.granStride;
+    const gptr<unsigned long long> go = G(a.gran) + off;
+    const gptr<unsigned long long> go2 = G(a.gran2) + off;
+    const unsigned long long ep = (unsigned long long)a.epoch << 32;
+    int dnext = 0;
+    uint64_t last = __builtin_amdgcn_s_memrealtime();
+    unsigned idle = 0;
+    while (dnext <= Cp)
+    {
+        const int avail = min(flag_ld(F + kr_prog(NS)) - 64, Cp + 1);
+        if (dnext < avail)
+        {
+            const int c = dnext + lane;
+            if (c < avail)
+            {
+                const uint32_t o = 4u * (uint32_t)((c + 64) & (kRing - 1));
+                const int v = lds_ld(ringN + o);
+                if constexpr (AG)
+                {
+                    const int v2 = lds_ld(ringN + kRing2Off + o);
+                    __hip_atomic_store(go2 + c, ep | (uint32_t)v2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+                __hip_atomic_store(go + c, ep | (uint32_t)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            dnext = min(dnext + 64, avail);
+            flag_st(F + kr_cons(NS), dnext > Cp ? kBig : dnext + 64);
+            last = __builtin_amdgcn_s_memrealtime();
+        }
+        else
+        {
+            if (__builtin_amdgcn_s_memrealtime() - last > a.spin || ((++idle & 63) == 0 && err_set(a)))
+            {
+                atomicOr(a.err, 1u);
+                return;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+}
+
+template <int MODE>
+__global__ void __launch_bounds__(64 * kr_waves<kKrowNSDefault>()) nw_kscore_kernel(StripArgs a)
+{
+    constexpr int NS = kKrowNSDefault;
+    constexpr int kThreads = 64 * kr_waves<NS>();
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const KsLds L = ks_layout(a.substsz);
+    // subT[x][y] = s(y, x) - go - ge (int16 range checked), row x = substsz: the NEG letter
+    bool bad = false;
+    for (int k = threadIdx.x; k < (a.substsz + 1) * kSubRow; k += kThreads)
+    {
+        const int x = k / kSubRow, yy = k % kSubRow;
+        int v = 0;
+        if (yy < a.substsz)
+        {
+            if (x < a.substsz)
+            {
+                v = G(a.subst)[yy * a.substsz + x] - a.go - a.ge;
+                bad |= v <= kNegQ || v > 32767;
+            }
+            else
+                v = kNegQ;
+        }
+        lds_st(L.sub + 4u * k, v);
+    }
+    if (bad) atomicOr(a.err, 2u);
+    for (;;)
+    {
+        __syncthreads();
+        if (threadIdx.x == 0) lds_st(L.flags + kFTicket, err_set(a) ? a.nTicketsTotal : (int)atomicAdd(a.ticket, 1u));
+        __syncthreads();
+        const int tk = __builtin_amdgcn_readfirstlane(lds_ld(L.flags + kFTicket));
+        if (tk >= a.nTicketsTotal) break;
+        // one pair (gsa_score): its descriptor
+        const PairDesc d = kr_desc(a.pairs);
+        StripArgs pa = a;
+        pa.seqY = d.seqY;
+        pa.seqX = d.seqX;
+        pa.R = d.R;
+        pa.C = d.C;
+        pa.Cp = d.Cp;
+        pa.nTickets = d.nTickets;
+        pa.granStride = gran_stride(d.Cp);
+        if (threadIdx.x < 32) lds_st(L.flags + 4u * threadIdx.x, 0);
+        // rings: -inf, so columns no writer reaches (past C at the strips' ends) hold nothing larger
+        for (int k = threadIdx.x; k < 2 * (NS + 1) * kRing; k += kThreads) lds_st(L.ring + 4u * k, kNegS);
+        __syncthreads();
+        if (w == NS + 1)
+            ks_drain<MODE>(pa, L, tk, lane);
+        else if (w == NS)
+            ks_feed<MODE>(pa, L, tk, lane);
+        else if (w == NS + 2)
+            ks_profile(pa, L, lane);
+        else
+        {
+            __builtin_amdgcn_s_setprio(3);
+            ks_strip<MODE>(pa, L, tk, w, lane);
+            __builtin_amdgcn_s_setprio(0);
+        }
+    }
+}
+
+template <int MODE>
+hipError_t launch_ks(const StripArgs& a, int grid, hipStream_t stream)
+{
+    const size_t lds = krow_score_lds_bytes(a.substsz);
+    auto kern = nw_kscore_kernel<MODE>;
+    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+    constexpr int kThreads = 64 * kr_waves<kKrowNSDefault>();
+    if ((e = record_foot((const void*)kern, lds, kThreads, grid)) != hipSuccess) return e;
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreads), lds, stream, a);
+    return hipGetLastError();
+}
+#endif  // GSA_KROW_SCORE
+
 }  // namespace
 
-#ifdef GSA_KROW_BATCH8
+#if defined(GSA_KROW_SCORE)
+// progress words (256 B) and the NW result cell's scratch (64 ints)
+size_t krow_score_lds_bytes(int substsz) { return (size_t)ks_layout(substsz).flags + 512; }
+
+hipError_t launch_krow_score(const StripArgs& a, int mode, int grid, hipStream_t stream)
+{
+    if (a.nPairs != 1 || grid <= 0) return hipErrorInvalidValue;
+    if (mode == kModeScoreAG) return launch_ks<kModeScoreAG>(a, grid, stream);
+    if (mode == kModeScoreAGL) return launch_ks<kModeScoreAGL>(a, grid, stream);
+    if (mode == kModeScoreSW) return launch_ks<kModeScoreSW>(a, grid, stream);
+    if (mode == kModeScoreSWL) return launch_ks<kModeScoreSWL>(a, grid, stream);
+    return hipErrorInvalidValue;
+}
+#elif defined(GSA_KROW_BATCH8)
 // nw_krow8.hip: the 8-strip batch instance in a translation unit of its own, so it can be built
 // with another instruction scheduler than the single-pair instances (Makefile)
 hipError_t launch_krow_fill_b8(const StripArgs& a, int grid, hipStream_t stream)
