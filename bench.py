@@ -303,7 +303,8 @@ def bench_config5(dev, eng, steps, warmup, cpu_sample, rank, world):
         out[name] = {"value": round(R * C / kms / 1e6, 2), "unit": "GCUPS", "kernel_ms": round(kms, 4),
                      "ms_per_call": round(wall * 1e3, 4), "score": r["score"], "end": [r["i_end"], r["j_end"]],
                      "golden_match": ok, "gapo": go, "gape": ge, "local": local,
-                     "kernel": "gsa::nw_strip_kernel score mode (%s)" % (
+                     "kernel": "gsa::nw_kscore_kernel<%d> (%s)" % (
+                         (5 if go == ge else 4) if local else (6 if go == ge else 3),
                          ("kModeScoreSWL" if go == ge else "kModeScoreSW") if local else
                          ("kModeScoreAGL" if go == ge else "kModeScoreAG"))}
         if cpu_sample > 0 and rank == 0 and world == 1:

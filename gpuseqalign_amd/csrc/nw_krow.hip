@@ -1068,14 +1068,15 @@ __device__ __forceinline__ void ks_strip(const StripArgs& a, const KsLds& L, int
     // wv = 15 - u - 16 z_0 shared by the rows: h_k - z_0 = H + k |ge| >= 0 is the score of row k
     // plus a per-row constant, so the maximum per row and its first step are those of H; the
     // block's best is folded (score - k |ge|, step) at the block end.  Rows past R never win.
-    int z[K], p[K], best[K], tb[K];
+    // (row k's floor at step u is row 0's at step u + k, the same anti-diagonal: one add per step)
+    int z0 = 0, p[K], best[K], tb[K];
     uint32_t wv = 0;  // (mod 2^32: the keys themselves stay below 2^31 while scores stay below 2^26)
     if constexpr (SW)
     {
+        z0 = -(rl - lane) * ge;
 #pragma unroll
         for (int k = 0; k < K; ++k)
         {
-            z[k] = -(rl + k - lane) * ge;
             p[k] = 0;
             best[k] = (rl + k <= a.R) ? 0 : 0x7fffffff;
             tb[k] = 0;
@@ -1137,6 +1138,13 @@ __device__ __forceinline__ void ks_strip(const StripArgs& a, const KsLds& L, int
         halo_load(b);
         const uint32_t pn = q_off(b + 1);
         int va[SW ? 1 : K][SW ? 1 : kBlk];  // NW: the block's Hgo' (result cell)
+        int zz[SW ? kBlk + K : 1];          // SW: row 0's floor at steps 0 .. 19 of the block
+        if constexpr (SW)
+        {
+            zz[0] = z0;
+#pragma unroll
+            for (int i = 1; i < kBlk + K; ++i) zz[i] = zz[i - 1] - ge;
+        }
 #pragma unroll
         for (int u = 0; u < kBlk; ++u)
         {
@@ -1153,14 +1161,14 @@ __device__ __forceinline__ void ks_strip(const StripArgs& a, const KsLds& L, int
                 if constexpr (AG)
                 {
                     const int fprev = (k == 0) ? upF : f;
-                    f = SW ? max3i(fprev, vup, z[k]) : max(fprev, vup);
+                    f = SW ? max3i(fprev, vup, zz[SW ? u + k : 0]) : max(fprev, vup);
                     ne[k] = max(E[k], H[k]);
                     h[k] = max3i(dg, ne[k], f);
                     nh[k] = h[k] + dd;
                 }
                 else
                 {
-                    f = SW ? max(vup, z[k]) : vup;
+                    f = SW ? max(vup, zz[SW ? u + k : 0]) : vup;
                     h[k] = max3i(dg, H[k], f);
                     nh[k] = h[k];
                 }
@@ -1171,7 +1179,6 @@ __device__ __forceinline__ void ks_strip(const StripArgs& a, const KsLds& L, int
                 for (int k = 0; k < K; ++k)
                 {
                     p[k] = max(p[k], (int)(((uint32_t)h[k] << 4) + wv));
-                    z[k] -= ge;
                 }
                 wv += 16u * (uint32_t)ge - 1u;
             }
@@ -1213,7 +1220,8 @@ __device__ __forceinline__ void ks_strip(const StripArgs& a, const KsLds& L, int
                 tb[k] = up ? kBlk * b + 15 - (p[k] & 15) : tb[k];
                 p[k] = 0;
             }
-            wv = 15u - 16u * (uint32_t)z[0];
+            z0 = zz[SW ? kBlk : 0];
+            wv = 15u - 16u * (uint32_t)z0;
         }
         else
         {
@@ -1236,7 +1244,7 @@ __device__ __forceinline__ void ks_strip(const StripArgs& a, const KsLds& L, int
         return true;
     };
 
-    if constexpr (SW) wv = 15u - 16u * (uint32_t)z[0];
+    if constexpr (SW) wv = 15u - 16u * (uint32_t)z0;
     for (int b = 0; b < NB; b += 2)
     {
         if (!block(b, qA, qB)) return;

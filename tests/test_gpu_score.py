@@ -129,3 +129,27 @@ def test_local_fallbacks_to_row_scan(engine, golden):
     assert ref[0] >= 1 << 26
     r = engine.score(Y, X, sub, -11, -1, True)
     assert (r["score"], r["i_end"], r["j_end"]) == ref
+
+
+@pytest.mark.parametrize("R,C", [(300, 1), (65, 63), (700, 130), (1500, 1000)])
+@pytest.mark.parametrize("go,ge,local", MODES)
+def test_strip_kernel_path(engine, golden, R, C, go, ge, local, monkeypatch):
+    """GSA_SCORE_KERNEL=strip: the strip kernel's score modes (nw_strip.hip), kept reachable beside
+    the K-rows score kernel (nw_kscore.hip) that runs by default."""
+    import oracle
+    monkeypatch.setenv("GSA_SCORE_KERNEL", "strip")
+    Y, X = random_pair(R, C, 7 * R + C)
+    r = engine.score(Y, X, golden.blosum62, go, ge, local)
+    assert (r["score"], r["i_end"], r["j_end"]) == oracle.score_ag(Y, X, golden.blosum62, go, ge, local)
+
+
+@pytest.mark.parametrize("R", [2048, 2049, 2050, 2051, 2052, 3071])
+@pytest.mark.parametrize("go,ge,local", MODES)
+def test_result_row_positions(engine, golden, R, go, ge, local):
+    """The K-rows score kernel reads the NW result cell (R, C) from the lane and row that hold it
+    (row kR = (R - 1) mod 4 of lane (R - r0) / 4 of a later ticket's strip): every kR, a strip's
+    first and last rows."""
+    import oracle
+    Y, X = random_pair(R, 257, R + 11)
+    r = engine.score(Y, X, golden.blosum62, go, ge, local)
+    assert (r["score"], r["i_end"], r["j_end"]) == oracle.score_ag(Y, X, golden.blosum62, go, ge, local)
