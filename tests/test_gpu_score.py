@@ -153,3 +153,16 @@ def test_result_row_positions(engine, golden, R, go, ge, local):
     Y, X = random_pair(R, 257, R + 11)
     r = engine.score(Y, X, golden.blosum62, go, ge, local)
     assert (r["score"], r["i_end"], r["j_end"]) == oracle.score_ag(Y, X, golden.blosum62, go, ge, local)
+
+
+@pytest.mark.parametrize("substsz", [4, 25, 26, 32])
+@pytest.mark.parametrize("go,ge,local", MODES)
+def test_alphabet_sizes(engine, golden, substsz, go, ge, local):
+    """Other alphabets: the K-rows score kernel's LDS holds a profile row per letter (substsz <= 25
+    or so fits; 32 letters exceed the 160 KB and take the strip kernel), so every path is reached."""
+    import oracle
+    rng = np.random.default_rng(substsz * 100 + 7)
+    sub = rng.integers(-6, 12, size=(substsz, substsz)).astype(np.int32)
+    Y, X = random_pair(1500, 1100, substsz + 5, alphabet=substsz)
+    r = engine.score(Y, X, sub, go, ge, local)
+    assert (r["score"], r["i_end"], r["j_end"]) == oracle.score_ag(Y, X, sub, go, ge, local)
