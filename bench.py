@@ -76,12 +76,15 @@ def lane_ns():
 
 def sparse_kernel_name():
     """The K-rows instantiation a single-pair sparse fill runs (gsa_capi.hip: GSA_KROW_NS / GSA_KROW_K,
-    default (4, 4); the profile ring is 512 columns with 2 strips, 1024 otherwise)."""
+    default (4, 4); the profile ring is 512 columns with 2 strips, 1024 otherwise; GSA_KROW_Q8=0: the
+    int16 profile instance instead of the int8 one)."""
     ns, k = os.environ.get("GSA_KROW_NS", "4"), os.environ.get("GSA_KROW_K", "4")
     ok = (k in ("2", "4") and ns in ("2", "4")) or (k == "4" and ns == "8")
     ns, k = (int(ns), int(k)) if ok else (4, 4)
     lw = 512 if ns == 2 else 1024
-    return f"gsa::nw_krow_kernel<{ns},{k},{lw},false> (sparse, K = {k} rows per lane)"
+    q8 = os.environ.get("GSA_KROW_Q8", "1") != "0"
+    return (f"gsa::nw_krow_kernel<{ns},{k},{lw},false,{'true' if q8 else 'false'}> (sparse, K = {k} rows per lane, "
+            f"{'int8' if q8 else 'int16'} column profile" + ("; the int16 instance behind it is a ~5 us no-op)" if q8 else ")"))
 
 
 def cpu_topology():

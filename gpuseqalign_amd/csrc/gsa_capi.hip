@@ -405,6 +405,11 @@ int enqueue_batch(gsa_ctx* ctx, int mode, int npairs, const gsa_pair_dev* pairs,
         krowNS = gsa::kKrowNSDefault;
     }
     a.ns = lane ? lane_ns() : krow ? krowNS : gsa::kSparseNS;
+    // the K-rows fill's int8 column profile (its instance declines a table outside int8 and the int16
+    // one runs instead) wherever its LDS fits; GSA_KROW_Q8=0 keeps the int16 profile
+    if (krow && env_int("GSA_KROW_Q8", 1) != 0)
+        a.q8 = gsa::krow_lds_bytes(krowNS, krowNS == 2 ? 512 : 1024, substsz, true) <= (size_t)ctx->lds_max ? 1 : 0;
+    a.q8flag = ctx->ctl + 2;
     const int fullRows = gsa::kLaneRows * a.ns;  // rows per ticket of a full fill
     if (mode == gsa::kModeSparse)
     {

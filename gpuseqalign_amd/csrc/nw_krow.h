@@ -24,7 +24,8 @@ __host__ __device__ constexpr int krow_tickets(int trows, int ns, int k)
 {
     return (trows * kSparseTileBy + krow_ticket_rows(ns, k) - 1) / krow_ticket_rows(ns, k);
 }
-size_t krow_lds_bytes(int ns, int lw, int substsz);
+// q8: the int8-profile instance's layout (nw_krow.hip)
+size_t krow_lds_bytes(int ns, int lw, int substsz, bool q8 = false);
 // StripArgs / PairDesc / granule contract as launch_strip_fill (sparse mode, a.tBx, a.tBy,
 // per-pair hrow/hcol/trows/tcols/Cp); tickets of a pair = krow_tickets(trows, ns, k).
 // Every |s - 2g| must fit int16 (the kernel sets error bit 2 otherwise).  grid <= 0: every resident slot.

@@ -51,11 +51,24 @@
 namespace gsa {
 namespace {
 
+// Column profile, int16 (Q8 = false): 2 copies, dword d of copy p = columns (2d-p, 2d-p+1); int8
+// (Q8): 4 copies, dword d of copy p = columns 4d-p .. 4d-p+3, so a lane reads its 16 columns of a row
+// as 4 aligned dwords (2 ds_read2_b32 instead of 4: 100k 5.51 -> 5.30 ms) -- used when every
+// s - 2g fits int8, the kernel falling back to int16 otherwise (uniform, decided in its prologue).
 // dwords per profile row: the ring + a guard, == 0 mod 32 (the row letter never moves a lane's bank)
-__host__ __device__ constexpr int kr_qrs(int lw) { return lw / 2 + 32; }
-// copy 1 starts 16 dwords past a multiple of 32: lanes 2m (copy 0) and 2m+1 (copy 1) read the same
-// dword index d, so copy 1 must sit in the other half of the banks (d and d + 16)
-__host__ __device__ constexpr uint32_t kr_copy1(int lw, int substsz) { return (uint32_t)substsz * kr_qrs(lw) + 16u; }
+__host__ __device__ constexpr int kr_qrs(int lw, bool q8 = false) { return (q8 ? lw / 4 : lw / 2) + 32; }
+// copy p at p * kr_copy1.  int16: copy 1 starts 16 dwords past a multiple of 32 (lanes 2m and 2m+1
+// read the same dword index d, so copy 1 sits in the other half of the banks); int8: copies 8 banks
+// apart (lanes 4m+p read the same index in copy p: 8 m's x 4 copies = 32 banks per 32-lane group)
+__host__ __device__ constexpr uint32_t kr_copy1(int lw, int substsz, bool q8 = false)
+{
+    return (uint32_t)substsz * kr_qrs(lw, q8) + (q8 ? 8u : 16u);
+}
+// dwords of the profile region
+__host__ __device__ constexpr uint32_t kr_qdwords(int lw, int substsz, bool q8)
+{
+    return q8 ? 4u * kr_copy1(lw, substsz, true) : kr_copy1(lw, substsz) + (uint32_t)substsz * kr_qrs(lw) + 16u;
+}
 constexpr int kBlk = 16;          // steps per block
 constexpr int kHalo = kBlk / 4;   // halo registers (int4) per block
 constexpr int kRing = 512;        // hand-off ring elements per strip boundary (power of 2)
@@ -134,11 +147,11 @@ struct KrLds
     uint32_t q, sub, ring, flags;
 };
 
-__host__ __device__ inline KrLds kr_layout(int ns, int lw, int substsz)
+__host__ __device__ inline KrLds kr_layout(int ns, int lw, int substsz, bool q8 = false)
 {
     KrLds L;
     L.q = 0;
-    L.sub = (kr_copy1(lw, substsz) + (uint32_t)substsz * kr_qrs(lw) + 16u) * 4u;
+    L.sub = kr_qdwords(lw, substsz, q8) * 4u;
     L.ring = L.sub + (uint32_t)substsz * kSubRow * 4u;
     L.flags = L.ring + (uint32_t)(ns + 1) * kRing * 4u;
     return L;
@@ -148,7 +161,7 @@ __host__ __device__ inline KrLds kr_layout(int ns, int lw, int substsz)
 // strip wave: 64K rows, K per lane
 // ------------------------------------------------------------------------------------
 // PT: mlsppt (a.done set; a kernel instance of its own, so the plain fill's strip loop is unchanged)
-template <int NS, int K, int LW, bool PT>
+template <int NS, int K, int LW, bool PT, bool Q8>
 __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int tk, int w, int lane)
 {
     const int g = a.g;
@@ -156,8 +169,9 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
     const int tBx = a.tBx, tBy = a.tBy, tcols = a.tcols;
     const int r0 = tk * (64 * K * NS) + 64 * K * w + 1;  // first row of the strip
     const int rl = r0 + K * lane;                          // this lane's first row
-    constexpr int kLW = LW, kQRS = kr_qrs(LW);
-    constexpr int kQW = kLW / 2;  // profile dwords per copy row (ring)
+    constexpr int kLW = LW, kQRS = kr_qrs(LW, Q8);
+    constexpr int kQW = Q8 ? kLW / 4 : kLW / 2;  // profile dwords per copy row (ring)
+    constexpr int kQD = Q8 ? 4 : 8;               // profile dwords per row per block
     uint32_t qrow[K];
 #pragma unroll
     for (int k = 0; k < K; ++k)
@@ -165,7 +179,7 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
         const int r = rl + k;
         int y = (r <= a.R) ? G(a.seqY)[r] : 0;
         y = ((unsigned)y < (unsigned)a.substsz) ? y : 0;
-        qrow[k] = L.q + 4u * ((lane & 1) * kr_copy1(LW, a.substsz) + (uint32_t)y * kQRS);
+        qrow[k] = L.q + 4u * ((uint32_t)(lane & (Q8 ? 3 : 1)) * kr_copy1(LW, a.substsz, Q8) + (uint32_t)y * kQRS);
     }
     const uint32_t ring_in = L.ring + (uint32_t)w * (kRing * 4u);
     const uint32_t ring_out = L.ring + (uint32_t)(w + 1) * (kRing * 4u);
@@ -226,21 +240,32 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
         }
     };
     // profile dwords of block b: columns 16b - lane .. +15 are dwords 8b - lane/2 .. +7 of copy
-    // (lane & 1); reads past the ring's end hit the guard copy
-    auto q_off = [&](int b) { return 4u * (uint32_t)((8 * b - (lane >> 1)) & (kQW - 1)); };
-    int qA[K][8], qB[K][8];
+    // (lane & 1) (int8: dwords 4b - lane/4 .. +3 of copy lane & 3); reads past the ring's end hit
+    // the guard copy
+    auto q_off = [&](int b) {
+        return Q8 ? 4u * (uint32_t)((4 * b - (lane >> 2)) & (kQW - 1)) : 4u * (uint32_t)((8 * b - (lane >> 1)) & (kQW - 1));
+    };
+    int qA[K][kQD], qB[K][kQD];
     {
         const uint32_t p = q_off(0);
 #pragma unroll
         for (int k = 0; k < K; ++k)
 #pragma unroll
-            for (int j = 0; j < 8; ++j) qA[k][j] = 0;
+            for (int j = 0; j < kQD; ++j) qA[k][j] = 0;
         if (!spin(-1)) return;
 #pragma unroll
         for (int k = 0; k < K; ++k)
 #pragma unroll
-            for (int j = 0; j < 8; ++j) qA[k][j] = lds_ld(qrow[k] + p + 4u * j);
+            for (int j = 0; j < kQD; ++j) qA[k][j] = lds_ld(qrow[k] + p + 4u * j);
     }
+    // column u of block's profile dword(s) for row k: int8 byte u & 3 of dword u / 4 (an SDWA
+    // BYTE operand of the add), int16 half u & 1 of dword u / 2
+    auto qv = [&](const int (&qc)[K][kQD], int k, int u) {
+        if constexpr (Q8)
+            return (int)(signed char)(qc[k][u >> 2] >> (8 * (u & 3)));
+        else
+            return (u & 1) ? qhi(qc[k][u >> 1]) : qlo(qc[k][u >> 1]);
+    };
     int H[K], D = 0;
 #pragma unroll
     for (int k = 0; k < K; ++k) H[k] = 0;
@@ -282,7 +307,7 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
 
     // One body for blocks with and without a header-column capture (cap, uniform): separate
     // bodies get different register assignments and ~100 v_mov per block to reconcile them.
-    auto block = [&](int b, int (&qc)[K][8], int (&qn)[K][8], auto rampT, bool cap) {
+    auto block = [&](int b, int (&qc)[K][kQD], int (&qn)[K][kQD], auto rampT, bool cap) {
         constexpr bool RAMP = decltype(rampT)::value;
         constexpr bool CAP = !RAMP;  // ramp blocks hold no boundary (tBx >= 64)
         {
@@ -303,16 +328,9 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
         {
             int nh[K];
             const int up = shr1z(H[K - 1]) + hc[u >> 2][u & 3];
-            {
-                const int q = (u & 1) ? qhi(qc[0][u >> 1]) : qlo(qc[0][u >> 1]);
-                nh[0] = max3i(D + q, up, H[0]);
-            }
+            nh[0] = max3i(D + qv(qc, 0, u), up, H[0]);
 #pragma unroll
-            for (int k = 1; k < K; ++k)
-            {
-                const int q = (u & 1) ? qhi(qc[k][u >> 1]) : qlo(qc[k][u >> 1]);
-                nh[k] = max3i(H[k - 1] + q, nh[k - 1], H[k]);
-            }
+            for (int k = 1; k < K; ++k) nh[k] = max3i(H[k - 1] + qv(qc, k, u), nh[k - 1], H[k]);
             if constexpr (RAMP)
             {
                 // column t - lane <= 0: the border (H' = 0)
@@ -320,8 +338,8 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
 #pragma unroll
                 for (int k = 0; k < K; ++k) nh[k] = border ? 0 : nh[k];
             }
-            // profile of block b+1: K dwords per step over the first half of the block
-            if (u < 8)
+            // profile of block b+1: K dwords per step over the first kQD steps of the block
+            if (u < kQD)
 #pragma unroll
                 for (int k = 0; k < K; ++k) qn[k][u] = lds_ld(qrow[k] + pn + 4u * u);
             lt[u] = H[K - 1];  // column t-64 of the lane's last row: ring element t
@@ -436,11 +454,11 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
 // super-strip, or row 0)
 // ------------------------------------------------------------------------------------
 // ROLE 0: both jobs in one wave; 1: the feed only; 2: the profile only
-template <int NS, int K, int LW, int ROLE>
+template <int NS, int K, int LW, int ROLE, bool Q8>
 __device__ __forceinline__ void kr_loader(const StripArgs& a, const KrLds& L, int tk, int lane)
 {
     const int Cp = a.Cp, C = a.C;
-    constexpr int kLW = LW, kQRS = kr_qrs(LW), kQW = kLW / 2;
+    constexpr int kLW = LW, kQRS = kr_qrs(LW, Q8), kQW = Q8 ? kLW / 4 : kLW / 2;
     const uint32_t F = L.flags;
     const uint32_t ring0 = L.ring;
     const gptr<const unsigned long long> gprev = G((const unsigned long long*)a.gran) + (size_t)(tk > 0 ? tk - 1 : 0) * a.granStride;
@@ -450,11 +468,21 @@ __device__ __forceinline__ void kr_loader(const StripArgs& a, const KrLds& L, in
     };
     int qn = 0;     // the profile holds columns < qn
     int hnext = 0;  // next column of the row above to feed into ring 0
-    // letters of the next profile batch (lane l: columns qn+2l-1 .. qn+2l+1), loaded a batch
-    // ahead: waited for inside the batch, a global load would stall the granule feed for a
-    // round trip every 128 columns, and strip 0's lag ratchets to the worst feed delay
-    int xm = letter(2 * lane - 1), x0 = letter(2 * lane), x1 = letter(2 * lane + 1);
-    int nxm = 0, nx0 = 0, nx1 = 0;  // the batch after (loaded in pass 0)
+    // letters of the next profile batch, loaded a batch ahead: waited for inside the batch, a global
+    // load would stall the granule feed for a round trip every 128 columns, and strip 0's lag
+    // ratchets to the worst feed delay.  int16: lane l builds dword qn/2 + l of both copies from
+    // columns qn+2l-1 .. qn+2l+1; int8: lane l builds dword qn/4 + (l & 31) of copies 2cp, 2cp+1
+    // (cp = l / 32) from the 5 columns from qn + lb
+    constexpr int kNX = Q8 ? 5 : 3;
+    const int cp = lane >> 5;
+    const int lb = Q8 ? 4 * (lane & 31) - 1 - 2 * cp : 2 * lane - 1;
+    int xl[kNX], nxl[kNX];  // this batch's letters, the next batch's (loaded in pass 0)
+#pragma unroll
+    for (int i = 0; i < kNX; ++i)
+    {
+        xl[i] = letter(lb + i);
+        nxl[i] = 0;
+    }
     int qsub = 0;                   // next pass (8 letters each) of the batch at qn
     int pl = 0, c0 = 0;  // progress words, re-read only when their cached values block
     // lanes of the next granule poll: the drain stores whole aligned 16-granule lines (gran_stride),
@@ -484,53 +512,61 @@ __device__ __forceinline__ void kr_loader(const StripArgs& a, const KrLds& L, in
         if (ROLE != 1 && qsub == 0 && qn <= Cp && qn + 192 > pl + kLW) pl = flag_ld(F + kr_prog(NS));
         if (ROLE != 1 && (qsub > 0 || (qn <= Cp && qn + 192 <= pl + kLW)))
         {
-            // letters yy = 8 qsub .. 8 qsub + 7: dwords 2 qsub, 2 qsub + 1 of the three subT rows
-            int4v vm[2], v0[2], v1[2];
+            // letters yy = 8 qsub .. 8 qsub + 7: dwords 2 qsub, 2 qsub + 1 of the subT rows of the
+            // lane's columns
+            int4v vx[kNX][2];
             {
                 const uint32_t o = 32u * (uint32_t)qsub;
 #pragma unroll
-                for (int j = 0; j < 2; ++j)
-                {
-                    vm[j] = lds_ld4(L.sub + 4u * kSubRow * (uint32_t)xm + o + 16u * j);
-                    v0[j] = lds_ld4(L.sub + 4u * kSubRow * (uint32_t)x0 + o + 16u * j);
-                    v1[j] = lds_ld4(L.sub + 4u * kSubRow * (uint32_t)x1 + o + 16u * j);
-                }
+                for (int i = 0; i < kNX; ++i)
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) vx[i][j] = lds_ld4(L.sub + 4u * kSubRow * (uint32_t)xl[i] + o + 16u * j);
             }
             if (qsub == 0)
             {
-                const int cn = qn + kBatch + 2 * lane;
-                nxm = letter(cn - 1);
-                nx0 = letter(cn);
-                nx1 = letter(cn + 1);
+#pragma unroll
+                for (int i = 0; i < kNX; ++i) nxl[i] = letter(qn + kBatch + lb + i);
             }
-            const uint32_t d = (uint32_t)((qn / 2 + lane) & (kQW - 1));  // dword of columns (cl, cl+1) / (cl-1, cl)
-            const bool guard = d < 8;                                     // ring head: also the guard copy at d + kQW
+            // int16: dword of columns (cl, cl+1) / (cl-1, cl); int8: of columns 4d-2cp .. +3 / 4d-2cp-1 .. +2
+            const uint32_t d = Q8 ? (uint32_t)((qn / 4 + (lane & 31)) & (kQW - 1)) : (uint32_t)((qn / 2 + lane) & (kQW - 1));
+            const bool guard = d < (Q8 ? 4u : 8u);  // ring head: also the guard copy at d + kQW
+            const uint32_t ce = L.q + 4u * ((Q8 ? (uint32_t)(2 * cp) * kr_copy1(LW, a.substsz, true) : 0u) + d);
+            const uint32_t co = ce + 4u * kr_copy1(LW, a.substsz, Q8);
 #pragma unroll
             for (int i = 0; i < 8; ++i)
             {
                 const int yy = 8 * qsub + i;
                 if (yy < a.substsz)
                 {
-                    const int s0 = v0[i >> 2][i & 3];
-                    const int p0 = (s0 & 0xffff) | (v1[i >> 2][i & 3] << 16);  // copy 0: (cl, cl+1)
-                    const int p1 = (vm[i >> 2][i & 3] & 0xffff) | (s0 << 16);  // copy 1: (cl-1, cl)
-                    const uint32_t r0a = L.q + 4u * (kQRS * (uint32_t)yy + d);
-                    const uint32_t r1a = L.q + 4u * (kr_copy1(LW, a.substsz) + kQRS * (uint32_t)yy + d);
-                    lds_st(r0a, p0);
-                    lds_st(r1a, p1);
+                    int ev, od;  // the lane's dword of the even / odd copy
+                    if constexpr (Q8)
+                    {
+                        const int w0 = vx[0][i >> 2][i & 3], w1 = vx[1][i >> 2][i & 3], w2 = vx[2][i >> 2][i & 3];
+                        const int w3 = vx[3][i >> 2][i & 3], w4 = vx[4][i >> 2][i & 3];
+                        od = (w0 & 0xff) | ((w1 & 0xff) << 8) | ((w2 & 0xff) << 16) | (w3 << 24);
+                        ev = (int)__builtin_amdgcn_alignbyte((unsigned)w4, (unsigned)od, 1u);
+                    }
+                    else
+                    {
+                        const int s0 = vx[1][i >> 2][i & 3];
+                        ev = (s0 & 0xffff) | (vx[2][i >> 2][i & 3] << 16);  // copy 0: (cl, cl+1)
+                        od = (vx[0][i >> 2][i & 3] & 0xffff) | (s0 << 16);  // copy 1: (cl-1, cl)
+                    }
+                    const uint32_t ra = 4u * kQRS * (uint32_t)yy;
+                    lds_st(ce + ra, ev);
+                    lds_st(co + ra, od);
                     if (guard)
                     {
-                        lds_st(r0a + 4u * kQW, p0);
-                        lds_st(r1a + 4u * kQW, p1);
+                        lds_st(ce + ra + 4u * kQW, ev);
+                        lds_st(co + ra + 4u * kQW, od);
                     }
                 }
             }
             if (++qsub == 4 || 8 * qsub >= a.substsz)
             {
                 qsub = 0;
-                xm = nxm;
-                x0 = nx0;
-                x1 = nx1;
+#pragma unroll
+                for (int i = 0; i < kNX; ++i) xl[i] = nxl[i];
                 qn += kBatch;
                 flag_st(F + kFXo, qn > Cp ? kBig : qn);
             }
@@ -819,21 +855,45 @@ constexpr bool kr_split() { return NS <= 4; }
 template <int NS>
 constexpr int kr_waves() { return NS + 2 + (kr_split<NS>() ? 1 : 0); }
 
-template <int NS, int K, int LW, bool PT>
+// Q8: the int8-profile instance.  It declines a table with some s - 2g outside int8 (every
+// workgroup exits before taking a ticket and the launch's word in a.q8flag is set to its epoch);
+// the host enqueues the int16 instance behind it with a.q8 = 2, which runs only in that case.  Both
+// profiles in one kernel (a uniform branch, or the int16 path out of line) cost the int8 path its
+// code generation: 5.49 / 5.75 ms against 5.30 for the int8 instance alone.
+template <int NS, int K, int LW, bool PT, bool Q8>
 __global__ void __launch_bounds__(64 * kr_waves<NS>()) nw_krow_kernel(StripArgs a)
 {
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
-    const KrLds L = kr_layout(NS, LW, a.substsz);
-    bool bad = false;
+    const KrLds L = kr_layout(NS, LW, a.substsz, Q8);
+    // the int16 fallback behind an int8 launch: nothing to do unless that launch declined the table
+    if (!Q8 && a.q8 == 2 && __hip_atomic_load(a.q8flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != a.epoch) return;
+    bool bad = false, bad8 = false;
     for (int k = threadIdx.x; k < a.substsz * kSubRow; k += 64 * kr_waves<NS>())
     {
         const int x = k / kSubRow, yy = k % kSubRow;
         const int v = yy < a.substsz ? G(a.subst)[yy * a.substsz + x] - 2 * a.g : 0;
         bad |= v < -32768 || v > 32767;  // the profile holds int16
+        bad8 |= v < -128 || v > 127;      // ... or int8
         lds_st(L.sub + 4u * k, v);
     }
-    if (bad) atomicOr(a.err, 2u);
+    if constexpr (Q8)
+    {
+        // a table outside int8: decline (every workgroup sees the same table).  Reduced through a
+        // word of the dynamic LDS: __syncthreads_or would allocate static LDS, which moves krsm off
+        // address 0, and the asm blocks address krsm by raw offsets.
+        if (threadIdx.x == 0) lds_st(L.flags + kFTicket, 0);
+        __syncthreads();
+        if (bad8) atomicOr((int*)(krsm + L.flags + kFTicket), 1);
+        __syncthreads();
+        if (lds_ld(L.flags + kFTicket) != 0)
+        {
+            if (threadIdx.x == 0) __hip_atomic_store(a.q8flag, a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return;
+        }
+    }
+    else if (bad)
+        atomicOr(a.err, 2u);  // (an int8 table never has this)
     for (;;)
     {
         __syncthreads();
@@ -881,23 +941,23 @@ __global__ void __launch_bounds__(64 * kr_waves<NS>()) nw_krow_kernel(StripArgs 
         if (w == NS + 1)
             kr_drain<NS, K, LW, PT>(pa, L, tk, lane);
         else if (w == NS)
-            kr_loader<NS, K, LW, kr_split<NS>() ? 1 : 0>(pa, L, tk, lane);
+            kr_loader<NS, K, LW, kr_split<NS>() ? 1 : 0, Q8>(pa, L, tk, lane);
         else if (kr_split<NS>() && w == NS + 2)
-            kr_loader<NS, K, LW, 2>(pa, L, tk, lane);
+            kr_loader<NS, K, LW, 2, Q8>(pa, L, tk, lane);
         else
         {
             __builtin_amdgcn_s_setprio(3);
-            kr_strip<NS, K, LW, PT>(pa, L, tk, w, lane);
+            kr_strip<NS, K, LW, PT, Q8>(pa, L, tk, w, lane);
             __builtin_amdgcn_s_setprio(0);
         }
     }
 }
 
-template <int NS, int K, int LW, bool PT = false>
-hipError_t launch_kr(const StripArgs& a, int grid, hipStream_t stream)
+template <int NS, int K, int LW, bool PT, bool Q8>
+hipError_t launch_kr1(const StripArgs& a, int grid, hipStream_t stream, bool foot = true)
 {
-    const size_t lds = krow_lds_bytes(NS, LW, a.substsz);
-    auto kern = nw_krow_kernel<NS, K, LW, PT>;
+    const size_t lds = krow_lds_bytes(NS, LW, a.substsz, Q8);
+    auto kern = nw_krow_kernel<NS, K, LW, PT, Q8>;
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     if (grid <= 0)
@@ -909,9 +969,22 @@ hipError_t launch_kr(const StripArgs& a, int grid, hipStream_t stream)
         if (e != hipSuccess) return e;
         grid = std::max(1, std::min(a.nTicketsTotal, std::max(1, per_cu) * cus));
     }
-    if ((e = record_foot((const void*)kern, lds, 64 * kr_waves<NS>(), grid)) != hipSuccess) return e;
+    if (foot && (e = record_foot((const void*)kern, lds, 64 * kr_waves<NS>(), grid)) != hipSuccess) return e;
     hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * kr_waves<NS>()), lds, stream, a);
     return hipGetLastError();
+}
+
+// a.q8: the int8 instance, then the int16 one behind it (a no-op unless the int8 launch declined
+// the table); otherwise the int16 instance alone
+template <int NS, int K, int LW, bool PT = false>
+hipError_t launch_kr(const StripArgs& a, int grid, hipStream_t stream)
+{
+    if (!a.q8) return launch_kr1<NS, K, LW, PT, false>(a, grid, stream);
+    hipError_t e = launch_kr1<NS, K, LW, PT, true>(a, grid, stream);
+    if (e != hipSuccess) return e;
+    StripArgs b = a;
+    b.q8 = 2;
+    return launch_kr1<NS, K, LW, PT, false>(b, grid, stream, false);
 }
 
 #ifdef GSA_KROW_SCORE
@@ -1606,7 +1679,7 @@ hipError_t launch_krow_fill_b8(const StripArgs& a, int grid, hipStream_t stream)
 #else
 hipError_t launch_krow_fill_b8(const StripArgs& a, int grid, hipStream_t stream);
 
-size_t krow_lds_bytes(int ns, int lw, int substsz) { return (size_t)kr_layout(ns, lw, substsz).flags + 256; }
+size_t krow_lds_bytes(int ns, int lw, int substsz, bool q8) { return (size_t)kr_layout(ns, lw, substsz, q8).flags + 256; }
 
 hipError_t launch_krow_fill(const StripArgs& a, int ns, int k, int lw, int grid, hipStream_t stream)
 {

@@ -77,6 +77,11 @@ struct StripArgs
     // columns each) are in memory (system-scope stores, acknowledged); null: no signalling
     unsigned long long* done;
     int ptChunk;
+    // K-rows fills (nw_krow.hip): 1 = launch the int8-profile instance, which declines a table with
+    // some s - 2g outside int8 by setting *q8flag to its epoch, then the int16 instance with q8 = 2,
+    // which runs only then; 0 = the int16 instance alone
+    int q8;
+    unsigned* q8flag;
     // kModeScoreAG: gap open / extend, the F' hand-off granules (same layout as gran), result H[R][C]
     int go, ge;
     unsigned long long* gran2;

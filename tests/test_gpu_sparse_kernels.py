@@ -58,3 +58,19 @@ def test_sparse_profile_range_is_checked(engine, golden):
     # the context is usable afterwards
     res = engine.align_sparse(Y, X, golden.blosum62, -11, tileBx=64)
     assert res.align_cost == oracle.fill_full(Y, X, golden.blosum62, -11)[1]
+
+
+@pytest.mark.parametrize("R,C", [(63, 2000), (1500, 1300), (3000, 2100)])
+@pytest.mark.parametrize("gapo,q8", [(-11, "0"), (-80, "1"), (-60, "1"), (-59, "1")])
+def test_krow_profile_width(engine, golden, R, C, gapo, q8, monkeypatch):
+    monkeypatch.delenv("GSA_SPARSE_KERNEL", raising=False)
+    """The K-rows fill keeps s - 2g in an int8 column profile when the table allows it and falls
+    back to int16 inside the kernel otherwise (gapo -80: s + 160 > 127 for blosum62; -60/-59 around
+    the edge, s <= 11); GSA_KROW_Q8=0 forces int16.  Headers word for word against the oracle."""
+    import oracle
+    monkeypatch.setenv("GSA_KROW_Q8", q8)
+    Y, X = random_pair(R, C, R + 3 * C)
+    res = engine.align_sparse(Y, X, golden.blosum62, gapo, tileBx=256)
+    hr, hc, _, _, cost = oracle.sparse_headers(Y, X, golden.blosum62, gapo, gsa.sparse_tile_by(), 256)
+    assert np.array_equal(res.hrow, hr) and np.array_equal(res.hcol, hc)
+    assert res.align_cost == cost
