@@ -76,3 +76,29 @@ def test_krow_profile_width(engine, golden, R, C, gapo, q8, monkeypatch):
     hr, hc, _, _, cost = oracle.sparse_headers(Y, X, golden.blosum62, gapo, gsa.sparse_tile_by(), 256)
     assert np.array_equal(res.hrow, hr) and np.array_equal(res.hcol, hc)
     assert res.align_cost == cost
+
+
+@pytest.mark.parametrize("kern,ns,k", KERNELS)
+def test_sparse_kernel_batch_declined_table(golden, monkeypatch, kern, ns, k):
+    """A batch whose table leaves int8 (gapo -80): every geometry's int8 instance declines and the
+    int16 instance behind it fills the batch."""
+    import torch
+    from gpuseqalign_amd import shard
+    _select(monkeypatch, kern, ns, k)
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU visible")
+    pairs = shard.synthetic_batch(12, 300, 2600, seed0=91)
+    costs, _ = shard.gpu_batch_align(0, mode="sparse", tileBx=128)(list(range(len(pairs))), pairs, golden.blosum62, -80)
+    for (y, x), c in zip(pairs, costs):
+        assert c == oracle.fill_full(y, x, golden.blosum62, -80)[1]
+
+
+@pytest.mark.parametrize("gapo", [-80, -11])
+def test_overlap_declined_table(engine, golden, gapo):
+    """mlsppt (the PT instances) with a table outside int8 and then inside it, headers against the
+    oracle."""
+    Y, X = random_pair(3000, 9000, 5)
+    hr, hc, _, _, cost = oracle.sparse_headers(Y, X, golden.blosum62, gapo, gsa.sparse_tile_by(), 256)
+    b = engine.align_sparse(Y, X, golden.blosum62, gapo, tileBx=256, overlap=True)
+    assert np.array_equal(b.hrow, hr) and np.array_equal(b.hcol, hc)
+    assert b.align_cost == cost
