@@ -146,6 +146,15 @@ def cpu_baseline(Y, X, sub, budget_s=20.0, n=20000):
 REHEARSE = os.environ.get("GSA_BENCH_REHEARSE") == "1"
 
 
+def gpu_fields(world):
+    """n_gpus / parallelism / rehearsal of the JSON line: a rehearsal's ranks share cuda:0, so it
+    reports the devices it used (1) and says what it was, never a multi-GPU result."""
+    if REHEARSE:
+        return {"n_gpus": 1, "rehearsal": True,
+                "parallelism": f"REHEARSAL: {world} gloo ranks sharing one GPU (not a scaling result)"}
+    return {"n_gpus": world, "rehearsal": False, "parallelism": f"pair-sharded x{world}"}
+
+
 def coll_dev(dev):
     """Where collective tensors live: the rank's GPU (RCCL), or the CPU in a gloo rehearsal."""
     import torch
@@ -213,6 +222,44 @@ def bench_config4(world, rank, local, n_pairs):
             "value": round(rep.gcups, 2), "unit": "GCUPS", "scaling": "strong", "cells": rep.cells,
             "seconds": round(rep.elapsed_s, 4), "pairs": n_pairs,
             "pairs_matching_golden": match, "golden_pairs": None if gold is None else gold.get("n_pairs")}
+
+
+def bench_config4_rank_share(local, n_pairs, cfg4, ranks=8):
+    """One-GPU fact that bounds the 8-GPU strong scaling of configs[3]: every rank's LPT share
+    (shard.lpt_partition(weights, 8)[k], ~64 pairs) timed as the one launch that rank would run,
+    one share after the other on this GPU.  An 8-GPU run cannot beat the slowest share, so
+    projected_8gpu_speedup = (time of all n_pairs on one GPU) / (slowest share); the longest pair
+    of share 0 alone is the critical path under it."""
+    from gpuseqalign_amd import shard
+    pairs = shard.synthetic_batch(n_pairs, 18000, 22000, seed0=1000)
+    sub = subst_blosum62()
+    weights = [(len(y) - 1) * (len(x) - 1) for y, x in pairs]
+    parts = shard.lpt_partition(weights, ranks)
+    gold = load_golden("config4_pairs.json")
+    fn = shard.gpu_batch_align(device=local, mode="sparse", tileBx=TILE_BX, warmup=1, repeats=3)
+    shares, match = [], 0
+    for idx in parts:
+        costs, secs = fn(idx, pairs, sub, -11)
+        if gold is not None:
+            match += sum(int(c == gold["align_cost"][i]) for i, c in zip(idx, costs))
+        cells = sum(weights[i] for i in idx)
+        shares.append({"pairs": len(idx), "cells": cells, "seconds": round(secs, 6),
+                       "gcups": round(cells / secs / 1e9, 2)})
+    longest = max(parts[0], key=lambda i: weights[i])
+    _, t1 = shard.gpu_batch_align(device=local, mode="sparse", tileBx=TILE_BX, warmup=1, repeats=3)(
+        [longest], pairs, sub, -11)
+    slowest = max(sh["seconds"] for sh in shares)
+    t_all = cfg4["seconds"] if cfg4 else None
+    return {"workload": f"configs[3] LPT shares for {ranks} ranks, each timed alone on this GPU (one launch per "
+                        "share, 1 untimed + 3 timed launches)",
+            "ranks": ranks, "share0": shares[0], "shares_seconds": [sh["seconds"] for sh in shares],
+            "slowest_share_seconds": slowest,
+            "share_gcups": round(sum(weights) / ranks / slowest / 1e9, 2),
+            "projected_8gpu_gcups": round(sum(weights) / slowest / 1e9, 2),
+            "projected_8gpu_speedup": None if t_all is None else round(t_all / slowest, 3),
+            "single_pair": {"pair": int(longest), "R": len(pairs[longest][0]) - 1, "C": len(pairs[longest][1]) - 1,
+                            "seconds": round(t1, 6)},
+            "pairs_matching_golden": match if gold is not None else None}
 
 
 CLOCK_GHZ = 2.4          # MI355X_MICROARCH.md chip table (max clock)
@@ -335,6 +382,7 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--config4-pairs", type=int, default=512, help="0 = skip the configs[3] batch field")
     ap.add_argument("--no-10k", action="store_true", help="skip the configs[1] full-matrix field")
+    ap.add_argument("--no-rank-share", action="store_true", help="skip the config4_rank_share field")
     ap.add_argument("--full-batch-pairs", type=int, default=64, help="0 = skip the full-matrix batch field")
     ap.add_argument("--no-config5", action="store_true", help="skip the configs[4] score-only field")
     ap.add_argument("--config5-cpu-sample", type=int, default=50000, help="n x n prefix for the config-5 CPU leg")
@@ -442,17 +490,22 @@ def main():
 
     # ---- configs[3]: 512 pairs, LPT-sharded (strong scaling field) ------------------------
     cfg4 = bench_config4(world, rank, local, a.config4_pairs) if a.config4_pairs > 0 else None
+    share = None
+    if a.config4_pairs > 0 and world == 1 and not REHEARSE and not a.no_rank_share:
+        share = bench_config4_rank_share(local, a.config4_pairs, cfg4)
 
     if rank == 0:
+        gf = gpu_fields(world)
         out = {
-            "metric": METRIC, "value": round(value, 3), "unit": "GCUPS", "n_gpus": world, "steps": a.steps,
+            "metric": METRIC, "value": round(value, 3), "unit": "GCUPS", "n_gpus": gf["n_gpus"], "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(elapsed * 1e3 / a.steps, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "int32",
             "data": "synthetic (splitmix64: seqX seed 100, seqY = seqX mutated seed 101); blosum62, gapo -11",
             "config": {"workload": f"BASELINE configs[2]: NW-LG {R}x{C} related pair, sparse tile-header (mlsp) "
                                    f"fill, tileBx {TILE_BX} x tileBy {geom.tileHcolLen - 1}, headers only in HBM",
                        "R": R, "C": C, "pairs_per_rank": 1, "representation": "sparse tile headers (mlsp)",
-                       "parallelism": f"pair-sharded x{world}"},
+                       "parallelism": gf["parallelism"]},
+            "rehearsal": gf["rehearsal"],
             "roofline": {"bound": "valu", "achieved": round(ops_achieved, 3), "peak": round(PEAK_VALU_TOPS, 2),
                          "unit": "T int32 lane-ops/s", "frac": round(ops_achieved / PEAK_VALU_TOPS, 4),
                          "traffic": traffic_for("traffic_config3.json", R, C, kname),
@@ -464,7 +517,7 @@ def main():
                          "critical_path": critical_path(C, -(-R // 256), 9, kern_ms, 256)},
             "align_costs": costs[:8], "golden_align_cost": gold_cost,
             "golden_match": None if gold_cost is None else all(c == gold_cost for c in costs),
-            "fill_10k_full": full10k, "config4": cfg4, "full_batch": fullb, "config5": cfg5,
+            "fill_10k_full": full10k, "config4": cfg4, "config4_rank_share": share, "full_batch": fullb, "config5": cfg5,
         }
         if not a.no_cpu_baseline and world == 1:  # the CPU leg runs on rank 0 at N = 1 only
             out["cpu_baseline"] = cpu_baseline(Y, X, sub, budget_s=a.cpu_budget)

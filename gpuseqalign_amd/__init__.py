@@ -14,7 +14,7 @@ from __future__ import annotations
 import ctypes
 import dataclasses
 import os
-from typing import Callable, Dict, Optional, Tuple
+from typing import Callable, Dict, Optional, Sequence, Tuple
 
 import numpy as np
 
@@ -121,6 +121,11 @@ SIGNATURES = {
     "gsa_mem_stats_get": (ctypes.c_int, [_vp, ctypes.POINTER(MemStats)]),
     "gsa_mem_stats_reset": (ctypes.c_int, [_vp]),
     "gsa_fill_full_batch_dev": (ctypes.c_int, [_vp, _i32, ctypes.POINTER(PairDev), _vp, _i32, _i32, _vp]),
+    "gsa_full_pitch": (_i32, [_i32]),
+    "gsa_full_base_offset": (_i32, []),
+    "gsa_fill_full_pitched_dev": (ctypes.c_int, [_vp, _vp, _i32, _vp, _i32, _vp, _i32, _i32, _vp, _i32, _vp]),
+    "gsa_fill_full_batch_pitched_dev": (ctypes.c_int, [_vp, _i32, ctypes.POINTER(PairDev), _i32p, _vp, _i32, _i32,
+                                                       _vp]),
     "gsa_fill_sparse_batch_dev": (ctypes.c_int, [_vp, _i32, ctypes.POINTER(PairDev), _vp, _i32, _i32, _i32, _vp]),
     "gsa_align_full": (ctypes.c_int, [_vp, _i32p, _i32, _i32p, _i32, _i32p, _i32, _i32, _i32p, _i32p,
                                       ctypes.POINTER(_Laps)]),
@@ -180,6 +185,16 @@ def _c32(a) -> np.ndarray:
 
 def sparse_tile_by() -> int:
     return int(lib().gsa_sparse_tile_by())
+
+
+def full_pitch(adjcols: int) -> int:
+    """Row pitch (ints) of the fastest device layout of a full matrix (gsa_full_pitch: = 1 mod 32)."""
+    return int(lib().gsa_full_pitch(adjcols))
+
+
+def full_base_offset() -> int:
+    """Ints from a 128-byte boundary to cell (0, 0) of that layout (cell (1, 0) on the boundary)."""
+    return int(lib().gsa_full_base_offset())
 
 
 def sparse_geometry(adjrows: int, adjcols: int, tileBx: int) -> SparseGeom:
@@ -281,10 +296,16 @@ class Engine:
 
     # -- hot path on device-resident buffers (torch tensors or raw pointers) -------------
     def fill_full_dev(self, seqY_ptr: int, adjrows: int, seqX_ptr: int, adjcols: int, subst_ptr: int, substsz: int,
-                      gapo: int, score_ptr: int, stream: Optional[int] = None):
-        st = lib().gsa_fill_full_dev(self._h, seqY_ptr, adjrows, seqX_ptr, adjcols, subst_ptr, substsz, gapo,
-                                     score_ptr, stream)
-        self._check(st, "gsa_fill_full_dev")
+                      gapo: int, score_ptr: int, stream: Optional[int] = None, ld: Optional[int] = None):
+        """Full matrix into device memory; ld = row pitch in ints (None: unpadded, adjcols)."""
+        if ld is None:
+            st = lib().gsa_fill_full_dev(self._h, seqY_ptr, adjrows, seqX_ptr, adjcols, subst_ptr, substsz, gapo,
+                                         score_ptr, stream)
+            self._check(st, "gsa_fill_full_dev")
+        else:
+            st = lib().gsa_fill_full_pitched_dev(self._h, seqY_ptr, adjrows, seqX_ptr, adjcols, subst_ptr, substsz,
+                                                 gapo, score_ptr, int(ld), stream)
+            self._check(st, "gsa_fill_full_pitched_dev")
 
     def fill_sparse_dev(self, seqY_ptr: int, adjrows: int, seqX_ptr: int, adjcols: int, subst_ptr: int,
                         substsz: int, gapo: int, tileBx: int, hrow_ptr: int, hcol_ptr: int,
@@ -294,9 +315,10 @@ class Engine:
         self._check(st, "gsa_fill_sparse_dev")
 
     def fill_batch_dev(self, pairs, subst_ptr: int, substsz: int, gapo: int, mode: str = "sparse",
-                       tileBx: int = 256, stream: Optional[int] = None):
+                       tileBx: int = 256, stream: Optional[int] = None, lds: Optional[Sequence[int]] = None):
         """One persistent launch over many pairs.  `pairs`: sequence of (seqY_ptr, adjrows,
-        seqX_ptr, adjcols, out) with out = score_ptr (full) or (hrow_ptr, hcol_ptr) (sparse)."""
+        seqX_ptr, adjcols, out) with out = score_ptr (full) or (hrow_ptr, hcol_ptr) (sparse);
+        lds: full matrices' row pitches (None: unpadded)."""
         arr = (PairDev * len(pairs))()
         for k, (yp, ar, xp, ac, out) in enumerate(pairs):
             arr[k].seqY, arr[k].adjrows, arr[k].seqX, arr[k].adjcols = yp, ar, xp, ac
@@ -306,8 +328,12 @@ class Engine:
                 arr[k].score = out
         if mode == "sparse":
             st = lib().gsa_fill_sparse_batch_dev(self._h, len(pairs), arr, subst_ptr, substsz, gapo, tileBx, stream)
-        else:
+        elif lds is None:
             st = lib().gsa_fill_full_batch_dev(self._h, len(pairs), arr, subst_ptr, substsz, gapo, stream)
+        else:
+            la = _c32(list(lds))
+            st = lib().gsa_fill_full_batch_pitched_dev(self._h, len(pairs), arr, _p(la), subst_ptr, substsz, gapo,
+                                                       stream)
         self._check(st, "gsa_fill_%s_batch_dev" % mode)
 
     def sync(self, stream: Optional[int] = None):

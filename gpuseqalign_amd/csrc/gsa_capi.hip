@@ -376,7 +376,8 @@ int score_ag_strip(gsa_ctx* ctx, const int32_t* seqY, int64_t R, const int32_t* 
 // One batched launch: headers of every pair, then the persistent strip kernel over the
 // tickets of all pairs (pair-major).  `pairs` holds device pointers.
 int enqueue_batch(gsa_ctx* ctx, int mode, int npairs, const gsa_pair_dev* pairs, const int32_t* subst, int32_t substsz,
-                  int32_t gapo, int32_t tileBx, hipStream_t st, unsigned long long* done = nullptr, int ptChunk = 0)
+                  int32_t gapo, int32_t tileBx, hipStream_t st, unsigned long long* done = nullptr, int ptChunk = 0,
+                  const int32_t* lds = nullptr)
 {
     if (npairs < 1 || !pairs || !subst) return GSA_ERROR_INVALID_VALUE;
     if (substsz < 1 || substsz > 32) return GSA_ERROR_INVALID_VALUE;  // LDS profile holds <= 32 letters
@@ -433,7 +434,10 @@ int enqueue_batch(gsa_ctx* ctx, int mode, int npairs, const gsa_pair_dev* pairs,
         {
             if (!in.score) return GSA_ERROR_INVALID_VALUE;
             d.score = in.score;
-            d.ld = in.adjcols;
+            // row pitch: unpadded, or the caller's (gsa_full_pitch gives the one whose anti-diagonals
+            // share their 128-byte line offset, so the strips' row segments are whole lines)
+            d.ld = lds ? lds[p] : in.adjcols;
+            if (d.ld < in.adjcols) return GSA_ERROR_INVALID_VALUE;
             d.Cp = d.C;
             // an empty row or column leaves nothing but headers to compute
             d.nTickets = (d.C == 0) ? 0 : (d.R + fullRows - 1) / fullRows;
@@ -539,10 +543,11 @@ int enqueue_batch(gsa_ctx* ctx, int mode, int npairs, const gsa_pair_dev* pairs,
 
 int enqueue_fill(gsa_ctx* ctx, int mode, const int32_t* seqY, int32_t adjrows, const int32_t* seqX, int32_t adjcols,
                  const int32_t* subst, int32_t substsz, int32_t gapo, int32_t* score, int32_t tileBx, int32_t* hrow,
-                 int32_t* hcol, hipStream_t st, unsigned long long* done = nullptr, int ptChunk = 0)
+                 int32_t* hcol, hipStream_t st, unsigned long long* done = nullptr, int ptChunk = 0,
+                 const int32_t* ld = nullptr)
 {
     gsa_pair_dev p {seqY, adjrows, seqX, adjcols, score, hrow, hcol};
-    return enqueue_batch(ctx, mode, 1, &p, subst, substsz, gapo, tileBx, st, done, ptChunk);
+    return enqueue_batch(ctx, mode, 1, &p, subst, substsz, gapo, tileBx, st, done, ptChunk, ld);
 }
 
 }  // namespace
@@ -670,6 +675,26 @@ int gsa_fill_full_dev(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, const 
                         nullptr, pick_stream(ctx, stream));
 }
 
+int32_t gsa_full_pitch(int32_t adjcols)
+{
+    if (adjcols < 1) return 0;
+    return (int32_t)(32 * (((int64_t)adjcols - 1 + 31) / 32) + 1);
+}
+
+int32_t gsa_full_base_offset(void) { return 31; }
+
+int gsa_fill_full_pitched_dev(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, const int32_t* seqX, int32_t adjcols,
+                              const int32_t* subst, int32_t substsz, int32_t gapo, int32_t* score, int32_t ld,
+                              void* stream)
+{
+    if (!ctx || !score) return GSA_ERROR_INVALID_VALUE;
+    int s = check_inputs(adjrows, adjcols, substsz);
+    if (s != GSA_SUCCESS) return s;
+    if (ld < adjcols) return GSA_ERROR_INVALID_VALUE;
+    return enqueue_fill(ctx, gsa::kModeFull, seqY, adjrows, seqX, adjcols, subst, substsz, gapo, score, 0, nullptr,
+                        nullptr, pick_stream(ctx, stream), nullptr, 0, &ld);
+}
+
 int gsa_fill_sparse_dev(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, const int32_t* seqX, int32_t adjcols,
                         const int32_t* subst, int32_t substsz, int32_t gapo, int32_t tileBx, int32_t* hrow,
                         int32_t* hcol, void* stream)
@@ -686,6 +711,14 @@ int gsa_fill_full_batch_dev(gsa_ctx* ctx, int32_t npairs, const gsa_pair_dev* pa
 {
     if (!ctx) return GSA_ERROR_INVALID_VALUE;
     return enqueue_batch(ctx, gsa::kModeFull, npairs, pairs, subst, substsz, gapo, 0, pick_stream(ctx, stream));
+}
+
+int gsa_fill_full_batch_pitched_dev(gsa_ctx* ctx, int32_t npairs, const gsa_pair_dev* pairs, const int32_t* lds,
+                                    const int32_t* subst, int32_t substsz, int32_t gapo, void* stream)
+{
+    if (!ctx || !lds) return GSA_ERROR_INVALID_VALUE;
+    return enqueue_batch(ctx, gsa::kModeFull, npairs, pairs, subst, substsz, gapo, 0, pick_stream(ctx, stream), nullptr,
+                         0, lds);
 }
 
 int gsa_fill_sparse_batch_dev(gsa_ctx* ctx, int32_t npairs, const gsa_pair_dev* pairs, const int32_t* subst,

@@ -234,25 +234,25 @@ NwStat NwPrintTrace1_Plain(std::ostream& os, const NwAlgInput&, const NwAlgResul
 
 void getNwAlgorithmMap(std::map<std::string, NwAlgorithm>& algMap)
 {
-    const NwAlgorithm plain {NwAlign_Amd_Strip_Full, NwTrace1_Plain, NwHash1_Plain, NwPrintScore1_Plain,
-                             NwPrintTrace1_Plain};
-    const NwAlgorithm sparse_pt {NwAlign_Amd_Strip_Mlsppt, NwTrace2_Sparse, NwHash2_Sparse, NwPrintScore2_Sparse,
-                                 NwPrintTrace1_Plain};
-    const NwAlgorithm sparse {NwAlign_Amd_Strip_Mlsp, NwTrace2_Sparse, NwHash2_Sparse, NwPrintScore2_Sparse,
-                              NwPrintTrace1_Plain};
+    auto plain = [](NwAlgorithm::NwAlignFn f) {
+        return NwAlgorithm {f, NwTrace1_Plain, NwHash1_Plain, NwPrintScore1_Plain, NwPrintTrace1_Plain};
+    };
+    auto sparse = [](NwAlgorithm::NwAlignFn f) {
+        return NwAlgorithm {f, NwTrace2_Sparse, NwHash2_Sparse, NwPrintScore2_Sparse, NwPrintTrace1_Plain};
+    };
     std::map<std::string, NwAlgorithm> m {
-        {"NwAlign_Gpu1_Ml_Diag", plain},
-        {"NwAlign_Gpu2_Ml_DiagRow2Pass", plain},
-        {"NwAlign_Gpu3_Ml_DiagDiag", plain},
-        {"NwAlign_Gpu4_Ml_DiagDiag2Pass", plain},
-        {"NwAlign_Gpu5_Coop_DiagDiag", plain},
-        {"NwAlign_Gpu6_Coop_DiagDiag2Pass", plain},
-        {"NwAlign_Gpu7_Mlsp_DiagDiag", sparse},
-        {"NwAlign_Gpu8_Mlsp_DiagDiag", sparse},
-        {"NwAlign_Gpu9_Mlsp_DiagDiagDiag", sparse},
-        {"NwAlign_Amd_Strip_Full", plain},
-        {"NwAlign_Amd_Strip_Mlsp", sparse},
-        {"NwAlign_Amd_Strip_Mlsppt", sparse_pt},
+        {"NwAlign_Gpu1_Ml_Diag", plain(NwAlign_Gpu1_Ml_Diag)},
+        {"NwAlign_Gpu2_Ml_DiagRow2Pass", plain(NwAlign_Gpu2_Ml_DiagRow2Pass)},
+        {"NwAlign_Gpu3_Ml_DiagDiag", plain(NwAlign_Gpu3_Ml_DiagDiag)},
+        {"NwAlign_Gpu4_Ml_DiagDiag2Pass", plain(NwAlign_Gpu4_Ml_DiagDiag2Pass)},
+        {"NwAlign_Gpu5_Coop_DiagDiag", plain(NwAlign_Gpu5_Coop_DiagDiag)},
+        {"NwAlign_Gpu6_Coop_DiagDiag2Pass", plain(NwAlign_Gpu6_Coop_DiagDiag2Pass)},
+        {"NwAlign_Gpu7_Mlsp_DiagDiag", sparse(NwAlign_Gpu7_Mlsp_DiagDiag)},
+        {"NwAlign_Gpu8_Mlsp_DiagDiag", sparse(NwAlign_Gpu8_Mlsp_DiagDiag)},
+        {"NwAlign_Gpu9_Mlsp_DiagDiagDiag", sparse(NwAlign_Gpu9_Mlsp_DiagDiagDiag)},
+        {"NwAlign_Amd_Strip_Full", plain(NwAlign_Amd_Strip_Full)},
+        {"NwAlign_Amd_Strip_Mlsp", sparse(NwAlign_Amd_Strip_Mlsp)},
+        {"NwAlign_Amd_Strip_Mlsppt", sparse(NwAlign_Amd_Strip_Mlsppt)},
     };
     algMap.swap(m);
 }

@@ -196,10 +196,28 @@ private:
 // are absent here ("out of scope").
 void getNwAlgorithmMap(std::map<std::string, NwAlgorithm>& algMap);
 
-// Individual functions (the reference's nw_fns.hpp names).
+// Individual functions (the reference's nw_fns.hpp names): one align adapter per slot name, each
+// with the parameter rules of the reference's function of that name (nwalign_amd.cpp).
+NwStat NwAlign_Gpu1_Ml_Diag(const NwAlgParams& pr, NwAlgInput& nw, NwAlgResult& res);
+NwStat NwAlign_Gpu2_Ml_DiagRow2Pass(const NwAlgParams& pr, NwAlgInput& nw, NwAlgResult& res);
+NwStat NwAlign_Gpu3_Ml_DiagDiag(const NwAlgParams& pr, NwAlgInput& nw, NwAlgResult& res);
+NwStat NwAlign_Gpu4_Ml_DiagDiag2Pass(const NwAlgParams& pr, NwAlgInput& nw, NwAlgResult& res);
+NwStat NwAlign_Gpu5_Coop_DiagDiag(const NwAlgParams& pr, NwAlgInput& nw, NwAlgResult& res);
+NwStat NwAlign_Gpu6_Coop_DiagDiag2Pass(const NwAlgParams& pr, NwAlgInput& nw, NwAlgResult& res);
+NwStat NwAlign_Gpu7_Mlsp_DiagDiag(const NwAlgParams& pr, NwAlgInput& nw, NwAlgResult& res);
+NwStat NwAlign_Gpu8_Mlsp_DiagDiag(const NwAlgParams& pr, NwAlgInput& nw, NwAlgResult& res);
+NwStat NwAlign_Gpu9_Mlsp_DiagDiagDiag(const NwAlgParams& pr, NwAlgInput& nw, NwAlgResult& res);
 NwStat NwAlign_Amd_Strip_Full(const NwAlgParams& pr, NwAlgInput& nw, NwAlgResult& res);
 NwStat NwAlign_Amd_Strip_Mlsp(const NwAlgParams& pr, NwAlgInput& nw, NwAlgResult& res);
 NwStat NwAlign_Amd_Strip_Mlsppt(const NwAlgParams& pr, NwAlgInput& nw, NwAlgResult& res);
+// The engine geometry a slot's parameters select (no device needed): errorInvalidValue where
+// the reference's function of that name rejects them; sparse slots give the tile width.
+struct SlotGeometry
+{
+    bool sparse = false;
+    int tileBx = 0;  // sparse: the engine's tile width (tile height: gsa_sparse_tile_by())
+};
+NwStat slotGeometry(const std::string& slot, const NwAlgParams& pr, SlotGeometry& out);
 NwStat NwTrace1_Plain(NwAlgInput& nw, NwAlgResult& res, bool calcDebugTrace);
 NwStat NwHash1_Plain(NwAlgInput& nw, NwAlgResult& res);
 NwStat NwTrace2_Sparse(NwAlgInput& nw, NwAlgResult& res, bool calcDebugTrace);

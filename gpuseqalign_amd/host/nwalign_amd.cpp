@@ -62,33 +62,28 @@ void update_peak_mem(const NwAlgInput& nw, NwAlgResult& res)
     res.regMemPeakAllocs = std::max(res.regMemPeakAllocs, (size_t)m.regmem_peak_allocs);
 }
 
-// Sparse family: tile header matrices.  Parameter "tileBx" (a multiple of 16, >= 64) selects the
-// tile width, default 256; the tile height is the engine's (gsa_sparse_tile_by()).
-NwStat alignMlsp(const NwAlgParams& pr, NwAlgInput& nw, NwAlgResult& res, bool overlap)
+// The sparse family's tile: width from the slot's parameters, height the engine's (1024).
+NwStat alignMlsp(int tileBx, NwAlgInput& nw, NwAlgResult& res, bool overlap)
 {
     if (NwStat s = checkInput(nw); s != NwStat::success) return s;
-    int tileBx = 256;
-    if (pr.has("tileBx"))
-    {
-        const int v = pr.at("tileBx").curr();
-        if (v >= 64 && v % 16 == 0) tileBx = v;
-    }
     gsa_sparse_geom g {};
     if (int st = gsa_sparse_geometry(nw.adjrows, nw.adjcols, tileBx, &g); st != GSA_SUCCESS) return (NwStat)st;
-    try
-    {
-        nw.tileHrowMat.resize((size_t)g.hrowElems);
-        nw.tileHcolMat.resize((size_t)g.hcolElems);
-    }
-    catch (const std::exception&)
-    {
-        return NwStat::errorMemoryAllocation;
-    }
     int cost = 0;
-    gsa_mem_stats_reset(nw.ctx);  // peaks of this call only (res keeps the max over runs)
     int st;
     {
+        // the stopwatch starts before the host result arrays are allocated, so that their
+        // allocation is part of align.alloc (nwalign_gpu9_mlsp_diagdiagdiag.cu:434-459)
         LapScope laps(nw.ctx, res.sw_align);
+        try
+        {
+            nw.tileHrowMat.resize((size_t)g.hrowElems);
+            nw.tileHcolMat.resize((size_t)g.hcolElems);
+        }
+        catch (const std::exception&)
+        {
+            return NwStat::errorMemoryAllocation;
+        }
+        gsa_mem_stats_reset(nw.ctx);  // peaks of this call only (res keeps the max over runs)
         st = (overlap ? gsa_align_sparse_pt : gsa_align_sparse)(nw.ctx, nw.seqY.data(), nw.adjrows, nw.seqX.data(),
                                                                 nw.adjcols, nw.subst.data(), nw.substsz, nw.gapoCost,
                                                                 tileBx, nw.tileHrowMat.data(), nw.tileHcolMat.data(),
@@ -108,27 +103,24 @@ NwStat alignMlsp(const NwAlgParams& pr, NwAlgInput& nw, NwAlgResult& res, bool o
     return NwStat::success;
 }
 
-}  // namespace
-
-// Plain family (the NwAlign_Gpu1..6 slots): the full (adjrows x adjcols) matrix in nw.score.  No
-// tunables: the wavefront geometry is fixed by the hardware; parameters the
-// reference's files list for these slots are accepted and ignored.
-NwStat NwAlign_Amd_Strip_Full(const NwAlgParams&, NwAlgInput& nw, NwAlgResult& res)
+// Plain family: the full (adjrows x adjcols) matrix in nw.score.  The wavefront geometry is the
+// engine's; the slots' tiling parameters are checked (slotGeometry) and noted.
+NwStat alignFull(NwAlgInput& nw, NwAlgResult& res)
 {
     if (NwStat s = checkInput(nw); s != NwStat::success) return s;
-    try
-    {
-        nw.score.resize((size_t)nw.adjrows * (size_t)nw.adjcols);
-    }
-    catch (const std::exception&)
-    {
-        return NwStat::errorMemoryAllocation;
-    }
     int cost = 0;
-    gsa_mem_stats_reset(nw.ctx);
     int st;
     {
-        LapScope laps(nw.ctx, res.sw_align);
+        LapScope laps(nw.ctx, res.sw_align);  // host allocation inside align.alloc, as the reference's
+        try
+        {
+            nw.score.resize((size_t)nw.adjrows * (size_t)nw.adjcols);
+        }
+        catch (const std::exception&)
+        {
+            return NwStat::errorMemoryAllocation;
+        }
+        gsa_mem_stats_reset(nw.ctx);
         st = gsa_align_full(nw.ctx, nw.seqY.data(), nw.adjrows, nw.seqX.data(), nw.adjcols, nw.subst.data(),
                             nw.substsz, nw.gapoCost, nw.score.data(), &cost, nullptr);
     }
@@ -140,17 +132,127 @@ NwStat NwAlign_Amd_Strip_Full(const NwAlgParams&, NwAlgInput& nw, NwAlgResult& r
     return NwStat::success;
 }
 
-// Sparse family (the NwAlign_Gpu7..9 slots).
-NwStat NwAlign_Amd_Strip_Mlsp(const NwAlgParams& pr, NwAlgInput& nw, NwAlgResult& res)
+// The slot's parameters -> the engine geometry that runs, noted in the TSV's alg_params column
+// (engine_tileBx / engine_tileBy) so a row says which tile the headers have.
+NwStat runSlot(const char* slot, const NwAlgParams& pr, NwAlgInput& nw, NwAlgResult& res, bool overlap)
 {
-    return alignMlsp(pr, nw, res, false);
+    SlotGeometry geo;
+    if (NwStat s = slotGeometry(slot, pr, geo); s != NwStat::success) return s;
+    if (geo.sparse)
+    {
+        std::string& j = res.algParamsJson;
+        const std::string note = "\"engine_tileBx\":" + std::to_string(geo.tileBx) +
+                                 ",\"engine_tileBy\":" + std::to_string(gsa_sparse_tile_by());
+        if (j.size() >= 2 && j.back() == '}' && j.find("engine_tileBx") == std::string::npos)
+            j.insert(j.size() - 1, (j.size() > 2 ? "," : "") + note);
+        return alignMlsp(geo.tileBx, nw, res, overlap);
+    }
+    return alignFull(nw, res);
 }
 
+}  // namespace
+
+// ---- the parameter contract of the reference's slots ---------------------------------------
+// Each reference slot reads its own parameters and returns errorInvalidValue for a value its
+// rules reject (nwalign_gpu1_ml_diag.cu:82-93, gpu2:125-141, gpu3:297-311, gpu4:292-310,
+// gpu5:322-333, gpu6:303-321, gpu7_mlsp:304-320, gpu8:325-340, gpu9:382-414).  The rules are
+// kept as written, with the reference's units: a warp is kParamWarp = 32 threads (the unit its
+// parameter files are tuned in, param_best.json:1, an RTX 3090), a block at most 1024 threads.
+// A parameter the file does not list is not required: the engine's geometry does not need it.
+// The sparse slots' tile width maps to the engine's nearest (a multiple of 16, >= 64):
+//   gpu7/gpu8: tileBx;
+//   gpu9: the reference's derived width, tileBx = k*subtileBx - (tileBy - 1) with tileBy =
+//         subtileRows*32 and k = ceil((subtileCols*subtileBx + tileBy - 1) / subtileBx) (:389-398);
+//   this engine's slots (and gpu9 given "tileBx" directly): tileBx itself, which must then be a
+//         multiple of 16 and >= 64.
+// The tile height is the engine's 1024 whatever the slot asks (gsa_sparse_tile_by).
+NwStat slotGeometry(const std::string& slot, const NwAlgParams& pr, SlotGeometry& out)
+{
+    constexpr int kParamWarp = 32, kMaxThreads = 1024;
+    const auto opt = [&](const char* n, int& v) {
+        if (!pr.has(n)) return false;
+        v = pr.at(n).curr();
+        return true;
+    };
+    const auto threads = [&](const char* n) {
+        int v = 0;
+        return !opt(n, v) || (v >= kParamWarp && v <= kMaxThreads);
+    };
+    const auto atLeast1 = [&](const char* n) {
+        int v = 0;
+        return !opt(n, v) || v >= 1;
+    };
+    const auto warpMultiple = [&](const char* n) {
+        int v = 0;
+        return !opt(n, v) || (v >= 1 && v % kParamWarp == 0);
+    };
+    const auto nearest16 = [](long long w) { return (int)std::max<long long>(64, ((w + 8) / 16) * 16); };
+    out = SlotGeometry {};
+    const auto bad = NwStat::errorInvalidValue;
+    try
+    {
+        if (slot == "NwAlign_Gpu1_Ml_Diag") return threads("threadsPerBlock") ? NwStat::success : bad;
+        if (slot == "NwAlign_Gpu2_Ml_DiagRow2Pass")
+            return atLeast1("tileBx") && atLeast1("tileBy") && threads("threadsPerBlock") ? NwStat::success : bad;
+        if (slot == "NwAlign_Gpu3_Ml_DiagDiag") return threads("threadsPerBlockA") && atLeast1("tileBx") ? NwStat::success : bad;
+        if (slot == "NwAlign_Gpu4_Ml_DiagDiag2Pass" || slot == "NwAlign_Gpu6_Coop_DiagDiag2Pass")
+            return warpMultiple("tileAx") && atLeast1("tileAy") && atLeast1("tileBx") ? NwStat::success : bad;
+        if (slot == "NwAlign_Gpu5_Coop_DiagDiag") return atLeast1("tileAx") ? NwStat::success : bad;
+        if (slot == "NwAlign_Amd_Strip_Full") return NwStat::success;
+        out.sparse = true;
+        int v = 256;
+        if (slot == "NwAlign_Gpu7_Mlsp_DiagDiag" || slot == "NwAlign_Gpu8_Mlsp_DiagDiag")
+        {
+            if (!threads("threadsPerBlockA") || !atLeast1("warpDivFactorB") || !atLeast1("tileBx")) return bad;
+            if (opt("tileBx", v)) v = nearest16(v);
+            out.tileBx = v;
+            return NwStat::success;
+        }
+        const bool gpu9 = slot == "NwAlign_Gpu9_Mlsp_DiagDiagDiag";
+        if (!gpu9 && slot != "NwAlign_Amd_Strip_Mlsp" && slot != "NwAlign_Amd_Strip_Mlsppt") return bad;
+        const int nSub = (int)pr.has("subtileRows") + (int)pr.has("subtileCols") + (int)pr.has("subtileBx");
+        if (gpu9 && nSub > 0)
+        {
+            if (nSub != 3 || pr.has("tileBx") || !threads("threadsPerBlockA")) return bad;
+            const long long rows = pr.at("subtileRows").curr(), cols = pr.at("subtileCols").curr();
+            const long long sbx = pr.at("subtileBx").curr();
+            if (rows < 1 || cols < 1 || sbx < 1) return bad;
+            const long long tileBy = rows * kParamWarp;
+            const long long k = (cols * sbx + tileBy - 1 + sbx - 1) / sbx;
+            const long long tileBx = k * sbx - (tileBy - 1);
+            if (sbx < kParamWarp || tileBx < tileBy) return bad;
+            out.tileBx = nearest16(tileBx);
+            return NwStat::success;
+        }
+        if (!threads("threadsPerBlockA")) return bad;
+        if (opt("tileBx", v) && (v < 64 || v % 16 != 0)) return bad;
+        out.tileBx = v;
+        return NwStat::success;
+    }
+    catch (const std::exception&)
+    {
+        return bad;  // as the reference's try / catch around pr.at()
+    }
+}
+
+// One adapter per slot name (NwAlignFn has no name argument): the reference's Gpu1..9 slots with
+// their parameter rules, and this engine's own three names.
+#define GSA_SLOT(name, overlap) \
+    NwStat name(const NwAlgParams& pr, NwAlgInput& nw, NwAlgResult& res) { return runSlot(#name, pr, nw, res, overlap); }
+GSA_SLOT(NwAlign_Gpu1_Ml_Diag, false)
+GSA_SLOT(NwAlign_Gpu2_Ml_DiagRow2Pass, false)
+GSA_SLOT(NwAlign_Gpu3_Ml_DiagDiag, false)
+GSA_SLOT(NwAlign_Gpu4_Ml_DiagDiag2Pass, false)
+GSA_SLOT(NwAlign_Gpu5_Coop_DiagDiag, false)
+GSA_SLOT(NwAlign_Gpu6_Coop_DiagDiag2Pass, false)
+GSA_SLOT(NwAlign_Gpu7_Mlsp_DiagDiag, false)
+GSA_SLOT(NwAlign_Gpu8_Mlsp_DiagDiag, false)
+GSA_SLOT(NwAlign_Gpu9_Mlsp_DiagDiagDiag, false)
+GSA_SLOT(NwAlign_Amd_Strip_Full, false)
+GSA_SLOT(NwAlign_Amd_Strip_Mlsp, false)
 // mlsppt ("multi-launch sparse with parallel transfer", README.md:39 of the reference, never
 // implemented there): the same outputs, the header copy-back overlapped with the fill.
-NwStat NwAlign_Amd_Strip_Mlsppt(const NwAlgParams& pr, NwAlgInput& nw, NwAlgResult& res)
-{
-    return alignMlsp(pr, nw, res, true);
-}
+GSA_SLOT(NwAlign_Amd_Strip_Mlsppt, true)
+#undef GSA_SLOT
 
 }  // namespace gsa_host

@@ -131,15 +131,18 @@ def shard_align(pairs: List[Tuple[np.ndarray, np.ndarray]], subst: Optional[np.n
 
 
 def gpu_batch_align(device: int = 0, mode: str = "sparse", tileBx: int = 256, repeats: int = 1,
-                    out_budget_bytes: Optional[int] = None, warmup: int = 0) -> AlignBatchFn:
+                    out_budget_bytes: Optional[int] = None, warmup: int = 0, pitched: bool = True) -> AlignBatchFn:
     """The GPU `align_batch` of one rank: inputs uploaded before the timed region, then the
     rank's pairs in as few persistent launches as the output memory allows (one launch for
     the whole share when it fits `out_budget_bytes`, default 60 % of free HBM): the launch's
     ticket space spans all its pairs, so every CU stays busy.  align_cost: the last cell of
     the full matrix, or the last tile's recompute from its headers for the sparse form (as
-    the reference's mlsp align functions, nwalign_gpu9_mlsp_diagdiagdiag.cu:713-716)."""
+    the reference's mlsp align functions, nwalign_gpu9_mlsp_diagdiagdiag.cu:713-716).
+    pitched (full mode): each matrix in the engine's fastest device layout (gsa_full_pitch row
+    pitch, cell (1, 0) on a 128-byte boundary), as the reference keeps its device matrix padded
+    (nwalign_gpu3_ml_diagdiag.cu:315-325); False: unpadded adjrows x adjcols."""
     import torch
-    from . import Engine, sparse_geometry, sparse_align_cost, SparseResult
+    from . import Engine, sparse_geometry, sparse_align_cost, SparseResult, full_pitch, full_base_offset
 
     def run(indices, pairs, subst, gapo):
         if not indices:
@@ -151,7 +154,13 @@ def gpu_batch_align(device: int = 0, mode: str = "sparse", tileBx: int = 256, re
         ts = torch.from_numpy(subst).to(dev)
         ins = [(torch.from_numpy(pairs[i][0]).to(dev), torch.from_numpy(pairs[i][1]).to(dev)) for i in indices]
         geoms = [sparse_geometry(len(y), len(x), tileBx) if mode == "sparse" else None for y, x in ins]
-        sizes = [(g.hrowElems + g.hcolElems) if g is not None else len(y) * len(x) for (y, x), g in zip(ins, geoms)]
+        pit = mode != "sparse" and pitched
+        lds = [full_pitch(len(x)) if pit else len(x) for y, x in ins]
+        boff = full_base_offset() if pit else 0
+        # a pitched matrix starts boff ints into a slot of whole 128-byte lines (flat is 256-B aligned)
+        sizes = [(g.hrowElems + g.hcolElems) if g is not None else
+                 (-(-(boff + len(y) * ld) // 32) * 32 if pit else len(y) * ld)
+                 for (y, x), g, ld in zip(ins, geoms, lds)]
         budget = out_budget_bytes
         if budget is None:
             free, _ = torch.cuda.mem_get_info(dev)
@@ -186,11 +195,11 @@ def gpu_batch_align(device: int = 0, mode: str = "sparse", tileBx: int = 256, re
                     gi.append(np.arange(g.tileHrowLen, dtype=np.int64) + off + last * g.tileHrowLen)
                     gi.append(np.arange(g.tileHcolLen, dtype=np.int64) + off + g.hrowElems + last * g.tileHcolLen)
                 else:
-                    sc = flat[off:off + sizes[j]]
+                    sc = flat[off + boff:off + boff + len(y) * lds[j]]
                     d.append((y.data_ptr(), len(y), x.data_ptr(), len(x), sc.data_ptr(), sc, None))
-                    gi.append(np.array([off + sizes[j] - 1], dtype=np.int64))
+                    gi.append(np.array([off + boff + (len(y) - 1) * lds[j] + len(x) - 1], dtype=np.int64))
                 off += sizes[j]
-            descs.append(d)
+            descs.append((d, [lds[j] for j in c] if pit else None))
             # chunk c's pairs are consecutive, so their slices of keepflat are one range
             gathers.append((torch.from_numpy(np.concatenate(gi)).to(dev), keepflat[kbase[c[0]]:kbase[c[-1] + 1]]))
         torch.cuda.synchronize(dev)
@@ -201,9 +210,9 @@ def gpu_batch_align(device: int = 0, mode: str = "sparse", tileBx: int = 256, re
                 eng.sync(stream.cuda_stream)
                 torch.cuda.synchronize(dev)
                 t0 = time.perf_counter()
-            for d, (gidx, gout) in zip(descs, gathers):
+            for (d, dl), (gidx, gout) in zip(descs, gathers):
                 eng.fill_batch_dev([e[:5] for e in d], ts.data_ptr(), substsz, gapo, mode=mode, tileBx=tileBx,
-                                   stream=stream.cuda_stream)
+                                   stream=stream.cuda_stream, lds=dl)
                 # result slices, in stream order behind the fill (before the next chunk reuses flat)
                 with torch.cuda.stream(stream):
                     torch.index_select(flat, 0, gidx, out=gout)

@@ -85,7 +85,8 @@ int gsa_device_cu_count(const gsa_ctx* ctx);
 const char* gsa_version(void);
 int gsa_set_lap_callback(gsa_ctx* ctx, gsa_lap_fn fn, void* user);
 
-/* Tile height of the sparse representation this build produces (63 * strips per workgroup). */
+/* Tile height (tileBy) of the sparse representation this build produces: 1024, the rows of one
+ * K-rows workgroup ticket (4 strip waves x 64 lanes x 4 rows per lane). */
 int32_t gsa_sparse_tile_by(void);
 /* Geometry for (adjrows, adjcols, tileBx); tileBx must be a multiple of 16 and >= 64. */
 int gsa_sparse_geometry(int32_t adjrows, int32_t adjcols, int32_t tileBx, gsa_sparse_geom* geom);
@@ -103,6 +104,20 @@ int gsa_fill_sparse_dev(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, cons
                         const int32_t* subst, int32_t substsz, int32_t gapo, int32_t tileBx, int32_t* tileHrowMat,
                         int32_t* tileHcolMat, void* stream);
 int gsa_sync(gsa_ctx* ctx, void* stream);
+
+/* Pitched device layout of a full matrix.  The reference keeps its device score matrix padded
+ * and crops it on the way back (nwalign_gpu3_ml_diagdiag.cu:315-325, cudaMemcpy2D at :585-588,
+ * src/memory.hpp:217); these entry points take the row pitch `ld` (>= adjcols, in ints) of such a
+ * device matrix: cell (i, j) at score[i*ld + j].  Every ld >= adjcols gives the same values.
+ * gsa_full_pitch(adjcols) is the pitch this engine writes fastest: ld = 1 (mod 32), and with the
+ * matrix placed gsa_full_base_offset() ints past a 128-byte boundary (cell (1, 0) on one), all
+ * cells of an anti-diagonal share their offset within a 128-byte line, so the wavefront's row
+ * segments are stored as whole aligned lines (no partial-line writes). */
+int32_t gsa_full_pitch(int32_t adjcols);
+int32_t gsa_full_base_offset(void);
+int gsa_fill_full_pitched_dev(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, const int32_t* seqX,
+                              int32_t adjcols, const int32_t* subst, int32_t substsz, int32_t gapo, int32_t* score,
+                              int32_t ld, void* stream);
 /* Peak resource use of the fills launched on this context since its creation or the last reset:
  * the reference's NwAlgResult peak-alloc columns (updateNwAlgPeakMemUsage, nwalign_shared.cpp:5-25).
  * shmem/locmem/regmem = per-workgroup LDS, per-lane scratch x threads, per-lane VGPRs x 4 B x
@@ -138,6 +153,10 @@ typedef struct gsa_pair_dev
  * Launches on one context must be ordered (same stream, or synchronised). */
 int gsa_fill_full_batch_dev(gsa_ctx* ctx, int32_t npairs, const gsa_pair_dev* pairs, const int32_t* subst,
                             int32_t substsz, int32_t gapo, void* stream);
+/* As gsa_fill_full_batch_dev, pair p's matrix with row pitch lds[p] (>= its adjcols; see
+ * gsa_full_pitch). */
+int gsa_fill_full_batch_pitched_dev(gsa_ctx* ctx, int32_t npairs, const gsa_pair_dev* pairs, const int32_t* lds,
+                                    const int32_t* subst, int32_t substsz, int32_t gapo, void* stream);
 int gsa_fill_sparse_batch_dev(gsa_ctx* ctx, int32_t npairs, const gsa_pair_dev* pairs, const int32_t* subst,
                               int32_t substsz, int32_t gapo, int32_t tileBx, void* stream);
 

@@ -39,3 +39,14 @@ def test_full_batch_write_ratio():
     assert r is not None and 1.0 <= r < 1.5
     assert bench.pmc_write_ratio(32, "gsa::nw_lane_kernel<4,false>") is None
     assert bench.pmc_write_ratio(64, "gsa::nw_krow_kernel<4>") is None
+
+
+def test_rehearsal_fields(monkeypatch):
+    """A GSA_BENCH_REHEARSE run (N gloo ranks sharing cuda:0) reports one GPU and says it is a
+    rehearsal, so its line can never pass as a multi-GPU result; a real run reports its ranks."""
+    monkeypatch.setattr(bench, "REHEARSE", True)
+    f = bench.gpu_fields(2)
+    assert f["n_gpus"] == 1 and f["rehearsal"] is True and "REHEARSAL" in f["parallelism"]
+    monkeypatch.setattr(bench, "REHEARSE", False)
+    f = bench.gpu_fields(8)
+    assert f == {"n_gpus": 8, "rehearsal": False, "parallelism": "pair-sharded x8"}

@@ -208,3 +208,69 @@ def test_full_fill_at_unaligned_base(engine, golden, R, C, off):
     S, _ = oracle.fill_full(Y, X, golden.blosum62, -11)
     assert (out[:off] == -7).all() and (out[off + n:] == -7).all()
     assert np.array_equal(out[off:off + n].reshape(len(Y), len(X)), S)
+
+
+@pytest.mark.parametrize("R,C,pad,off", [(1, 1, 0, 31), (2, 3, 5, 31), (63, 64, -1, 31), (64, 65, -1, 31),
+                                         (129, 1029, -1, 31), (300, 1, -1, 31), (385, 1500, -1, 0),
+                                         (1100, 2222, -1, 31), (2049, 777, 33, 17), (700, 4099, -1, 31)])
+def test_full_fill_pitched(engine, golden, R, C, pad, off):
+    """Pitched device layout (gsa_fill_full_pitched_dev): row pitch gsa_full_pitch (pad -1) or
+    adjcols + pad, the matrix `off` ints past a 128-byte boundary.  Every cell equals the oracle;
+    the padding columns and the words around the matrix stay untouched."""
+    import torch
+    Y, X = random_pair(R, C, 5 * R + C + off)
+    dev = torch.device("cuda:0")
+    y, x = torch.from_numpy(Y).to(dev), torch.from_numpy(X).to(dev)
+    s = torch.from_numpy(golden.blosum62).to(dev)
+    ld = gsa.full_pitch(len(X)) if pad < 0 else len(X) + pad
+    assert ld >= len(X) and (pad >= 0 or ld % 32 == 1)
+    n = len(Y) * ld
+    buf = torch.full((n + 64 + off,), -7, dtype=torch.int32, device=dev)
+    engine.fill_full_dev(y.data_ptr(), len(Y), x.data_ptr(), len(X), s.data_ptr(), 25, -11, buf.data_ptr() + 4 * off,
+                         ld=ld)
+    engine.sync()
+    out = buf.cpu().numpy()
+    S, _ = oracle.fill_full(Y, X, golden.blosum62, -11)
+    assert (out[:off] == -7).all() and (out[off + n:] == -7).all()
+    M = out[off:off + n].reshape(len(Y), ld)
+    assert np.array_equal(M[:, :len(X)], S)
+    assert (M[:, len(X):] == -7).all()
+
+
+def test_full_pitch_contract(engine):
+    """gsa_full_pitch: the smallest ld >= adjcols with ld = 1 (mod 32); a pitch below adjcols is
+    rejected with errorInvalidValue."""
+    for ac in (1, 2, 32, 33, 34, 64, 65, 10001, 20001, 20032):
+        ld = gsa.full_pitch(ac)
+        assert ld >= ac and ld % 32 == 1 and ld - 32 < ac
+    assert gsa.full_base_offset() == 31
+    import torch
+    dev = torch.device("cuda:0")
+    t = torch.zeros(64, dtype=torch.int32, device=dev)
+    with pytest.raises(gsa.NwError) as ei:
+        engine.fill_full_dev(t.data_ptr(), 4, t.data_ptr(), 4, t.data_ptr(), 1, -11, t.data_ptr(), ld=3)
+    assert ei.value.stat == gsa.NwStat.errorInvalidValue
+
+
+@pytest.mark.parametrize("ns", ["2", "4", "8"])
+def test_full_batch_pitched(engine, golden, ns, monkeypatch):
+    """A batched launch into pitched matrices (gsa_fill_full_batch_pitched_dev), every cell of
+    every pair against the oracle."""
+    import torch
+    from gpuseqalign_amd import shard
+    monkeypatch.setenv("GSA_LANE_NS", ns)
+    pairs = [random_pair(r, c, 11 * r + c) for r, c in ((700, 900), (1, 5), (1500, 333), (257, 2049), (64, 64))]
+    dev = torch.device("cuda:0")
+    s = torch.from_numpy(golden.blosum62).to(dev)
+    ins = [(torch.from_numpy(Y).to(dev), torch.from_numpy(X).to(dev)) for Y, X in pairs]
+    lds = [gsa.full_pitch(len(X)) for _, X in pairs]
+    bufs = [torch.full((len(Y) * ld + 64,), -7, dtype=torch.int32, device=dev) for (Y, _), ld in zip(pairs, lds)]
+    engine.fill_batch_dev([(y.data_ptr(), len(y), x.data_ptr(), len(x), b.data_ptr() + 4 * 31)
+                           for (y, x), b in zip(ins, bufs)], s.data_ptr(), 25, -11, mode="full", lds=lds)
+    engine.sync()
+    for (Y, X), b, ld in zip(pairs, bufs, lds):
+        out = b.cpu().numpy()[31:31 + len(Y) * ld].reshape(len(Y), ld)
+        S, _ = oracle.fill_full(Y, X, golden.blosum62, -11)
+        assert np.array_equal(out[:, :len(X)], S)
+    costs, _ = shard.gpu_batch_align(0, mode="full")(list(range(len(pairs))), pairs, golden.blosum62, -11)
+    assert costs == [int(oracle.fill_full(Y, X, golden.blosum62, -11)[1]) for Y, X in pairs]

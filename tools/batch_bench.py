@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--repeats", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--check", action="store_true")
+    ap.add_argument("--unpadded", action="store_true", help="full mode: adjcols pitch instead of gsa_full_pitch")
     a = ap.parse_args()
 
     import torch
@@ -40,7 +41,8 @@ def main():
     sd = F.read_subst_json(os.path.join(ROOT, "tests", "golden", "resrc", "subst.json"))
     subst = sd.matrix("blosum62") if rank == 0 else None
     pairs = shard.synthetic_batch(a.pairs, a.lo, a.hi, seed0=1000)
-    fn = shard.gpu_batch_align(local, mode=a.mode, tileBx=a.tileBx, repeats=a.repeats, warmup=a.warmup)
+    fn = shard.gpu_batch_align(local, mode=a.mode, tileBx=a.tileBx, repeats=a.repeats, warmup=a.warmup,
+                                pitched=not a.unpadded)
     rep = shard.shard_align(pairs, subst, -11, fn, device=torch.device("cuda", local) if world > 1 else None)
     if a.check and rank == 0:
         import oracle
@@ -50,7 +52,7 @@ def main():
     if rank == 0:
         print(json.dumps({"metric": "GCUPS, batch of independent NW-LG pairs (BASELINE configs[3] shape)",
                           "value": round(rep.gcups, 2), "unit": "GCUPS", "n_gpus": rep.world, "pairs": a.pairs,
-                          "lengths": [a.lo, a.hi], "mode": a.mode, "tileBx": a.tileBx, "cells": rep.cells,
+                          "lengths": [a.lo, a.hi], "mode": a.mode, "pitched": a.mode == "full" and not a.unpadded, "tileBx": a.tileBx, "cells": rep.cells,
                           "seconds": round(rep.elapsed_s, 5), "repeats": a.repeats, "warmup": a.warmup,
                           "order": os.environ.get("GSA_BATCH_ORDER", "round-robin"),
                           "costs_head": [r.align_cost for r in rep.results[:4]], "checked": a.check}), flush=True)
