@@ -74,6 +74,17 @@ def lane_ns():
     return int(v) if v in ("1", "2", "3", "4", "6", "8") else 4
 
 
+def lane_kernel_name(single):
+    """The lane instantiation a full fill runs (nw_lane.hip launch_lane_fill): <NS, feeder wave,
+    paired stores>; the feeder wave for single pairs at NS = 4 (GSA_LANE_FEED), paired stores for
+    batches (GSA_LANE_PAIR)."""
+    ns = lane_ns()
+    fe, pe = os.environ.get("GSA_LANE_FEED", ""), os.environ.get("GSA_LANE_PAIR", "")
+    fd = ns == 4 and (int(fe) != 0 if fe else single)
+    pair = (int(pe) != 0 if pe else not fd) if ns == 4 else True
+    return f"gsa::nw_lane_kernel<{ns},{'true' if fd else 'false'},{'true' if pair else 'false'}>"
+
+
 def sparse_kernel_name():
     """The K-rows instantiation a single-pair sparse fill runs (gsa_capi.hip: GSA_KROW_NS / GSA_KROW_K,
     default (4, 4); the profile ring is 512 columns with 2 strips, 1024 otherwise; GSA_KROW_Q8=0: the
@@ -299,10 +310,11 @@ def bench_full_batch(world, rank, local, n_pairs):
                         f"matrices ({out_bytes / 1e9:.1f} GB), one persistent launch, LPT-sharded over {world} rank(s) "
                         "(1 untimed + 3 timed launches; seconds per launch)",
             "value": round(rep.gcups, 2), "unit": "GCUPS", "scaling": "strong", "seconds": round(rep.elapsed_s, 4),
-            "kernel": f"gsa::nw_lane_kernel<{lane_ns()},false> (full, one row per lane)",
+            "kernel": f"{lane_kernel_name(False)} (full, one row per lane, pitched layout, paired stores)",
+            "layout": "pitched: row pitch gsa_full_pitch(adjcols) = 1 mod 32, cell (1,0) on a 128-byte boundary",
             "hbm_write_GBps": round(gbps * world, 1), "hbm_frac": round(gbps / PEAK_HBM_GBPS, 4),
             "bound": "hbm (4 B written per cell; MI355X 8 TB/s spec)",
-            "pmc_write_over_algorithmic": pmc_write_ratio(n_pairs, f"gsa::nw_lane_kernel<{lane_ns()},false>"),
+            "pmc_write_over_algorithmic": pmc_write_ratio(n_pairs, lane_kernel_name(False)),
             "pairs": n_pairs, "pairs_matching_golden": match}
 
 
@@ -321,6 +333,18 @@ def pmc_write_ratio(n_pairs, kernel):
 
 
 CFG5 = [("SW-LG", -11, -11, True), ("NW-AG", -11, -1, False)]
+
+
+def score_kernel_name(go, ge, local, substsz=25):
+    """The kernel gsa_score_dev runs (gsa_capi.hip score_dev_impl): the K-rows score kernel unless
+    GSA_SCORE_KERNEL=strip, SW with ge > 0, or its LDS does not fit (a 25-letter table fits); the
+    strip kernel's score modes otherwise (4 strips per workgroup)."""
+    mode = (5 if go == ge else 4) if local else (6 if go == ge else 3)
+    mname = (("kModeScoreSWL" if go == ge else "kModeScoreSW") if local else
+             ("kModeScoreAGL" if go == ge else "kModeScoreAG"))
+    krow = os.environ.get("GSA_SCORE_KERNEL", "") != "strip" and (not local or ge <= 0) and substsz <= 32
+    return (f"gsa::nw_kscore_kernel<{mode}> ({mname})" if krow else
+            f"gsa::nw_strip_kernel<4,{mode}> ({mname}, strip kernel)")
 
 
 def bench_config5(dev, eng, steps, warmup, cpu_sample, rank, world):
@@ -353,10 +377,7 @@ def bench_config5(dev, eng, steps, warmup, cpu_sample, rank, world):
         out[name] = {"value": round(R * C / kms / 1e6, 2), "unit": "GCUPS", "kernel_ms": round(kms, 4),
                      "ms_per_call": round(wall * 1e3, 4), "score": r["score"], "end": [r["i_end"], r["j_end"]],
                      "golden_match": ok, "gapo": go, "gape": ge, "local": local,
-                     "kernel": "gsa::nw_kscore_kernel<%d> (%s)" % (
-                         (5 if go == ge else 4) if local else (6 if go == ge else 3),
-                         ("kModeScoreSWL" if go == ge else "kModeScoreSW") if local else
-                         ("kModeScoreAGL" if go == ge else "kModeScoreAG"))}
+                     "kernel": score_kernel_name(go, ge, local)}
         if cpu_sample > 0 and rank == 0 and world == 1:
             import oracle
             ncpu, phys, quota, nproc = cpu_topology()
@@ -468,7 +489,7 @@ def main():
                                "(resrc/seq_generated.fa), full int32 score matrix in HBM",
                    "value": round(world * R2 * C2 * a.steps / el2 / 1e9, 2), "unit": "GCUPS",
                    "ms_per_step": round(el2 * 1e3 / a.steps, 4), "kernel_ms": round(km2, 4),
-                   "kernel": (f"gsa::nw_lane_kernel<{lane_ns()},{'true' if lane_ns() == 4 else 'false'}> "
+                   "kernel": (f"{lane_kernel_name(True)} "
                               "(full, one row per lane" + (", feeder wave)" if lane_ns() == 4 else ")")),
                    "hbm_write_GBps": round(b2 / (km2 * 1e-3) / 1e9, 1),
                    "hbm_frac": round(b2 / (km2 * 1e-3) / 1e9 / PEAK_HBM_GBPS, 4),

@@ -75,7 +75,7 @@ struct gsa_ctx
     // mlsppt: host-mapped per-tile-row words (epoch << 32 | column chunks in memory); a pinned
     // host buffer the strided column chunks are packed into by a kernel on ptstream
     unsigned long long* ptflags = nullptr;
-    void* ptpin = nullptr;  // pinned, device-mapped, ptpin_cap bytes (>= kPtPin)
+    void* ptpin = nullptr;  // pinned host memory (hipHostMallocDefault), ptpin_cap bytes (>= kPtPin)
     size_t ptpin_cap = 0;
     hipEvent_t ptev[2] = {nullptr, nullptr};
     static constexpr size_t kPtPin = 64u << 20;  // two slots
@@ -831,68 +831,6 @@ hipError_t copy_d2h(gsa_ctx* ctx, void* dst, const void* src, size_t bytes)
     work(0);
     for (auto& x : th) x.join();
     for (int k = 0; k < T; ++k)
-        if (errs[k] != hipSuccess) return errs[k];
-    return hipSuccess;
-}
-
-// Device -> pageable host copy of `height` rows of `width` bytes, source rows `spitch` apart,
-// destination rows `dpitch` apart (a column chunk of a tile-major header matrix): the rows are split
-// over the copy threads, each moving groups of rows by one DMA into a pinned chunk and copying them
-// into place while the next group's DMA runs.  width <= kCopyChunk.  A packed source (spitch ==
-// width) moves by plain copies: the runtime splits a strided device-to-host copy into one DMA per
-// row (~4 us each, measured: 25 column chunks of 98 tile rows took 20 ms).
-hipError_t copy_d2h_2d(gsa_ctx* ctx, char* dst, size_t dpitch, const char* src, size_t spitch, size_t width,
-                       size_t height)
-{
-    constexpr int T = gsa_ctx::kCopyThreads;
-    constexpr size_t kC = gsa_ctx::kCopyChunk;
-    if (width == 0 || height == 0) return hipSuccess;
-    if (width > kC) return hipErrorInvalidValue;
-    hipError_t e = hipSuccess;
-    for (int k = 0; k < T && e == hipSuccess; ++k)
-    {
-        if (!ctx->xstream[k]) e = hipStreamCreateWithFlags(&ctx->xstream[k], hipStreamNonBlocking);
-        for (int j = 0; j < 2 && e == hipSuccess; ++j)
-        {
-            if (!ctx->xstage[k][j]) e = hipHostMalloc(&ctx->xstage[k][j], kC, hipHostMallocDefault);
-            if (e == hipSuccess && !ctx->xev[k][j]) e = hipEventCreateWithFlags(&ctx->xev[k][j], hipEventDisableTiming);
-        }
-    }
-    if (e != hipSuccess) return e;
-    const size_t perGroup = std::max<size_t>(1, kC / width);
-    const int nT = (int)std::min<size_t>(T, (height + perGroup - 1) / perGroup);
-    const size_t perT = (height + nT - 1) / nT;
-    hipError_t errs[T];
-    auto work = [&](int k) {
-        hipError_t r = hipSetDevice(ctx->device);
-        const size_t lo = std::min(height, (size_t)k * perT), hi = std::min(height, (size_t)(k + 1) * perT);
-        const size_t n = (hi - lo + perGroup - 1) / perGroup;
-        auto issue = [&](size_t i) {
-            const size_t r0 = lo + i * perGroup, rows = std::min(perGroup, hi - r0);
-            hipError_t q = spitch == width
-                               ? hipMemcpyAsync(ctx->xstage[k][i & 1], src + r0 * spitch, rows * width,
-                                                hipMemcpyDeviceToHost, ctx->xstream[k])
-                               : hipMemcpy2DAsync(ctx->xstage[k][i & 1], width, src + r0 * spitch, spitch, width, rows,
-                                                  hipMemcpyDeviceToHost, ctx->xstream[k]);
-            return q == hipSuccess ? hipEventRecord(ctx->xev[k][i & 1], ctx->xstream[k]) : q;
-        };
-        if (r == hipSuccess && n > 0) r = issue(0);
-        for (size_t i = 0; r == hipSuccess && i < n; ++i)
-        {
-            if (i + 1 < n && (r = issue(i + 1)) != hipSuccess) break;
-            if ((r = hipEventSynchronize(ctx->xev[k][i & 1])) != hipSuccess) break;
-            const size_t r0 = lo + i * perGroup, rows = std::min(perGroup, hi - r0);
-            for (size_t j = 0; j < rows; ++j)
-                std::memcpy(dst + (r0 + j) * dpitch, (const char*)ctx->xstage[k][i & 1] + j * width, width);
-        }
-        if (r != hipSuccess) (void)hipStreamSynchronize(ctx->xstream[k]);
-        errs[k] = r;
-    };
-    std::vector<std::thread> th;
-    for (int k = 1; k < nT; ++k) th.emplace_back(work, k);
-    work(0);
-    for (auto& x : th) x.join();
-    for (int k = 0; k < nT; ++k)
         if (errs[k] != hipSuccess) return errs[k];
     return hipSuccess;
 }

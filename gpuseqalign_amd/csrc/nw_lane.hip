@@ -119,7 +119,7 @@ __host__ __device__ inline LaneLds lane_layout(int ns, int substsz)
 // ------------------------------------------------------------------------------------
 // strip wave: 64 rows, one per lane
 // ------------------------------------------------------------------------------------
-template <int NS>
+template <int NS, bool PAIR>
 __device__ __forceinline__ void lane_strip(const StripArgs& a, const LaneLds& L, int tk, int w, int lane)
 {
     const int g = a.g;
@@ -186,6 +186,10 @@ __device__ __forceinline__ void lane_strip(const StripArgs& a, const LaneLds& L,
     }
     int H = rg, U = rg;
     int rpin = 0, rpco = 0, rpxo = 0;  // progress words read in the previous block, checked now
+    int tE[kLBlk];                     // PAIR: the even block's transposed values, stored with the odd one's
+    bool held = false;
+#pragma unroll
+    for (int e = 0; e < kLBlk; ++e) tE[e] = 0;
 
     auto block = [&](int b, int (&qc)[kLBlk], int (&qn)[kLBlk], int4v (&hc)[kLH], int4v (&hn)[kLH], auto rampT) {
         constexpr bool RAMP = decltype(rampT)::value;
@@ -259,15 +263,35 @@ __device__ __forceinline__ void lane_strip(const StripArgs& a, const LaneLds& L,
                     t[4 * k + d] = sw[0];
                     t[4 * (k + 1) + d] = sw[1];
                 }
-            if (kLBlk * b - 63 >= 1 && kLBlk * b + kLBlk - 1 <= C && r0 + 63 <= a.R)
+            // interior blocks (uniform): every chunk is in the matrix; scalar row bases.  PAIR: an
+            // even interior block's stores wait for the odd block after it, and the two blocks' stores
+            // of each 16-row group go out back to back, so both 64-byte halves of a 128-byte line
+            // (pitched layout, gsa_full_pitch) leave the wave one after the other
+            auto interior = [&](int bb) { return kLBlk * bb - 63 >= 1 && kLBlk * bb + kLBlk - 1 <= C && r0 + 63 <= a.R; };
+            auto store4 = [&](int bb, int k, const int (&v)[kLBlk]) {
+                const gptr<int> ub = G(a.score) + ((ptrdiff_t)(r0 + 16 * k) * a.ld - 16 * k + kLBlk * bb);
+                *(gptr<int4a>)(ub + xoff) = int4a {v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]};
+            };
+            if (PAIR && !RAMP && (b & 1) == 0 && b + 1 < NB && interior(b) && interior(b + 1))
             {
-                // interior block (uniform): every chunk is in the matrix; scalar row bases
+#pragma unroll
+                for (int e = 0; e < kLBlk; ++e) tE[e] = t[e];
+                held = true;
+            }
+            else if (PAIR && held)
+            {
 #pragma unroll
                 for (int k = 0; k < 4; ++k)
                 {
-                    const gptr<int> ub = G(a.score) + ((ptrdiff_t)(r0 + 16 * k) * a.ld - 16 * k + kLBlk * b);
-                    *(gptr<int4a>)(ub + xoff) = int4a {t[4 * k], t[4 * k + 1], t[4 * k + 2], t[4 * k + 3]};
+                    store4(b - 1, k, tE);
+                    store4(b, k, t);
                 }
+                held = false;
+            }
+            else if (interior(b))
+            {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) store4(b, k, t);
             }
             else
 #pragma unroll
@@ -475,8 +499,10 @@ __device__ __forceinline__ PairDesc lane_desc(const PairDesc* p)
     return u.d;
 }
 
-template <int NS, bool FD>
-__global__ void __launch_bounds__(64 * (NS + 2 + FD)) nw_lane_kernel(StripArgs a)
+// PAIR: an even block's output stores wait for the odd block after it (lane_strip).  Batches run two
+// workgroups per CU (three waves per SIMD): the register budget is held to 168
+template <int NS, bool FD, bool PAIR>
+__global__ void __launch_bounds__(64 * (NS + 2 + FD), FD ? 2 : 3) nw_lane_kernel(StripArgs a)
 {
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
@@ -538,17 +564,17 @@ __global__ void __launch_bounds__(64 * (NS + 2 + FD)) nw_lane_kernel(StripArgs a
         else
         {
             __builtin_amdgcn_s_setprio(3);
-            lane_strip<NS>(pa, L, tk, w, lane);
+            lane_strip<NS, PAIR>(pa, L, tk, w, lane);
             __builtin_amdgcn_s_setprio(0);
         }
     }
 }
 
-template <int NS, bool FD = false>
+template <int NS, bool FD = false, bool PAIR = true>
 hipError_t launch_lane(const StripArgs& a, int grid, hipStream_t stream)
 {
     const size_t lds = lane_lds_bytes(NS, a.substsz);
-    auto kern = nw_lane_kernel<NS, FD>;
+    auto kern = nw_lane_kernel<NS, FD, PAIR>;
     constexpr int kThreads = 64 * (NS + 2 + FD);
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
@@ -581,7 +607,14 @@ hipError_t launch_lane_fill(const StripArgs& a, int ns, int grid, hipStream_t st
     // workgroup per CU); GSA_LANE_FEED=0/1 overrides
     const char* fe = getenv("GSA_LANE_FEED");
     const bool fd = fe && *fe ? atoi(fe) != 0 : a.nPairs == 1;
-    if (ns == 4) return fd ? launch_lane<4, true>(a, grid, stream) : launch_lane<4>(a, grid, stream);
+    // paired output stores (lane_strip) for batches: 64 x 20k pitched 977-988 -> 1097 GCUPS; a single
+    // pair's strips run on their critical path, where the held block costs (10k 100 -> 93 GCUPS,
+    // profiles/r04_full_pitch_pair.txt); GSA_LANE_PAIR=0/1 overrides
+    const char* pe = getenv("GSA_LANE_PAIR");
+    const bool pair = pe && *pe ? atoi(pe) != 0 : !fd;
+    if (ns == 4)
+        return fd ? (pair ? launch_lane<4, true, true>(a, grid, stream) : launch_lane<4, true, false>(a, grid, stream))
+                  : (pair ? launch_lane<4, false, true>(a, grid, stream) : launch_lane<4, false, false>(a, grid, stream));
     if (ns == 6) return launch_lane<6>(a, grid, stream);
     if (ns == 8) return launch_lane<8>(a, grid, stream);
     return launch_lane<2>(a, grid, stream);

@@ -50,3 +50,13 @@ def test_rehearsal_fields(monkeypatch):
     monkeypatch.setattr(bench, "REHEARSE", False)
     f = bench.gpu_fields(8)
     assert f == {"n_gpus": 8, "rehearsal": False, "parallelism": "pair-sharded x8"}
+
+
+def test_score_kernel_label(monkeypatch):
+    """The config5 field names the kernel that gsa_score_dev runs (K-rows by default,
+    the strip kernel under GSA_SCORE_KERNEL=strip)."""
+    monkeypatch.delenv("GSA_SCORE_KERNEL", raising=False)
+    assert bench.score_kernel_name(-11, -1, False).startswith("gsa::nw_kscore_kernel<3>")
+    assert bench.score_kernel_name(-11, -11, True).startswith("gsa::nw_kscore_kernel<5>")
+    monkeypatch.setenv("GSA_SCORE_KERNEL", "strip")
+    assert "nw_strip_kernel" in bench.score_kernel_name(-11, -1, False)

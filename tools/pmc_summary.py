@@ -1,4 +1,4 @@
-"""Summarise tools/pmc_probe.sh output: per-counter value of the LAST fill dispatch (kernel name
+"""Summarise rocprofv3 --pmc output directories (p*/run_counter_collection.csv): per-counter value of the LAST fill dispatch (kernel name
 containing argv[2], default nw_lane|nw_strip)."""
 import csv, collections, glob, json, sys
 out = {}
