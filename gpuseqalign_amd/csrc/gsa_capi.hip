@@ -20,6 +20,7 @@
 #include "../../include/gsa.h"
 #include "nw_check.h"
 #include "nw_lane.h"
+#include "nw_expand.h"
 #include "nw_krow.h"
 #include "nw_strip.h"
 #include "nw_trace_dev.h"
@@ -57,6 +58,17 @@ struct gsa_ctx
     hipEvent_t stage_ev[kStage] = {nullptr, nullptr, nullptr, nullptr};
     bool stage_used[kStage] = {false, false, false, false};
     int stage_next = 0;
+    // two-pass full fill (nw_expand.h): pass-1 outputs (header rows / columns, rows 64m) of the
+    // last launch, grow-only; the expansion's pair descriptors: device copy + pinned staging slots
+    void* exbuf = nullptr;
+    size_t excap = 0;
+    void* exdesc = nullptr;
+    size_t exdesc_cap = 0;
+    void* expin[kStage] = {nullptr, nullptr, nullptr, nullptr};
+    size_t expin_cap[kStage] = {0, 0, 0, 0};
+    hipEvent_t expin_ev[kStage] = {nullptr, nullptr, nullptr, nullptr};
+    bool expin_used[kStage] = {false, false, false, false};
+    int expin_next = 0;
     unsigned long long* chk = nullptr;  // verification results (nw_check.hip)
     // device traceback (nw_trace_dev.hip): move bytes, [moves, cost], global move codes
     unsigned char* tmoves = nullptr;
@@ -377,7 +389,7 @@ int score_ag_strip(gsa_ctx* ctx, const int32_t* seqY, int64_t R, const int32_t* 
 // tickets of all pairs (pair-major).  `pairs` holds device pointers.
 int enqueue_batch(gsa_ctx* ctx, int mode, int npairs, const gsa_pair_dev* pairs, const int32_t* subst, int32_t substsz,
                   int32_t gapo, int32_t tileBx, hipStream_t st, unsigned long long* done = nullptr, int ptChunk = 0,
-                  const int32_t* lds = nullptr)
+                  const int32_t* lds = nullptr, int* const* rows64 = nullptr)
 {
     if (npairs < 1 || !pairs || !subst) return GSA_ERROR_INVALID_VALUE;
     if (substsz < 1 || substsz > 32) return GSA_ERROR_INVALID_VALUE;  // LDS profile holds <= 32 letters
@@ -388,7 +400,7 @@ int enqueue_batch(gsa_ctx* ctx, int mode, int npairs, const gsa_pair_dev* pairs,
     a.g = gapo;
     const bool lane = mode == gsa::kModeFull;
     // mlsppt publishes column chunks from the K-rows kernel only
-    const bool krow = mode == gsa::kModeSparse && (sparse_kernel() == kSpKrow || done);
+    const bool krow = mode == gsa::kModeSparse && (sparse_kernel() == kSpKrow || done || rows64);
     // single pairs: 4 strips per workgroup (each on its own SIMD: the pair's critical path);
     // batches: 8 (two strips per SIMD share the issue slots a single strip leaves idle, 512 x 20k
     // 5.7 -> 7.3 TCUPS; a single 100k pair 5.9 -> 8.4 ms), unless the batch's 4-strip tickets
@@ -399,6 +411,11 @@ int enqueue_batch(gsa_ctx* ctx, int mode, int npairs, const gsa_pair_dev* pairs,
     const bool fitsChip = tileRows <= (long long)std::max(1, ctx->cu_count);
     const int nsDefault = (npairs > 1 && !fitsChip) ? gsa::kKrowNSBatchDefault : gsa::kKrowNSDefault;
     int krowK = env_int("GSA_KROW_K", gsa::kKrowKDefault), krowNS = env_int("GSA_KROW_NS", nsDefault);
+    if (rows64)  // pass 1 of the two-pass full fill: the XR instances, K = 4 on 4 or 8 strips
+    {
+        krowK = 4;
+        krowNS = env_int("GSA_KROW_NS", (npairs > 1 && !fitsChip) ? 8 : 4) == 8 ? 8 : 4;
+    }
     // mlsppt flags one ticket per tile row: only the geometry whose ticket is one tile row
     if (!gsa::krow_ok(krowNS, krowK) || (done && gsa::krow_ticket_rows(krowNS, krowK) != gsa::kSparseTileBy))
     {
@@ -455,6 +472,11 @@ int enqueue_batch(gsa_ctx* ctx, int mode, int npairs, const gsa_pair_dev* pairs,
             d.tcols = geom.tileHdrMatCols;
             d.Cp = d.tcols * tileBx;
             d.nTickets = krow ? gsa::krow_tickets(d.trows, krowNS, krowK) : d.trows;
+            if (rows64)
+            {
+                d.rows64 = rows64[p];
+                d.rpitch = gsa::rows64_pitch(d.Cp);
+            }
             maxWork = std::max<long long>(maxWork, std::max((long long)d.tcols * (tileBx + 1),
                                                             (long long)d.trows * (gsa::kSparseTileBy + 1)));
         }
@@ -533,9 +555,10 @@ int enqueue_batch(gsa_ctx* ctx, int mode, int npairs, const gsa_pair_dev* pairs,
     if (e != hipSuccess) return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
     // one pair: one workgroup per CU (its tickets are a chain); a batch: all resident slots
     int grid = (npairs == 1) ? std::max(1, std::min((int)tickets, ctx->cu_count)) : 0;
-    e = lane    ? gsa::launch_lane_fill(a, a.ns, grid, st)
-        : krow  ? gsa::launch_krow_fill(a, krowNS, krowK, 0, grid, st)
-                : gsa::launch_strip_fill(a, mode, grid, st);
+    e = lane     ? gsa::launch_lane_fill(a, a.ns, grid, st)
+        : rows64 ? gsa::launch_krow_fill_xr(a, krowNS, grid, st)
+        : krow   ? gsa::launch_krow_fill(a, krowNS, krowK, 0, grid, st)
+                 : gsa::launch_strip_fill(a, mode, grid, st);
     if (e != hipSuccess) return fail(ctx, e, GSA_ERROR_KERNEL_FAILURE);
     note_launch(ctx);
     return GSA_SUCCESS;
@@ -548,6 +571,161 @@ int enqueue_fill(gsa_ctx* ctx, int mode, const int32_t* seqY, int32_t adjrows, c
 {
     gsa_pair_dev p {seqY, adjrows, seqX, adjcols, score, hrow, hcol};
     return enqueue_batch(ctx, mode, 1, &p, subst, substsz, gapo, tileBx, st, done, ptChunk, ld);
+}
+
+// Full fills in two passes (nw_expand.h): pass 1 = the K-rows sparse fill of every pair with tile
+// width kExpTW, which also keeps rows 64m (XR instance), into the context's scratch; pass 2 =
+// every 64-row x kExpTW tile of every matrix recomputed from its top row and left column at once.
+// lds: row pitches (null: unpadded).
+int enqueue_full_twopass(gsa_ctx* ctx, int npairs, const gsa_pair_dev* pairs, const int32_t* lds, const int32_t* subst,
+                         int32_t substsz, int32_t gapo, hipStream_t st)
+{
+    if (npairs < 1 || !pairs || !subst) return GSA_ERROR_INVALID_VALUE;
+    if (substsz < 1 || substsz > 32) return GSA_ERROR_INVALID_VALUE;
+    // pass-1 geometry as enqueue_batch derives it for the XR instances
+    long long tileRows = 0;
+    for (int p = 0; p < npairs; ++p)
+        tileRows += std::max<long long>(1, ((long long)pairs[p].adjrows - 1 + gsa::kSparseTileBy - 1) / gsa::kSparseTileBy);
+    const bool fitsChip = tileRows <= (long long)std::max(1, ctx->cu_count);
+    const int ns = env_int("GSA_KROW_NS", (npairs > 1 && !fitsChip) ? 8 : 4) == 8 ? 8 : 4;  // as enqueue_batch
+    std::vector<gsa_pair_dev> p1((size_t)npairs);
+    std::vector<gsa::ExpandPair> ex((size_t)npairs);
+    std::vector<size_t> off((size_t)npairs * 3);
+    size_t bytes = 0;
+    auto take = [&](size_t b) {
+        const size_t o = bytes;
+        bytes += (b + 255) & ~(size_t)255;
+        return o;
+    };
+    long long tasks = 0;
+    for (int p = 0; p < npairs; ++p)
+    {
+        const gsa_pair_dev& in = pairs[p];
+        if (in.adjrows < 1 || in.adjcols < 1 || !in.seqY || !in.seqX || !in.score) return GSA_ERROR_INVALID_VALUE;
+        const long long ld = lds ? lds[p] : in.adjcols;
+        if (ld < in.adjcols) return GSA_ERROR_INVALID_VALUE;
+        gsa_sparse_geom geom;
+        int s = gsa_sparse_geometry(in.adjrows, in.adjcols, gsa::kExpTW, &geom);
+        if (s != GSA_SUCCESS) return s;
+        const int Cp = geom.tileHdrMatCols * gsa::kExpTW;
+        const long long tickets = gsa::krow_tickets(geom.tileHdrMatRows, ns, 4);
+        const long long nrows = tickets * ns * 4;  // rows 64m written by pass 1, m = 1 .. nrows
+        off[3 * p] = take((size_t)geom.hrowElems * 4);
+        off[3 * p + 1] = take((size_t)geom.hcolElems * 4);
+        off[3 * p + 2] = take((size_t)(nrows * gsa::rows64_pitch(Cp)) * 4);
+        gsa::ExpandPair& e = ex[(size_t)p];
+        std::memset(&e, 0, sizeof(e));
+        e.seqY = in.seqY;
+        e.seqX = in.seqX;
+        e.R = in.adjrows - 1;
+        e.C = in.adjcols - 1;
+        e.score = in.score;
+        e.ld = ld;
+        e.rpitch = gsa::rows64_pitch(Cp);
+        e.tcols = geom.tileHdrMatCols;
+        // (an empty sequence still has its header row or column: at least one task per dimension)
+        e.colTiles = std::max(1, (e.C + gsa::kExpTW - 1) / gsa::kExpTW);
+        e.rowChunks = std::max(1, (e.R + gsa::kExpWaves * gsa::kExpRows - 1) / (gsa::kExpWaves * gsa::kExpRows));
+        e.taskBase = (int)tasks;
+        tasks += (long long)e.colTiles * e.rowChunks;
+        if (tasks > (1ll << 30)) return GSA_ERROR_INVALID_VALUE;
+    }
+    hipError_t e = hipSetDevice(ctx->device);
+    if (e != hipSuccess) return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
+    if (ctx->excap < bytes || !ctx->exbuf)
+    {
+        if (ctx->exbuf) (void)hipFree(ctx->exbuf);
+        ctx->exbuf = nullptr;
+        ctx->excap = 0;
+        if ((e = hipMalloc(&ctx->exbuf, std::max<size_t>(bytes, 256))) != hipSuccess)
+            return fail(ctx, e, GSA_ERROR_MEMORY_ALLOCATION);
+        ctx->excap = std::max<size_t>(bytes, 256);
+    }
+    char* base = (char*)ctx->exbuf;
+    std::vector<int*> rows((size_t)npairs);
+    for (int p = 0; p < npairs; ++p)
+    {
+        p1[(size_t)p] = pairs[p];
+        p1[(size_t)p].score = nullptr;
+        p1[(size_t)p].tileHrowMat = (int32_t*)(base + off[3 * p]);
+        p1[(size_t)p].tileHcolMat = (int32_t*)(base + off[3 * p + 1]);
+        rows[(size_t)p] = (int*)(base + off[3 * p + 2]);
+        ex[(size_t)p].rows64 = rows[(size_t)p];
+        ex[(size_t)p].hcol = p1[(size_t)p].tileHcolMat;
+    }
+    int s = enqueue_batch(ctx, gsa::kModeSparse, npairs, p1.data(), subst, substsz, gapo, gsa::kExpTW, st, nullptr, 0,
+                          nullptr, rows.data());
+    if (s != GSA_SUCCESS) return s;
+    // the expansion's descriptors and (batches) its round-robin schedule, staged in a pinned slot and
+    // copied in stream order
+    std::vector<int> xs;
+    if (npairs > 1 && env_int("GSA_EXPAND_RR", 1))
+    {
+        std::vector<int> ord((size_t)npairs);
+        for (int p = 0; p < npairs; ++p) ord[(size_t)p] = p;
+        auto ntask = [&](int p) { return ex[(size_t)p].colTiles * ex[(size_t)p].rowChunks; };
+        std::stable_sort(ord.begin(), ord.end(), [&](int x, int y) { return ntask(x) > ntask(y); });
+        xs.reserve(2 * (size_t)tasks);
+        for (int j = 0; j < ntask(ord[0]); ++j)
+            for (int p : ord)
+            {
+                if (ntask(p) <= j) break;
+                xs.push_back(p);
+                xs.push_back(j);
+            }
+    }
+    const size_t descBytes = ((size_t)npairs * sizeof(gsa::ExpandPair) + 15) & ~(size_t)15;
+    const size_t exBytes = descBytes + xs.size() * sizeof(int);
+    if (ctx->exdesc_cap < exBytes || !ctx->exdesc)
+    {
+        if (ctx->exdesc) (void)hipFree(ctx->exdesc);
+        ctx->exdesc = nullptr;
+        ctx->exdesc_cap = 0;
+        if ((e = hipMalloc(&ctx->exdesc, std::max<size_t>(exBytes, 4096))) != hipSuccess)
+            return fail(ctx, e, GSA_ERROR_MEMORY_ALLOCATION);
+        ctx->exdesc_cap = std::max<size_t>(exBytes, 4096);
+    }
+    const int slot = ctx->expin_next;
+    ctx->expin_next = (slot + 1) % gsa_ctx::kStage;
+    if (ctx->expin_used[slot] && (e = hipEventSynchronize(ctx->expin_ev[slot])) != hipSuccess)
+        return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
+    if (ctx->expin_cap[slot] < exBytes)
+    {
+        if (ctx->expin[slot]) (void)hipHostFree(ctx->expin[slot]);
+        ctx->expin[slot] = nullptr;
+        ctx->expin_cap[slot] = 0;
+        if ((e = hipHostMalloc(&ctx->expin[slot], exBytes)) != hipSuccess) return fail(ctx, e, GSA_ERROR_MEMORY_ALLOCATION);
+        ctx->expin_cap[slot] = exBytes;
+    }
+    std::memcpy(ctx->expin[slot], ex.data(), (size_t)npairs * sizeof(gsa::ExpandPair));
+    if (!xs.empty()) std::memcpy((char*)ctx->expin[slot] + descBytes, xs.data(), xs.size() * sizeof(int));
+    e = hipMemcpyAsync(ctx->exdesc, ctx->expin[slot], exBytes, hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) e = hipEventRecord(ctx->expin_ev[slot], st);
+    if (e != hipSuccess) return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
+    ctx->expin_used[slot] = true;
+    gsa::ExpandArgs xa;
+    xa.subst = subst;
+    xa.substsz = substsz;
+    xa.g = gapo;
+    xa.pairs = (const gsa::ExpandPair*)ctx->exdesc;
+    xa.nPairs = npairs;
+    xa.nTasks = (int)tasks;
+    xa.sched = xs.empty() ? nullptr : (const int*)((char*)ctx->exdesc + descBytes);
+    xa.knob = env_int("GSA_EXPAND_KNOB", 0);
+    if ((e = gsa::launch_expand(xa, st)) != hipSuccess) return fail(ctx, e, GSA_ERROR_KERNEL_FAILURE);
+    note_launch(ctx);
+    return GSA_SUCCESS;
+}
+
+// full fills: the two-pass fill for single pairs (10k: 100 -> 137 GCUPS, profiles/r04_twopass.txt),
+// the one-pass lane fill for batches (its stores keep up with its wavefronts there);
+// GSA_FULL_KERNEL=lane / twopass overrides
+bool full_twopass(int npairs)
+{
+    const char* e = std::getenv("GSA_FULL_KERNEL");
+    if (e && std::strcmp(e, "lane") == 0) return false;
+    if (e && std::strcmp(e, "twopass") == 0) return true;
+    return npairs == 1;
 }
 
 }  // namespace
@@ -585,6 +763,8 @@ int gsa_ctx_create(int device, gsa_ctx** out)
     for (int k = 0; k < gsa_ctx::kStage && e == hipSuccess; ++k)
         e = hipEventCreateWithFlags(&ctx->stage_ev[k], hipEventDisableTiming);
     for (int k = 0; k < 2 && e == hipSuccess; ++k) e = hipEventCreateWithFlags(&ctx->ptev[k], hipEventDisableTiming);
+    for (int k = 0; k < gsa_ctx::kStage && e == hipSuccess; ++k)
+        e = hipEventCreateWithFlags(&ctx->expin_ev[k], hipEventDisableTiming);
     if (e != hipSuccess)
     {
         int code = (int)e;
@@ -606,6 +786,13 @@ void gsa_ctx_destroy(gsa_ctx* ctx)
     if (ctx->gran) (void)hipFree(ctx->gran);
     if (ctx->desc) (void)hipFree(ctx->desc);
     if (ctx->chk) (void)hipFree(ctx->chk);
+    if (ctx->exbuf) (void)hipFree(ctx->exbuf);
+    if (ctx->exdesc) (void)hipFree(ctx->exdesc);
+    for (int k = 0; k < gsa_ctx::kStage; ++k)
+    {
+        if (ctx->expin[k]) (void)hipHostFree(ctx->expin[k]);
+        if (ctx->expin_ev[k]) (void)hipEventDestroy(ctx->expin_ev[k]);
+    }
     if (ctx->tmoves) (void)hipFree(ctx->tmoves);
     if (ctx->tres) (void)hipFree(ctx->tres);
     if (ctx->tdirs) (void)hipFree(ctx->tdirs);
@@ -671,6 +858,11 @@ int gsa_fill_full_dev(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, const 
     if (!ctx || !score) return GSA_ERROR_INVALID_VALUE;
     int s = check_inputs(adjrows, adjcols, substsz);
     if (s != GSA_SUCCESS) return s;
+    if (full_twopass(1))
+    {
+        gsa_pair_dev p {seqY, adjrows, seqX, adjcols, score, nullptr, nullptr};
+        return enqueue_full_twopass(ctx, 1, &p, nullptr, subst, substsz, gapo, pick_stream(ctx, stream));
+    }
     return enqueue_fill(ctx, gsa::kModeFull, seqY, adjrows, seqX, adjcols, subst, substsz, gapo, score, 0, nullptr,
                         nullptr, pick_stream(ctx, stream));
 }
@@ -691,6 +883,11 @@ int gsa_fill_full_pitched_dev(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows
     int s = check_inputs(adjrows, adjcols, substsz);
     if (s != GSA_SUCCESS) return s;
     if (ld < adjcols) return GSA_ERROR_INVALID_VALUE;
+    if (full_twopass(1))
+    {
+        gsa_pair_dev p {seqY, adjrows, seqX, adjcols, score, nullptr, nullptr};
+        return enqueue_full_twopass(ctx, 1, &p, &ld, subst, substsz, gapo, pick_stream(ctx, stream));
+    }
     return enqueue_fill(ctx, gsa::kModeFull, seqY, adjrows, seqX, adjcols, subst, substsz, gapo, score, 0, nullptr,
                         nullptr, pick_stream(ctx, stream), nullptr, 0, &ld);
 }
@@ -710,6 +907,7 @@ int gsa_fill_full_batch_dev(gsa_ctx* ctx, int32_t npairs, const gsa_pair_dev* pa
                             int32_t substsz, int32_t gapo, void* stream)
 {
     if (!ctx) return GSA_ERROR_INVALID_VALUE;
+    if (full_twopass(npairs)) return enqueue_full_twopass(ctx, npairs, pairs, nullptr, subst, substsz, gapo, pick_stream(ctx, stream));
     return enqueue_batch(ctx, gsa::kModeFull, npairs, pairs, subst, substsz, gapo, 0, pick_stream(ctx, stream));
 }
 
@@ -717,6 +915,7 @@ int gsa_fill_full_batch_pitched_dev(gsa_ctx* ctx, int32_t npairs, const gsa_pair
                                     const int32_t* subst, int32_t substsz, int32_t gapo, void* stream)
 {
     if (!ctx || !lds) return GSA_ERROR_INVALID_VALUE;
+    if (full_twopass(npairs)) return enqueue_full_twopass(ctx, npairs, pairs, lds, subst, substsz, gapo, pick_stream(ctx, stream));
     return enqueue_batch(ctx, gsa::kModeFull, npairs, pairs, subst, substsz, gapo, 0, pick_stream(ctx, stream), nullptr,
                          0, lds);
 }

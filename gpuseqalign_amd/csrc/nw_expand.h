@@ -1,0 +1,58 @@
+// nw_expand.h -- launch interface of the full-matrix expansion (nw_expand.hip): pass 2 of the
+// two-pass full fill.  Pass 1 is the K-rows sparse fill (nw_krow.hip, its XR instance), which
+// leaves the tile header columns (tBx = kExpTW) and every 64th row; pass 2 recomputes every
+// 64-row x kExpTW-column tile from its top row and left column, all tiles at once.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+
+#include "nw_strip.h"
+
+namespace gsa {
+
+constexpr int kExpTW = 256;       // tile width (= the pass-1 tile width, tBx)
+constexpr int kExpRows = 64;      // rows of a wave's tile (one per lane)
+constexpr int kExpWaves = 8;      // waves per workgroup: a 512-row chunk of one tile column
+constexpr int kRowsPad = 64;      // left pad (columns) of the pass-1 row buffer
+
+// Pass-1 row buffer of a pair: row 64m (m = 1 .. 4 x strips of pass 1) as shifted values
+// H' = H - (64m + c) g, column c (-64 <= c <= Cp + 63: the strips' segments past both ends land in
+// the pads) at rows64[(m - 1) * rpitch + kRowsPad + c]; rpitch is a multiple of 16 (64-byte segments)
+__host__ __device__ inline long long rows64_pitch(int Cp) { return ((long long)kRowsPad + Cp + 64 + 15) & ~15ll; }
+
+struct ExpandPair
+{
+    const int* seqY;
+    const int* seqX;
+    int R, C;
+    int* score;
+    long long ld;
+    const int* rows64;  // pass-1 rows (rows64_pitch / rows64_count), shifted values
+    long long rpitch;
+    const int* hcol;    // pass-1 tile header columns, tile-major, 1 + kSparseTileBy per tile, unshifted
+    int tcols;          // pass-1 tile columns (tBx = kExpTW)
+    int colTiles;       // ceil(C / kExpTW)
+    int rowChunks;      // ceil(R / (kExpWaves * kExpRows))
+    int taskBase;       // first workgroup task of this pair (colTiles * rowChunks tasks)
+};
+
+struct ExpandArgs
+{
+    const int* subst;
+    int substsz;
+    int g;
+    const ExpandPair* pairs;
+    int nPairs;
+    int nTasks;
+    // round-robin over the pairs (task k of every pair, then task k+1): {pair, task within the pair}
+    // per workgroup, or null (pair-major by taskBase).  Workgroups in flight then write all the
+    // matrices of a batch at once, not one matrix's rows
+    const int* sched;
+    int knob;  // probes only (GSA_EXPAND_KNOB): 1 = no output stores (results wrong)
+};
+
+size_t expand_lds_bytes(int substsz);
+// one workgroup per task; pair arrays in device memory
+hipError_t launch_expand(const ExpandArgs& a, hipStream_t stream);
+
+}  // namespace gsa

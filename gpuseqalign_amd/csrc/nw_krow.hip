@@ -46,6 +46,7 @@
 
 #include <algorithm>
 
+#include "nw_expand.h"
 #include "nw_krow.h"
 
 namespace gsa {
@@ -160,8 +161,10 @@ __host__ __device__ inline KrLds kr_layout(int ns, int lw, int substsz, bool q8 
 // ------------------------------------------------------------------------------------
 // strip wave: 64K rows, K per lane
 // ------------------------------------------------------------------------------------
-// PT: mlsppt (a.done set; a kernel instance of its own, so the plain fill's strip loop is unchanged)
-template <int NS, int K, int LW, bool PT, bool Q8>
+// PT: 1 = mlsppt (a.done set), 2 = XR, pass 1 of the two-pass full fill (nw_expand.hip): lanes
+// 15, 31, 47 and 63 also store their last row (rows 64m of the matrix) into a.rows64.  Each is a
+// kernel instance of its own, so the plain fill's strip loop is unchanged.
+template <int NS, int K, int LW, int PT, bool Q8>
 __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int tk, int w, int lane)
 {
     const int g = a.g;
@@ -270,6 +273,14 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
 #pragma unroll
     for (int k = 0; k < K; ++k) H[k] = 0;
     int lt[kBlk];  // lane 63's hand-off values of the last block (H[K-1] of columns t-64)
+    // XR: byte address of block 0's segment of this lane's row 64m (lanes 16j - 1 only)
+    uint64_t xrBase = 0;
+    if constexpr (PT == 2)
+    {
+        const int j = (lane + 1) >> 4;
+        const long long m = (long long)(K * NS) * tk + 4ll * w + j;  // a ticket holds 64 K NS rows
+        xrBase = (uint64_t)(uintptr_t)a.rows64 + 4ull * (uint64_t)((m - 1) * a.rpitch + kRowsPad - 16 * j);
+    }
     // hand-off of block bb: lane 63's 16 values, then the progress word
     auto handoff = [&](int bb) {
         {
@@ -289,6 +300,27 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
                   "v"(int4v {lt[8], lt[9], lt[10], lt[11]}), "v"(int4v {lt[12], lt[13], lt[14], lt[15]})
                 : "memory");
         }
+        if constexpr (PT == 2)
+        {
+            // XR: lanes 16j - 1 (j = 1..4) hold row r0 + 64j - 1 = 64m, m = K NS tk + 4 w + j; their
+            // values of the block are columns 16(bb - j) .. +15 (shifted), one 64-byte row segment
+            // each (columns < 0 fall in the row buffer's left pad)
+            const uint64_t addr = xrBase + 64ull * (uint64_t)bb;
+            uint64_t sv;
+            asm volatile(
+                "s_mov_b64 %0, exec\n"
+                "s_mov_b64 exec, %1\n"
+                "global_store_dwordx4 %2, %3, off\n"
+                "global_store_dwordx4 %2, %4, off offset:16\n"
+                "global_store_dwordx4 %2, %5, off offset:32\n"
+                "global_store_dwordx4 %2, %6, off offset:48\n"
+                "s_mov_b64 exec, %0"
+                : "=&s"(sv)
+                : "s"(0x8000800080008000ull), "v"(addr), "v"(int4v {lt[0], lt[1], lt[2], lt[3]}),
+                  "v"(int4v {lt[4], lt[5], lt[6], lt[7]}), "v"(int4v {lt[8], lt[9], lt[10], lt[11]}),
+                  "v"(int4v {lt[12], lt[13], lt[14], lt[15]})
+                : "memory");
+        }
         // {prog[w+1], cons[w]}: block bb's 16 elements handed off; ring_in elements < 16bb+80
         // (block bb's halo, read at its start) no longer needed
         flag_st2(f_out, bb + 1 == NB ? kBig : kBlk * bb + kBlk, kBlk * bb + 64 + kBlk);
@@ -302,7 +334,7 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
     int nbb = tBx / kBlk, jb = 1;
     // mlsppt: tile columns [0, ptPend) captured, to be published once their stores are acknowledged
     // (at the next capture block, or at the strip's end); header stores are then system-scope
-    constexpr bool pt = PT;
+    constexpr bool pt = PT == 1;
     int ptPend = 0;
 
     // One body for blocks with and without a header-column capture (cap, uniform): separate
@@ -621,7 +653,7 @@ __device__ __forceinline__ void kr_loader(const StripArgs& a, const KrLds& L, in
 // element e once it has published e - kRing + 16): it stays within a few columns of the strips, and
 // a lag of kRing - 96 elements would end the launch with the error word rather than a wrong header.
 // ------------------------------------------------------------------------------------
-template <int NS, int K, int LW, bool PT>
+template <int NS, int K, int LW, int PT>
 __device__ __forceinline__ void kr_drain(const StripArgs& a, const KrLds& L, int tk, int lane)
 {
     const int Cp = a.Cp, g = a.g, tBx = a.tBx, tBy = a.tBy, tcols = a.tcols;
@@ -632,7 +664,7 @@ __device__ __forceinline__ void kr_drain(const StripArgs& a, const KrLds& L, int
         // mlsppt (one tile row per ticket): publish to the host the column chunks of this tile row
         // whose headers are in memory -- header columns captured by every strip (their words in
         // LDS follow their acknowledged stores) and the header row below written by this wave
-        constexpr bool pt = PT;
+        constexpr bool pt = PT == 1;
         const int cw = pt ? a.ptChunk : 1;
         const int nCh = (tcols + cw - 1) / cw;
         int pub = 0;
@@ -860,7 +892,7 @@ constexpr int kr_waves() { return NS + 2 + (kr_split<NS>() ? 1 : 0); }
 // the host enqueues the int16 instance behind it with a.q8 = 2, which runs only in that case.  Both
 // profiles in one kernel (a uniform branch, or the int16 path out of line) cost the int8 path its
 // code generation: 5.49 / 5.75 ms against 5.30 for the int8 instance alone.
-template <int NS, int K, int LW, bool PT, bool Q8>
+template <int NS, int K, int LW, int PT, bool Q8>
 __global__ void __launch_bounds__(64 * kr_waves<NS>()) nw_krow_kernel(StripArgs a)
 {
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -934,6 +966,8 @@ __global__ void __launch_bounds__(64 * kr_waves<NS>()) nw_krow_kernel(StripArgs 
         pa.tcols = d.tcols;
         pa.gran = a.gran + d.granOff;
         pa.granStride = gran_stride(d.Cp);
+        pa.rows64 = d.rows64;
+        pa.rpitch = d.rpitch;
         const int tk = (tks >= 0) ? tks : tkg - d.ticketBase;
         if (threadIdx.x < 32) lds_st(L.flags + 4u * threadIdx.x, 0);  // prog[], cons[], xo
         if (threadIdx.x >= kFCap / 4 && threadIdx.x < kFCap / 4 + 8) lds_st(L.flags + 4u * threadIdx.x, 0);
@@ -953,7 +987,7 @@ __global__ void __launch_bounds__(64 * kr_waves<NS>()) nw_krow_kernel(StripArgs 
     }
 }
 
-template <int NS, int K, int LW, bool PT, bool Q8>
+template <int NS, int K, int LW, int PT, bool Q8>
 hipError_t launch_kr1(const StripArgs& a, int grid, hipStream_t stream, bool foot = true)
 {
     const size_t lds = krow_lds_bytes(NS, LW, a.substsz, Q8);
@@ -976,7 +1010,7 @@ hipError_t launch_kr1(const StripArgs& a, int grid, hipStream_t stream, bool foo
 
 // a.q8: the int8 instance, then the int16 one behind it (a no-op unless the int8 launch declined
 // the table); otherwise the int16 instance alone
-template <int NS, int K, int LW, bool PT = false>
+template <int NS, int K, int LW, int PT = 0>
 hipError_t launch_kr(const StripArgs& a, int grid, hipStream_t stream)
 {
     if (!a.q8) return launch_kr1<NS, K, LW, PT, false>(a, grid, stream);
@@ -1669,6 +1703,13 @@ hipError_t launch_krow_score(const StripArgs& a, int mode, int grid, hipStream_t
     if (mode == kModeScoreSWL) return launch_ks<kModeScoreSWL>(a, grid, stream);
     return hipErrorInvalidValue;
 }
+#elif defined(GSA_KROW_XR)
+// pass 1 of the two-pass full fill (nw_krowx.hip): the XR instances, (4, 4) for single pairs and
+// (8, 4) for batches
+hipError_t launch_krow_fill_xr(const StripArgs& a, int ns, int grid, hipStream_t stream)
+{
+    return ns == 8 ? launch_kr<8, 4, 1024, 2>(a, grid, stream) : launch_kr<4, 4, 1024, 2>(a, grid, stream);
+}
 #elif defined(GSA_KROW_BATCH8)
 // nw_krow8.hip: the 8-strip batch instance in a translation unit of its own, so it can be built
 // with another instruction scheduler than the single-pair instances (Makefile)
@@ -1687,7 +1728,7 @@ hipError_t launch_krow_fill(const StripArgs& a, int ns, int k, int lw, int grid,
     (void)lw;  // 512 for (4, 4) measured slower for one pair and for batches (the first strip
                // is throttled by the window): 1024
     if (ns == 8) return launch_krow_fill_b8(a, grid, stream);
-    if (a.done) return launch_kr<4, 4, 1024, true>(a, grid, stream);  // mlsppt: (4, 4) only (enqueue_batch)
+    if (a.done) return launch_kr<4, 4, 1024, 1>(a, grid, stream);  // mlsppt: (4, 4) only (enqueue_batch)
     return ns == 2 ? launch_kr<2, 4, 512>(a, grid, stream) : launch_kr<4, 4, 1024>(a, grid, stream);
 }
 #endif

@@ -40,6 +40,8 @@ struct PairDesc
     int* hrow;
     int* hcol;
     long long granOff;  // first granule of this pair in the hand-off buffer
+    int* rows64;        // two-pass full fill, pass 1: rows 64m (nw_expand.h), or null
+    long long rpitch;
 };
 
 // Granules per super-strip boundary of a pair whose last computed column is Cp: Cp + 1 rounded up
@@ -65,6 +67,8 @@ struct StripArgs
     int* hrow;
     int* hcol;
     int trows, tcols, tBx, tBy;
+    int* rows64;          // two-pass full fill, pass 1 (K-rows XR instance): rows 64m, shifted (nw_expand.h)
+    long long rpitch;
     // inter-workgroup hand-off + control
     unsigned long long* gran;
     long long granStride;

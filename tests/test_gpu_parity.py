@@ -170,6 +170,7 @@ def test_full_kernel_shapes(engine, golden, ns, R, C, monkeypatch):
     """The full-fill kernel (nw_lane.hip, one row per lane) with 1..4, 6, 8 strips per workgroup
     (GSA_LANE_NS, read per launch): every super-strip boundary, ragged last strips, rows beyond
     R, every word."""
+    monkeypatch.setenv("GSA_FULL_KERNEL", "lane")
     monkeypatch.setenv("GSA_LANE_NS", ns)
     Y, X = random_pair(R, C, 3 * R + C)
     r = engine.align_full(Y, X, golden.blosum62, -11)
@@ -181,6 +182,7 @@ def test_full_kernel_shapes(engine, golden, ns, R, C, monkeypatch):
 def test_lane_kernel_wide_pair(engine, golden, ns, monkeypatch):
     """Columns past the profile ring (512 columns, 1024 from NS = 5) and its guard copies,
     several super-strips."""
+    monkeypatch.setenv("GSA_FULL_KERNEL", "lane")
     monkeypatch.setenv("GSA_LANE_NS", ns)
     Y, X = related_pair(5000, 17)
     r = engine.align_full(Y, X, golden.blosum62, -11)
@@ -274,3 +276,45 @@ def test_full_batch_pitched(engine, golden, ns, monkeypatch):
         assert np.array_equal(out[:, :len(X)], S)
     costs, _ = shard.gpu_batch_align(0, mode="full")(list(range(len(pairs))), pairs, golden.blosum62, -11)
     assert costs == [int(oracle.fill_full(Y, X, golden.blosum62, -11)[1]) for Y, X in pairs]
+
+
+@pytest.mark.parametrize("kernel", ["lane", "twopass"])
+@pytest.mark.parametrize("R,C", [(1, 1), (1, 300), (300, 1), (63, 64), (64, 64), (65, 257), (255, 256), (256, 512),
+                                 (511, 513), (513, 1024), (1023, 700), (1025, 1029), (2049, 300), (3100, 2222)])
+def test_full_fill_kernels(engine, golden, kernel, R, C, monkeypatch):
+    """Both full-fill kernels (GSA_FULL_KERNEL): the one-pass lane fill and the two-pass fill (K-rows
+    pass 1 keeping every 64th row and the 256-column tile header columns, then every 64 x 256 tile
+    recomputed by nw_expand.hip): every word, around the 64-row, 256-column and 1024-row tile edges."""
+    monkeypatch.setenv("GSA_FULL_KERNEL", kernel)
+    Y, X = random_pair(R, C, 13 * R + C)
+    r = engine.align_full(Y, X, golden.blosum62, -11)
+    S, cost = oracle.fill_full(Y, X, golden.blosum62, -11)
+    assert np.array_equal(r.score, S) and r.align_cost == cost
+
+
+@pytest.mark.parametrize("ns", ["4", "8"])
+@pytest.mark.parametrize("name,gapo", [("blosum45", -5), ("blosum80", -30), ("blosum62", 3), ("blosum50", -70)])
+def test_twopass_tables_and_batches(engine, golden, ns, name, gapo, monkeypatch):
+    """The two-pass fill of a batch in both pass-1 geometries (4 strips: 1024-row tickets, 8 strips:
+    2048-row tickets, GSA_KROW_NS), other tables and gap costs (a positive gap included; at gap -70
+    s - 2g leaves int8 and pass 1 runs its int16 instance), pitched layout, every word of every pair
+    against the oracle."""
+    import torch
+    monkeypatch.setenv("GSA_FULL_KERNEL", "twopass")
+    monkeypatch.setenv("GSA_KROW_NS", ns)
+    sub = golden.subst_data.matrix(name)
+    pairs = [random_pair(r, c, 7 * r + c, alphabet=25) for r, c in ((2100, 900), (1, 5), (700, 2500), (64, 64), (4097, 300))]
+    dev = torch.device("cuda:0")
+    s = torch.from_numpy(np.ascontiguousarray(sub, dtype=np.int32)).to(dev)
+    ins = [(torch.from_numpy(Y).to(dev), torch.from_numpy(X).to(dev)) for Y, X in pairs]
+    lds = [gsa.full_pitch(len(X)) for _, X in pairs]
+    bufs = [torch.full((len(Y) * ld + 64,), -7, dtype=torch.int32, device=dev) for (Y, _), ld in zip(pairs, lds)]
+    engine.fill_batch_dev([(y.data_ptr(), len(y), x.data_ptr(), len(x), b.data_ptr() + 4 * 31)
+                           for (y, x), b in zip(ins, bufs)], s.data_ptr(), 25, gapo, mode="full", lds=lds)
+    engine.sync()
+    for (Y, X), b, ld in zip(pairs, bufs, lds):
+        out = b.cpu().numpy()
+        M = out[31:31 + len(Y) * ld].reshape(len(Y), ld)
+        S, _ = oracle.fill_full(Y, X, sub, gapo)
+        assert np.array_equal(M[:, :len(X)], S)
+        assert (out[:31] == -7).all() and (out[31 + len(Y) * ld:] == -7).all()
