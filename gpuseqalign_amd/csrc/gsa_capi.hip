@@ -605,9 +605,9 @@ int enqueue_full_twopass(gsa_ctx* ctx, int npairs, const gsa_pair_dev* pairs, co
         const long long ld = lds ? lds[p] : in.adjcols;
         if (ld < in.adjcols) return GSA_ERROR_INVALID_VALUE;
         gsa_sparse_geom geom;
-        int s = gsa_sparse_geometry(in.adjrows, in.adjcols, gsa::kExpTW, &geom);
+        int s = gsa_sparse_geometry(in.adjrows, in.adjcols, gsa::kExpHB, &geom);
         if (s != GSA_SUCCESS) return s;
-        const int Cp = geom.tileHdrMatCols * gsa::kExpTW;
+        const int Cp = geom.tileHdrMatCols * gsa::kExpHB;
         const long long tickets = gsa::krow_tickets(geom.tileHdrMatRows, ns, 4);
         const long long nrows = tickets * ns * 4;  // rows 64m written by pass 1, m = 1 .. nrows
         off[3 * p] = take((size_t)geom.hrowElems * 4);
@@ -653,7 +653,7 @@ int enqueue_full_twopass(gsa_ctx* ctx, int npairs, const gsa_pair_dev* pairs, co
         ex[(size_t)p].rows64 = rows[(size_t)p];
         ex[(size_t)p].hcol = p1[(size_t)p].tileHcolMat;
     }
-    int s = enqueue_batch(ctx, gsa::kModeSparse, npairs, p1.data(), subst, substsz, gapo, gsa::kExpTW, st, nullptr, 0,
+    int s = enqueue_batch(ctx, gsa::kModeSparse, npairs, p1.data(), subst, substsz, gapo, gsa::kExpHB, st, nullptr, 0,
                           nullptr, rows.data());
     if (s != GSA_SUCCESS) return s;
     // the expansion's descriptors and (batches) its round-robin schedule, staged in a pinned slot and

@@ -10,9 +10,11 @@
 
 namespace gsa {
 
-constexpr int kExpTW = 256;       // tile width (= the pass-1 tile width, tBx)
+constexpr int kExpHB = 256;       // pass-1 tile width (tBx): its header columns are every kExpHB columns
+constexpr int kExpTW = 512;       // pass-2 tile width, a multiple of kExpHB (the header columns between
+                                  // are recomputed: fewer ramp blocks per tile, 8 of 36)
 constexpr int kExpRows = 64;      // rows of a wave's tile (one per lane)
-constexpr int kExpWaves = 8;      // waves per workgroup: a 512-row chunk of one tile column
+constexpr int kExpWaves = 16;     // waves per workgroup: a 1024-row chunk of one tile column
 constexpr int kRowsPad = 64;      // left pad (columns) of the pass-1 row buffer
 
 // Pass-1 row buffer of a pair: row 64m (m = 1 .. 4 x strips of pass 1) as shifted values
@@ -30,7 +32,7 @@ struct ExpandPair
     const int* rows64;  // pass-1 rows (rows64_pitch / rows64_count), shifted values
     long long rpitch;
     const int* hcol;    // pass-1 tile header columns, tile-major, 1 + kSparseTileBy per tile, unshifted
-    int tcols;          // pass-1 tile columns (tBx = kExpTW)
+    int tcols;          // pass-1 tile columns (tBx = kExpHB)
     int colTiles;       // ceil(C / kExpTW)
     int rowChunks;      // ceil(R / (kExpWaves * kExpRows))
     int taskBase;       // first workgroup task of this pair (colTiles * rowChunks tasks)

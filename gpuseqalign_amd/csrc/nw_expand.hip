@@ -5,7 +5,7 @@
 // (R+1) x (C+1) matrix.  A single wavefront that also stores every cell is bound by its critical
 // path and couples its strips to the store stream (nw_lane.hip).  The two-pass fill splits the
 // two: pass 1 is the K-rows sparse fill (nw_krow.hip, XR instance: 4 rows per lane, the
-// headline's wavefront) and keeps every 256th column (the tile header columns, tBx = kExpTW) and
+// headline's wavefront) and keeps every 256th column (the tile header columns, tBx = kExpHB) and
 // every 64th row; pass 2 (this file) recomputes all 64-row x kExpTW-column tiles from their top
 // row and left column at once -- tiles are independent, so it is bound by HBM writes, not by a
 // dependency chain.  This is the reference's own tile recompute (NwTrace2_AlignTile,
@@ -31,8 +31,9 @@ constexpr int kBlk = 16;           // steps per block
 constexpr int kH = kBlk / 4;       // halo registers (int4) per block
 constexpr int kSubRow = 36;        // dwords per subT row (32 letters + 4)
 constexpr int kQOff = 64;          // Q[y][kQOff + j], j = 1..kExpTW; reads reach j = -63 .. kExpTW + 15
-constexpr int kQS = 352;           // Q row stride (dwords), = 0 mod 32: the bank is the column alone
-constexpr int kTopS = 336;         // per-wave top row: topw[t] = H(r0 - 1, cb + t) + g, t < 320
+constexpr int kQS = kQOff + kExpTW + 32;  // Q row stride (dwords), = 0 mod 32: the bank is the column alone
+constexpr int kTopS = kExpTW + 80;        // per-wave top row: topw[t] = H(r0 - 1, cb + t) + g, t < kExpTW + 80
+static_assert(kQS % 32 == 0 && kTopS % 4 == 0 && kExpTW % kExpHB == 0, "LDS strides");
 
 extern __shared__ __attribute__((aligned(16))) char xsm[];
 
@@ -90,22 +91,22 @@ __device__ __forceinline__ void ex_tile(const ExpandArgs& a, const ExpandPair& d
     const int r = r0 + lane;
     int y = (r <= d.R) ? G(d.seqY)[r] : 0;
     y = ((unsigned)y < (unsigned)a.substsz) ? y : 0;
-    // left boundary H(r, cb): column 0, or the pass-1 header column of tile (iT, jT) (element
-    // r - iT tBy; rows up to the last tile row's end are computed there, padding included)
+    // left boundary H(r, cb): column 0, or the pass-1 header column of its tile (iT, cb / kExpHB)
+    // (element r - iT tBy; rows up to the last tile row's end are computed there, padding included)
     int lb;
     if (jT == 0)
         lb = r * g;
     else
     {
         const int iT = (r - 1) / kSparseTileBy;
-        lb = G(d.hcol)[((size_t)iT * (size_t)d.tcols + (size_t)jT) * (size_t)(kSparseTileBy + 1) +
+        lb = G(d.hcol)[((size_t)iT * (size_t)d.tcols + (size_t)jT * (kExpTW / kExpHB)) * (size_t)(kSparseTileBy + 1) +
                        (size_t)(r - iT * kSparseTileBy)];
     }
     // top row H(r0 - 1, cb .. cb + kExpTW) + g into LDS: row 0, or pass-1 row 64m (shifted values)
     const uint32_t topw = L.top + 4u * (uint32_t)(kTopS * w);
     {
         const int m = (r0 - 1) / kExpRows;
-        for (int j = lane; j <= kExpTW; j += 64)
+        for (int j = lane; j <= cols + 3; j += 64)  // (+3: the chunks that straddle the tile's end)
         {
             const int c = cb + j;
             const int v = m == 0 ? c * g
@@ -115,7 +116,11 @@ __device__ __forceinline__ void ex_tile(const ExpandArgs& a, const ExpandPair& d
     }
     const uint32_t qrow = L.q + 4u * (uint32_t)(y * kQS + kQOff);
     const uint32_t hbase = (lane == 0) ? topw : L.gfill;  // lanes >= 1 read a row of g (no branch)
-    const int NB = (cols + 64 + kBlk - 1) / kBlk;          // lane 63 reaches column cb + cols at step cols + 63
+    // lane 63 reaches column cb + cols + 3 at step cols + 66: a chunk that straddles the tile's end is
+    // stored whole by this tile's wave, and skipped by the next tile's, whose ramp stores only the
+    // chunks that start inside it -- no per-element stores except at the matrix's own edges
+    const int ce = min(cols + 3, d.C - cb);                // last column this wave computes validly
+    const int NB = (ce + 64 + kBlk - 1) / kBlk;
     // transposed output (as nw_lane.hip): store k has lane 16h + n write columns 4h .. 4h+3 of the
     // block's 16 for row r0 + 16k + n
     const gptr<int> xbase = G(d.score) + (ptrdiff_t)(r0 + (lane & 15)) * d.ld + cb + 4 * (lane >> 4) - (lane & 15);
@@ -208,18 +213,21 @@ __device__ __forceinline__ void ex_tile(const ExpandArgs& a, const ExpandPair& d
 #pragma unroll
             for (int k = 0; k < 4; ++k)
             {
-                const int rr = 16 * k + (lane & 15);  // row r0 + rr, tile columns xc .. xc+3
+                // edge block: a chunk (row r0 + rr, tile columns xc .. xc+3) is this wave's if it starts
+                // in the tile; whole (x4) unless it passes the matrix's last column; the first tile also
+                // stores the valid part of the chunk that straddles column 1 (no tile before it)
+                const int rr = 16 * k + (lane & 15);
                 const int xc = kBlk * b - rr + 4 * (lane >> 4);
                 if (r0 + rr <= d.R)
                 {
                     const gptr<int> p = xbase + (size_t)k * 16u * (size_t)(d.ld - 1) + kBlk * b;
-                    if (xc >= 1 && xc + 3 <= cols)
+                    if (xc >= 1 && xc <= cols && xc + 3 <= ce)
                         *(gptr<int4a>)p = int4a {t[4 * k], t[4 * k + 1], t[4 * k + 2], t[4 * k + 3]};
-                    else if (xc + 3 >= 1 && xc <= cols)
+                    else if ((xc >= 1 && xc <= cols) || (jT == 0 && xc + 3 >= 1 && xc <= 0))
                     {
 #pragma unroll
                         for (int e = 0; e < 4; ++e)
-                            if (xc + e >= 1 && xc + e <= cols) p[e] = t[4 * k + e];
+                            if (xc + e >= 1 && xc + e <= ce) p[e] = t[4 * k + e];
                     }
                 }
             }
@@ -277,9 +285,10 @@ __global__ void __launch_bounds__(64 * kExpWaves, 4) nw_expand_kernel(ExpandArgs
     __syncthreads();
     // column profile of the tile column: Q[y][kQOff + j] = s(y, X[cb + j]) - g, j = 1..kExpTW
     // (columns past C: letter 0, never stored)
-    for (int k = threadIdx.x; k < a.substsz * kExpTW; k += 64 * kExpWaves)
+    constexpr int kQCols = kExpTW + 4;  // the tile and the 3 columns past it (straddling chunks)
+    for (int k = threadIdx.x; k < a.substsz * kQCols; k += 64 * kExpWaves)
     {
-        const int yy = k / kExpTW, j = k % kExpTW + 1;
+        const int yy = k / kQCols, j = k % kQCols + 1;
         const int c = cb + j;
         int x = c <= d.C ? G(d.seqX)[c] : 0;
         x = ((unsigned)x < (unsigned)a.substsz) ? x : 0;
