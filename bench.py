@@ -74,6 +74,17 @@ def lane_ns():
     return int(v) if v in ("1", "2", "3", "4", "6", "8") else 4
 
 
+def full_kernel_name(single):
+    """Kernels of a full fill (gsa_capi.hip full_twopass): the two-pass fill (pass 1: K-rows XR
+    instance, (4, 4) for one pair and (8, 4) for a batch that overfills the chip; pass 2: the tile
+    expansion), or under GSA_FULL_KERNEL=lane the one-pass lane fill."""
+    if os.environ.get("GSA_FULL_KERNEL", "") == "lane":
+        return lane_kernel_name(single)
+    ns = 4 if single else 8
+    return (f"gsa::nw_krow_kernel<{ns},4,1024,2,true> (pass 1: sparse wavefront keeping every 64th row and the "
+            f"256-column header columns) + gsa::nw_expand_kernel (pass 2: every 64 x 512 tile recomputed)")
+
+
 def lane_kernel_name(single):
     """The lane instantiation a full fill runs (nw_lane.hip launch_lane_fill): <NS, feeder wave,
     paired stores>; the feeder wave for single pairs at NS = 4 (GSA_LANE_FEED), paired stores for
@@ -310,11 +321,11 @@ def bench_full_batch(world, rank, local, n_pairs):
                         f"matrices ({out_bytes / 1e9:.1f} GB), one persistent launch, LPT-sharded over {world} rank(s) "
                         "(1 untimed + 3 timed launches; seconds per launch)",
             "value": round(rep.gcups, 2), "unit": "GCUPS", "scaling": "strong", "seconds": round(rep.elapsed_s, 4),
-            "kernel": f"{lane_kernel_name(False)} (full, one row per lane, pitched layout, paired stores)",
+            "kernel": full_kernel_name(False),
             "layout": "pitched: row pitch gsa_full_pitch(adjcols) = 1 mod 32, cell (1,0) on a 128-byte boundary",
             "hbm_write_GBps": round(gbps * world, 1), "hbm_frac": round(gbps / PEAK_HBM_GBPS, 4),
             "bound": "hbm (4 B written per cell; MI355X 8 TB/s spec)",
-            "pmc_write_over_algorithmic": pmc_write_ratio(n_pairs, lane_kernel_name(False)),
+            "pmc_write_over_algorithmic": pmc_write_ratio(n_pairs, full_kernel_name(False)),
             "pairs": n_pairs, "pairs_matching_golden": match}
 
 
@@ -489,12 +500,13 @@ def main():
                                "(resrc/seq_generated.fa), full int32 score matrix in HBM",
                    "value": round(world * R2 * C2 * a.steps / el2 / 1e9, 2), "unit": "GCUPS",
                    "ms_per_step": round(el2 * 1e3 / a.steps, 4), "kernel_ms": round(km2, 4),
-                   "kernel": (f"{lane_kernel_name(True)} "
-                              "(full, one row per lane" + (", feeder wave)" if lane_ns() == 4 else ")")),
+                   "kernel": full_kernel_name(True),
                    "hbm_write_GBps": round(b2 / (km2 * 1e-3) / 1e9, 1),
                    "hbm_frac": round(b2 / (km2 * 1e-3) / 1e9 / PEAK_HBM_GBPS, 4),
                    "align_cost": int(score[-1].item()), "golden_align_cost": -4922,
-                   "critical_path": critical_path(C2, -(-R2 // (64 * lane_ns())) * lane_ns(), 4, km2, 64)}
+                   "critical_path": (critical_path(C2, -(-R2 // (64 * lane_ns())) * lane_ns(), 4, km2, 64)
+                                     if os.environ.get("GSA_FULL_KERNEL", "") == "lane" else
+                                     critical_path(C2, -(-R2 // 256), 9, km2, 256))}
         del score
         torch.cuda.empty_cache()
     cfg5 = None

@@ -717,15 +717,12 @@ int enqueue_full_twopass(gsa_ctx* ctx, int npairs, const gsa_pair_dev* pairs, co
     return GSA_SUCCESS;
 }
 
-// full fills: the two-pass fill for single pairs (10k: 100 -> 137 GCUPS, profiles/r04_twopass.txt),
-// the one-pass lane fill for batches (its stores keep up with its wavefronts there);
-// GSA_FULL_KERNEL=lane / twopass overrides
-bool full_twopass(int npairs)
+// full fills: the two-pass fill (same box: 10k 100 -> 141 GCUPS, 64 x 20k batch 1084 -> 1093-1102
+// GCUPS, profiles/r04_twopass.txt); GSA_FULL_KERNEL=lane: the one-pass lane fill (nw_lane.hip)
+bool full_twopass(int)
 {
     const char* e = std::getenv("GSA_FULL_KERNEL");
-    if (e && std::strcmp(e, "lane") == 0) return false;
-    if (e && std::strcmp(e, "twopass") == 0) return true;
-    return npairs == 1;
+    return !(e && std::strcmp(e, "lane") == 0);
 }
 
 }  // namespace

@@ -188,7 +188,7 @@ __device__ __forceinline__ void ex_tile(const ExpandArgs& a, const ExpandPair& d
             const gptr<int> ub = G(d.score) + ((ptrdiff_t)(r0 + 16 * k) * d.ld - 16 * k + kBlk * bb + cb);
             *(gptr<int4a>)(ub + xoff) = int4a {v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]};
         };
-        if (!RAMP && (b & 1) == 0 && b + 1 < NB && interior(b) && interior(b + 1))
+        if (!RAMP && !(a.knob & 16) && (b & 1) == 0 && b + 1 < NB && interior(b) && interior(b + 1))
         {
 #pragma unroll
             for (int e = 0; e < kBlk; ++e) tE[e] = t[e];
