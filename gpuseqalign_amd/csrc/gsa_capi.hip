@@ -64,6 +64,10 @@ struct gsa_ctx
     size_t excap = 0;
     void* exdesc = nullptr;
     size_t exdesc_cap = 0;
+    // fused single-pair fill: one progress word per pass-1 strip (epoch-tagged, cleared once per
+    // allocation)
+    unsigned long long* xdone = nullptr;
+    size_t xdone_cap = 0;
     void* expin[kStage] = {nullptr, nullptr, nullptr, nullptr};
     size_t expin_cap[kStage] = {0, 0, 0, 0};
     hipEvent_t expin_ev[kStage] = {nullptr, nullptr, nullptr, nullptr};
@@ -389,7 +393,7 @@ int score_ag_strip(gsa_ctx* ctx, const int32_t* seqY, int64_t R, const int32_t* 
 // tickets of all pairs (pair-major).  `pairs` holds device pointers.
 int enqueue_batch(gsa_ctx* ctx, int mode, int npairs, const gsa_pair_dev* pairs, const int32_t* subst, int32_t substsz,
                   int32_t gapo, int32_t tileBx, hipStream_t st, unsigned long long* done = nullptr, int ptChunk = 0,
-                  const int32_t* lds = nullptr, int* const* rows64 = nullptr)
+                  const int32_t* lds = nullptr, int* const* rows64 = nullptr, const gsa::ExpandArgs* fused = nullptr)
 {
     if (npairs < 1 || !pairs || !subst) return GSA_ERROR_INVALID_VALUE;
     if (substsz < 1 || substsz > 32) return GSA_ERROR_INVALID_VALUE;  // LDS profile holds <= 32 letters
@@ -414,7 +418,7 @@ int enqueue_batch(gsa_ctx* ctx, int mode, int npairs, const gsa_pair_dev* pairs,
     if (rows64)  // pass 1 of the two-pass full fill: the XR instances, K = 4 on 4 or 8 strips
     {
         krowK = 4;
-        krowNS = env_int("GSA_KROW_NS", (npairs > 1 && !fitsChip) ? 8 : 4) == 8 ? 8 : 4;
+        krowNS = env_int("GSA_KROW_NS", (npairs > 1 && !fitsChip) ? 8 : 4) == 8 && !fused ? 8 : 4;
     }
     // mlsppt flags one ticket per tile row: only the geometry whose ticket is one tile row
     if (!gsa::krow_ok(krowNS, krowK) || (done && gsa::krow_ticket_rows(krowNS, krowK) != gsa::kSparseTileBy))
@@ -551,11 +555,37 @@ int enqueue_batch(gsa_ctx* ctx, int mode, int npairs, const gsa_pair_dev* pairs,
     a.ptChunk = std::max(1, ptChunk);
     a.epoch = ++ctx->epoch;
     if (a.epoch == 0) a.epoch = ++ctx->epoch;  // 0 is the cleared-tag value
+    const bool probePT3 = rows64 && !fused && npairs == 1 && env_int("GSA_XR_PT3", 0);  // PROBE
+    if (fused || probePT3)
+    {
+        if (npairs != 1 || !rows64) return GSA_ERROR_INVALID_VALUE;
+        const size_t words = (size_t)tickets * (size_t)krowNS;
+        if (ctx->xdone_cap < words || !ctx->xdone)
+        {
+            if (ctx->xdone) (void)hipFree(ctx->xdone);
+            ctx->xdone = nullptr;
+            ctx->xdone_cap = 0;
+            const size_t cap = std::max<size_t>(words, 1024);
+            if ((e = hipMalloc(&ctx->xdone, cap * sizeof(unsigned long long))) != hipSuccess)
+                return fail(ctx, e, GSA_ERROR_MEMORY_ALLOCATION);
+            if ((e = hipMemsetAsync(ctx->xdone, 0, cap * sizeof(unsigned long long), st)) != hipSuccess)
+                return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
+            ctx->xdone_cap = cap;
+        }
+        if (fused)
+        {
+            a.xpair = fused->pairs;
+            a.xTasks = fused->nTasks;
+            a.xknob = fused->knob;
+        }
+        a.xdone = ctx->xdone;
+    }
     e = hipMemsetAsync(ctx->ctl, 0, 4, st);  // the ticket; the error word stays sticky
     if (e != hipSuccess) return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
     // one pair: one workgroup per CU (its tickets are a chain); a batch: all resident slots
     int grid = (npairs == 1) ? std::max(1, std::min((int)tickets, ctx->cu_count)) : 0;
     e = lane     ? gsa::launch_lane_fill(a, a.ns, grid, st)
+        : fused  ? gsa::launch_full_fused(a, 0, st)
         : rows64 ? gsa::launch_krow_fill_xr(a, krowNS, grid, st)
         : krow   ? gsa::launch_krow_fill(a, krowNS, krowK, 0, grid, st)
                  : gsa::launch_strip_fill(a, mode, grid, st);
@@ -587,7 +617,15 @@ int enqueue_full_twopass(gsa_ctx* ctx, int npairs, const gsa_pair_dev* pairs, co
     for (int p = 0; p < npairs; ++p)
         tileRows += std::max<long long>(1, ((long long)pairs[p].adjrows - 1 + gsa::kSparseTileBy - 1) / gsa::kSparseTileBy);
     const bool fitsChip = tileRows <= (long long)std::max(1, ctx->cu_count);
-    const int ns = env_int("GSA_KROW_NS", (npairs > 1 && !fitsChip) ? 8 : 4) == 8 ? 8 : 4;  // as enqueue_batch
+    // one pair: both passes in one launch (nw_full_fused_kernel), unless GSA_FULL_FUSED=0
+    // (a matrix without interior cells has no pass-1 tickets: the expansion alone writes its headers)
+    const bool fused = npairs == 1 && pairs[0].adjrows > 1 && pairs[0].adjcols > 1 && env_int("GSA_FULL_FUSED", 1) != 0;
+    // two launches: pass 2 one workgroup of kExpWaves waves per task, or (GSA_EXPAND_GRID > 0)
+    // that many persistent workgroups of GSA_EXPAND_WAVES (8, 12, 16) waves
+    const int xGrid = fused ? 0 : std::max(0, env_int("GSA_EXPAND_GRID", 0));
+    const int xw = env_int("GSA_EXPAND_WAVES", gsa::kExpWaves);
+    const int xWaves = fused ? gsa::kExpFusedWaves : xGrid > 0 && (xw == 8 || xw == 12) ? xw : gsa::kExpWaves;
+    const int ns = env_int("GSA_KROW_NS", (npairs > 1 && !fitsChip) ? 8 : 4) == 8 && !fused ? 8 : 4;  // as enqueue_batch
     std::vector<gsa_pair_dev> p1((size_t)npairs);
     std::vector<gsa::ExpandPair> ex((size_t)npairs);
     std::vector<size_t> off((size_t)npairs * 3);
@@ -625,7 +663,7 @@ int enqueue_full_twopass(gsa_ctx* ctx, int npairs, const gsa_pair_dev* pairs, co
         e.tcols = geom.tileHdrMatCols;
         // (an empty sequence still has its header row or column: at least one task per dimension)
         e.colTiles = std::max(1, (e.C + gsa::kExpTW - 1) / gsa::kExpTW);
-        e.rowChunks = std::max(1, (e.R + gsa::kExpWaves * gsa::kExpRows - 1) / (gsa::kExpWaves * gsa::kExpRows));
+        e.rowChunks = std::max(1, (e.R + xWaves * gsa::kExpRows - 1) / (xWaves * gsa::kExpRows));
         e.taskBase = (int)tasks;
         tasks += (long long)e.colTiles * e.rowChunks;
         if (tasks > (1ll << 30)) return GSA_ERROR_INVALID_VALUE;
@@ -653,9 +691,6 @@ int enqueue_full_twopass(gsa_ctx* ctx, int npairs, const gsa_pair_dev* pairs, co
         ex[(size_t)p].rows64 = rows[(size_t)p];
         ex[(size_t)p].hcol = p1[(size_t)p].tileHcolMat;
     }
-    int s = enqueue_batch(ctx, gsa::kModeSparse, npairs, p1.data(), subst, substsz, gapo, gsa::kExpHB, st, nullptr, 0,
-                          nullptr, rows.data());
-    if (s != GSA_SUCCESS) return s;
     // the expansion's descriptors and (batches) its round-robin schedule, staged in a pinned slot and
     // copied in stream order
     std::vector<int> xs;
@@ -703,7 +738,7 @@ int enqueue_full_twopass(gsa_ctx* ctx, int npairs, const gsa_pair_dev* pairs, co
     if (e == hipSuccess) e = hipEventRecord(ctx->expin_ev[slot], st);
     if (e != hipSuccess) return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
     ctx->expin_used[slot] = true;
-    gsa::ExpandArgs xa;
+    gsa::ExpandArgs xa {};
     xa.subst = subst;
     xa.substsz = substsz;
     xa.g = gapo;
@@ -712,7 +747,12 @@ int enqueue_full_twopass(gsa_ctx* ctx, int npairs, const gsa_pair_dev* pairs, co
     xa.nTasks = (int)tasks;
     xa.sched = xs.empty() ? nullptr : (const int*)((char*)ctx->exdesc + descBytes);
     xa.knob = env_int("GSA_EXPAND_KNOB", 0);
-    if ((e = gsa::launch_expand(xa, st)) != hipSuccess) return fail(ctx, e, GSA_ERROR_KERNEL_FAILURE);
+    int s = enqueue_batch(ctx, gsa::kModeSparse, npairs, p1.data(), subst, substsz, gapo, gsa::kExpHB, st, nullptr, 0,
+                          nullptr, rows.data(), fused ? &xa : nullptr);
+    if (s != GSA_SUCCESS || fused) return s;
+    xa.counter = ctx->ctl + 4;
+    if (xGrid > 0 && (e = hipMemsetAsync(xa.counter, 0, 4, st)) != hipSuccess) return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
+    if ((e = gsa::launch_expand(xa, st, xWaves, xGrid)) != hipSuccess) return fail(ctx, e, GSA_ERROR_KERNEL_FAILURE);
     note_launch(ctx);
     return GSA_SUCCESS;
 }
@@ -785,6 +825,7 @@ void gsa_ctx_destroy(gsa_ctx* ctx)
     if (ctx->chk) (void)hipFree(ctx->chk);
     if (ctx->exbuf) (void)hipFree(ctx->exbuf);
     if (ctx->exdesc) (void)hipFree(ctx->exdesc);
+    if (ctx->xdone) (void)hipFree(ctx->xdone);
     for (int k = 0; k < gsa_ctx::kStage; ++k)
     {
         if (ctx->expin[k]) (void)hipHostFree(ctx->expin[k]);

@@ -16,6 +16,8 @@ constexpr int kExpTW = 512;       // pass-2 tile width, a multiple of kExpHB (th
 constexpr int kExpRows = 64;      // rows of a wave's tile (one per lane)
 constexpr int kExpWaves = 16;     // waves per workgroup: a 1024-row chunk of one tile column
 constexpr int kRowsPad = 64;      // left pad (columns) of the pass-1 row buffer
+constexpr int kExpFusedWaves = 8; // waves per workgroup of the fused single-pair fill (512-row chunks)
+constexpr unsigned kXDone = 0x3fffffffu;  // a pass-1 strip's progress word: the strip has finished
 
 // Pass-1 row buffer of a pair: row 64m (m = 1 .. 4 x strips of pass 1) as shifted values
 // H' = H - (64m + c) g, column c (-64 <= c <= Cp + 63: the strips' segments past both ends land in
@@ -34,7 +36,7 @@ struct ExpandPair
     const int* hcol;    // pass-1 tile header columns, tile-major, 1 + kSparseTileBy per tile, unshifted
     int tcols;          // pass-1 tile columns (tBx = kExpHB)
     int colTiles;       // ceil(C / kExpTW)
-    int rowChunks;      // ceil(R / (kExpWaves * kExpRows))
+    int rowChunks;      // ceil(R / (waves * kExpRows)), waves = kExpWaves (kExpFusedWaves when fused)
     int taskBase;       // first workgroup task of this pair (colTiles * rowChunks tasks)
 };
 
@@ -50,11 +52,15 @@ struct ExpandArgs
     // per workgroup, or null (pair-major by taskBase).  Workgroups in flight then write all the
     // matrices of a batch at once, not one matrix's rows
     const int* sched;
-    int knob;  // probes only (GSA_EXPAND_KNOB): 1 = no output stores (results wrong)
+    int knob;  // probes only (GSA_EXPAND_KNOB): 1 = no tile computed or stored (results wrong)
+    // persistent launches: workgroups claim tasks from *counter (zeroed before the launch)
+    unsigned* counter;
 };
 
-size_t expand_lds_bytes(int substsz);
-// one workgroup per task; pair arrays in device memory
-hipError_t launch_expand(const ExpandArgs& a, hipStream_t stream);
+size_t expand_lds_bytes(int substsz, int waves);
+// one workgroup per task (waves = kExpWaves); or, grid > 0, `grid` persistent workgroups of
+// `waves` (8, 12, 16) waves claiming tasks from a.counter.  rowChunks of every pair must be counted
+// in chunks of waves x kExpRows rows.  Pair arrays in device memory.
+hipError_t launch_expand(const ExpandArgs& a, hipStream_t stream, int waves = kExpWaves, int grid = 0);
 
 }  // namespace gsa

@@ -32,8 +32,13 @@ size_t krow_lds_bytes(int ns, int lw, int substsz, bool q8 = false);
 // The profile ring holds 512 columns for ns = 2, 1024 otherwise (lw is reserved).
 hipError_t launch_krow_fill(const StripArgs& a, int ns, int k, int lw, int grid, hipStream_t stream);
 // Pass 1 of the two-pass full fill (nw_expand.h): the sparse fill (K = 4, ns = 4 or 8, a.tBx =
-// kExpTW) that also stores rows 64m into each pair's rows64 / rpitch (PairDesc).
+// kExpHB) that also stores rows 64m into each pair's rows64 / rpitch (PairDesc).
 hipError_t launch_krow_fill_xr(const StripArgs& a, int ns, int grid, hipStream_t stream);
+// Both passes of one pair's two-pass full fill in one launch (ns = 4): workgroups take the pass-1
+// tickets, then expansion tasks (a.xpair, a.xTasks; 8-wave row chunks, kExpFusedWaves), each task
+// waiting for the words a.xdone of the strips whose rows and header column it reads.  grid <= 0:
+// every resident slot.
+hipError_t launch_full_fused(const StripArgs& a, int grid, hipStream_t stream);
 
 // Score-only NW / SW (modes kModeScoreAG/AGL/SW/SWL of nw_strip.h, same StripArgs contract as
 // launch_strip_fill for one pair: go, ge, gran + gran2, agResult, swBest, idxBits) on the K-rows

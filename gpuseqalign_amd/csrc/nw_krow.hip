@@ -48,6 +48,9 @@
 
 #include "nw_expand.h"
 #include "nw_krow.h"
+#ifdef GSA_KROW_XR
+#include "nw_expand_dev.h"  // the fused fill's expansion tasks
+#endif
 
 namespace gsa {
 namespace {
@@ -162,7 +165,9 @@ __host__ __device__ inline KrLds kr_layout(int ns, int lw, int substsz, bool q8 
 // strip wave: 64K rows, K per lane
 // ------------------------------------------------------------------------------------
 // PT: 1 = mlsppt (a.done set), 2 = XR, pass 1 of the two-pass full fill (nw_expand.hip): lanes
-// 15, 31, 47 and 63 also store their last row (rows 64m of the matrix) into a.rows64.  Each is a
+// 15, 31, 47 and 63 also store their last row (rows 64m of the matrix) into a.rows64; 3 = XR inside
+// the fused single-pair fill (nw_full_fused_kernel), which also publishes the strip's progress to
+// the expansion workgroups of the same launch (write-through stores, a word per strip).  Each is a
 // kernel instance of its own, so the plain fill's strip loop is unchanged.
 template <int NS, int K, int LW, int PT, bool Q8>
 __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int tk, int w, int lane)
@@ -275,7 +280,7 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
     int lt[kBlk];  // lane 63's hand-off values of the last block (H[K-1] of columns t-64)
     // XR: byte address of block 0's segment of this lane's row 64m (lanes 16j - 1 only)
     uint64_t xrBase = 0;
-    if constexpr (PT == 2)
+    if constexpr (PT >= 2)
     {
         const int j = (lane + 1) >> 4;
         const long long m = (long long)(K * NS) * tk + 4ll * w + j;  // a ticket holds 64 K NS rows
@@ -300,26 +305,32 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
                   "v"(int4v {lt[8], lt[9], lt[10], lt[11]}), "v"(int4v {lt[12], lt[13], lt[14], lt[15]})
                 : "memory");
         }
-        if constexpr (PT == 2)
+        if constexpr (PT >= 2)
         {
             // XR: lanes 16j - 1 (j = 1..4) hold row r0 + 64j - 1 = 64m, m = K NS tk + 4 w + j; their
             // values of the block are columns 16(bb - j) .. +15 (shifted), one 64-byte row segment
             // each (columns < 0 fall in the row buffer's left pad)
             const uint64_t addr = xrBase + 64ull * (uint64_t)bb;
             uint64_t sv;
-            asm volatile(
-                "s_mov_b64 %0, exec\n"
-                "s_mov_b64 exec, %1\n"
-                "global_store_dwordx4 %2, %3, off\n"
-                "global_store_dwordx4 %2, %4, off offset:16\n"
-                "global_store_dwordx4 %2, %5, off offset:32\n"
-                "global_store_dwordx4 %2, %6, off offset:48\n"
-                "s_mov_b64 exec, %0"
-                : "=&s"(sv)
-                : "s"(0x8000800080008000ull), "v"(addr), "v"(int4v {lt[0], lt[1], lt[2], lt[3]}),
-                  "v"(int4v {lt[4], lt[5], lt[6], lt[7]}), "v"(int4v {lt[8], lt[9], lt[10], lt[11]}),
-                  "v"(int4v {lt[12], lt[13], lt[14], lt[15]})
-                : "memory");
+            // fused fill: write-through (sc1) stores, read by other workgroups of the launch
+#define GSA_XR_STORES(MOD)                                                                              \
+    asm volatile("s_mov_b64 %0, exec\n"                                                                 \
+                 "s_mov_b64 exec, %1\n"                                                                 \
+                 "global_store_dwordx4 %2, %3, off" MOD "\n"                                            \
+                 "global_store_dwordx4 %2, %4, off offset:16" MOD "\n"                                  \
+                 "global_store_dwordx4 %2, %5, off offset:32" MOD "\n"                                  \
+                 "global_store_dwordx4 %2, %6, off offset:48" MOD "\n"                                  \
+                 "s_mov_b64 exec, %0"                                                                    \
+                 : "=&s"(sv)                                                                             \
+                 : "s"(0x8000800080008000ull), "v"(addr), "v"(int4v {lt[0], lt[1], lt[2], lt[3]}),       \
+                   "v"(int4v {lt[4], lt[5], lt[6], lt[7]}), "v"(int4v {lt[8], lt[9], lt[10], lt[11]}),   \
+                   "v"(int4v {lt[12], lt[13], lt[14], lt[15]})                                           \
+                 : "memory")
+            if constexpr (PT == 3)
+                GSA_XR_STORES(" sc1");
+            else
+                GSA_XR_STORES("");
+#undef GSA_XR_STORES
         }
         // {prog[w+1], cons[w]}: block bb's 16 elements handed off; ring_in elements < 16bb+80
         // (block bb's halo, read at its start) no longer needed
@@ -335,7 +346,15 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
     // mlsppt: tile columns [0, ptPend) captured, to be published once their stores are acknowledged
     // (at the next capture block, or at the strip's end); header stores are then system-scope
     constexpr bool pt = PT == 1;
+    constexpr bool fx = PT == 3;  // fused: publish every boundary to a.xdone (agent scope)
     int ptPend = 0;
+    // fused: this strip's progress word, epoch << 32 | n: header columns of boundaries < n and row
+    // 64m columns < (n - 1) tBx stored and acknowledged (kXDone: all)
+    auto fx_publish = [&](unsigned n) {
+        if (lane == 0)
+            __hip_atomic_store(a.xdone + (size_t)tk * NS + w, ((unsigned long long)a.epoch << 32) | n, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+    };
 
     // One body for blocks with and without a header-column capture (cap, uniform): separate
     // bodies get different register assignments and ~100 v_mov per block to reconcile them.
@@ -411,6 +430,15 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
                 flag_st(L.flags + kFCap + 4u * (uint32_t)w, ptPend);
                 ptPend = 0;
             }
+            if (fx && ptPend)
+            {
+                // the previous boundary's stores were issued >= 13 blocks ago, and every block since
+                // has issued 4 row stores: all but the last 16 vector-memory operations complete
+                // covers them (vmcnt retires in order) without waiting for this block's
+                if (!(a.xknob & 8)) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // (8: probe only)
+                fx_publish((unsigned)ptPend);
+                ptPend = 0;
+            }
             // lanes 16m .. 16m+15 (m = b - nbb) hold column bc at step lane & 15: 16 -> 1 by its
             // bits (v_cndmask tree with constant lane masks, 15 per row)
             constexpr uint64_t m1 = 0xAAAAAAAAAAAAAAAAull, m2 = 0xCCCCCCCCCCCCCCCCull;
@@ -437,6 +465,12 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
                     for (int k = 0; k < K; ++k)
                         __hip_atomic_store(&hcolP[k], v[k] + gb + k * g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 }
+                else if (fx)
+                {
+#pragma unroll
+                    for (int k = 0; k < K; ++k)
+                        __hip_atomic_store(&hcolP[k], v[k] + gb + k * g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
                 else
                 {
 #pragma unroll
@@ -449,6 +483,7 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
                 ++jb;
                 hcolP += (size_t)(tBy + 1);
                 if (pt && (jb % a.ptChunk == 0 || jb == tcols)) ptPend = jb;
+                if (fx) ptPend = jb;
             }
         }
         return true;
@@ -478,6 +513,11 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
     {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         flag_st(L.flags + kFCap + 4u * (uint32_t)w, kBig);
+    }
+    if (fx)
+    {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        fx_publish(kXDone);
     }
 }
 
@@ -1708,7 +1748,182 @@ hipError_t launch_krow_score(const StripArgs& a, int mode, int grid, hipStream_t
 // (8, 4) for batches
 hipError_t launch_krow_fill_xr(const StripArgs& a, int ns, int grid, hipStream_t stream)
 {
+    if (ns == 4 && a.xdone) return launch_kr<4, 4, 1024, 3>(a, grid, stream);  // PROBE
     return ns == 8 ? launch_kr<8, 4, 1024, 2>(a, grid, stream) : launch_kr<4, 4, 1024, 2>(a, grid, stream);
+}
+
+namespace {
+
+// ------------------------------------------------------------------------------------
+// The fused single-pair full fill: both passes of the two-pass fill in one launch.  A single pair's
+// pass 1 is a chain of ceil(R / 1024) tickets -- ten workgroups for the 10k pair, on ten CUs -- and
+// its pass 2 needs a 64-row tile's rows only once the strips above and beside it have passed its
+// columns.  So workgroups of 8 waves take the pass-1 tickets first (waves 0..6 run the (4, 4)
+// K-rows roles, wave 7 idles) and then the expansion tasks, in row-chunk-major order (512-row
+// chunks x kExpTW columns, nw_expand_dev.h), from the same counter: every task's producers hold
+// earlier claims, so they are resident and the waits end.  Hand-off, per the guide's
+// inter-workgroup rules: the strips store row 64m and the header columns write-through (sc1), wait
+// for those stores (vmcnt) and publish a word per strip -- epoch << 32 | n, n = boundaries captured
+// -- with a relaxed agent-scope store; a task's lane 0 polls the words of the strips it reads, then
+// an agent acquire, vmcnt(0) and a workgroup barrier precede the plain loads.
+// ------------------------------------------------------------------------------------
+template <bool Q8>
+__global__ void __launch_bounds__(64 * kExpFusedWaves) nw_full_fused_kernel(StripArgs a)
+{
+    constexpr int NS = 4, K = 4, LW = 1024;
+    static_assert(kr_waves<NS>() <= kExpFusedWaves, "the pass-1 roles fit the workgroup");
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const KrLds L = kr_layout(NS, LW, a.substsz, Q8);
+    if (!Q8 && a.q8 == 2 && __hip_atomic_load(a.q8flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != a.epoch) return;
+    bool bad = false, bad8 = false;
+    for (int k = threadIdx.x; k < a.substsz * kSubRow; k += 64 * kExpFusedWaves)
+    {
+        const int x = k / kSubRow, yy = k % kSubRow;
+        const int v = yy < a.substsz ? G(a.subst)[yy * a.substsz + x] - 2 * a.g : 0;
+        bad |= v < -32768 || v > 32767;
+        bad8 |= v < -128 || v > 127;
+        lds_st(L.sub + 4u * k, v);
+    }
+    if constexpr (Q8)
+    {
+        // a table outside int8: decline before claiming anything (nw_krow_kernel)
+        if (threadIdx.x == 0) lds_st(L.flags + kFTicket, 0);
+        __syncthreads();
+        if (bad8) atomicOr((int*)(krsm + L.flags + kFTicket), 1);
+        __syncthreads();
+        if (lds_ld(L.flags + kFTicket) != 0)
+        {
+            if (threadIdx.x == 0) __hip_atomic_store(a.q8flag, a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return;
+        }
+    }
+    else if (bad)
+        atomicOr(a.err, 2u);
+    const int nAll = a.nTicketsTotal + a.xTasks;
+    const ExpandArgs xa {a.subst, a.substsz, a.g, a.xpair, 1, a.xTasks, nullptr, a.xknob, nullptr};
+    for (;;)
+    {
+        __syncthreads();
+        if (threadIdx.x == 0) lds_st(L.flags + kFTicket, err_set(a) ? nAll : (int)atomicAdd(a.ticket, 1u));
+        __syncthreads();
+        const int c = __builtin_amdgcn_readfirstlane(lds_ld(L.flags + kFTicket));
+        if (c >= nAll) break;
+        if (c < a.nTicketsTotal)
+        {
+            // pass 1, ticket c of the pair (the LDS still holds subT: pass-1 claims all come first)
+            const PairDesc d = kr_desc(a.pairs);
+            StripArgs pa = a;
+            pa.seqY = d.seqY;
+            pa.seqX = d.seqX;
+            pa.R = d.R;
+            pa.C = d.C;
+            pa.Cp = d.Cp;
+            pa.nTickets = d.nTickets;
+            pa.hrow = d.hrow;
+            pa.hcol = d.hcol;
+            pa.trows = d.trows;
+            pa.tcols = d.tcols;
+            pa.gran = a.gran + d.granOff;
+            pa.granStride = gran_stride(d.Cp);
+            pa.rows64 = d.rows64;
+            pa.rpitch = d.rpitch;
+            if (threadIdx.x < 32) lds_st(L.flags + 4u * threadIdx.x, 0);
+            if (threadIdx.x >= kFCap / 4 && threadIdx.x < kFCap / 4 + 8) lds_st(L.flags + 4u * threadIdx.x, 0);
+            __syncthreads();
+            if (w == NS + 1)
+                kr_drain<NS, K, LW, 3>(pa, L, c, lane);
+            else if (w == NS)
+                kr_loader<NS, K, LW, 1, Q8>(pa, L, c, lane);
+            else if (w == NS + 2)
+                kr_loader<NS, K, LW, 2, Q8>(pa, L, c, lane);
+            else if (w < NS)
+            {
+                __builtin_amdgcn_s_setprio(3);
+                kr_strip<NS, K, LW, 3, Q8>(pa, L, c, w, lane);
+                __builtin_amdgcn_s_setprio(0);
+            }
+            continue;
+        }
+        // pass 2, task tt: tile column jT of row chunk rc.  Its waves read rows 64m, m = 8 rc .. 8 rc + 7,
+        // at columns < need, and (jT > 0) the header column of boundary 2 jT for rows 512 rc + 1 ..
+        // 512 rc + 512: global strips 2 rc - 1 .. 2 rc + 1 (4 per ticket), words >= pneed
+        const ExpandPair xd = xdev::ex_desc(a.xpair);
+        const int tt = c - a.nTicketsTotal;
+        const int jT = tt % xd.colTiles, rc = tt / xd.colTiles;
+        if (threadIdx.x == 0)
+        {
+            const int cb = jT * kExpTW;
+            const int need = min(cb + min(kExpTW, xd.C - cb) + 3, xd.C) + 1;
+            unsigned pneed = (unsigned)((need + kExpHB - 1) / kExpHB + 1);
+            if (pneed >= (unsigned)xd.tcols) pneed = kXDone;  // (a strip's last boundary is published at its end)
+            const int s1 = min(2 * rc + 1, a.nTicketsTotal * NS - 1);
+            bool ok = true;
+            uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            for (int s = (a.xknob & 4) ? s1 + 1 : max(0, 2 * rc - 1); s <= s1 && ok;)  // (4: probe, no wait)
+            {
+                const unsigned long long v = __hip_atomic_load(a.xdone + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if ((unsigned)(v >> 32) == a.epoch && (unsigned)v >= pneed)
+                {
+                    ++s;
+                    t0 = __builtin_amdgcn_s_memrealtime();
+                    continue;
+                }
+                if (a.xknob & 0xf0)  // probe: (knob >> 4) x 1024 cycles between polls
+                    for (int z = 0; z < ((a.xknob >> 4) & 15); ++z) __builtin_amdgcn_s_sleep(16);
+                else
+                    __builtin_amdgcn_s_sleep(2);
+                if (__builtin_amdgcn_s_memrealtime() - t0 > a.spin || err_set(a))
+                {
+                    atomicOr(a.err, 1u);
+                    ok = false;
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            lds_st(L.flags + kFTicket, ok ? c : nAll);
+        }
+        __syncthreads();
+        const int go = __builtin_amdgcn_readfirstlane(lds_ld(L.flags + kFTicket));
+        __syncthreads();  // (the task's LDS may overlap the word)
+        if (go >= nAll) break;
+        xdev::ex_task<kExpFusedWaves>(xa, xd, tt, w, lane);
+    }
+}
+
+template <bool Q8>
+hipError_t launch_fused1(const StripArgs& a, int grid, hipStream_t stream, bool foot)
+{
+    const size_t lds = std::max(krow_lds_bytes(4, 1024, a.substsz, Q8), expand_lds_bytes(a.substsz, kExpFusedWaves));
+    auto kern = nw_full_fused_kernel<Q8>;
+    constexpr int kThreads = 64 * kExpFusedWaves;
+    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+    if (grid <= 0)
+    {
+        int per_cu = 0, dev = 0, cus = 0;
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)kern, kThreads, lds);
+        if (e == hipSuccess) e = hipGetDevice(&dev);
+        if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        if (e != hipSuccess) return e;
+        grid = std::max(1, std::min(a.nTicketsTotal + a.xTasks, std::max(1, per_cu) * cus));
+    }
+    if (foot && (e = record_foot((const void*)kern, lds, kThreads, grid)) != hipSuccess) return e;
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreads), lds, stream, a);
+    return hipGetLastError();
+}
+
+}  // namespace
+
+hipError_t launch_full_fused(const StripArgs& a, int grid, hipStream_t stream)
+{
+    if (a.nPairs != 1 || !a.xpair || !a.xdone) return hipErrorInvalidValue;
+    if (!a.q8) return launch_fused1<false>(a, grid, stream, true);
+    hipError_t e = launch_fused1<true>(a, grid, stream, true);
+    if (e != hipSuccess) return e;
+    StripArgs b = a;
+    b.q8 = 2;
+    return launch_fused1<false>(b, grid, stream, false);
 }
 #elif defined(GSA_KROW_BATCH8)
 // nw_krow8.hip: the 8-strip batch instance in a translation unit of its own, so it can be built

@@ -6,6 +6,8 @@
 
 namespace gsa {
 
+struct ExpandPair;  // nw_expand.h
+
 constexpr int kModeFull = 0;  // full matrix (nw_lane.hip; launch_headers)
 constexpr int kModeSparse = 1;
 // Score-only global alignment with affine gaps on the strip layout (gsa_score_dev, global):
@@ -99,6 +101,13 @@ struct StripArgs
     // batch schedule: {pair, ticket within the pair} of every global ticket, round-robin over the
     // pairs (null: pair-major by ticketBase).  Ticket j of a pair always follows its ticket j-1.
     const int* sched;
+    // fused single-pair full fill (nw_full_fused_kernel): the expansion's pair descriptor and task
+    // count (tasks are claimed from *ticket after the nTicketsTotal pass-1 tickets), its probe
+    // knob, and one progress word per pass-1 strip (epoch << 32 | tile columns published)
+    const ExpandPair* xpair;
+    int xTasks;
+    int xknob;
+    unsigned long long* xdone;
 };
 
 // Resource footprint of the last fill launched from this host thread: what the reference's

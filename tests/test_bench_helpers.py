@@ -60,3 +60,17 @@ def test_score_kernel_label(monkeypatch):
     assert bench.score_kernel_name(-11, -11, True).startswith("gsa::nw_kscore_kernel<5>")
     monkeypatch.setenv("GSA_SCORE_KERNEL", "strip")
     assert "nw_strip_kernel" in bench.score_kernel_name(-11, -1, False)
+
+
+def test_full_kernel_label(monkeypatch):
+    """The 10k and full_batch fields name the kernels gsa_capi.hip's full-fill routing runs: the fused
+    single-pair kernel by default, the two launches under GSA_FULL_FUSED=0 and for batches, the lane
+    fill under GSA_FULL_KERNEL=lane."""
+    for k in ("GSA_FULL_KERNEL", "GSA_FULL_FUSED", "GSA_LANE_NS", "GSA_LANE_FEED", "GSA_LANE_PAIR"):
+        monkeypatch.delenv(k, raising=False)
+    assert bench.full_kernel_name(True).startswith("gsa::nw_full_fused_kernel<true>")
+    assert bench.full_kernel_name(False).startswith("gsa::nw_krow_kernel<8,4,1024,2,true>")
+    monkeypatch.setenv("GSA_FULL_FUSED", "0")
+    assert bench.full_kernel_name(True).startswith("gsa::nw_krow_kernel<4,4,1024,2,true>")
+    monkeypatch.setenv("GSA_FULL_KERNEL", "lane")
+    assert bench.full_kernel_name(True).startswith("gsa::nw_lane_kernel<4,true,false>")

@@ -278,14 +278,16 @@ def test_full_batch_pitched(engine, golden, ns, monkeypatch):
     assert costs == [int(oracle.fill_full(Y, X, golden.blosum62, -11)[1]) for Y, X in pairs]
 
 
-@pytest.mark.parametrize("kernel", ["lane", "twopass"])
+@pytest.mark.parametrize("kernel", ["lane", "twopass", "fused"])
 @pytest.mark.parametrize("R,C", [(1, 1), (1, 300), (300, 1), (63, 64), (64, 64), (65, 257), (255, 256), (256, 512),
                                  (511, 513), (513, 1024), (1023, 700), (1025, 1029), (2049, 300), (3100, 2222)])
 def test_full_fill_kernels(engine, golden, kernel, R, C, monkeypatch):
-    """Both full-fill kernels (GSA_FULL_KERNEL): the one-pass lane fill and the two-pass fill (K-rows
-    pass 1 keeping every 64th row and the 256-column tile header columns, then every 64 x 256 tile
-    recomputed by nw_expand.hip): every word, around the 64-row, 256-column and 1024-row tile edges."""
-    monkeypatch.setenv("GSA_FULL_KERNEL", kernel)
+    """The full-fill kernels (GSA_FULL_KERNEL, GSA_FULL_FUSED): the one-pass lane fill, the two-pass
+    fill in two launches (K-rows pass 1 keeping every 64th row and the 256-column tile header columns,
+    then every 64 x 512 tile recomputed by nw_expand.hip) and in one (the fused single-pair kernel):
+    every word, around the 64-row, 256-column and 1024-row tile edges."""
+    monkeypatch.setenv("GSA_FULL_KERNEL", "lane" if kernel == "lane" else "twopass")
+    monkeypatch.setenv("GSA_FULL_FUSED", "1" if kernel == "fused" else "0")
     Y, X = random_pair(R, C, 13 * R + C)
     r = engine.align_full(Y, X, golden.blosum62, -11)
     S, cost = oracle.fill_full(Y, X, golden.blosum62, -11)
@@ -318,3 +320,37 @@ def test_twopass_tables_and_batches(engine, golden, ns, name, gapo, monkeypatch)
         S, _ = oracle.fill_full(Y, X, sub, gapo)
         assert np.array_equal(M[:, :len(X)], S)
         assert (out[:31] == -7).all() and (out[31 + len(Y) * ld:] == -7).all()
+
+
+@pytest.mark.parametrize("name,gapo", [("blosum45", -5), ("blosum62", 3), ("blosum50", -70)])
+def test_fused_tables_pitched_repeated(engine, golden, name, gapo, monkeypatch):
+    """The fused single-pair fill (pass-1 tickets and expansion tasks in one launch, hand-off through
+    per-strip progress words): other tables and gaps (-70: the int16 instance behind the declining
+    int8 one), pitched and unpadded, launched back to back on one stream (a task that ran ahead of
+    its strips' words would read the previous launch's rows): every word every time."""
+    import torch
+    monkeypatch.setenv("GSA_FULL_KERNEL", "twopass")
+    monkeypatch.setenv("GSA_FULL_FUSED", "1")
+    sub = golden.subst_data.matrix(name)
+    dev = torch.device("cuda:0")
+    s = torch.from_numpy(np.ascontiguousarray(sub, dtype=np.int32)).to(dev)
+    for R, C, pitched in ((3100, 4700, True), (2049, 1537, False)):
+        Y, X = random_pair(R, C, 5 * R + C, alphabet=25)
+        S, _ = oracle.fill_full(Y, X, sub, gapo)
+        y, x = torch.from_numpy(Y).to(dev), torch.from_numpy(X).to(dev)
+        ld = gsa.full_pitch(len(X)) if pitched else len(X)
+        off = gsa.full_base_offset() if pitched else 0
+        n = len(Y) * ld
+        bufs = [torch.full((n + 64 + off,), -7, dtype=torch.int32, device=dev) for _ in range(6)]
+        for rep in range(2):
+            for b in bufs:
+                if rep:
+                    b.fill_(-7)
+                engine.fill_full_dev(y.data_ptr(), len(Y), x.data_ptr(), len(X), s.data_ptr(), 25, gapo,
+                                     b.data_ptr() + 4 * off, ld=ld if pitched else None)
+            engine.sync()
+            for b in bufs:
+                out = b.cpu().numpy()
+                M = out[off:off + n].reshape(len(Y), ld)
+                assert np.array_equal(M[:, :len(X)], S)
+                assert (out[:off] == -7).all() and (out[off + n:] == -7).all()

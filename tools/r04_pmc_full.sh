@@ -1,6 +1,7 @@
 #!/bin/bash
-# round-4 PMC evidence of the 64-pair full batch in the pitched layout with paired stores:
-# kernel-trace stats, WRITE_SIZE, FETCH_SIZE and an SQ pass, one rocprofv3 run each
+# round-4 PMC evidence of the 64-pair full batch (two-pass fill, pitched layout): kernel-trace stats,
+# WRITE_SIZE, FETCH_SIZE and an SQ pass, one rocprofv3 run each; summaries per kernel (pass 1 =
+# nw_krow_kernel XR instance, pass 2 = nw_expand_kernel)
 set -e
 ROOT=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 O=$ROOT/gpurun_out/${1:-pmcfb4}; mkdir -p $O
@@ -13,6 +14,7 @@ for ctr in "WRITE_SIZE" "FETCH_SIZE" "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_WR SQ
   timeout -s KILL 180 rocprofv3 --pmc $ctr -d $O/p$i -o run --output-format csv -- \
       python3 $ROOT/tools/batch_bench.py --mode full --pairs 64 --repeats 1 --warmup 0 > $O/log$i.txt 2>&1
 done
-python3 $ROOT/tools/pmc_summary.py $O nw_lane > $O/summary.json
-cat $O/summary.json
+python3 $ROOT/tools/pmc_summary.py $O nw_expand > $O/summary_expand.json
+python3 $ROOT/tools/pmc_summary.py $O nw_krow > $O/summary_krow.json
+cat $O/summary_expand.json $O/summary_krow.json
 find $O/kt -name "*kernel_stats.csv" -exec cat {} \;

@@ -1,0 +1,10 @@
+# pass-2 (expansion) geometry probe on the 64 x 20k full batch: one workgroup per task (default) vs
+# persistent workgroups (GSA_EXPAND_GRID) of 8 / 12 / 16 waves (GSA_EXPAND_WAVES), same process
+set -e
+mkdir -p gpurun_out
+timeout -k 10 300 python -u tools/full_ab.py --no-10k --rounds 1 --batch 64 --variants \
+  "GSA_EXPAND_GRID=0" "GSA_EXPAND_GRID=256,GSA_EXPAND_WAVES=16" "GSA_EXPAND_GRID=256,GSA_EXPAND_WAVES=12" \
+  "GSA_EXPAND_GRID=256,GSA_EXPAND_WAVES=8" "GSA_EXPAND_GRID=192,GSA_EXPAND_WAVES=16" \
+  "GSA_EXPAND_GRID=128,GSA_EXPAND_WAVES=16" "GSA_EXPAND_GRID=128,GSA_EXPAND_WAVES=12" \
+  "GSA_EXPAND_GRID=0" > gpurun_out/r04_x1.log 2>&1
+cat gpurun_out/r04_x1.log
