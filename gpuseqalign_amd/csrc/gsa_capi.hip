@@ -389,11 +389,20 @@ int score_ag_strip(gsa_ctx* ctx, const int32_t* seqY, int64_t R, const int32_t* 
     return GSA_SUCCESS;
 }
 
+// The fused two-pass full fill's launch (enqueue_full_twopass): the expansion's arguments, the
+// pass-1 geometry (ns strips per ticket), the workgroup's waves and the workgroups that take pass-1
+// tickets first
+struct FusedLaunch
+{
+    const gsa::ExpandArgs* xa;
+    int ns, waves, p1;
+};
+
 // One batched launch: headers of every pair, then the persistent strip kernel over the
 // tickets of all pairs (pair-major).  `pairs` holds device pointers.
 int enqueue_batch(gsa_ctx* ctx, int mode, int npairs, const gsa_pair_dev* pairs, const int32_t* subst, int32_t substsz,
                   int32_t gapo, int32_t tileBx, hipStream_t st, unsigned long long* done = nullptr, int ptChunk = 0,
-                  const int32_t* lds = nullptr, int* const* rows64 = nullptr, const gsa::ExpandArgs* fused = nullptr)
+                  const int32_t* lds = nullptr, int* const* rows64 = nullptr, const FusedLaunch* fused = nullptr)
 {
     if (npairs < 1 || !pairs || !subst) return GSA_ERROR_INVALID_VALUE;
     if (substsz < 1 || substsz > 32) return GSA_ERROR_INVALID_VALUE;  // LDS profile holds <= 32 letters
@@ -418,7 +427,7 @@ int enqueue_batch(gsa_ctx* ctx, int mode, int npairs, const gsa_pair_dev* pairs,
     if (rows64)  // pass 1 of the two-pass full fill: the XR instances, K = 4 on 4 or 8 strips
     {
         krowK = 4;
-        krowNS = env_int("GSA_KROW_NS", (npairs > 1 && !fitsChip) ? 8 : 4) == 8 && !fused ? 8 : 4;
+        krowNS = fused ? fused->ns : env_int("GSA_KROW_NS", (npairs > 1 && !fitsChip) ? 8 : 4) == 8 ? 8 : 4;
     }
     // mlsppt flags one ticket per tile row: only the geometry whose ticket is one tile row
     if (!gsa::krow_ok(krowNS, krowK) || (done && gsa::krow_ticket_rows(krowNS, krowK) != gsa::kSparseTileBy))
@@ -558,7 +567,7 @@ int enqueue_batch(gsa_ctx* ctx, int mode, int npairs, const gsa_pair_dev* pairs,
     const bool probePT3 = rows64 && !fused && npairs == 1 && env_int("GSA_XR_PT3", 0);  // PROBE
     if (fused || probePT3)
     {
-        if (npairs != 1 || !rows64) return GSA_ERROR_INVALID_VALUE;
+        if (!rows64) return GSA_ERROR_INVALID_VALUE;
         const size_t words = (size_t)tickets * (size_t)krowNS;
         if (ctx->xdone_cap < words || !ctx->xdone)
         {
@@ -574,9 +583,14 @@ int enqueue_batch(gsa_ctx* ctx, int mode, int npairs, const gsa_pair_dev* pairs,
         }
         if (fused)
         {
-            a.xpair = fused->pairs;
-            a.xTasks = fused->nTasks;
-            a.xknob = fused->knob;
+            a.xpair = fused->xa->pairs;
+            a.xsched = fused->xa->sched;
+            a.xTasks = fused->xa->nTasks;
+            a.xknob = fused->xa->knob;
+            a.xP = fused->p1;
+            a.xrole = ctx->ctl + 4;
+            a.xcounter = ctx->ctl + 5;
+            if ((e = hipMemsetAsync(a.xrole, 0, 8, st)) != hipSuccess) return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
         }
         a.xdone = ctx->xdone;
     }
@@ -585,7 +599,7 @@ int enqueue_batch(gsa_ctx* ctx, int mode, int npairs, const gsa_pair_dev* pairs,
     // one pair: one workgroup per CU (its tickets are a chain); a batch: all resident slots
     int grid = (npairs == 1) ? std::max(1, std::min((int)tickets, ctx->cu_count)) : 0;
     e = lane     ? gsa::launch_lane_fill(a, a.ns, grid, st)
-        : fused  ? gsa::launch_full_fused(a, 0, st)
+        : fused  ? gsa::launch_full_fused(a, fused->ns, fused->waves, 0, st)
         : rows64 ? gsa::launch_krow_fill_xr(a, krowNS, grid, st)
         : krow   ? gsa::launch_krow_fill(a, krowNS, krowK, 0, grid, st)
                  : gsa::launch_strip_fill(a, mode, grid, st);
@@ -617,15 +631,21 @@ int enqueue_full_twopass(gsa_ctx* ctx, int npairs, const gsa_pair_dev* pairs, co
     for (int p = 0; p < npairs; ++p)
         tileRows += std::max<long long>(1, ((long long)pairs[p].adjrows - 1 + gsa::kSparseTileBy - 1) / gsa::kSparseTileBy);
     const bool fitsChip = tileRows <= (long long)std::max(1, ctx->cu_count);
-    // one pair: both passes in one launch (nw_full_fused_kernel), unless GSA_FULL_FUSED=0
-    // (a matrix without interior cells has no pass-1 tickets: the expansion alone writes its headers)
-    const bool fused = npairs == 1 && pairs[0].adjrows > 1 && pairs[0].adjcols > 1 && env_int("GSA_FULL_FUSED", 1) != 0;
+    // both passes in one launch (nw_full_fused_kernel): GSA_FULL_FUSED = 0 never, 1 (default) single
+    // pairs, 2 batches too.  (A matrix without interior cells has no pass-1 tickets: the expansion
+    // alone writes its headers.)
+    const int fusedMode = env_int("GSA_FULL_FUSED", 1);
+    bool interior = true;
+    for (int p = 0; p < npairs; ++p) interior = interior && pairs[p].adjrows > 1 && pairs[p].adjcols > 1;
+    const bool fused = interior && (npairs == 1 ? fusedMode >= 1 : fusedMode >= 2);
     // two launches: pass 2 one workgroup of kExpWaves waves per task, or (GSA_EXPAND_GRID > 0)
     // that many persistent workgroups of GSA_EXPAND_WAVES (8, 12, 16) waves
     const int xGrid = fused ? 0 : std::max(0, env_int("GSA_EXPAND_GRID", 0));
     const int xw = env_int("GSA_EXPAND_WAVES", gsa::kExpWaves);
-    const int xWaves = fused ? gsa::kExpFusedWaves : xGrid > 0 && (xw == 8 || xw == 12) ? xw : gsa::kExpWaves;
-    const int ns = env_int("GSA_KROW_NS", (npairs > 1 && !fitsChip) ? 8 : 4) == 8 && !fused ? 8 : 4;  // as enqueue_batch
+    const int ns = env_int("GSA_KROW_NS", (npairs > 1 && !fitsChip) ? 8 : 4) == 8 ? 8 : 4;  // as enqueue_batch
+    // fused: (4, 4) tickets under 8-wave workgroups, (8, 4) under 12
+    const int fusedW = ns == 4 ? gsa::kExpFusedWaves : gsa::kExpFusedWavesBatch;
+    const int xWaves = fused ? fusedW : xGrid > 0 && (xw == 8 || xw == 12) ? xw : gsa::kExpWaves;
     std::vector<gsa_pair_dev> p1((size_t)npairs);
     std::vector<gsa::ExpandPair> ex((size_t)npairs);
     std::vector<size_t> off((size_t)npairs * 3);
@@ -635,7 +655,7 @@ int enqueue_full_twopass(gsa_ctx* ctx, int npairs, const gsa_pair_dev* pairs, co
         bytes += (b + 255) & ~(size_t)255;
         return o;
     };
-    long long tasks = 0;
+    long long tasks = 0, strips = 0;
     for (int p = 0; p < npairs; ++p)
     {
         const gsa_pair_dev& in = pairs[p];
@@ -666,7 +686,10 @@ int enqueue_full_twopass(gsa_ctx* ctx, int npairs, const gsa_pair_dev* pairs, co
         e.rowChunks = std::max(1, (e.R + xWaves * gsa::kExpRows - 1) / (xWaves * gsa::kExpRows));
         e.taskBase = (int)tasks;
         tasks += (long long)e.colTiles * e.rowChunks;
-        if (tasks > (1ll << 30)) return GSA_ERROR_INVALID_VALUE;
+        e.p1Strip0 = (int)strips;  // (enqueue_batch's ticketBase x ns: pair-major)
+        e.p1Strips = (int)(tickets * ns);
+        strips += tickets * ns;
+        if (tasks > (1ll << 30) || strips > (1ll << 30)) return GSA_ERROR_INVALID_VALUE;
     }
     hipError_t e = hipSetDevice(ctx->device);
     if (e != hipSuccess) return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
@@ -747,8 +770,10 @@ int enqueue_full_twopass(gsa_ctx* ctx, int npairs, const gsa_pair_dev* pairs, co
     xa.nTasks = (int)tasks;
     xa.sched = xs.empty() ? nullptr : (const int*)((char*)ctx->exdesc + descBytes);
     xa.knob = env_int("GSA_EXPAND_KNOB", 0);
+    // fused batches: GSA_FUSED_P1 workgroups take the pass-1 tickets first (a single pair: all)
+    const FusedLaunch fl {&xa, ns, fusedW, npairs == 1 ? (1 << 30) : std::max(1, env_int("GSA_FUSED_P1", 128))};
     int s = enqueue_batch(ctx, gsa::kModeSparse, npairs, p1.data(), subst, substsz, gapo, gsa::kExpHB, st, nullptr, 0,
-                          nullptr, rows.data(), fused ? &xa : nullptr);
+                          nullptr, rows.data(), fused ? &fl : nullptr);
     if (s != GSA_SUCCESS || fused) return s;
     xa.counter = ctx->ctl + 4;
     if (xGrid > 0 && (e = hipMemsetAsync(xa.counter, 0, 4, st)) != hipSuccess) return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
@@ -769,7 +794,7 @@ bool full_twopass(int)
 
 extern "C" {
 
-const char* gsa_version(void) { return "gpuseqalign_amd 0.2 (gfx950 wavefront: K-rows sparse, lane full)"; }
+const char* gsa_version(void) { return "gpuseqalign_amd 0.3 (gfx950 wavefront: K-rows sparse, two-pass full)"; }
 
 int32_t gsa_sparse_tile_by(void) { return gsa::kSparseTileBy; }
 

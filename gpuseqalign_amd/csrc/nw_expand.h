@@ -17,6 +17,7 @@ constexpr int kExpRows = 64;      // rows of a wave's tile (one per lane)
 constexpr int kExpWaves = 16;     // waves per workgroup: a 1024-row chunk of one tile column
 constexpr int kRowsPad = 64;      // left pad (columns) of the pass-1 row buffer
 constexpr int kExpFusedWaves = 8; // waves per workgroup of the fused single-pair fill (512-row chunks)
+constexpr int kExpFusedWavesBatch = 12;  // ... of the fused batch fill (768-row chunks; (8, 4) pass 1)
 constexpr unsigned kXDone = 0x3fffffffu;  // a pass-1 strip's progress word: the strip has finished
 
 // Pass-1 row buffer of a pair: row 64m (m = 1 .. 4 x strips of pass 1) as shifted values
@@ -38,6 +39,8 @@ struct ExpandPair
     int colTiles;       // ceil(C / kExpTW)
     int rowChunks;      // ceil(R / (waves * kExpRows)), waves = kExpWaves (kExpFusedWaves when fused)
     int taskBase;       // first workgroup task of this pair (colTiles * rowChunks tasks)
+    int p1Strip0;       // fused fill: the pair's first pass-1 strip word (ticketBase x ns)
+    int p1Strips;       // ... and its strip count (tickets x ns)
 };
 
 struct ExpandArgs

@@ -34,11 +34,12 @@ hipError_t launch_krow_fill(const StripArgs& a, int ns, int k, int lw, int grid,
 // Pass 1 of the two-pass full fill (nw_expand.h): the sparse fill (K = 4, ns = 4 or 8, a.tBx =
 // kExpHB) that also stores rows 64m into each pair's rows64 / rpitch (PairDesc).
 hipError_t launch_krow_fill_xr(const StripArgs& a, int ns, int grid, hipStream_t stream);
-// Both passes of one pair's two-pass full fill in one launch (ns = 4): workgroups take the pass-1
-// tickets, then expansion tasks (a.xpair, a.xTasks; 8-wave row chunks, kExpFusedWaves), each task
-// waiting for the words a.xdone of the strips whose rows and header column it reads.  grid <= 0:
-// every resident slot.
-hipError_t launch_full_fused(const StripArgs& a, int grid, hipStream_t stream);
+// Both passes of the two-pass full fill in one launch: the first a.xP workgroups take pass-1
+// tickets (the XR fill on (ns, 4) tickets) until none is left, then, like the rest, expansion
+// tasks of `waves` x 64 rows (a.xpair, a.xsched, a.xTasks), each task waiting for the progress
+// words a.xdone of the strips whose rows and header column it reads.  (ns, waves): (4, 8) or
+// (8, 12).  grid <= 0: every resident slot.
+hipError_t launch_full_fused(const StripArgs& a, int ns, int waves, int grid, hipStream_t stream);
 
 // Score-only NW / SW (modes kModeScoreAG/AGL/SW/SWL of nw_strip.h, same StripArgs contract as
 // launch_strip_fill for one pair: go, ge, gran + gran2, agResult, swBest, idxBits) on the K-rows

@@ -1767,17 +1767,23 @@ namespace {
 // -- with a relaxed agent-scope store; a task's lane 0 polls the words of the strips it reads, then
 // an agent acquire, vmcnt(0) and a workgroup barrier precede the plain loads.
 // ------------------------------------------------------------------------------------
-template <bool Q8>
-__global__ void __launch_bounds__(64 * kExpFusedWaves) nw_full_fused_kernel(StripArgs a)
+// NS: pass-1 strips per ticket ((4, 4): 1024-row tickets; (8, 4): 2048 rows, two tile rows); W: waves
+// per workgroup, also the expansion's tile waves (a task = W x 64 rows of one tile column).  The
+// first a.xP workgroups to arrive take pass-1 tickets until none is left, then expansion tasks; the
+// others take expansion tasks only.  A task waits only for tickets, every ticket only for lower
+// ones, and tickets are taken only by workgroups that are running: every wait ends.
+template <int NS, int W, bool Q8>
+__global__ void __launch_bounds__(64 * W) nw_full_fused_kernel(StripArgs a)
 {
-    constexpr int NS = 4, K = 4, LW = 1024;
-    static_assert(kr_waves<NS>() <= kExpFusedWaves, "the pass-1 roles fit the workgroup");
+    constexpr int K = 4, LW = 1024;
+    static_assert(kr_waves<NS>() <= W, "the pass-1 roles fit the workgroup");
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     const KrLds L = kr_layout(NS, LW, a.substsz, Q8);
+    const uint32_t word = L.flags + kFTicket;  // the workgroup's claims, via LDS
     if (!Q8 && a.q8 == 2 && __hip_atomic_load(a.q8flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != a.epoch) return;
     bool bad = false, bad8 = false;
-    for (int k = threadIdx.x; k < a.substsz * kSubRow; k += 64 * kExpFusedWaves)
+    for (int k = threadIdx.x; k < a.substsz * kSubRow; k += 64 * W)
     {
         const int x = k / kSubRow, yy = k % kSubRow;
         const int v = yy < a.substsz ? G(a.subst)[yy * a.substsz + x] - 2 * a.g : 0;
@@ -1788,91 +1794,135 @@ __global__ void __launch_bounds__(64 * kExpFusedWaves) nw_full_fused_kernel(Stri
     if constexpr (Q8)
     {
         // a table outside int8: decline before claiming anything (nw_krow_kernel)
-        if (threadIdx.x == 0) lds_st(L.flags + kFTicket, 0);
+        if (threadIdx.x == 0) lds_st(word, 0);
         __syncthreads();
-        if (bad8) atomicOr((int*)(krsm + L.flags + kFTicket), 1);
+        if (bad8) atomicOr((int*)(krsm + word), 1);
         __syncthreads();
-        if (lds_ld(L.flags + kFTicket) != 0)
+        if (lds_ld(word) != 0)
         {
             if (threadIdx.x == 0) __hip_atomic_store(a.q8flag, a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             return;
         }
+        __syncthreads();
     }
     else if (bad)
         atomicOr(a.err, 2u);
-    const int nAll = a.nTicketsTotal + a.xTasks;
-    const ExpandArgs xa {a.subst, a.substsz, a.g, a.xpair, 1, a.xTasks, nullptr, a.xknob, nullptr};
+    if (threadIdx.x == 0) lds_st(word, (int)atomicAdd(a.xrole, 1u));
+    __syncthreads();
+    bool p1 = __builtin_amdgcn_readfirstlane(lds_ld(word)) < a.xP;
+    // pass 1 (the LDS holds subT until the workgroup's last ticket)
+    while (p1)
+    {
+        __syncthreads();
+        if (threadIdx.x == 0) lds_st(word, err_set(a) ? a.nTicketsTotal : (int)atomicAdd(a.ticket, 1u));
+        __syncthreads();
+        const int tkg = __builtin_amdgcn_readfirstlane(lds_ld(word));
+        if (tkg >= a.nTicketsTotal) break;
+        int lo = 0, tks = -1;
+        if (a.sched)
+        {
+            lo = __builtin_amdgcn_readfirstlane(G(a.sched)[2 * tkg]);
+            tks = __builtin_amdgcn_readfirstlane(G(a.sched)[2 * tkg + 1]);
+        }
+        else
+        {
+            int hi = a.nPairs - 1;
+            while (lo < hi)
+            {
+                const int mid = (lo + hi + 1) >> 1;
+                if (__builtin_amdgcn_readfirstlane(G(a.pairs)[mid].ticketBase) <= tkg)
+                    lo = mid;
+                else
+                    hi = mid - 1;
+            }
+        }
+        const PairDesc d = kr_desc(a.pairs + lo);
+        const int tk = (tks >= 0) ? tks : tkg - d.ticketBase;
+        StripArgs pa = a;
+        pa.seqY = d.seqY;
+        pa.seqX = d.seqX;
+        pa.R = d.R;
+        pa.C = d.C;
+        pa.Cp = d.Cp;
+        pa.nTickets = d.nTickets;
+        pa.hrow = d.hrow;
+        pa.hcol = d.hcol;
+        pa.trows = d.trows;
+        pa.tcols = d.tcols;
+        pa.gran = a.gran + d.granOff;
+        pa.granStride = gran_stride(d.Cp);
+        pa.rows64 = d.rows64;
+        pa.rpitch = d.rpitch;
+        pa.xdone = a.xdone + (size_t)d.ticketBase * NS;  // the pair's strip words
+        if (threadIdx.x < 32) lds_st(L.flags + 4u * threadIdx.x, 0);
+        if (threadIdx.x >= kFCap / 4 && threadIdx.x < kFCap / 4 + 8) lds_st(L.flags + 4u * threadIdx.x, 0);
+        __syncthreads();
+        if (w == NS + 1)
+            kr_drain<NS, K, LW, 3>(pa, L, tk, lane);
+        else if (w == NS)
+            kr_loader<NS, K, LW, kr_split<NS>() ? 1 : 0, Q8>(pa, L, tk, lane);
+        else if (kr_split<NS>() && w == NS + 2)
+            kr_loader<NS, K, LW, 2, Q8>(pa, L, tk, lane);
+        else if (w < NS)
+        {
+            __builtin_amdgcn_s_setprio(3);
+            kr_strip<NS, K, LW, 3, Q8>(pa, L, tk, w, lane);
+            __builtin_amdgcn_s_setprio(0);
+        }
+    }
+    // pass 2: task tt of a pair is tile column jT of row chunk rc.  Its waves read rows 64m,
+    // m = W rc .. W rc + W - 1, at columns < need, and (jT > 0) the header column of boundary
+    // 2 jT for rows 64 W rc + 1 .. 64 W (rc + 1): the pair's strips (W rc - 1) / 4 .. (W (rc + 1) - 1) / 4
+    // (256 rows each), words >= pneed
+    const ExpandArgs xa {a.subst, a.substsz, a.g, a.xpair, a.nPairs, a.xTasks, a.xsched, a.xknob, nullptr};
     for (;;)
     {
         __syncthreads();
-        if (threadIdx.x == 0) lds_st(L.flags + kFTicket, err_set(a) ? nAll : (int)atomicAdd(a.ticket, 1u));
+        if (threadIdx.x == 0) lds_st(word, err_set(a) ? a.xTasks : (int)atomicAdd(a.xcounter, 1u));
         __syncthreads();
-        const int c = __builtin_amdgcn_readfirstlane(lds_ld(L.flags + kFTicket));
-        if (c >= nAll) break;
-        if (c < a.nTicketsTotal)
+        const int task = __builtin_amdgcn_readfirstlane(lds_ld(word));
+        if (task >= a.xTasks) break;
+        int lo = 0, tt = -1;
+        if (a.xsched)
         {
-            // pass 1, ticket c of the pair (the LDS still holds subT: pass-1 claims all come first)
-            const PairDesc d = kr_desc(a.pairs);
-            StripArgs pa = a;
-            pa.seqY = d.seqY;
-            pa.seqX = d.seqX;
-            pa.R = d.R;
-            pa.C = d.C;
-            pa.Cp = d.Cp;
-            pa.nTickets = d.nTickets;
-            pa.hrow = d.hrow;
-            pa.hcol = d.hcol;
-            pa.trows = d.trows;
-            pa.tcols = d.tcols;
-            pa.gran = a.gran + d.granOff;
-            pa.granStride = gran_stride(d.Cp);
-            pa.rows64 = d.rows64;
-            pa.rpitch = d.rpitch;
-            if (threadIdx.x < 32) lds_st(L.flags + 4u * threadIdx.x, 0);
-            if (threadIdx.x >= kFCap / 4 && threadIdx.x < kFCap / 4 + 8) lds_st(L.flags + 4u * threadIdx.x, 0);
-            __syncthreads();
-            if (w == NS + 1)
-                kr_drain<NS, K, LW, 3>(pa, L, c, lane);
-            else if (w == NS)
-                kr_loader<NS, K, LW, 1, Q8>(pa, L, c, lane);
-            else if (w == NS + 2)
-                kr_loader<NS, K, LW, 2, Q8>(pa, L, c, lane);
-            else if (w < NS)
-            {
-                __builtin_amdgcn_s_setprio(3);
-                kr_strip<NS, K, LW, 3, Q8>(pa, L, c, w, lane);
-                __builtin_amdgcn_s_setprio(0);
-            }
-            continue;
+            lo = __builtin_amdgcn_readfirstlane(G(a.xsched)[2 * task]);
+            tt = __builtin_amdgcn_readfirstlane(G(a.xsched)[2 * task + 1]);
         }
-        // pass 2, task tt: tile column jT of row chunk rc.  Its waves read rows 64m, m = 8 rc .. 8 rc + 7,
-        // at columns < need, and (jT > 0) the header column of boundary 2 jT for rows 512 rc + 1 ..
-        // 512 rc + 512: global strips 2 rc - 1 .. 2 rc + 1 (4 per ticket), words >= pneed
-        const ExpandPair xd = xdev::ex_desc(a.xpair);
-        const int tt = c - a.nTicketsTotal;
-        const int jT = tt % xd.colTiles, rc = tt / xd.colTiles;
+        else
+        {
+            int hi = a.nPairs - 1;
+            while (lo < hi)
+            {
+                const int mid = (lo + hi + 1) >> 1;
+                if (__builtin_amdgcn_readfirstlane(G(a.xpair)[mid].taskBase) <= task)
+                    lo = mid;
+                else
+                    hi = mid - 1;
+            }
+        }
+        const ExpandPair xd = xdev::ex_desc(a.xpair + lo);
+        if (tt < 0) tt = task - xd.taskBase;
         if (threadIdx.x == 0)
         {
+            const int jT = tt % xd.colTiles, rc = tt / xd.colTiles;
             const int cb = jT * kExpTW;
             const int need = min(cb + min(kExpTW, xd.C - cb) + 3, xd.C) + 1;
             unsigned pneed = (unsigned)((need + kExpHB - 1) / kExpHB + 1);
             if (pneed >= (unsigned)xd.tcols) pneed = kXDone;  // (a strip's last boundary is published at its end)
-            const int s1 = min(2 * rc + 1, a.nTicketsTotal * NS - 1);
+            const int s1 = min((W * (rc + 1) - 1) / 4, xd.p1Strips - 1);
+            const unsigned long long* words = a.xdone + xd.p1Strip0;
             bool ok = true;
             uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-            for (int s = (a.xknob & 4) ? s1 + 1 : max(0, 2 * rc - 1); s <= s1 && ok;)  // (4: probe, no wait)
+            for (int s = (a.xknob & 4) ? s1 + 1 : rc > 0 ? (W * rc - 1) / 4 : 0; s <= s1 && ok;)  // (4: probe, no wait)
             {
-                const unsigned long long v = __hip_atomic_load(a.xdone + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const unsigned long long v = __hip_atomic_load(words + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if ((unsigned)(v >> 32) == a.epoch && (unsigned)v >= pneed)
                 {
                     ++s;
                     t0 = __builtin_amdgcn_s_memrealtime();
                     continue;
                 }
-                if (a.xknob & 0xf0)  // probe: (knob >> 4) x 1024 cycles between polls
-                    for (int z = 0; z < ((a.xknob >> 4) & 15); ++z) __builtin_amdgcn_s_sleep(16);
-                else
-                    __builtin_amdgcn_s_sleep(2);
+                __builtin_amdgcn_s_sleep(2);
                 if (__builtin_amdgcn_s_memrealtime() - t0 > a.spin || err_set(a))
                 {
                     atomicOr(a.err, 1u);
@@ -1881,22 +1931,22 @@ __global__ void __launch_bounds__(64 * kExpFusedWaves) nw_full_fused_kernel(Stri
             }
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            lds_st(L.flags + kFTicket, ok ? c : nAll);
+            lds_st(word, ok ? 0 : 1);
         }
         __syncthreads();
-        const int go = __builtin_amdgcn_readfirstlane(lds_ld(L.flags + kFTicket));
+        const int stop = __builtin_amdgcn_readfirstlane(lds_ld(word));
         __syncthreads();  // (the task's LDS may overlap the word)
-        if (go >= nAll) break;
-        xdev::ex_task<kExpFusedWaves>(xa, xd, tt, w, lane);
+        if (stop) break;
+        xdev::ex_task<W>(xa, xd, tt, w, lane);
     }
 }
 
-template <bool Q8>
+template <int NS, int W, bool Q8>
 hipError_t launch_fused1(const StripArgs& a, int grid, hipStream_t stream, bool foot)
 {
-    const size_t lds = std::max(krow_lds_bytes(4, 1024, a.substsz, Q8), expand_lds_bytes(a.substsz, kExpFusedWaves));
-    auto kern = nw_full_fused_kernel<Q8>;
-    constexpr int kThreads = 64 * kExpFusedWaves;
+    const size_t lds = std::max(krow_lds_bytes(NS, 1024, a.substsz, Q8), expand_lds_bytes(a.substsz, W));
+    auto kern = nw_full_fused_kernel<NS, W, Q8>;
+    constexpr int kThreads = 64 * W;
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     if (grid <= 0)
@@ -1913,17 +1963,25 @@ hipError_t launch_fused1(const StripArgs& a, int grid, hipStream_t stream, bool 
     return hipGetLastError();
 }
 
-}  // namespace
-
-hipError_t launch_full_fused(const StripArgs& a, int grid, hipStream_t stream)
+template <int NS, int W>
+hipError_t launch_fused(const StripArgs& a, int grid, hipStream_t stream)
 {
-    if (a.nPairs != 1 || !a.xpair || !a.xdone) return hipErrorInvalidValue;
-    if (!a.q8) return launch_fused1<false>(a, grid, stream, true);
-    hipError_t e = launch_fused1<true>(a, grid, stream, true);
+    if (!a.q8) return launch_fused1<NS, W, false>(a, grid, stream, true);
+    hipError_t e = launch_fused1<NS, W, true>(a, grid, stream, true);
     if (e != hipSuccess) return e;
     StripArgs b = a;
     b.q8 = 2;
-    return launch_fused1<false>(b, grid, stream, false);
+    return launch_fused1<NS, W, false>(b, grid, stream, false);
+}
+
+}  // namespace
+
+hipError_t launch_full_fused(const StripArgs& a, int ns, int waves, int grid, hipStream_t stream)
+{
+    if (!a.xpair || !a.xdone || !a.xrole || !a.xcounter) return hipErrorInvalidValue;
+    if (ns == 4 && waves == 8) return launch_fused<4, 8>(a, grid, stream);
+    if (ns == 8 && waves == 12) return launch_fused<8, 12>(a, grid, stream);
+    return hipErrorInvalidValue;
 }
 #elif defined(GSA_KROW_BATCH8)
 // nw_krow8.hip: the 8-strip batch instance in a translation unit of its own, so it can be built

@@ -101,12 +101,17 @@ struct StripArgs
     // batch schedule: {pair, ticket within the pair} of every global ticket, round-robin over the
     // pairs (null: pair-major by ticketBase).  Ticket j of a pair always follows its ticket j-1.
     const int* sched;
-    // fused single-pair full fill (nw_full_fused_kernel): the expansion's pair descriptor and task
-    // count (tasks are claimed from *ticket after the nTicketsTotal pass-1 tickets), its probe
-    // knob, and one progress word per pass-1 strip (epoch << 32 | tile columns published)
+    // fused full fill (nw_full_fused_kernel): the expansion's descriptors (nPairs) and schedule
+    // ({pair, task} per task, or null), its task count, the workgroups that take pass-1 tickets
+    // first, the probe knob; claim counters (role, expansion task; zeroed per launch); one progress
+    // word per pass-1 strip (epoch << 32 | tile columns published), pair p's at its ticketBase x ns
     const ExpandPair* xpair;
+    const int* xsched;
     int xTasks;
+    int xP;
     int xknob;
+    unsigned* xrole;
+    unsigned* xcounter;
     unsigned long long* xdone;
 };
 
