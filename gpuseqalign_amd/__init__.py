@@ -111,6 +111,7 @@ SIGNATURES = {
     "gsa_last_hip_error": (ctypes.c_int, [_vp]),
     "gsa_device_cu_count": (ctypes.c_int, [_vp]),
     "gsa_version": (ctypes.c_char_p, []),
+    "gsa_debug_stamps": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64)]),
     "gsa_set_lap_callback": (ctypes.c_int, [_vp, _vp, _vp]),
     "gsa_sparse_tile_by": (_i32, []),
     "gsa_sparse_geometry": (ctypes.c_int, [_i32, _i32, _i32, ctypes.POINTER(SparseGeom)]),
@@ -340,6 +341,18 @@ class Engine:
         """Wait for `stream`; raises NwError if a hand-off of ANY fill enqueued since the last
         sync gave up (the error word is sticky until this call clears it)."""
         self._check(lib().gsa_sync(self._h, stream), "gsa_sync")
+
+    def debug_stamps(self):
+        """The fused full fill's s_memrealtime stamps of the last launch made under GSA_STAMPS=1
+        (gsa_debug_stamps): uint64 array, [start, end] per pass-1 strip, then [claimed, ready,
+        done] per expansion task; empty if none were recorded."""
+        import numpy as np
+        n = ctypes.c_int64(0)
+        self._check(lib().gsa_debug_stamps(self._h, None, 0, ctypes.byref(n)), "gsa_debug_stamps")
+        out = np.zeros(n.value, dtype=np.uint64)
+        if n.value:
+            self._check(lib().gsa_debug_stamps(self._h, out.ctypes.data, n.value, ctypes.byref(n)), "gsa_debug_stamps")
+        return out
 
     def set_lap_callback(self, fn: Optional[Callable[[str], None]]):
         """fn(lap_name) at every phase boundary of the host-buffer entry points (align_full,

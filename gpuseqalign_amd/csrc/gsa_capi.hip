@@ -68,6 +68,9 @@ struct gsa_ctx
     // allocation)
     unsigned long long* xdone = nullptr;
     size_t xdone_cap = 0;
+    // GSA_STAMPS=1: the fused fill's stamps of the last launch (gsa_debug_stamps)
+    unsigned long long* stamps = nullptr;
+    size_t stamps_cap = 0, stamps_n = 0;
     void* expin[kStage] = {nullptr, nullptr, nullptr, nullptr};
     size_t expin_cap[kStage] = {0, 0, 0, 0};
     hipEvent_t expin_ev[kStage] = {nullptr, nullptr, nullptr, nullptr};
@@ -591,6 +594,24 @@ int enqueue_batch(gsa_ctx* ctx, int mode, int npairs, const gsa_pair_dev* pairs,
             a.xrole = ctx->ctl + 4;
             a.xcounter = ctx->ctl + 5;
             if ((e = hipMemsetAsync(a.xrole, 0, 8, st)) != hipSuccess) return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
+            ctx->stamps_n = 0;
+            if (env_int("GSA_STAMPS", 0))
+            {
+                const size_t n = 2 * words + 3 * (size_t)a.xTasks;
+                if (ctx->stamps_cap < n)
+                {
+                    if (ctx->stamps) (void)hipFree(ctx->stamps);
+                    ctx->stamps = nullptr;
+                    ctx->stamps_cap = 0;
+                    if ((e = hipMalloc(&ctx->stamps, n * sizeof(unsigned long long))) != hipSuccess)
+                        return fail(ctx, e, GSA_ERROR_MEMORY_ALLOCATION);
+                    ctx->stamps_cap = n;
+                }
+                if ((e = hipMemsetAsync(ctx->stamps, 0, n * sizeof(unsigned long long), st)) != hipSuccess)
+                    return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
+                a.stamps = ctx->stamps;
+                ctx->stamps_n = n;
+            }
         }
         a.xdone = ctx->xdone;
     }
@@ -798,6 +819,18 @@ const char* gsa_version(void) { return "gpuseqalign_amd 0.3 (gfx950 wavefront: K
 
 int32_t gsa_sparse_tile_by(void) { return gsa::kSparseTileBy; }
 
+int gsa_debug_stamps(gsa_ctx* ctx, uint64_t* out, int64_t cap, int64_t* n)
+{
+    if (!ctx || !n) return GSA_ERROR_INVALID_VALUE;
+    *n = (int64_t)ctx->stamps_n;
+    if (ctx->stamps_n == 0 || !out) return GSA_SUCCESS;
+    if (cap < (int64_t)ctx->stamps_n) return GSA_ERROR_MEMORY_ALLOCATION;
+    hipError_t e = hipSetDevice(ctx->device);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e == hipSuccess) e = hipMemcpy(out, ctx->stamps, ctx->stamps_n * sizeof(uint64_t), hipMemcpyDeviceToHost);
+    return e == hipSuccess ? GSA_SUCCESS : fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
+}
+
 int gsa_ctx_create(int device, gsa_ctx** out)
 {
     if (!out) return GSA_ERROR_INVALID_VALUE;
@@ -851,6 +884,7 @@ void gsa_ctx_destroy(gsa_ctx* ctx)
     if (ctx->exbuf) (void)hipFree(ctx->exbuf);
     if (ctx->exdesc) (void)hipFree(ctx->exdesc);
     if (ctx->xdone) (void)hipFree(ctx->xdone);
+    if (ctx->stamps) (void)hipFree(ctx->stamps);
     for (int k = 0; k < gsa_ctx::kStage; ++k)
     {
         if (ctx->expin[k]) (void)hipHostFree(ctx->expin[k]);
@@ -1610,11 +1644,15 @@ int gsa_align_sparse_pt(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, cons
     // super-strip within the wavefront's fill-in, so chunks complete left to right while the fill
     // runs, and each is copied back (one strided copy per matrix) as soon as it is complete.
     const int tcols = geom.tileHdrMatCols;
-    const int cw = std::max(1, std::min(tcols, (4096 + tileBx - 1) / tileBx));
+    // ~4096 columns per chunk, fewer (down to one tile column) while two chunks of every tile row
+    // overfill the kPtPin staging slots: the pinned buffer stays 64 MB up to ~7.8M rows at tBx 64
+    const size_t chunkCol = trows * (size_t)(geom.tileHrowLen + geom.tileHcolLen) * 4;  // one tile column
+    int cw = std::max(1, std::min(tcols, (4096 + tileBx - 1) / tileBx));
+    while (cw > 1 && 2 * chunkCol * (size_t)cw > gsa_ctx::kPtPin) cw = (cw + 1) / 2;
     const int nCh = (tcols + cw - 1) / cw;
     {
         // room for a batch of at least one chunk
-        const size_t need = std::max(gsa_ctx::kPtPin, 2 * trows * (size_t)cw * (geom.tileHrowLen + geom.tileHcolLen) * 4);
+        const size_t need = std::max(gsa_ctx::kPtPin, 2 * chunkCol * (size_t)cw);
         if (ctx->ptpin_cap < need)
         {
             if (ctx->ptpin) (void)hipHostFree(ctx->ptpin);

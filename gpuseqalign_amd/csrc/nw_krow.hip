@@ -497,6 +497,7 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
     using T = std::integral_constant<bool, true>;
     using F = std::integral_constant<bool, false>;
     constexpr int kRampBlocks = 64 / kBlk;  // columns <= 0 occur only in the first 64 steps
+    if (fx && a.stamps && lane == 0) a.stamps[2 * ((size_t)tk * NS + w)] = __builtin_amdgcn_s_memrealtime();
     int b = 0;
     for (; b < kRampBlocks; b += 2)
     {
@@ -518,6 +519,7 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
     {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         fx_publish(kXDone);
+        if (a.stamps && lane == 0) a.stamps[2 * ((size_t)tk * NS + w) + 1] = __builtin_amdgcn_s_memrealtime();
     }
 }
 
@@ -1854,6 +1856,7 @@ __global__ void __launch_bounds__(64 * W) nw_full_fused_kernel(StripArgs a)
         pa.rows64 = d.rows64;
         pa.rpitch = d.rpitch;
         pa.xdone = a.xdone + (size_t)d.ticketBase * NS;  // the pair's strip words
+        if (a.stamps) pa.stamps = a.stamps + 2 * (size_t)d.ticketBase * NS;
         if (threadIdx.x < 32) lds_st(L.flags + 4u * threadIdx.x, 0);
         if (threadIdx.x >= kFCap / 4 && threadIdx.x < kFCap / 4 + 8) lds_st(L.flags + 4u * threadIdx.x, 0);
         __syncthreads();
@@ -1902,8 +1905,10 @@ __global__ void __launch_bounds__(64 * W) nw_full_fused_kernel(StripArgs a)
         }
         const ExpandPair xd = xdev::ex_desc(a.xpair + lo);
         if (tt < 0) tt = task - xd.taskBase;
+        unsigned long long* tstamp = a.stamps ? a.stamps + 2 * (size_t)a.nTicketsTotal * NS + 3 * (size_t)task : nullptr;
         if (threadIdx.x == 0)
         {
+            if (tstamp) tstamp[0] = __builtin_amdgcn_s_memrealtime();
             const int jT = tt % xd.colTiles, rc = tt / xd.colTiles;
             const int cb = jT * kExpTW;
             const int need = min(cb + min(kExpTW, xd.C - cb) + 3, xd.C) + 1;
@@ -1932,12 +1937,14 @@ __global__ void __launch_bounds__(64 * W) nw_full_fused_kernel(StripArgs a)
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             lds_st(word, ok ? 0 : 1);
+            if (tstamp) tstamp[1] = __builtin_amdgcn_s_memrealtime();
         }
         __syncthreads();
         const int stop = __builtin_amdgcn_readfirstlane(lds_ld(word));
         __syncthreads();  // (the task's LDS may overlap the word)
         if (stop) break;
         xdev::ex_task<W>(xa, xd, tt, w, lane);
+        if (tstamp && threadIdx.x == 0) tstamp[2] = __builtin_amdgcn_s_memrealtime();  // (wave 0's tile)
     }
 }
 

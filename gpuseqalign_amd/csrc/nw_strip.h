@@ -113,6 +113,10 @@ struct StripArgs
     unsigned* xrole;
     unsigned* xcounter;
     unsigned long long* xdone;
+    // measurement aid (GSA_STAMPS=1, gsa_debug_stamps): s_memrealtime stamps of the fused fill,
+    // [start, end] per pass-1 strip (global strip index), then [claimed, ready, done] per expansion
+    // task; null otherwise
+    unsigned long long* stamps;
 };
 
 // Resource footprint of the last fill launched from this host thread: what the reference's

@@ -178,6 +178,12 @@ int gsa_align_sparse_pt(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, cons
                         const int32_t* subst, int32_t substsz, int32_t gapo, int32_t tileBx, int32_t* tileHrowMat_out,
                         int32_t* tileHcolMat_out, gsa_sparse_geom* geom, int32_t* align_cost, gsa_laps* laps);
 
+/* Measurement aid, not part of the reference's interface: with GSA_STAMPS=1 in the environment a
+ * fused full fill records s_memrealtime stamps (100 MHz): [start, end] per pass-1
+ * strip, then [claimed, ready, done] per expansion task.  Copies the last such launch's *n stamps
+ * into out (cap >= *n; out may be null to query *n); synchronizes the device. */
+int gsa_debug_stamps(gsa_ctx* ctx, uint64_t* out, int64_t cap, int64_t* n);
+
 /* ---- consumers (host), the reference's L4 ----------------------------------------- */
 /* NwHash1_Plain (src/nwtrace1_plain.cpp:133-154). */
 uint32_t gsa_hash_full(const int32_t* score, int32_t adjrows, int32_t adjcols);

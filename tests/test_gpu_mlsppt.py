@@ -73,3 +73,14 @@ def test_overlap_error_then_recovers(golden):
         r = eng.align_sparse(Y, X, sub, -11, tileBx=256, overlap=True)
     hr, hc, _, _, cost = oracle.sparse_headers(Y, X, sub, -11, gsa.sparse_tile_by(), 256)
     assert np.array_equal(r.hrow, hr) and np.array_equal(r.hcol, hc) and r.align_cost == cost
+
+
+def test_overlap_tall_pair_narrow_chunks(engine, golden):
+    """A tall pair at tBx 64: two 4096-column chunks of every tile row would need
+    ~150 MB of pinned staging, so the chunk width shrinks until two chunks fit the 64 MB slots;
+    the headers still equal the plain mlsp path's word for word."""
+    Y, X = random_pair(140000, 5000, 77)
+    a = engine.align_sparse(Y, X, golden.blosum62, -11, tileBx=64)
+    b = engine.align_sparse(Y, X, golden.blosum62, -11, tileBx=64, overlap=True)
+    assert np.array_equal(a.hrow, b.hrow) and np.array_equal(a.hcol, b.hcol)
+    assert a.align_cost == b.align_cost
