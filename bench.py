@@ -80,9 +80,14 @@ def full_kernel_name(single):
     expansion), or under GSA_FULL_KERNEL=lane the one-pass lane fill."""
     if os.environ.get("GSA_FULL_KERNEL", "") == "lane":
         return lane_kernel_name(single)
-    if single and os.environ.get("GSA_FULL_FUSED", "1") != "0":
-        return ("gsa::nw_full_fused_kernel<true> (both passes in one launch: (4, 4) K-rows pass-1 tickets publishing "
-                "per-strip progress, then 8-wave expansion tasks of 64 x 512 tiles waiting on those words)")
+    fm = os.environ.get("GSA_FULL_FUSED", "1")
+    if single and fm != "0":
+        return ("gsa::nw_full_fused_kernel<4,8,true> (both passes in one launch: (4, 4) K-rows pass-1 tickets "
+                "publishing per-strip progress, then 8-wave expansion tasks of 64 x 512 tiles waiting on those words)")
+    if not single and fm == "2":
+        return (f"gsa::nw_full_fused_kernel<8,12,true> (both passes in one launch: GSA_FUSED_P1="
+                f"{os.environ.get('GSA_FUSED_P1', '128')} workgroups take the (8, 4) pass-1 tickets first, the rest "
+                "12-wave expansion tasks of 64 x 512 tiles as their rows come in)")
     ns = 4 if single else 8
     return (f"gsa::nw_krow_kernel<{ns},4,1024,2,true> (pass 1: sparse wavefront keeping every 64th row and the "
             f"256-column header columns) + gsa::nw_expand_kernel (pass 2: every 64 x 512 tile recomputed)")

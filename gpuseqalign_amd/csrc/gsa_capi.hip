@@ -590,6 +590,7 @@ int enqueue_batch(gsa_ctx* ctx, int mode, int npairs, const gsa_pair_dev* pairs,
             a.xsched = fused->xa->sched;
             a.xTasks = fused->xa->nTasks;
             a.xknob = fused->xa->knob;
+            a.xmt = fused->xa->mt;
             a.xP = fused->p1;
             a.xrole = ctx->ctl + 4;
             a.xcounter = ctx->ctl + 5;
@@ -667,6 +668,8 @@ int enqueue_full_twopass(gsa_ctx* ctx, int npairs, const gsa_pair_dev* pairs, co
     // fused: (4, 4) tickets under 8-wave workgroups, (8, 4) under 12
     const int fusedW = ns == 4 ? gsa::kExpFusedWaves : gsa::kExpFusedWavesBatch;
     const int xWaves = fused ? fusedW : xGrid > 0 && (xw == 8 || xw == 12) ? xw : gsa::kExpWaves;
+    // tiles per wave per expansion task (GSA_EXPAND_MT, 1..16; default 1)
+    const int xmt = std::min(16, std::max(1, env_int("GSA_EXPAND_MT", 1)));
     std::vector<gsa_pair_dev> p1((size_t)npairs);
     std::vector<gsa::ExpandPair> ex((size_t)npairs);
     std::vector<size_t> off((size_t)npairs * 3);
@@ -704,7 +707,7 @@ int enqueue_full_twopass(gsa_ctx* ctx, int npairs, const gsa_pair_dev* pairs, co
         e.tcols = geom.tileHdrMatCols;
         // (an empty sequence still has its header row or column: at least one task per dimension)
         e.colTiles = std::max(1, (e.C + gsa::kExpTW - 1) / gsa::kExpTW);
-        e.rowChunks = std::max(1, (e.R + xWaves * gsa::kExpRows - 1) / (xWaves * gsa::kExpRows));
+        e.rowChunks = std::max(1, (e.R + xWaves * gsa::kExpRows * xmt - 1) / (xWaves * gsa::kExpRows * xmt));
         e.taskBase = (int)tasks;
         tasks += (long long)e.colTiles * e.rowChunks;
         e.p1Strip0 = (int)strips;  // (enqueue_batch's ticketBase x ns: pair-major)
@@ -791,6 +794,7 @@ int enqueue_full_twopass(gsa_ctx* ctx, int npairs, const gsa_pair_dev* pairs, co
     xa.nTasks = (int)tasks;
     xa.sched = xs.empty() ? nullptr : (const int*)((char*)ctx->exdesc + descBytes);
     xa.knob = env_int("GSA_EXPAND_KNOB", 0);
+    xa.mt = xmt;
     // fused batches: GSA_FUSED_P1 workgroups take the pass-1 tickets first (a single pair: all)
     const FusedLaunch fl {&xa, ns, fusedW, npairs == 1 ? (1 << 30) : std::max(1, env_int("GSA_FUSED_P1", 128))};
     int s = enqueue_batch(ctx, gsa::kModeSparse, npairs, p1.data(), subst, substsz, gapo, gsa::kExpHB, st, nullptr, 0,

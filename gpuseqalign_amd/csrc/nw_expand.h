@@ -37,7 +37,7 @@ struct ExpandPair
     const int* hcol;    // pass-1 tile header columns, tile-major, 1 + kSparseTileBy per tile, unshifted
     int tcols;          // pass-1 tile columns (tBx = kExpHB)
     int colTiles;       // ceil(C / kExpTW)
-    int rowChunks;      // ceil(R / (waves * kExpRows)), waves = kExpWaves (kExpFusedWaves when fused)
+    int rowChunks;      // ceil(R / (waves * kExpRows * mt)), waves = kExpWaves (kExpFusedWaves when fused)
     int taskBase;       // first workgroup task of this pair (colTiles * rowChunks tasks)
     int p1Strip0;       // fused fill: the pair's first pass-1 strip word (ticketBase x ns)
     int p1Strips;       // ... and its strip count (tickets x ns)
@@ -58,6 +58,7 @@ struct ExpandArgs
     int knob;  // probes only (GSA_EXPAND_KNOB): 1 = no tile computed or stored (results wrong)
     // persistent launches: workgroups claim tasks from *counter (zeroed before the launch)
     unsigned* counter;
+    int mt;  // tiles per wave per task: a task is waves x 64 x mt rows of one tile column
 };
 
 size_t expand_lds_bytes(int substsz, int waves);

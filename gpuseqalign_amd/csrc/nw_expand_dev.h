@@ -233,8 +233,9 @@ __device__ __forceinline__ void ex_tile(const ExpandArgs& a, const ExpandPair& d
 }
 
 
-// one task: the tile column jT of the `WAVES * kExpRows`-row chunk rc of pair d (all threads of the
-// workgroup): subT and the column profile into LDS, the matrix headers the task owns, one tile per wave
+// one task: the tile column jT of the `WAVES * kExpRows * a.mt`-row chunk rc of pair d (all threads
+// of the workgroup): subT and the column profile into LDS, the matrix headers the task owns, a.mt
+// tiles per wave
 template <int WAVES>
 __device__ __forceinline__ void ex_task(const ExpandArgs& a, const ExpandPair& d, int tt, int w, int lane)
 {
@@ -263,7 +264,7 @@ __device__ __forceinline__ void ex_task(const ExpandArgs& a, const ExpandPair& d
     __syncthreads();
     // the matrix headers H(i, 0) = i g, H(0, j) = j g: column 0 of the chunk's rows (first tile
     // column), row 0 of the tile's columns (first row chunk)
-    constexpr int kChunk = WAVES * kExpRows;
+    const int kChunk = WAVES * kExpRows * a.mt;
     if (jT == 0)
         for (int r = rc * kChunk + 1 + (int)threadIdx.x; r <= min(d.R, rc * kChunk + kChunk); r += 64 * WAVES)
             G(d.score)[(size_t)r * (size_t)d.ld] = r * a.g;
@@ -272,8 +273,13 @@ __device__ __forceinline__ void ex_task(const ExpandArgs& a, const ExpandPair& d
         for (int c = cb + 1 + (int)threadIdx.x; c <= min(d.C, cb + kExpTW); c += 64 * WAVES) G(d.score)[c] = c * a.g;
         if (jT == 0 && threadIdx.x == 0) G(d.score)[0] = 0;
     }
-    const int r0 = rc * kChunk + kExpRows * w + 1;
-    if (r0 <= d.R && cb < d.C && !(a.knob & 1)) ex_tile(a, d, L, w, lane, jT, r0);
+    // the wave's tiles: rows 64 (w + WAVES i) of the chunk, i < mt (no barrier between them: each
+    // wave has its own top-row buffer)
+    for (int i = 0; i < a.mt; ++i)
+    {
+        const int r0 = rc * kChunk + kExpRows * (w + WAVES * i) + 1;
+        if (r0 <= d.R && cb < d.C && !(a.knob & 1)) ex_tile(a, d, L, w, lane, jT, r0);
+    }
 }
 
 }  // namespace xdev

@@ -1873,11 +1873,11 @@ __global__ void __launch_bounds__(64 * W) nw_full_fused_kernel(StripArgs a)
             __builtin_amdgcn_s_setprio(0);
         }
     }
-    // pass 2: task tt of a pair is tile column jT of row chunk rc.  Its waves read rows 64m,
-    // m = W rc .. W rc + W - 1, at columns < need, and (jT > 0) the header column of boundary
-    // 2 jT for rows 64 W rc + 1 .. 64 W (rc + 1): the pair's strips (W rc - 1) / 4 .. (W (rc + 1) - 1) / 4
-    // (256 rows each), words >= pneed
-    const ExpandArgs xa {a.subst, a.substsz, a.g, a.xpair, a.nPairs, a.xTasks, a.xsched, a.xknob, nullptr};
+    // pass 2: task tt of a pair is tile column jT of row chunk rc (cm = W xmt tiles of 64 rows).  Its
+    // waves read rows 64m, m = cm rc .. cm rc + cm - 1, at columns < need, and (jT > 0) the header
+    // column of boundary 2 jT for rows 64 cm rc + 1 .. 64 cm (rc + 1): the pair's strips
+    // (cm rc - 1) / 4 .. (cm (rc + 1) - 1) / 4 (256 rows each), words >= pneed
+    const ExpandArgs xa {a.subst, a.substsz, a.g, a.xpair, a.nPairs, a.xTasks, a.xsched, a.xknob, nullptr, a.xmt};
     for (;;)
     {
         __syncthreads();
@@ -1914,11 +1914,12 @@ __global__ void __launch_bounds__(64 * W) nw_full_fused_kernel(StripArgs a)
             const int need = min(cb + min(kExpTW, xd.C - cb) + 3, xd.C) + 1;
             unsigned pneed = (unsigned)((need + kExpHB - 1) / kExpHB + 1);
             if (pneed >= (unsigned)xd.tcols) pneed = kXDone;  // (a strip's last boundary is published at its end)
-            const int s1 = min((W * (rc + 1) - 1) / 4, xd.p1Strips - 1);
+            const int cm = W * a.xmt;  // 64-row tiles per chunk
+            const int s1 = min((cm * (rc + 1) - 1) / 4, xd.p1Strips - 1);
             const unsigned long long* words = a.xdone + xd.p1Strip0;
             bool ok = true;
             uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-            for (int s = (a.xknob & 4) ? s1 + 1 : rc > 0 ? (W * rc - 1) / 4 : 0; s <= s1 && ok;)  // (4: probe, no wait)
+            for (int s = (a.xknob & 4) ? s1 + 1 : rc > 0 ? (cm * rc - 1) / 4 : 0; s <= s1 && ok;)  // (4: probe, no wait)
             {
                 const unsigned long long v = __hip_atomic_load(words + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if ((unsigned)(v >> 32) == a.epoch && (unsigned)v >= pneed)

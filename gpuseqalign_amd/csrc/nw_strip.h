@@ -109,6 +109,7 @@ struct StripArgs
     const int* xsched;
     int xTasks;
     int xP;
+    int xmt;  // expansion tiles per wave per task
     int xknob;
     unsigned* xrole;
     unsigned* xcounter;

@@ -301,14 +301,17 @@ def test_twopass_tables_and_batches(engine, golden, fused, ns, name, gapo, monke
     """The two-pass fill of a batch in both pass-1 geometries (4 strips: 1024-row tickets, 8 strips:
     2048-row tickets, GSA_KROW_NS), in two launches and fused into one (GSA_FULL_FUSED=2; with 3
     pass-1 workgroups for two of the tables, GSA_FUSED_P1, so most tasks wait on tickets not yet
-    taken), other tables and gap costs (a positive gap included; at gap -70 s - 2g leaves int8 and
-    pass 1 runs its int16 instance), pitched layout, every word of every pair against the oracle."""
+    taken; the other two with 3 tiles per wave per expansion task, GSA_EXPAND_MT), other tables and
+    gap costs (a positive gap included; at gap -70 s - 2g leaves int8 and pass 1 runs its int16
+    instance), pitched layout, every word of every pair against the oracle."""
     import torch
     monkeypatch.setenv("GSA_FULL_KERNEL", "twopass")
     monkeypatch.setenv("GSA_KROW_NS", ns)
     monkeypatch.setenv("GSA_FULL_FUSED", fused)
     if name in ("blosum45", "blosum80"):
         monkeypatch.setenv("GSA_FUSED_P1", "3")
+    else:
+        monkeypatch.setenv("GSA_EXPAND_MT", "3")  # 3 tiles per wave per expansion task
     sub = golden.subst_data.matrix(name)
     pairs = [random_pair(r, c, 7 * r + c, alphabet=25) for r, c in ((2100, 900), (1, 5), (700, 2500), (64, 64), (4097, 300))]
     dev = torch.device("cuda:0")
@@ -336,6 +339,8 @@ def test_fused_tables_pitched_repeated(engine, golden, name, gapo, monkeypatch):
     import torch
     monkeypatch.setenv("GSA_FULL_KERNEL", "twopass")
     monkeypatch.setenv("GSA_FULL_FUSED", "1")
+    if gapo == 3:
+        monkeypatch.setenv("GSA_EXPAND_MT", "2")
     sub = golden.subst_data.matrix(name)
     dev = torch.device("cuda:0")
     s = torch.from_numpy(np.ascontiguousarray(sub, dtype=np.int32)).to(dev)
