@@ -338,13 +338,13 @@ def bench_full_batch(world, rank, local, n_pairs):
 
 
 def pmc_write_ratio(n_pairs, kernel):
-    """HBM bytes written (PMC WRITE_SIZE, profiles/r03_pmc_full_batch.json, collected by
-    tools/r03_pmc.sh on the same batch) over the matrix bytes, or None for another shape/kernel:
-    the physical write rate is hbm_write_GBps times this."""
-    p = os.path.join(ROOT, "profiles", "r03_pmc_full_batch.json")
+    """HBM bytes written (PMC WRITE_SIZE of both passes, profiles/r04_pmc_full_batch.json, collected
+    by tools/r04_pmc_full.sh on the same batch) over the matrix bytes, or None for another
+    shape/kernel: the physical write rate is hbm_write_GBps times this."""
+    p = os.path.join(ROOT, "profiles", "r04_pmc_full_batch.json")
     try:
         j = json.load(open(p))
-        if n_pairs == 64 and j.get("kernel", "").startswith(kernel):
+        if n_pairs == 64 and j.get("kernel", "").split(" ")[0] == kernel.split(" ")[0]:
             return round(j["write_over_algorithmic"], 4)
     except Exception:
         return None

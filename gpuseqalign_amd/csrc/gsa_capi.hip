@@ -567,8 +567,7 @@ int enqueue_batch(gsa_ctx* ctx, int mode, int npairs, const gsa_pair_dev* pairs,
     a.ptChunk = std::max(1, ptChunk);
     a.epoch = ++ctx->epoch;
     if (a.epoch == 0) a.epoch = ++ctx->epoch;  // 0 is the cleared-tag value
-    const bool probePT3 = rows64 && !fused && npairs == 1 && env_int("GSA_XR_PT3", 0);  // PROBE
-    if (fused || probePT3)
+    if (fused)
     {
         if (!rows64) return GSA_ERROR_INVALID_VALUE;
         const size_t words = (size_t)tickets * (size_t)krowNS;
@@ -584,7 +583,6 @@ int enqueue_batch(gsa_ctx* ctx, int mode, int npairs, const gsa_pair_dev* pairs,
                 return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
             ctx->xdone_cap = cap;
         }
-        if (fused)
         {
             a.xpair = fused->xa->pairs;
             a.xsched = fused->xa->sched;
@@ -667,7 +665,7 @@ int enqueue_full_twopass(gsa_ctx* ctx, int npairs, const gsa_pair_dev* pairs, co
     const int ns = env_int("GSA_KROW_NS", (npairs > 1 && !fitsChip) ? 8 : 4) == 8 ? 8 : 4;  // as enqueue_batch
     // fused: (4, 4) tickets under 8-wave workgroups, (8, 4) under 12
     const int fusedW = ns == 4 ? gsa::kExpFusedWaves : gsa::kExpFusedWavesBatch;
-    const int xWaves = fused ? fusedW : xGrid > 0 && (xw == 8 || xw == 12) ? xw : gsa::kExpWaves;
+    const int xWaves = fused ? fusedW : (xw == 8 || (xGrid > 0 && xw == 12)) ? xw : gsa::kExpWaves;
     // tiles per wave per expansion task (GSA_EXPAND_MT, 1..16; default 1)
     const int xmt = std::min(16, std::max(1, env_int("GSA_EXPAND_MT", 1)));
     std::vector<gsa_pair_dev> p1((size_t)npairs);

@@ -62,9 +62,9 @@ struct ExpandArgs
 };
 
 size_t expand_lds_bytes(int substsz, int waves);
-// one workgroup per task (waves = kExpWaves); or, grid > 0, `grid` persistent workgroups of
+// one workgroup of `waves` (8, 16) waves per task; or, grid > 0, `grid` persistent workgroups of
 // `waves` (8, 12, 16) waves claiming tasks from a.counter.  rowChunks of every pair must be counted
-// in chunks of waves x kExpRows rows.  Pair arrays in device memory.
+// in chunks of waves x kExpRows x mt rows.  Pair arrays in device memory.
 hipError_t launch_expand(const ExpandArgs& a, hipStream_t stream, int waves = kExpWaves, int grid = 0);
 
 }  // namespace gsa

@@ -29,7 +29,9 @@ namespace {
 
 using namespace xdev;
 
-__global__ void __launch_bounds__(64 * kExpWaves, 4) nw_expand_kernel(ExpandArgs a)
+// one workgroup per task: 16 waves (one workgroup per CU: 102 KB of LDS) or 8 (two per CU)
+template <int WAVES>
+__global__ void __launch_bounds__(64 * WAVES, 4) nw_expand_kernel(ExpandArgs a)
 {
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
@@ -54,12 +56,24 @@ __global__ void __launch_bounds__(64 * kExpWaves, 4) nw_expand_kernel(ExpandArgs
     }
     const ExpandPair d = ex_desc(a.pairs + lo);
     if (tt < 0) tt = task - d.taskBase;
-    ex_task<kExpWaves>(a, d, tt, w, lane);
+    ex_task<WAVES>(a, d, tt, w, lane);
+}
+
+template <int WAVES>
+hipError_t launch_pertask(const ExpandArgs& a, hipStream_t stream)
+{
+    const size_t lds = expand_lds_bytes(a.substsz, WAVES);
+    auto kern = nw_expand_kernel<WAVES>;
+    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+    if ((e = record_foot((const void*)kern, lds, 64 * WAVES, a.nTasks)) != hipSuccess) return e;
+    hipLaunchKernelGGL(kern, dim3(a.nTasks), dim3(64 * WAVES), lds, stream, a);
+    return hipGetLastError();
 }
 
 // persistent: `gridDim.x` workgroups claim tasks in schedule order until none is left
 template <int WAVES>
-__global__ void __launch_bounds__(64 * WAVES) nw_expand_persist_kernel(ExpandArgs a)
+__global__ void __launch_bounds__(64 * WAVES, 4) nw_expand_persist_kernel(ExpandArgs a)
 {
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
@@ -122,13 +136,7 @@ hipError_t launch_expand(const ExpandArgs& a, hipStream_t stream, int waves, int
                : waves == 12 ? launch_persist<12>(a, stream, grid)
                              : launch_persist<16>(a, stream, grid);
     }
-    if (waves != kExpWaves) return hipErrorInvalidValue;
-    const size_t lds = expand_lds_bytes(a.substsz, kExpWaves);
-    hipError_t e = hipFuncSetAttribute((const void*)nw_expand_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return e;
-    if ((e = record_foot((const void*)nw_expand_kernel, lds, 64 * kExpWaves, a.nTasks)) != hipSuccess) return e;
-    hipLaunchKernelGGL(nw_expand_kernel, dim3(a.nTasks), dim3(64 * kExpWaves), lds, stream, a);
-    return hipGetLastError();
+    return waves == 8 ? launch_pertask<8>(a, stream) : waves == 16 ? launch_pertask<16>(a, stream) : hipErrorInvalidValue;
 }
 
 }  // namespace gsa

@@ -42,14 +42,17 @@ struct ExLds
 {
     uint32_t sub, q, top, gfill;
 };
-// LDS of a workgroup of `waves` tile waves: subT, the column profile, one top row per wave, a row of g
+// LDS of a workgroup of `waves` tile waves: the column profile; subT, which only the profile build
+// reads, overlaid by one top row per wave; a row of g.  (79.9 KB for 8 waves and 25 letters: two
+// workgroups per CU)
 __host__ __device__ inline ExLds ex_layout(int substsz, int waves)
 {
     ExLds L;
-    L.sub = 0;
-    L.q = (uint32_t)substsz * kSubRow * 4u;
-    L.top = L.q + (uint32_t)substsz * kQS * 4u;
-    L.gfill = L.top + (uint32_t)waves * kTopS * 4u;
+    L.q = 0;
+    L.sub = (uint32_t)substsz * kQS * 4u;
+    L.top = L.sub;
+    const uint32_t subB = (uint32_t)substsz * kSubRow * 4u, topB = (uint32_t)waves * kTopS * 4u;
+    L.gfill = L.top + (subB > topB ? subB : topB);
     return L;
 }
 

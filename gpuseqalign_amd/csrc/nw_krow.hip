@@ -346,15 +346,10 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
     // mlsppt: tile columns [0, ptPend) captured, to be published once their stores are acknowledged
     // (at the next capture block, or at the strip's end); header stores are then system-scope
     constexpr bool pt = PT == 1;
-    constexpr bool fx = PT == 3;  // fused: publish every boundary to a.xdone (agent scope)
+    // fused: every boundary, in LDS (kFCap + 4w) for the publisher wave (kr_publisher): header
+    // columns of boundaries < n and row 64m columns < (n - 1) tBx stored and acknowledged (kBig: all)
+    constexpr bool fx = PT == 3;
     int ptPend = 0;
-    // fused: this strip's progress word, epoch << 32 | n: header columns of boundaries < n and row
-    // 64m columns < (n - 1) tBx stored and acknowledged (kXDone: all)
-    auto fx_publish = [&](unsigned n) {
-        if (lane == 0)
-            __hip_atomic_store(a.xdone + (size_t)tk * NS + w, ((unsigned long long)a.epoch << 32) | n, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-    };
 
     // One body for blocks with and without a header-column capture (cap, uniform): separate
     // bodies get different register assignments and ~100 v_mov per block to reconcile them.
@@ -435,8 +430,8 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
                 // the previous boundary's stores were issued >= 13 blocks ago, and every block since
                 // has issued 4 row stores: all but the last 16 vector-memory operations complete
                 // covers them (vmcnt retires in order) without waiting for this block's
-                if (!(a.xknob & 8)) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // (8: probe only)
-                fx_publish((unsigned)ptPend);
+                asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+                flag_st(L.flags + kFCap + 4u * (uint32_t)w, ptPend);
                 ptPend = 0;
             }
             // lanes 16m .. 16m+15 (m = b - nbb) hold column bc at step lane & 15: 16 -> 1 by its
@@ -497,7 +492,6 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
     using T = std::integral_constant<bool, true>;
     using F = std::integral_constant<bool, false>;
     constexpr int kRampBlocks = 64 / kBlk;  // columns <= 0 occur only in the first 64 steps
-    if (fx && a.stamps && lane == 0) a.stamps[2 * ((size_t)tk * NS + w)] = __builtin_amdgcn_s_memrealtime();
     int b = 0;
     for (; b < kRampBlocks; b += 2)
     {
@@ -518,8 +512,7 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
     if (fx)
     {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        fx_publish(kXDone);
-        if (a.stamps && lane == 0) a.stamps[2 * ((size_t)tk * NS + w) + 1] = __builtin_amdgcn_s_memrealtime();
+        flag_st(L.flags + kFCap + 4u * (uint32_t)w, kBig);
     }
 }
 
@@ -904,6 +897,54 @@ __device__ __forceinline__ void kr_drain(const StripArgs& a, const KrLds& L, int
                 }
                 __builtin_amdgcn_s_sleep(1);
             }
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// publisher wave of the fused fill (a wave the pass-1 roles leave idle): forwards the strips'
+// progress words (kFCap + 4s, written by each strip after its stores are acknowledged) to the
+// ticket's global words a.xdone[tk NS + s] = epoch << 32 | n (kXDone once the strip has finished),
+// so the strips themselves carry no global publication
+// ------------------------------------------------------------------------------------
+template <int NS>
+__device__ __forceinline__ void kr_publisher(const StripArgs& a, const KrLds& L, int tk, int lane)
+{
+    int pub[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) pub[s] = 0;
+    unsigned long long* const words = a.xdone + (size_t)tk * NS;
+    const unsigned long long ep = (unsigned long long)a.epoch << 32;
+    uint64_t last = __builtin_amdgcn_s_memrealtime();
+    unsigned idle = 0;
+    for (;;)
+    {
+        bool moved = false, all = true;
+#pragma unroll
+        for (int s = 0; s < NS; ++s)
+        {
+            const int v = flag_ld(L.flags + kFCap + 4u * (uint32_t)s);
+            if (v != pub[s])
+            {
+                if (lane == 0)
+                    __hip_atomic_store(words + s, ep | (v == kBig ? kXDone : (unsigned)v), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+                pub[s] = v;
+                moved = true;
+            }
+            all = all && v == kBig;
+        }
+        if (all) return;
+        if (moved)
+            last = __builtin_amdgcn_s_memrealtime();
+        else
+        {
+            if (__builtin_amdgcn_s_memrealtime() - last > a.spin || ((++idle & 63) == 0 && err_set(a)))
+            {
+                atomicOr(a.err, 1u);
+                return;
+            }
+            __builtin_amdgcn_s_sleep(4);
         }
     }
 }
@@ -1750,7 +1791,6 @@ hipError_t launch_krow_score(const StripArgs& a, int mode, int grid, hipStream_t
 // (8, 4) for batches
 hipError_t launch_krow_fill_xr(const StripArgs& a, int ns, int grid, hipStream_t stream)
 {
-    if (ns == 4 && a.xdone) return launch_kr<4, 4, 1024, 3>(a, grid, stream);  // PROBE
     return ns == 8 ? launch_kr<8, 4, 1024, 2>(a, grid, stream) : launch_kr<4, 4, 1024, 2>(a, grid, stream);
 }
 
@@ -1778,7 +1818,7 @@ template <int NS, int W, bool Q8>
 __global__ void __launch_bounds__(64 * W) nw_full_fused_kernel(StripArgs a)
 {
     constexpr int K = 4, LW = 1024;
-    static_assert(kr_waves<NS>() <= W, "the pass-1 roles fit the workgroup");
+    static_assert(kr_waves<NS>() < W, "the pass-1 roles and the publisher fit the workgroup");
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     const KrLds L = kr_layout(NS, LW, a.substsz, Q8);
@@ -1856,7 +1896,9 @@ __global__ void __launch_bounds__(64 * W) nw_full_fused_kernel(StripArgs a)
         pa.rows64 = d.rows64;
         pa.rpitch = d.rpitch;
         pa.xdone = a.xdone + (size_t)d.ticketBase * NS;  // the pair's strip words
-        if (a.stamps) pa.stamps = a.stamps + 2 * (size_t)d.ticketBase * NS;
+        // (stamps: the ticket's start, and each strip's end -- the strips of a pair sweep the same
+        // columns at the same pace, so their ends are spaced by the wavefront's lag)
+        unsigned long long* const sst = a.stamps ? a.stamps + 2 * ((size_t)d.ticketBase + tk) * NS : nullptr;
         if (threadIdx.x < 32) lds_st(L.flags + 4u * threadIdx.x, 0);
         if (threadIdx.x >= kFCap / 4 && threadIdx.x < kFCap / 4 + 8) lds_st(L.flags + 4u * threadIdx.x, 0);
         __syncthreads();
@@ -1866,11 +1908,15 @@ __global__ void __launch_bounds__(64 * W) nw_full_fused_kernel(StripArgs a)
             kr_loader<NS, K, LW, kr_split<NS>() ? 1 : 0, Q8>(pa, L, tk, lane);
         else if (kr_split<NS>() && w == NS + 2)
             kr_loader<NS, K, LW, 2, Q8>(pa, L, tk, lane);
+        else if (w == kr_waves<NS>())
+            kr_publisher<NS>(pa, L, tk, lane);
         else if (w < NS)
         {
+            if (sst && lane == 0) sst[2 * w] = __builtin_amdgcn_s_memrealtime();
             __builtin_amdgcn_s_setprio(3);
             kr_strip<NS, K, LW, 3, Q8>(pa, L, tk, w, lane);
             __builtin_amdgcn_s_setprio(0);
+            if (sst && lane == 0) sst[2 * w + 1] = __builtin_amdgcn_s_memrealtime();
         }
     }
     // pass 2: task tt of a pair is tile column jT of row chunk rc (cm = W xmt tiles of 64 rows).  Its
@@ -1919,7 +1965,7 @@ __global__ void __launch_bounds__(64 * W) nw_full_fused_kernel(StripArgs a)
             const unsigned long long* words = a.xdone + xd.p1Strip0;
             bool ok = true;
             uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-            for (int s = (a.xknob & 4) ? s1 + 1 : rc > 0 ? (cm * rc - 1) / 4 : 0; s <= s1 && ok;)  // (4: probe, no wait)
+            for (int s = rc > 0 ? (cm * rc - 1) / 4 : 0; s <= s1 && ok;)
             {
                 const unsigned long long v = __hip_atomic_load(words + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if ((unsigned)(v >> 32) == a.epoch && (unsigned)v >= pneed)

@@ -115,8 +115,8 @@ struct StripArgs
     unsigned* xcounter;
     unsigned long long* xdone;
     // measurement aid (GSA_STAMPS=1, gsa_debug_stamps): s_memrealtime stamps of the fused fill,
-    // [start, end] per pass-1 strip (global strip index), then [claimed, ready, done] per expansion
-    // task; null otherwise
+    // [start, end] per pass-1 strip (global strip index; start = the ticket's start, before the
+    // strip's first wait), then [claimed, ready, done] per expansion task; null otherwise
     unsigned long long* stamps;
 };
 

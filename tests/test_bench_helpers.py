@@ -34,11 +34,15 @@ def test_traffic_file_matches_the_bench_kernel():
     assert tj["hbm_bytes_per_launch"] == pytest.approx(sum(alg.values()), rel=0.05)
 
 
-def test_full_batch_write_ratio():
-    r = bench.pmc_write_ratio(64, "gsa::nw_lane_kernel<4,false>")
-    assert r is not None and 1.0 <= r < 1.5
-    assert bench.pmc_write_ratio(32, "gsa::nw_lane_kernel<4,false>") is None
-    assert bench.pmc_write_ratio(64, "gsa::nw_krow_kernel<4>") is None
+def test_full_batch_write_ratio(monkeypatch):
+    """The full_batch field's PMC write ratio comes from the round-4 profile of the kernels the
+    batch runs by default (the two-pass fill in two launches), and only for them."""
+    for k in ("GSA_FULL_KERNEL", "GSA_FULL_FUSED"):
+        monkeypatch.delenv(k, raising=False)
+    r = bench.pmc_write_ratio(64, bench.full_kernel_name(False))
+    assert r is not None and 1.0 <= r <= 1.05
+    assert bench.pmc_write_ratio(32, bench.full_kernel_name(False)) is None
+    assert bench.pmc_write_ratio(64, "gsa::nw_lane_kernel<4,false,true>") is None
 
 
 def test_rehearsal_fields(monkeypatch):

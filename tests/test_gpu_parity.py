@@ -312,6 +312,7 @@ def test_twopass_tables_and_batches(engine, golden, fused, ns, name, gapo, monke
         monkeypatch.setenv("GSA_FUSED_P1", "3")
     else:
         monkeypatch.setenv("GSA_EXPAND_MT", "3")  # 3 tiles per wave per expansion task
+        monkeypatch.setenv("GSA_EXPAND_WAVES", "8")  # (two launches: 8-wave expansion workgroups)
     sub = golden.subst_data.matrix(name)
     pairs = [random_pair(r, c, 7 * r + c, alphabet=25) for r, c in ((2100, 900), (1, 5), (700, 2500), (64, 64), (4097, 300))]
     dev = torch.device("cuda:0")

@@ -43,13 +43,13 @@ def main():
     nstrips = tickets * ns
     out = []
     for st in runs:
-        strips = st[:2 * nstrips].reshape(nstrips, 2)
+        strips = st[:2 * nstrips].reshape(nstrips, 2)  # [ticket start, strip end]
         tasks = st[2 * nstrips:].reshape(-1, 3)
         t0 = min(strips[:, 0].min(), tasks[tasks[:, 0] > 0, 0].min())
         cyc = 24.0
         start = (strips[:, 0] - t0) * cyc
         end = (strips[:, 1] - t0) * cyc
-        lag = np.diff(start)
+        lag = np.diff(end)  # strips end in wavefront order, spaced by the lag
         intra = [lag[i - 1] for i in range(1, nstrips) if i % ns]
         inter = [lag[i - 1] for i in range(1, nstrips) if i % ns == 0]
         wait = (tasks[:, 1] - tasks[:, 0]) * cyc
@@ -62,7 +62,7 @@ def main():
             "strip_lag_inter_cycles_median": round(float(np.median(inter)), 0),
             "strip_lag_inter_cycles": [round(float(v), 0) for v in inter],
             "lag_per_256_rows_cycles_mean": round(float(np.mean(lag)), 0),
-            "strip_duration_cycles_median": round(float(np.median(end - start)), 0),
+            "strip_duration_from_ticket_start_cycles_median": round(float(np.median(end - start)), 0),
             "task_wait_cycles_median": round(float(np.median(wait)), 0),
             "task_duration_cycles_median": round(float(np.median(dur)), 0),
             "tasks": int(len(tasks)), "strips": int(nstrips),

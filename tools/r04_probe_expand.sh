@@ -4,9 +4,5 @@
 set -e
 mkdir -p gpurun_out
 timeout -k 10 600 python -u tools/full_ab.py --no-10k --rounds 1 --batch 64 --variants \
-  "GSA_EXPAND_GRID=0" "GSA_EXPAND_GRID=256,GSA_EXPAND_WAVES=16" "GSA_EXPAND_GRID=256,GSA_EXPAND_WAVES=12" \
-  "GSA_EXPAND_GRID=256,GSA_EXPAND_WAVES=8" "GSA_EXPAND_GRID=128,GSA_EXPAND_WAVES=16" "GSA_EXPAND_MT=4" \
-  "GSA_EXPAND_GRID=256,GSA_EXPAND_WAVES=16,GSA_EXPAND_MT=4" "GSA_FULL_FUSED=2,GSA_FUSED_P1=128,GSA_EXPAND_MT=4" \
-  "GSA_FULL_FUSED=2,GSA_FUSED_P1=64" "GSA_FULL_FUSED=2,GSA_FUSED_P1=96" "GSA_FULL_FUSED=2,GSA_FUSED_P1=128" \
-  "GSA_FULL_FUSED=2,GSA_FUSED_P1=192" "GSA_FULL_FUSED=2,GSA_FUSED_P1=256" "GSA_EXPAND_GRID=0" > gpurun_out/r04_x1.log 2>&1
-cat gpurun_out/r04_x1.log
+  "GSA_EXPAND_GRID=0" "GSA_EXPAND_WAVES=8" "GSA_EXPAND_GRID=0" "GSA_EXPAND_WAVES=8" "GSA_EXPAND_GRID=512,GSA_EXPAND_WAVES=8" "GSA_EXPAND_WAVES=8,GSA_EXPAND_MT=2" "GSA_EXPAND_GRID=0" "GSA_EXPAND_WAVES=8" > gpurun_out/r04_x2.log 2>&1
+cat gpurun_out/r04_x2.log
