@@ -346,10 +346,17 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
     // mlsppt: tile columns [0, ptPend) captured, to be published once their stores are acknowledged
     // (at the next capture block, or at the strip's end); header stores are then system-scope
     constexpr bool pt = PT == 1;
-    // fused: every boundary, in LDS (kFCap + 4w) for the publisher wave (kr_publisher): header
-    // columns of boundaries < n and row 64m columns < (n - 1) tBx stored and acknowledged (kBig: all)
+    // fused: this strip's progress word, epoch << 32 | n: header columns of boundaries < n and row
+    // 64m columns < (n - 1) tBx stored and acknowledged (kXDone: all).  (A publisher wave forwarding
+    // LDS words instead costs the strip on its SIMD more than the store: 10k 0.668 -> 0.683 ms.)
     constexpr bool fx = PT == 3;
     int ptPend = 0;
+    unsigned long long* const xword = fx ? a.xdone + (size_t)tk * NS + w : nullptr;
+    auto fx_publish = [&](unsigned n) {
+        if constexpr (PT == 3)
+            if (lane == 0)
+                __hip_atomic_store(xword, ((unsigned long long)a.epoch << 32) | n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
 
     // One body for blocks with and without a header-column capture (cap, uniform): separate
     // bodies get different register assignments and ~100 v_mov per block to reconcile them.
@@ -431,7 +438,7 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
                 // has issued 4 row stores: all but the last 16 vector-memory operations complete
                 // covers them (vmcnt retires in order) without waiting for this block's
                 asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-                flag_st(L.flags + kFCap + 4u * (uint32_t)w, ptPend);
+                fx_publish((unsigned)ptPend);
                 ptPend = 0;
             }
             // lanes 16m .. 16m+15 (m = b - nbb) hold column bc at step lane & 15: 16 -> 1 by its
@@ -512,7 +519,7 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
     if (fx)
     {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        flag_st(L.flags + kFCap + 4u * (uint32_t)w, kBig);
+        fx_publish(kXDone);
     }
 }
 
@@ -897,54 +904,6 @@ __device__ __forceinline__ void kr_drain(const StripArgs& a, const KrLds& L, int
                 }
                 __builtin_amdgcn_s_sleep(1);
             }
-        }
-    }
-}
-
-// ------------------------------------------------------------------------------------
-// publisher wave of the fused fill (a wave the pass-1 roles leave idle): forwards the strips'
-// progress words (kFCap + 4s, written by each strip after its stores are acknowledged) to the
-// ticket's global words a.xdone[tk NS + s] = epoch << 32 | n (kXDone once the strip has finished),
-// so the strips themselves carry no global publication
-// ------------------------------------------------------------------------------------
-template <int NS>
-__device__ __forceinline__ void kr_publisher(const StripArgs& a, const KrLds& L, int tk, int lane)
-{
-    int pub[NS];
-#pragma unroll
-    for (int s = 0; s < NS; ++s) pub[s] = 0;
-    unsigned long long* const words = a.xdone + (size_t)tk * NS;
-    const unsigned long long ep = (unsigned long long)a.epoch << 32;
-    uint64_t last = __builtin_amdgcn_s_memrealtime();
-    unsigned idle = 0;
-    for (;;)
-    {
-        bool moved = false, all = true;
-#pragma unroll
-        for (int s = 0; s < NS; ++s)
-        {
-            const int v = flag_ld(L.flags + kFCap + 4u * (uint32_t)s);
-            if (v != pub[s])
-            {
-                if (lane == 0)
-                    __hip_atomic_store(words + s, ep | (v == kBig ? kXDone : (unsigned)v), __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-                pub[s] = v;
-                moved = true;
-            }
-            all = all && v == kBig;
-        }
-        if (all) return;
-        if (moved)
-            last = __builtin_amdgcn_s_memrealtime();
-        else
-        {
-            if (__builtin_amdgcn_s_memrealtime() - last > a.spin || ((++idle & 63) == 0 && err_set(a)))
-            {
-                atomicOr(a.err, 1u);
-                return;
-            }
-            __builtin_amdgcn_s_sleep(4);
         }
     }
 }
@@ -1818,7 +1777,7 @@ template <int NS, int W, bool Q8>
 __global__ void __launch_bounds__(64 * W) nw_full_fused_kernel(StripArgs a)
 {
     constexpr int K = 4, LW = 1024;
-    static_assert(kr_waves<NS>() < W, "the pass-1 roles and the publisher fit the workgroup");
+    static_assert(kr_waves<NS>() <= W, "the pass-1 roles fit the workgroup");
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     const KrLds L = kr_layout(NS, LW, a.substsz, Q8);
@@ -1908,8 +1867,6 @@ __global__ void __launch_bounds__(64 * W) nw_full_fused_kernel(StripArgs a)
             kr_loader<NS, K, LW, kr_split<NS>() ? 1 : 0, Q8>(pa, L, tk, lane);
         else if (kr_split<NS>() && w == NS + 2)
             kr_loader<NS, K, LW, 2, Q8>(pa, L, tk, lane);
-        else if (w == kr_waves<NS>())
-            kr_publisher<NS>(pa, L, tk, lane);
         else if (w < NS)
         {
             if (sst && lane == 0) sst[2 * w] = __builtin_amdgcn_s_memrealtime();
