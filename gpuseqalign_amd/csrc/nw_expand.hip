@@ -77,7 +77,7 @@ __global__ void __launch_bounds__(64 * WAVES, 4) nw_expand_persist_kernel(Expand
 {
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
-    const uint32_t word = ex_layout(a.substsz, WAVES).gfill + 64u;  // past the row of g
+    const uint32_t word = ex_word(a.substsz, WAVES);
     for (;;)
     {
         __syncthreads();

@@ -237,10 +237,10 @@ __device__ __forceinline__ void ex_tile(const ExpandArgs& a, const ExpandPair& d
 
 
 // one task: the tile column jT of the `WAVES * kExpRows * a.mt`-row chunk rc of pair d (all threads
-// of the workgroup): subT and the column profile into LDS, the matrix headers the task owns, a.mt
-// tiles per wave
+// of the workgroup).  ex_prep: subT and the column profile into LDS, the matrix headers the task
+// owns -- none of it reads pass-1 output; ex_tiles: a.mt tiles per wave
 template <int WAVES>
-__device__ __forceinline__ void ex_task(const ExpandArgs& a, const ExpandPair& d, int tt, int w, int lane)
+__device__ __forceinline__ void ex_prep(const ExpandArgs& a, const ExpandPair& d, int tt)
 {
     const ExLds L = ex_layout(a.substsz, WAVES);
     const int jT = tt % d.colTiles, rc = tt / d.colTiles;
@@ -276,14 +276,33 @@ __device__ __forceinline__ void ex_task(const ExpandArgs& a, const ExpandPair& d
         for (int c = cb + 1 + (int)threadIdx.x; c <= min(d.C, cb + kExpTW); c += 64 * WAVES) G(d.score)[c] = c * a.g;
         if (jT == 0 && threadIdx.x == 0) G(d.score)[0] = 0;
     }
-    // the wave's tiles: rows 64 (w + WAVES i) of the chunk, i < mt (no barrier between them: each
-    // wave has its own top-row buffer)
+}
+
+// the tiles of task tt: wave w's are rows 64 (w + WAVES i) of the chunk, i < mt (no barrier between
+// them: each wave has its own top-row buffer).  After ex_prep and a barrier.
+template <int WAVES>
+__device__ __forceinline__ void ex_tiles(const ExpandArgs& a, const ExpandPair& d, int tt, int w, int lane)
+{
+    const ExLds L = ex_layout(a.substsz, WAVES);
+    const int jT = tt % d.colTiles, rc = tt / d.colTiles;
+    const int cb = jT * kExpTW;
+    const int kChunk = WAVES * kExpRows * a.mt;
     for (int i = 0; i < a.mt; ++i)
     {
         const int r0 = rc * kChunk + kExpRows * (w + WAVES * i) + 1;
         if (r0 <= d.R && cb < d.C && !(a.knob & 1)) ex_tile(a, d, L, w, lane, jT, r0);
     }
 }
+
+template <int WAVES>
+__device__ __forceinline__ void ex_task(const ExpandArgs& a, const ExpandPair& d, int tt, int w, int lane)
+{
+    ex_prep<WAVES>(a, d, tt);
+    ex_tiles<WAVES>(a, d, tt, w, lane);
+}
+
+// a word of the expansion's LDS that ex_prep / ex_tiles never write (expand_lds_bytes counts it)
+__host__ __device__ inline uint32_t ex_word(int substsz, int waves) { return ex_layout(substsz, waves).gfill + 64u; }
 
 }  // namespace xdev
 }  // namespace gsa

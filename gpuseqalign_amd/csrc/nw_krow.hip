@@ -1880,13 +1880,16 @@ __global__ void __launch_bounds__(64 * W) nw_full_fused_kernel(StripArgs a)
     // waves read rows 64m, m = cm rc .. cm rc + cm - 1, at columns < need, and (jT > 0) the header
     // column of boundary 2 jT for rows 64 cm rc + 1 .. 64 cm (rc + 1): the pair's strips
     // (cm rc - 1) / 4 .. (cm (rc + 1) - 1) / 4 (256 rows each), words >= pneed
+    // (the task's profile is built before its wait: it reads no pass-1 output; the claim and ready
+    // words live where the expansion's LDS never writes)
     const ExpandArgs xa {a.subst, a.substsz, a.g, a.xpair, a.nPairs, a.xTasks, a.xsched, a.xknob, nullptr, a.xmt};
+    const uint32_t xw = xdev::ex_word(a.substsz, W);
     for (;;)
     {
         __syncthreads();
-        if (threadIdx.x == 0) lds_st(word, err_set(a) ? a.xTasks : (int)atomicAdd(a.xcounter, 1u));
+        if (threadIdx.x == 0) lds_st(xw, err_set(a) ? a.xTasks : (int)atomicAdd(a.xcounter, 1u));
         __syncthreads();
-        const int task = __builtin_amdgcn_readfirstlane(lds_ld(word));
+        const int task = __builtin_amdgcn_readfirstlane(lds_ld(xw));
         if (task >= a.xTasks) break;
         int lo = 0, tt = -1;
         if (a.xsched)
@@ -1908,6 +1911,7 @@ __global__ void __launch_bounds__(64 * W) nw_full_fused_kernel(StripArgs a)
         }
         const ExpandPair xd = xdev::ex_desc(a.xpair + lo);
         if (tt < 0) tt = task - xd.taskBase;
+        xdev::ex_prep<W>(xa, xd, tt);
         unsigned long long* tstamp = a.stamps ? a.stamps + 2 * (size_t)a.nTicketsTotal * NS + 3 * (size_t)task : nullptr;
         if (threadIdx.x == 0)
         {
@@ -1940,14 +1944,12 @@ __global__ void __launch_bounds__(64 * W) nw_full_fused_kernel(StripArgs a)
             }
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            lds_st(word, ok ? 0 : 1);
+            lds_st(xw + 4u, ok ? 0 : 1);
             if (tstamp) tstamp[1] = __builtin_amdgcn_s_memrealtime();
         }
         __syncthreads();
-        const int stop = __builtin_amdgcn_readfirstlane(lds_ld(word));
-        __syncthreads();  // (the task's LDS may overlap the word)
-        if (stop) break;
-        xdev::ex_task<W>(xa, xd, tt, w, lane);
+        if (__builtin_amdgcn_readfirstlane(lds_ld(xw + 4u))) break;
+        xdev::ex_tiles<W>(xa, xd, tt, w, lane);
         if (tstamp && threadIdx.x == 0) tstamp[2] = __builtin_amdgcn_s_memrealtime();  // (wave 0's tile)
     }
 }
