@@ -705,6 +705,10 @@ int enqueue_full_twopass(gsa_ctx* ctx, int npairs, const gsa_pair_dev* pairs, co
         e.tcols = geom.tileHdrMatCols;
         // (an empty sequence still has its header row or column: at least one task per dimension)
         e.colTiles = std::max(1, (e.C + gsa::kExpTW - 1) / gsa::kExpTW);
+        // a last tile column wider than one pass-1 tile is split at its boundary: the pair's last
+        // tiles, which wait for the end of pass 1 in a fused fill, are then at most kExpHB wide
+        e.lastSplit = e.C - (e.colTiles - 1) * gsa::kExpTW > gsa::kExpHB ? 1 : 0;
+        e.colTiles += e.lastSplit;
         e.rowChunks = std::max(1, (e.R + xWaves * gsa::kExpRows * xmt - 1) / (xWaves * gsa::kExpRows * xmt));
         e.taskBase = (int)tasks;
         tasks += (long long)e.colTiles * e.rowChunks;

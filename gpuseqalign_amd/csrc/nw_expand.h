@@ -41,7 +41,23 @@ struct ExpandPair
     int taskBase;       // first workgroup task of this pair (colTiles * rowChunks tasks)
     int p1Strip0;       // fused fill: the pair's first pass-1 strip word (ticketBase x ns)
     int p1Strips;       // ... and its strip count (tickets x ns)
+    // the last kExpTW tile column is wider than kExpHB: it is split at its pass-1 boundary into
+    // two tile columns (colTiles counts both), so the pair's last tiles are at most kExpHB wide
+    int lastSplit;
+    int pad;
 };
+
+// tile column jT of a pair: left boundary column and width
+__host__ __device__ inline int ex_cb(const ExpandPair& d, int jT)
+{
+    return (d.lastSplit && jT == d.colTiles - 1) ? (jT - 1) * kExpTW + kExpHB : jT * kExpTW;
+}
+__host__ __device__ inline int ex_cols(const ExpandPair& d, int jT)
+{
+    const int cb = ex_cb(d, jT);
+    const int w = (d.lastSplit && jT == d.colTiles - 2) ? kExpHB : kExpTW;
+    return d.C - cb < w ? d.C - cb : w;
+}
 
 struct ExpandArgs
 {

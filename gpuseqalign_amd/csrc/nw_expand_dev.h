@@ -72,23 +72,22 @@ __device__ __forceinline__ ExpandPair ex_desc(const ExpandPair* p)
 
 // one 64-row x kExpTW-column tile of the full matrix, one row per lane
 __device__ __forceinline__ void ex_tile(const ExpandArgs& a, const ExpandPair& d, const ExLds& L, int w, int lane,
-                                        int jT, int r0)
+                                        int cb, int cols, int r0)
 {
     const int g = a.g;
-    const int cb = jT * kExpTW;                    // left boundary column of the tile
-    const int cols = min(kExpTW, d.C - cb);        // columns cb+1 .. cb+cols
+    // left boundary column cb of the tile, columns cb+1 .. cb+cols (ex_cb, ex_cols)
     const int r = r0 + lane;
     int y = (r <= d.R) ? G(d.seqY)[r] : 0;
     y = ((unsigned)y < (unsigned)a.substsz) ? y : 0;
     // left boundary H(r, cb): column 0, or the pass-1 header column of its tile (iT, cb / kExpHB)
     // (element r - iT tBy; rows up to the last tile row's end are computed there, padding included)
     int lb;
-    if (jT == 0)
+    if (cb == 0)
         lb = r * g;
     else
     {
         const int iT = (r - 1) / kSparseTileBy;
-        lb = G(d.hcol)[((size_t)iT * (size_t)d.tcols + (size_t)jT * (kExpTW / kExpHB)) * (size_t)(kSparseTileBy + 1) +
+        lb = G(d.hcol)[((size_t)iT * (size_t)d.tcols + (size_t)(cb / kExpHB)) * (size_t)(kSparseTileBy + 1) +
                        (size_t)(r - iT * kSparseTileBy)];
     }
     // top row H(r0 - 1, cb .. cb + kExpTW) + g into LDS: row 0, or pass-1 row 64m (shifted values)
@@ -211,7 +210,7 @@ __device__ __forceinline__ void ex_tile(const ExpandArgs& a, const ExpandPair& d
                     const gptr<int> p = xbase + (size_t)k * 16u * (size_t)(d.ld - 1) + kBlk * b;
                     if (xc >= 1 && xc <= cols && xc + 3 <= ce)
                         *(gptr<int4a>)p = int4a {t[4 * k], t[4 * k + 1], t[4 * k + 2], t[4 * k + 3]};
-                    else if ((xc >= 1 && xc <= cols) || (jT == 0 && xc + 3 >= 1 && xc <= 0))
+                    else if ((xc >= 1 && xc <= cols) || (cb == 0 && xc + 3 >= 1 && xc <= 0))
                     {
 #pragma unroll
                         for (int e = 0; e < 4; ++e)
@@ -244,7 +243,7 @@ __device__ __forceinline__ void ex_prep(const ExpandArgs& a, const ExpandPair& d
 {
     const ExLds L = ex_layout(a.substsz, WAVES);
     const int jT = tt % d.colTiles, rc = tt / d.colTiles;
-    const int cb = jT * kExpTW;
+    const int cb = ex_cb(d, jT), cols = ex_cols(d, jT);
     for (int k = threadIdx.x; k < a.substsz * kSubRow; k += 64 * WAVES)
     {
         const int x = k / kSubRow, yy = k % kSubRow;
@@ -268,13 +267,13 @@ __device__ __forceinline__ void ex_prep(const ExpandArgs& a, const ExpandPair& d
     // the matrix headers H(i, 0) = i g, H(0, j) = j g: column 0 of the chunk's rows (first tile
     // column), row 0 of the tile's columns (first row chunk)
     const int kChunk = WAVES * kExpRows * a.mt;
-    if (jT == 0)
+    if (cb == 0)
         for (int r = rc * kChunk + 1 + (int)threadIdx.x; r <= min(d.R, rc * kChunk + kChunk); r += 64 * WAVES)
             G(d.score)[(size_t)r * (size_t)d.ld] = r * a.g;
     if (rc == 0)
     {
-        for (int c = cb + 1 + (int)threadIdx.x; c <= min(d.C, cb + kExpTW); c += 64 * WAVES) G(d.score)[c] = c * a.g;
-        if (jT == 0 && threadIdx.x == 0) G(d.score)[0] = 0;
+        for (int c = cb + 1 + (int)threadIdx.x; c <= cb + cols; c += 64 * WAVES) G(d.score)[c] = c * a.g;
+        if (cb == 0 && threadIdx.x == 0) G(d.score)[0] = 0;
     }
 }
 
@@ -285,12 +284,12 @@ __device__ __forceinline__ void ex_tiles(const ExpandArgs& a, const ExpandPair& 
 {
     const ExLds L = ex_layout(a.substsz, WAVES);
     const int jT = tt % d.colTiles, rc = tt / d.colTiles;
-    const int cb = jT * kExpTW;
+    const int cb = ex_cb(d, jT), cols = ex_cols(d, jT);
     const int kChunk = WAVES * kExpRows * a.mt;
     for (int i = 0; i < a.mt; ++i)
     {
         const int r0 = rc * kChunk + kExpRows * (w + WAVES * i) + 1;
-        if (r0 <= d.R && cb < d.C && !(a.knob & 1)) ex_tile(a, d, L, w, lane, jT, r0);
+        if (r0 <= d.R && cb < d.C && !(a.knob & 1)) ex_tile(a, d, L, w, lane, cb, cols, r0);
     }
 }
 

@@ -346,9 +346,10 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
     // mlsppt: tile columns [0, ptPend) captured, to be published once their stores are acknowledged
     // (at the next capture block, or at the strip's end); header stores are then system-scope
     constexpr bool pt = PT == 1;
-    // fused: this strip's progress word, epoch << 32 | n: header columns of boundaries < n and row
-    // 64m columns < (n - 1) tBx stored and acknowledged (kXDone: all).  (A publisher wave forwarding
-    // LDS words instead costs the strip on its SIMD more than the store: 10k 0.668 -> 0.683 ms.)
+    // fused: this strip's progress word, epoch << 32 | X: row 64m columns < X and the header columns
+    // of boundaries <= X stored and acknowledged (kXDone: all), published every 16 blocks.  (A
+    // publisher wave forwarding LDS words instead costs the strip on its SIMD more than the store:
+    // 10k 0.668 -> 0.683 ms.)
     constexpr bool fx = PT == 3;
     int ptPend = 0;
     unsigned long long* const xword = fx ? a.xdone + (size_t)tk * NS + w : nullptr;
@@ -423,6 +424,16 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
         // written behind the next block's halo reads: measured 1 % faster at 100k, slightly slower
         // per block)
         handoff(b);
+        if constexpr (fx && !RAMP)
+            if ((b & 15) == 15)
+            {
+                // every block issues >= 4 stores (its row-buffer segments), so all but the last 16
+                // vector-memory operations complete covers blocks <= b - 4: row 64m columns
+                // < 16 (b - 7) (block bb stores columns <= 16 (bb - 4) + 15 of its 4 rows) and the
+                // header columns captured by block b - 4 (boundaries <= 16 (b - 7))
+                asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+                fx_publish((unsigned)(kBlk * (b - 7)));
+            }
         if (CAP && cap)
         {
             if (pt && ptPend)
@@ -430,15 +441,6 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
                 // the previous boundary's stores, issued blocks ago, are acknowledged: publish them
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 flag_st(L.flags + kFCap + 4u * (uint32_t)w, ptPend);
-                ptPend = 0;
-            }
-            if (fx && ptPend)
-            {
-                // the previous boundary's stores were issued >= 13 blocks ago, and every block since
-                // has issued 4 row stores: all but the last 16 vector-memory operations complete
-                // covers them (vmcnt retires in order) without waiting for this block's
-                asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-                fx_publish((unsigned)ptPend);
                 ptPend = 0;
             }
             // lanes 16m .. 16m+15 (m = b - nbb) hold column bc at step lane & 15: 16 -> 1 by its
@@ -485,7 +487,6 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
                 ++jb;
                 hcolP += (size_t)(tBy + 1);
                 if (pt && (jb % a.ptChunk == 0 || jb == tcols)) ptPend = jb;
-                if (fx) ptPend = jb;
             }
         }
         return true;
@@ -1879,7 +1880,7 @@ __global__ void __launch_bounds__(64 * W) nw_full_fused_kernel(StripArgs a)
     // pass 2: task tt of a pair is tile column jT of row chunk rc (cm = W xmt tiles of 64 rows).  Its
     // waves read rows 64m, m = cm rc .. cm rc + cm - 1, at columns < need, and (jT > 0) the header
     // column of boundary 2 jT for rows 64 cm rc + 1 .. 64 cm (rc + 1): the pair's strips
-    // (cm rc - 1) / 4 .. (cm (rc + 1) - 1) / 4 (256 rows each), words >= pneed
+    // (cm rc - 1) / 4 .. (cm (rc + 1) - 1) / 4 (256 rows each), words >= need
     // (the task's profile is built before its wait: it reads no pass-1 output; the claim and ready
     // words live where the expansion's LDS never writes)
     const ExpandArgs xa {a.subst, a.substsz, a.g, a.xpair, a.nPairs, a.xTasks, a.xsched, a.xknob, nullptr, a.xmt};
@@ -1917,10 +1918,8 @@ __global__ void __launch_bounds__(64 * W) nw_full_fused_kernel(StripArgs a)
         {
             if (tstamp) tstamp[0] = __builtin_amdgcn_s_memrealtime();
             const int jT = tt % xd.colTiles, rc = tt / xd.colTiles;
-            const int cb = jT * kExpTW;
-            const int need = min(cb + min(kExpTW, xd.C - cb) + 3, xd.C) + 1;
-            unsigned pneed = (unsigned)((need + kExpHB - 1) / kExpHB + 1);
-            if (pneed >= (unsigned)xd.tcols) pneed = kXDone;  // (a strip's last boundary is published at its end)
+            const int cb = ex_cb(xd, jT);
+            const unsigned need = (unsigned)(min(cb + ex_cols(xd, jT) + 3, xd.C) + 1);  // row-buffer columns < need
             const int cm = W * a.xmt;  // 64-row tiles per chunk
             const int s1 = min((cm * (rc + 1) - 1) / 4, xd.p1Strips - 1);
             const unsigned long long* words = a.xdone + xd.p1Strip0;
@@ -1929,7 +1928,7 @@ __global__ void __launch_bounds__(64 * W) nw_full_fused_kernel(StripArgs a)
             for (int s = rc > 0 ? (cm * rc - 1) / 4 : 0; s <= s1 && ok;)
             {
                 const unsigned long long v = __hip_atomic_load(words + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if ((unsigned)(v >> 32) == a.epoch && (unsigned)v >= pneed)
+                if ((unsigned)(v >> 32) == a.epoch && (unsigned)v >= need)
                 {
                     ++s;
                     t0 = __builtin_amdgcn_s_memrealtime();
