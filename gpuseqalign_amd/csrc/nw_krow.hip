@@ -1934,7 +1934,7 @@ __global__ void __launch_bounds__(64 * W) nw_full_fused_kernel(StripArgs a)
                     t0 = __builtin_amdgcn_s_memrealtime();
                     continue;
                 }
-                __builtin_amdgcn_s_sleep(2);
+                __builtin_amdgcn_s_sleep(2);  // (s_sleep 32 between polls: same time)
                 if (__builtin_amdgcn_s_memrealtime() - t0 > a.spin || err_set(a))
                 {
                     atomicOr(a.err, 1u);
