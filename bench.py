@@ -362,7 +362,10 @@ def score_kernel_name(go, ge, local, substsz=25):
     mname = (("kModeScoreSWL" if go == ge else "kModeScoreSW") if local else
              ("kModeScoreAGL" if go == ge else "kModeScoreAG"))
     krow = os.environ.get("GSA_SCORE_KERNEL", "") != "strip" and (not local or ge <= 0) and substsz <= 32
-    return (f"gsa::nw_kscore_kernel<{mode}> ({mname})" if krow else
+    # the int8-profile instance for linear modes (gsa_capi.hip score_ag_strip; GSA_KROW_Q8 0 / 2: never / always)
+    q8env = os.environ.get("GSA_KROW_Q8", "1")
+    q8 = q8env != "0" and (q8env == "2" or go == ge)
+    return (f"gsa::nw_kscore_kernel<{mode}, {'true' if q8 else 'false'}> ({mname})" if krow else
             f"gsa::nw_strip_kernel<4,{mode}> ({mname}, strip kernel)")
 
 

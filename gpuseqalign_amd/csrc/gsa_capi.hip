@@ -361,6 +361,13 @@ int score_ag_strip(gsa_ctx* ctx, const int32_t* seqY, int64_t R, const int32_t* 
     // the K-rows score kernel (nw_kscore.hip) unless GSA_SCORE_KERNEL=strip, or its LDS (a profile of
     // substsz rows) does not fit, or SW with ge > 0 (its per-row key offsets assume z grows along j)
     const bool krow = score_kernel_krow() && (!local || gape <= 0) && gsa::krow_score_lds_bytes(substsz) <= ctx->lds_max;
+    // linear modes read the int8 column profile where its LDS fits (the instance declines a table
+    // outside int8 and the int16 instance behind it runs): 50k SW-LG 3.87 -> 3.82 ms; the affine step
+    // is slower with it (NW-AG 4.20 -> 4.38 ms: the byte extraction costs more than the halved reads
+    // save there), so affine modes keep the int16 profile.  GSA_KROW_Q8=0 / 2: int16 / int8 always
+    const int q8env = env_int("GSA_KROW_Q8", 1);
+    a.q8 = (q8env != 0 && (q8env == 2 || gapo == gape) && gsa::krow_score_lds_bytes(substsz, true) <= (size_t)ctx->lds_max) ? 1 : 0;
+    a.q8flag = ctx->ctl + 2;
     if ((e = krow ? gsa::launch_krow_score(a, mode, grid, st) : gsa::launch_strip_fill(a, mode, grid, st)) != hipSuccess)
         return fail(ctx, e, GSA_ERROR_KERNEL_FAILURE);
     note_launch(ctx);

@@ -44,8 +44,9 @@ hipError_t launch_full_fused(const StripArgs& a, int ns, int waves, int grid, hi
 // Score-only NW / SW (modes kModeScoreAG/AGL/SW/SWL of nw_strip.h, same StripArgs contract as
 // launch_strip_fill for one pair: go, ge, gran + gran2, agResult, swBest, idxBits) on the K-rows
 // layout (nw_kscore.hip): 1024-row tickets, grid > 0 workgroups.  Every s - go - ge must lie in
-// (-32768, 32767] (error bit 2 otherwise); SW needs go < 0 and ge <= 0.
-size_t krow_score_lds_bytes(int substsz);
+// (-32768, 32767] (error bit 2 otherwise); SW needs go < 0 and ge <= 0.  a.q8 as launch_kr: the
+// int8-profile instance (values in [-127, 127]) with the int16 one behind it.
+size_t krow_score_lds_bytes(int substsz, bool q8 = false);
 hipError_t launch_krow_score(const StripArgs& a, int mode, int grid, hipStream_t stream);
 
 }  // namespace gsa

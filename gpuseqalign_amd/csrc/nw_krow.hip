@@ -1090,12 +1090,12 @@ struct KsLds
     uint32_t q, sub, ring, ring2, flags;
 };
 
-__host__ __device__ inline KsLds ks_layout(int substsz)
+__host__ __device__ inline KsLds ks_layout(int substsz, bool q8 = false)
 {
     constexpr int LW = 1024;
     KsLds L;
     L.q = 0;
-    L.sub = (kr_copy1(LW, substsz) + (uint32_t)substsz * kr_qrs(LW) + 16u) * 4u;
+    L.sub = kr_qdwords(LW, substsz, q8) * 4u;
     L.ring = L.sub + (uint32_t)(substsz + 1) * kSubRow * 4u;
     L.ring2 = L.ring + kRing2Off;
     L.flags = L.ring2 + kRing2Off;
@@ -1103,7 +1103,7 @@ __host__ __device__ inline KsLds ks_layout(int substsz)
 }
 
 // strip wave (NS = 4, K = 4): 256 rows, 4 per lane
-template <int MODE>
+template <int MODE, bool Q8>
 __device__ __forceinline__ void ks_strip(const StripArgs& a, const KsLds& L, int tk, int w, int lane)
 {
     constexpr int NS = kKrowNSDefault, K = 4, LW = 1024;
@@ -1114,7 +1114,10 @@ __device__ __forceinline__ void ks_strip(const StripArgs& a, const KsLds& L, int
     const int dd = AG ? a.go - a.ge : 0;
     const int r0 = tk * (64 * K * NS) + 64 * K * w + 1;
     const int rl = r0 + K * lane;
-    constexpr int kQRS = kr_qrs(LW), kQW = LW / 2;
+    // the column profile as the sparse fill's (kr_strip): int16 pairs in 2 shifted copies, or (Q8) int8
+    // in 4 byte-shifted copies
+    constexpr int kQRS = kr_qrs(LW, Q8), kQW = Q8 ? LW / 4 : LW / 2;
+    constexpr int kQD = Q8 ? 4 : 8;  // profile dwords per row per block
     uint32_t qrow[K];
 #pragma unroll
     for (int k = 0; k < K; ++k)
@@ -1122,7 +1125,7 @@ __device__ __forceinline__ void ks_strip(const StripArgs& a, const KsLds& L, int
         const int r = rl + k;
         int y = (r <= a.R) ? G(a.seqY)[r] : 0;
         y = ((unsigned)y < (unsigned)a.substsz) ? y : 0;
-        qrow[k] = L.q + 4u * ((lane & 1) * kr_copy1(LW, a.substsz) + (uint32_t)y * kQRS);
+        qrow[k] = L.q + 4u * ((uint32_t)(lane & (Q8 ? 3 : 1)) * kr_copy1(LW, a.substsz, Q8) + (uint32_t)y * kQRS);
     }
     const uint32_t ring_in = L.ring + (uint32_t)w * (kRing * 4u);
     const uint32_t ring_out = L.ring + (uint32_t)(w + 1) * (kRing * 4u);
@@ -1191,19 +1194,21 @@ __device__ __forceinline__ void ks_strip(const StripArgs& a, const KsLds& L, int
                 : "v"(hb)
                 : "memory");
     };
-    auto q_off = [&](int b) { return 4u * (uint32_t)((8 * b - (lane >> 1)) & (kQW - 1)); };
-    int qA[K][8], qB[K][8];
+    auto q_off = [&](int b) {
+        return Q8 ? 4u * (uint32_t)((4 * b - (lane >> 2)) & (kQW - 1)) : 4u * (uint32_t)((8 * b - (lane >> 1)) & (kQW - 1));
+    };
+    int qA[K][kQD], qB[K][kQD];
     {
         const uint32_t p = q_off(0);
 #pragma unroll
         for (int k = 0; k < K; ++k)
 #pragma unroll
-            for (int j = 0; j < 8; ++j) qA[k][j] = 0;
+            for (int j = 0; j < kQD; ++j) qA[k][j] = 0;
         if (!spin(-1)) return;
 #pragma unroll
         for (int k = 0; k < K; ++k)
 #pragma unroll
-            for (int j = 0; j < 8; ++j) qA[k][j] = lds_ld(qrow[k] + p + 4u * j);
+            for (int j = 0; j < kQD; ++j) qA[k][j] = lds_ld(qrow[k] + p + 4u * j);
     }
     // Hgo' (H' when linear), E' of the K rows, F' of the last row, the diagonal of row 0
     int H[K], E[K], FD = kNegS, D = kNegS;
@@ -1278,7 +1283,7 @@ __device__ __forceinline__ void ks_strip(const StripArgs& a, const KsLds& L, int
     };
     int rpin = 0, rpco = 0, rpxo = 0, rsink = 0;
 
-    auto block = [&](int b, int (&qc)[K][8], int (&qn)[K][8]) {
+    auto block = [&](int b, int (&qc)[K][kQD], int (&qn)[K][kQD]) {
         {
             const int pin = __builtin_amdgcn_readfirstlane(rpin), pco = __builtin_amdgcn_readfirstlane(rpco);
             const int pxo = (w == 0) ? __builtin_amdgcn_readfirstlane(rpxo) : 0;
@@ -1305,7 +1310,11 @@ __device__ __forceinline__ void ks_strip(const StripArgs& a, const KsLds& L, int
 #pragma unroll
             for (int k = 0; k < K; ++k)
             {
-                const int q = (u & 1) ? qhi(qc[k][u >> 1]) : qlo(qc[k][u >> 1]);
+                int q;
+                if constexpr (Q8)
+                    q = (int)(signed char)(qc[k][u >> 2] >> (8 * (u & 3)));
+                else
+                    q = (u & 1) ? qhi(qc[k][u >> 1]) : qlo(qc[k][u >> 1]);
                 const int dg = (k == 0 ? D : H[k - 1]) + q;
                 const int vup = (k == 0) ? upH : nh[k - 1];
                 if constexpr (AG)
@@ -1332,7 +1341,7 @@ __device__ __forceinline__ void ks_strip(const StripArgs& a, const KsLds& L, int
                 }
                 wv += 16u * (uint32_t)ge - 1u;
             }
-            if (u < 8)
+            if (u < kQD)
 #pragma unroll
                 for (int k = 0; k < K; ++k) qn[k][u] = lds_ld(qrow[k] + pn + 4u * u);
             lt[u] = H[K - 1];
@@ -1502,87 +1511,114 @@ __device__ __forceinline__ void ks_feed(const StripArgs& a, const KsLds& L, int 
     }
 }
 
-// profiler wave: kr_loader's profile job (ROLE 2) with the NEG letter for columns <= 0 and > C
+// profiler wave: kr_loader's profile job (ROLE 2) with the NEG letter for columns <= 0 and > C; Q8:
+// the int8 profile in 4 byte-shifted copies (kr_loader's Q8 build), NEG = -128 (the int8 instance
+// runs only for tables whose s - go - ge all lie in [-127, 127])
+template <bool Q8>
 __device__ __forceinline__ void ks_profile(const StripArgs& a, const KsLds& L, int lane)
 {
     constexpr int NS = kKrowNSDefault, LW = 1024;
     const int Cp = a.Cp, C = a.C;
-    constexpr int kQRS = kr_qrs(LW), kQW = LW / 2;
+    constexpr int kQRS = kr_qrs(LW, Q8), kQW = Q8 ? LW / 4 : LW / 2;
     const uint32_t F = L.flags;
+    const uint32_t copy1 = kr_copy1(LW, a.substsz, Q8);
     auto letter = [&](int c) {
         if (c < 1 || c > C) return a.substsz;  // NEG
         const int x = G(a.seqX)[c];
         return ((unsigned)x < (unsigned)a.substsz) ? x : 0;
     };
-    // columns -64 .. -1 (the ring's last 32 dwords of both copies, read by lanes still left of
-    // column 0 in the first 4 blocks): NEG, or a stale profile there would lift the SW floor's
-    // values at negative columns and flow into column 0 through E'.  The first batch that
-    // overwrites them (columns 960..) waits until every strip is past them.
-    for (int i = lane; i < 2 * 32 * a.substsz; i += 64)
+    // columns -64 .. -1 (the ring's last dwords of every copy, read by lanes still left of column 0
+    // in the first 4 blocks): NEG, or a stale profile there would lift the SW floor's values at
+    // negative columns and flow into column 0 through E'.  The first batch that overwrites them
+    // (columns 960..) waits until every strip is past them.
     {
-        const int yy = i >> 6, cp = (i >> 5) & 1, dw = kQW - 32 + (i & 31);
-        lds_st(L.q + 4u * ((cp ? kr_copy1(LW, a.substsz) : 0u) + kQRS * (uint32_t)yy + (uint32_t)dw), (int)0x80008000u);
+        constexpr int kNeg = Q8 ? 17 : 32;  // dwords (int8: 64 columns + the copies' shift)
+        constexpr int kCopies = Q8 ? 4 : 2;
+        for (int i = lane; i < kCopies * kNeg * a.substsz; i += 64)
+        {
+            const int yy = i / (kCopies * kNeg), cp = (i / kNeg) % kCopies, dw = kQW - kNeg + i % kNeg;
+            lds_st(L.q + 4u * ((uint32_t)cp * copy1 + kQRS * (uint32_t)yy + (uint32_t)dw), Q8 ? (int)0x80808080u : (int)0x80008000u);
+        }
+    }
+    constexpr int kNX = Q8 ? 5 : 3;
+    const int cp = lane >> 5;
+    const int lb = Q8 ? 4 * (lane & 31) - 1 - 2 * cp : 2 * lane - 1;
+    int xl[kNX], nxl[kNX];
+#pragma unroll
+    for (int i = 0; i < kNX; ++i)
+    {
+        xl[i] = letter(lb + i);
+        nxl[i] = 0;
     }
     int qn = 0;
-    int xm = letter(2 * lane - 1), x0 = letter(2 * lane), x1 = letter(2 * lane + 1);
-    int nxm = 0, nx0 = 0, nx1 = 0;
     int qsub = 0, pl = 0;
     uint64_t last = __builtin_amdgcn_s_memrealtime();
     unsigned idle = 0;
-    while (qn <= Cp)
+    // every column a strip reads (lane 0 reaches column 16 NB - 1), not only those up to Cp: SW tracks
+    // the cells right of C too, which the NEG letter keeps below the real maximum, so a stale profile
+    // there (another launch's letters, or any bytes) must never be read
+    const int qEnd = kBlk * ((Cp + 65 + kBlk - 1) / kBlk);
+    while (qn < qEnd)
     {
         bool moved = false;
         if (qsub == 0 && qn + 192 > pl + LW) pl = flag_ld(F + kr_prog(NS));
         if (qsub > 0 || qn + 192 <= pl + LW)
         {
-            int4v vm[2], v0[2], v1[2];
+            int4v vx[kNX][2];
             {
                 const uint32_t o = 32u * (uint32_t)qsub;
 #pragma unroll
-                for (int j = 0; j < 2; ++j)
-                {
-                    vm[j] = lds_ld4(L.sub + 4u * kSubRow * (uint32_t)xm + o + 16u * j);
-                    v0[j] = lds_ld4(L.sub + 4u * kSubRow * (uint32_t)x0 + o + 16u * j);
-                    v1[j] = lds_ld4(L.sub + 4u * kSubRow * (uint32_t)x1 + o + 16u * j);
-                }
+                for (int i = 0; i < kNX; ++i)
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) vx[i][j] = lds_ld4(L.sub + 4u * kSubRow * (uint32_t)xl[i] + o + 16u * j);
             }
             if (qsub == 0)
             {
-                const int cn = qn + kBatch + 2 * lane;
-                nxm = letter(cn - 1);
-                nx0 = letter(cn);
-                nx1 = letter(cn + 1);
+#pragma unroll
+                for (int i = 0; i < kNX; ++i) nxl[i] = letter(qn + kBatch + lb + i);
             }
-            const uint32_t d = (uint32_t)((qn / 2 + lane) & (kQW - 1));
-            const bool guard = d < 8;
+            // int16: dword of columns (cl, cl+1) / (cl-1, cl); int8: of columns 4d-2cp .. +3 / 4d-2cp-1 .. +2
+            const uint32_t d = Q8 ? (uint32_t)((qn / 4 + (lane & 31)) & (kQW - 1)) : (uint32_t)((qn / 2 + lane) & (kQW - 1));
+            const bool guard = d < (Q8 ? 4u : 8u);
+            const uint32_t ce = L.q + 4u * ((Q8 ? (uint32_t)(2 * cp) * copy1 : 0u) + d);
+            const uint32_t co = ce + 4u * copy1;
 #pragma unroll
             for (int i = 0; i < 8; ++i)
             {
                 const int yy = 8 * qsub + i;
                 if (yy < a.substsz)
                 {
-                    const int s0 = v0[i >> 2][i & 3];
-                    const int p0 = (s0 & 0xffff) | (v1[i >> 2][i & 3] << 16);
-                    const int p1 = (vm[i >> 2][i & 3] & 0xffff) | (s0 << 16);
-                    const uint32_t r0a = L.q + 4u * (kQRS * (uint32_t)yy + d);
-                    const uint32_t r1a = L.q + 4u * (kr_copy1(LW, a.substsz) + kQRS * (uint32_t)yy + d);
-                    lds_st(r0a, p0);
-                    lds_st(r1a, p1);
+                    int ev, od;
+                    if constexpr (Q8)
+                    {
+                        const int w0 = vx[0][i >> 2][i & 3], w1 = vx[1][i >> 2][i & 3], w2 = vx[2][i >> 2][i & 3];
+                        const int w3 = vx[3][i >> 2][i & 3], w4 = vx[4][i >> 2][i & 3];
+                        od = (w0 & 0xff) | ((w1 & 0xff) << 8) | ((w2 & 0xff) << 16) | (w3 << 24);
+                        ev = (int)__builtin_amdgcn_alignbyte((unsigned)w4, (unsigned)od, 1u);
+                    }
+                    else
+                    {
+                        const int s0 = vx[1][i >> 2][i & 3];
+                        ev = (s0 & 0xffff) | (vx[2][i >> 2][i & 3] << 16);  // copy 0: (cl, cl+1)
+                        od = (vx[0][i >> 2][i & 3] & 0xffff) | (s0 << 16);  // copy 1: (cl-1, cl)
+                    }
+                    const uint32_t ra = 4u * kQRS * (uint32_t)yy;
+                    lds_st(ce + ra, ev);
+                    lds_st(co + ra, od);
                     if (guard)
                     {
-                        lds_st(r0a + 4u * kQW, p0);
-                        lds_st(r1a + 4u * kQW, p1);
+                        lds_st(ce + ra + 4u * kQW, ev);
+                        lds_st(co + ra + 4u * kQW, od);
                     }
                 }
             }
             if (++qsub == 4 || 8 * qsub >= a.substsz)
             {
                 qsub = 0;
-                xm = nxm;
-                x0 = nx0;
-                x1 = nx1;
+#pragma unroll
+                for (int i = 0; i < kNX; ++i) xl[i] = nxl[i];
                 qn += kBatch;
-                flag_st(F + kFXo, qn > Cp ? kBig : qn);
+                flag_st(F + kFXo, qn >= qEnd ? kBig : qn);
             }
             moved = true;
         }
@@ -1654,16 +1690,19 @@ __device__ __forceinline__ void ks_drain(const StripArgs& a, const KsLds& L, int
     }
 }
 
-template <int MODE>
+// Q8: the int8-profile instance; it declines a table with some s - go - ge outside [-127, 127] as
+// nw_krow_kernel's does (a.q8flag), and the int16 instance behind it (a.q8 = 2) runs only then
+template <int MODE, bool Q8>
 __global__ void __launch_bounds__(64 * kr_waves<kKrowNSDefault>()) nw_kscore_kernel(StripArgs a)
 {
     constexpr int NS = kKrowNSDefault;
     constexpr int kThreads = 64 * kr_waves<NS>();
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
-    const KsLds L = ks_layout(a.substsz);
+    const KsLds L = ks_layout(a.substsz, Q8);
+    if (!Q8 && a.q8 == 2 && __hip_atomic_load(a.q8flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != a.epoch) return;
     // subT[x][y] = s(y, x) - go - ge (int16 range checked), row x = substsz: the NEG letter
-    bool bad = false;
+    bool bad = false, bad8 = false;
     for (int k = threadIdx.x; k < (a.substsz + 1) * kSubRow; k += kThreads)
     {
         const int x = k / kSubRow, yy = k % kSubRow;
@@ -1674,13 +1713,28 @@ __global__ void __launch_bounds__(64 * kr_waves<kKrowNSDefault>()) nw_kscore_ker
             {
                 v = G(a.subst)[yy * a.substsz + x] - a.go - a.ge;
                 bad |= v <= kNegQ || v > 32767;
+                bad8 |= v <= -128 || v > 127;
             }
             else
-                v = kNegQ;
+                v = Q8 ? -128 : kNegQ;
         }
         lds_st(L.sub + 4u * k, v);
     }
-    if (bad) atomicOr(a.err, 2u);
+    if constexpr (Q8)
+    {
+        // decline (every workgroup sees the same table), reduced through a word of the dynamic LDS
+        if (threadIdx.x == 0) lds_st(L.flags + kFTicket, 0);
+        __syncthreads();
+        if (bad8) atomicOr((int*)(krsm + L.flags + kFTicket), 1);
+        __syncthreads();
+        if (lds_ld(L.flags + kFTicket) != 0)
+        {
+            if (threadIdx.x == 0) __hip_atomic_store(a.q8flag, a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return;
+        }
+    }
+    else if (bad)
+        atomicOr(a.err, 2u);
     for (;;)
     {
         __syncthreads();
@@ -1707,27 +1761,39 @@ __global__ void __launch_bounds__(64 * kr_waves<kKrowNSDefault>()) nw_kscore_ker
         else if (w == NS)
             ks_feed<MODE>(pa, L, tk, lane);
         else if (w == NS + 2)
-            ks_profile(pa, L, lane);
+            ks_profile<Q8>(pa, L, lane);
         else
         {
             __builtin_amdgcn_s_setprio(3);
-            ks_strip<MODE>(pa, L, tk, w, lane);
+            ks_strip<MODE, Q8>(pa, L, tk, w, lane);
             __builtin_amdgcn_s_setprio(0);
         }
     }
 }
 
-template <int MODE>
-hipError_t launch_ks(const StripArgs& a, int grid, hipStream_t stream)
+template <int MODE, bool Q8>
+hipError_t launch_ks1(const StripArgs& a, int grid, hipStream_t stream, bool foot)
 {
-    const size_t lds = krow_score_lds_bytes(a.substsz);
-    auto kern = nw_kscore_kernel<MODE>;
+    const size_t lds = krow_score_lds_bytes(a.substsz, Q8);
+    auto kern = nw_kscore_kernel<MODE, Q8>;
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     constexpr int kThreads = 64 * kr_waves<kKrowNSDefault>();
-    if ((e = record_foot((const void*)kern, lds, kThreads, grid)) != hipSuccess) return e;
+    if (foot && (e = record_foot((const void*)kern, lds, kThreads, grid)) != hipSuccess) return e;
     hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreads), lds, stream, a);
     return hipGetLastError();
+}
+
+// a.q8: the int8 instance, then the int16 one behind it (a no-op unless the int8 launch declined)
+template <int MODE>
+hipError_t launch_ks(const StripArgs& a, int grid, hipStream_t stream)
+{
+    if (!a.q8) return launch_ks1<MODE, false>(a, grid, stream, true);
+    hipError_t e = launch_ks1<MODE, true>(a, grid, stream, true);
+    if (e != hipSuccess) return e;
+    StripArgs b = a;
+    b.q8 = 2;
+    return launch_ks1<MODE, false>(b, grid, stream, false);
 }
 #endif  // GSA_KROW_SCORE
 
@@ -1735,7 +1801,7 @@ hipError_t launch_ks(const StripArgs& a, int grid, hipStream_t stream)
 
 #if defined(GSA_KROW_SCORE)
 // progress words (256 B) and the NW result cell's scratch (64 ints)
-size_t krow_score_lds_bytes(int substsz) { return (size_t)ks_layout(substsz).flags + 512; }
+size_t krow_score_lds_bytes(int substsz, bool q8) { return (size_t)ks_layout(substsz, q8).flags + 512; }
 
 hipError_t launch_krow_score(const StripArgs& a, int mode, int grid, hipStream_t stream)
 {

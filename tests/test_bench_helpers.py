@@ -60,8 +60,9 @@ def test_score_kernel_label(monkeypatch):
     """The config5 field names the kernel that gsa_score_dev runs (K-rows by default,
     the strip kernel under GSA_SCORE_KERNEL=strip)."""
     monkeypatch.delenv("GSA_SCORE_KERNEL", raising=False)
-    assert bench.score_kernel_name(-11, -1, False).startswith("gsa::nw_kscore_kernel<3>")
-    assert bench.score_kernel_name(-11, -11, True).startswith("gsa::nw_kscore_kernel<5>")
+    monkeypatch.delenv("GSA_KROW_Q8", raising=False)
+    assert bench.score_kernel_name(-11, -1, False).startswith("gsa::nw_kscore_kernel<3, false>")
+    assert bench.score_kernel_name(-11, -11, True).startswith("gsa::nw_kscore_kernel<5, true>")
     monkeypatch.setenv("GSA_SCORE_KERNEL", "strip")
     assert "nw_strip_kernel" in bench.score_kernel_name(-11, -1, False)
 

@@ -166,3 +166,20 @@ def test_alphabet_sizes(engine, golden, substsz, go, ge, local):
     Y, X = random_pair(1500, 1100, substsz + 5, alphabet=substsz)
     r = engine.score(Y, X, sub, go, ge, local)
     assert (r["score"], r["i_end"], r["j_end"]) == oracle.score_ag(Y, X, sub, go, ge, local)
+
+
+@pytest.mark.parametrize("q8", ["0", "1", "2"])
+@pytest.mark.parametrize("go,ge,local", MODES + [(-120, -120, False), (-120, -120, True), (-70, -60, False)])
+def test_profile_widths_and_stale_columns(engine, golden, monkeypatch, q8, go, ge, local):
+    """The K-rows score kernel's int16 and int8 column profiles (GSA_KROW_Q8 = 0 / 2; 1 = int8 for
+    linear modes only), the int8 instance's decline for s - go - ge outside int8 (gap -120, -70/-60:
+    the int16 instance runs), and columns right of C: a long pair first leaves real letters in the
+    profile ring, then a short one's strips read the columns past C up to 16 NB - 1, which the
+    profiler must have rebuilt with the NEG letter (SW tracks those cells; a stale profile there
+    once gave SW-AG 64 x 65 the score 197)."""
+    import oracle
+    monkeypatch.setenv("GSA_KROW_Q8", q8)
+    for R, C in [(3, 3000), (64, 65), (200, 3000), (65, 100), (1, 200), (64, 65)]:
+        Y, X = random_pair(R, C, 11 * R + C)
+        r = engine.score(Y, X, golden.blosum62, go, ge, local)
+        assert (r["score"], r["i_end"], r["j_end"]) == oracle.score_ag(Y, X, golden.blosum62, go, ge, local), (R, C)
