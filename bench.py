@@ -365,7 +365,10 @@ def score_kernel_name(go, ge, local, substsz=25):
     # the int8-profile instance for linear modes (gsa_capi.hip score_ag_strip; GSA_KROW_Q8 0 / 2: never / always)
     q8env = os.environ.get("GSA_KROW_Q8", "1")
     q8 = q8env != "0" and (q8env == "2" or go == ge)
-    return (f"gsa::nw_kscore_kernel<{mode}, {'true' if q8 else 'false'}> ({mname})" if krow else
+    # rows per lane: 4 for NW-LG, 2 otherwise (GSA_SCORE_K forces one)
+    kenv = os.environ.get("GSA_SCORE_K", "")
+    k = int(kenv) if kenv in ("2", "4") else (4 if (not local and go == ge) else 2)
+    return (f"gsa::nw_kscore_kernel<{mode}, {'true' if q8 else 'false'}, {k}> ({mname})" if krow else
             f"gsa::nw_strip_kernel<4,{mode}> ({mname}, strip kernel)")
 
 

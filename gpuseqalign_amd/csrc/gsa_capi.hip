@@ -310,7 +310,14 @@ int sw_idx_bits(int64_t R, int64_t C)
 int score_ag_strip(gsa_ctx* ctx, const int32_t* seqY, int64_t R, const int32_t* seqX, int64_t C, const int32_t* subst,
                    int32_t substsz, int32_t gapo, int32_t gape, int32_t local, gsa_score_result* out, hipStream_t st)
 {
-    const int64_t TR = (int64_t)gsa::kWaveRows * gsa::kSparseNS;
+    // the K-rows score kernel's rows per lane, tickets of 64 K NS rows: 2 in the modes with the
+    // longer step (SW tracking, affine gaps: the block's fixed part is a smaller share there, and
+    // twice the strips shorten it), 4 for NW-LG; same box, 5k-100k pairs: NW-AG -5..-7 %, SW-AG
+    // -9..-11 %, SW-LG -2..-5 % with 2, NW-LG +12..18 % (profiles/r04_score_k.txt).  GSA_SCORE_K
+    // = 2 / 4 forces one
+    const int kenv = env_int("GSA_SCORE_K", 0);
+    const int scoreK = kenv == 2 || kenv == 4 ? kenv : (!local && gapo == gape) ? 4 : 2;
+    const int64_t TR = (int64_t)(64 * scoreK) * gsa::kSparseNS;
     const int64_t tickets = (R + TR - 1) / TR;
     if (tickets > (1ll << 30) || C > (1ll << 30)) return GSA_ERROR_INVALID_VALUE;
     gsa::StripArgs a;
@@ -368,7 +375,7 @@ int score_ag_strip(gsa_ctx* ctx, const int32_t* seqY, int64_t R, const int32_t* 
     const int q8env = env_int("GSA_KROW_Q8", 1);
     a.q8 = (q8env != 0 && (q8env == 2 || gapo == gape) && gsa::krow_score_lds_bytes(substsz, true) <= (size_t)ctx->lds_max) ? 1 : 0;
     a.q8flag = ctx->ctl + 2;
-    if ((e = krow ? gsa::launch_krow_score(a, mode, grid, st) : gsa::launch_strip_fill(a, mode, grid, st)) != hipSuccess)
+    if ((e = krow ? gsa::launch_krow_score(a, mode, scoreK, grid, st) : gsa::launch_strip_fill(a, mode, grid, st)) != hipSuccess)
         return fail(ctx, e, GSA_ERROR_KERNEL_FAILURE);
     note_launch(ctx);
     (void)hipEventRecord(ctx->ev1, st);

@@ -47,6 +47,6 @@ hipError_t launch_full_fused(const StripArgs& a, int ns, int waves, int grid, hi
 // (-32768, 32767] (error bit 2 otherwise); SW needs go < 0 and ge <= 0.  a.q8 as launch_kr: the
 // int8-profile instance (values in [-127, 127]) with the int16 one behind it.
 size_t krow_score_lds_bytes(int substsz, bool q8 = false);
-hipError_t launch_krow_score(const StripArgs& a, int mode, int grid, hipStream_t stream);
+hipError_t launch_krow_score(const StripArgs& a, int mode, int k, int grid, hipStream_t stream);
 
 }  // namespace gsa

@@ -1102,11 +1102,11 @@ __host__ __device__ inline KsLds ks_layout(int substsz, bool q8 = false)
     return L;
 }
 
-// strip wave (NS = 4, K = 4): 256 rows, 4 per lane
-template <int MODE, bool Q8>
+// strip wave (NS = 4): 64 K rows, K (4, or 2) per lane
+template <int MODE, bool Q8, int K>
 __device__ __forceinline__ void ks_strip(const StripArgs& a, const KsLds& L, int tk, int w, int lane)
 {
-    constexpr int NS = kKrowNSDefault, K = 4, LW = 1024;
+    constexpr int NS = kKrowNSDefault, LW = 1024;
     constexpr bool AG = !is_lin_mode(MODE);  // E' and F' carried
     constexpr bool SW = is_sw_mode(MODE);
     const int Cp = a.Cp;
@@ -1237,11 +1237,11 @@ __device__ __forceinline__ void ks_strip(const StripArgs& a, const KsLds& L, int
             tb[k] = 0;
         }
     }
-    // NW: the cell (R, C) lies in this strip iff r0 <= R < r0 + 256; lane laneR reaches column C
+    // NW: the cell (R, C) lies in this strip iff r0 <= R < r0 + 64 K; lane laneR reaches column C
     // at step tStar, in block tStar / 16, row kR
     const int rR = a.R - r0;
     const bool hasR = !SW && rR >= 0 && rR < 64 * K;
-    const int laneR = rR >> 2, kR = rR & 3, tStar = a.C + laneR;
+    const int laneR = rR / K, kR = rR % K, tStar = a.C + laneR;
     int lt[kBlk], lf[kBlk];  // lane 63's hand-off values of the last block (Hgo', F' of columns t-64)
     auto handoff = [&](int bb) {
         const uint32_t eb = ring_out + 4u * (uint32_t)((kBlk * bb) & (kRing - 1));
@@ -1692,7 +1692,7 @@ __device__ __forceinline__ void ks_drain(const StripArgs& a, const KsLds& L, int
 
 // Q8: the int8-profile instance; it declines a table with some s - go - ge outside [-127, 127] as
 // nw_krow_kernel's does (a.q8flag), and the int16 instance behind it (a.q8 = 2) runs only then
-template <int MODE, bool Q8>
+template <int MODE, bool Q8, int K>
 __global__ void __launch_bounds__(64 * kr_waves<kKrowNSDefault>()) nw_kscore_kernel(StripArgs a)
 {
     constexpr int NS = kKrowNSDefault;
@@ -1765,17 +1765,17 @@ __global__ void __launch_bounds__(64 * kr_waves<kKrowNSDefault>()) nw_kscore_ker
         else
         {
             __builtin_amdgcn_s_setprio(3);
-            ks_strip<MODE, Q8>(pa, L, tk, w, lane);
+            ks_strip<MODE, Q8, K>(pa, L, tk, w, lane);
             __builtin_amdgcn_s_setprio(0);
         }
     }
 }
 
-template <int MODE, bool Q8>
+template <int MODE, bool Q8, int K>
 hipError_t launch_ks1(const StripArgs& a, int grid, hipStream_t stream, bool foot)
 {
     const size_t lds = krow_score_lds_bytes(a.substsz, Q8);
-    auto kern = nw_kscore_kernel<MODE, Q8>;
+    auto kern = nw_kscore_kernel<MODE, Q8, K>;
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     constexpr int kThreads = 64 * kr_waves<kKrowNSDefault>();
@@ -1785,15 +1785,15 @@ hipError_t launch_ks1(const StripArgs& a, int grid, hipStream_t stream, bool foo
 }
 
 // a.q8: the int8 instance, then the int16 one behind it (a no-op unless the int8 launch declined)
-template <int MODE>
+template <int MODE, int K>
 hipError_t launch_ks(const StripArgs& a, int grid, hipStream_t stream)
 {
-    if (!a.q8) return launch_ks1<MODE, false>(a, grid, stream, true);
-    hipError_t e = launch_ks1<MODE, true>(a, grid, stream, true);
+    if (!a.q8) return launch_ks1<MODE, false, K>(a, grid, stream, true);
+    hipError_t e = launch_ks1<MODE, true, K>(a, grid, stream, true);
     if (e != hipSuccess) return e;
     StripArgs b = a;
     b.q8 = 2;
-    return launch_ks1<MODE, false>(b, grid, stream, false);
+    return launch_ks1<MODE, false, K>(b, grid, stream, false);
 }
 #endif  // GSA_KROW_SCORE
 
@@ -1803,13 +1803,21 @@ hipError_t launch_ks(const StripArgs& a, int grid, hipStream_t stream)
 // progress words (256 B) and the NW result cell's scratch (64 ints)
 size_t krow_score_lds_bytes(int substsz, bool q8) { return (size_t)ks_layout(substsz, q8).flags + 512; }
 
-hipError_t launch_krow_score(const StripArgs& a, int mode, int grid, hipStream_t stream)
+hipError_t launch_krow_score(const StripArgs& a, int mode, int k, int grid, hipStream_t stream)
 {
-    if (a.nPairs != 1 || grid <= 0) return hipErrorInvalidValue;
-    if (mode == kModeScoreAG) return launch_ks<kModeScoreAG>(a, grid, stream);
-    if (mode == kModeScoreAGL) return launch_ks<kModeScoreAGL>(a, grid, stream);
-    if (mode == kModeScoreSW) return launch_ks<kModeScoreSW>(a, grid, stream);
-    if (mode == kModeScoreSWL) return launch_ks<kModeScoreSWL>(a, grid, stream);
+    if (a.nPairs != 1 || grid <= 0 || (k != 2 && k != 4)) return hipErrorInvalidValue;
+    if (k == 2)
+    {
+        if (mode == kModeScoreAG) return launch_ks<kModeScoreAG, 2>(a, grid, stream);
+        if (mode == kModeScoreAGL) return launch_ks<kModeScoreAGL, 2>(a, grid, stream);
+        if (mode == kModeScoreSW) return launch_ks<kModeScoreSW, 2>(a, grid, stream);
+        if (mode == kModeScoreSWL) return launch_ks<kModeScoreSWL, 2>(a, grid, stream);
+        return hipErrorInvalidValue;
+    }
+    if (mode == kModeScoreAG) return launch_ks<kModeScoreAG, 4>(a, grid, stream);
+    if (mode == kModeScoreAGL) return launch_ks<kModeScoreAGL, 4>(a, grid, stream);
+    if (mode == kModeScoreSW) return launch_ks<kModeScoreSW, 4>(a, grid, stream);
+    if (mode == kModeScoreSWL) return launch_ks<kModeScoreSWL, 4>(a, grid, stream);
     return hipErrorInvalidValue;
 }
 #elif defined(GSA_KROW_XR)

@@ -143,13 +143,15 @@ def test_strip_kernel_path(engine, golden, R, C, go, ge, local, monkeypatch):
     assert (r["score"], r["i_end"], r["j_end"]) == oracle.score_ag(Y, X, golden.blosum62, go, ge, local)
 
 
+@pytest.mark.parametrize("k", ["2", "4"])
 @pytest.mark.parametrize("R", [2048, 2049, 2050, 2051, 2052, 3071])
 @pytest.mark.parametrize("go,ge,local", MODES)
-def test_result_row_positions(engine, golden, R, go, ge, local):
+def test_result_row_positions(engine, golden, monkeypatch, k, R, go, ge, local):
     """The K-rows score kernel reads the NW result cell (R, C) from the lane and row that hold it
-    (row kR = (R - 1) mod 4 of lane (R - r0) / 4 of a later ticket's strip): every kR, a strip's
-    first and last rows."""
+    (row kR = (R - r0) mod K of lane (R - r0) / K of a later ticket's strip): every kR, a strip's
+    first and last rows, at K = 2 and 4 rows per lane (GSA_SCORE_K)."""
     import oracle
+    monkeypatch.setenv("GSA_SCORE_K", k)
     Y, X = random_pair(R, 257, R + 11)
     r = engine.score(Y, X, golden.blosum62, go, ge, local)
     assert (r["score"], r["i_end"], r["j_end"]) == oracle.score_ag(Y, X, golden.blosum62, go, ge, local)
@@ -168,17 +170,20 @@ def test_alphabet_sizes(engine, golden, substsz, go, ge, local):
     assert (r["score"], r["i_end"], r["j_end"]) == oracle.score_ag(Y, X, sub, go, ge, local)
 
 
+@pytest.mark.parametrize("k", ["2", "4"])
 @pytest.mark.parametrize("q8", ["0", "1", "2"])
 @pytest.mark.parametrize("go,ge,local", MODES + [(-120, -120, False), (-120, -120, True), (-70, -60, False)])
-def test_profile_widths_and_stale_columns(engine, golden, monkeypatch, q8, go, ge, local):
+def test_profile_widths_and_stale_columns(engine, golden, monkeypatch, q8, k, go, ge, local):
     """The K-rows score kernel's int16 and int8 column profiles (GSA_KROW_Q8 = 0 / 2; 1 = int8 for
     linear modes only), the int8 instance's decline for s - go - ge outside int8 (gap -120, -70/-60:
     the int16 instance runs), and columns right of C: a long pair first leaves real letters in the
     profile ring, then a short one's strips read the columns past C up to 16 NB - 1, which the
     profiler must have rebuilt with the NEG letter (SW tracks those cells; a stale profile there
-    once gave SW-AG 64 x 65 the score 197)."""
+    once gave SW-AG 64 x 65 the score 197).  Both strip heights: 2 and 4 rows per lane (GSA_SCORE_K;
+    by default 4 for NW-LG, 2 otherwise), so the result cell falls at every row of a lane."""
     import oracle
     monkeypatch.setenv("GSA_KROW_Q8", q8)
+    monkeypatch.setenv("GSA_SCORE_K", k)
     for R, C in [(3, 3000), (64, 65), (200, 3000), (65, 100), (1, 200), (64, 65)]:
         Y, X = random_pair(R, C, 11 * R + C)
         r = engine.score(Y, X, golden.blosum62, go, ge, local)
