@@ -317,7 +317,11 @@ int score_ag_strip(gsa_ctx* ctx, const int32_t* seqY, int64_t R, const int32_t* 
     // = 2 / 4 forces one
     const int kenv = env_int("GSA_SCORE_K", 0);
     const int scoreK = kenv == 2 || kenv == 4 ? kenv : (!local && gapo == gape) ? 4 : 2;
-    const int64_t TR = (int64_t)(64 * scoreK) * gsa::kSparseNS;
+    // the K-rows score kernel unless GSA_SCORE_KERNEL=strip, or its LDS (a profile of substsz rows)
+    // does not fit, or SW with ge > 0 (its per-row key offsets assume z grows along j); the strip
+    // kernel's score modes otherwise, on its own 1024-row tickets
+    const bool krow = score_kernel_krow() && (!local || gape <= 0) && gsa::krow_score_lds_bytes(substsz) <= ctx->lds_max;
+    const int64_t TR = krow ? (int64_t)(64 * scoreK) * gsa::kSparseNS : (int64_t)gsa::kWaveRows * gsa::kSparseNS;
     const int64_t tickets = (R + TR - 1) / TR;
     if (tickets > (1ll << 30) || C > (1ll << 30)) return GSA_ERROR_INVALID_VALUE;
     gsa::StripArgs a;
@@ -365,9 +369,6 @@ int score_ag_strip(gsa_ctx* ctx, const int32_t* seqY, int64_t R, const int32_t* 
     // a linear gap (gapo == gape) runs the step without E' and F' (d = 0)
     const int mode = local ? (gapo == gape ? gsa::kModeScoreSWL : gsa::kModeScoreSW)
                            : (gapo == gape ? gsa::kModeScoreAGL : gsa::kModeScoreAG);
-    // the K-rows score kernel (nw_kscore.hip) unless GSA_SCORE_KERNEL=strip, or its LDS (a profile of
-    // substsz rows) does not fit, or SW with ge > 0 (its per-row key offsets assume z grows along j)
-    const bool krow = score_kernel_krow() && (!local || gape <= 0) && gsa::krow_score_lds_bytes(substsz) <= ctx->lds_max;
     // linear modes read the int8 column profile where its LDS fits (the instance declines a table
     // outside int8 and the int16 instance behind it runs): 50k SW-LG 3.87 -> 3.82 ms; the affine step
     // is slower with it (NW-AG 4.20 -> 4.38 ms: the byte extraction costs more than the halved reads
