@@ -362,12 +362,12 @@ def score_kernel_name(go, ge, local, substsz=25):
     mname = (("kModeScoreSWL" if go == ge else "kModeScoreSW") if local else
              ("kModeScoreAGL" if go == ge else "kModeScoreAG"))
     krow = os.environ.get("GSA_SCORE_KERNEL", "") != "strip" and (not local or ge <= 0) and substsz <= 32
-    # the int8-profile instance for linear modes (gsa_capi.hip score_ag_strip; GSA_KROW_Q8 0 / 2: never / always)
-    q8env = os.environ.get("GSA_KROW_Q8", "1")
-    q8 = q8env != "0" and (q8env == "2" or go == ge)
-    # rows per lane: 4 for NW-LG, 2 otherwise (GSA_SCORE_K forces one)
+    # rows per lane: 4 for NW-LG, 2 otherwise (GSA_SCORE_K forces one); the int8-profile instance at
+    # 4 rows per lane (gsa_capi.hip score_ag_strip; GSA_KROW_Q8 0 / 2: never / always)
     kenv = os.environ.get("GSA_SCORE_K", "")
     k = int(kenv) if kenv in ("2", "4") else (4 if (not local and go == ge) else 2)
+    q8env = os.environ.get("GSA_KROW_Q8", "1")
+    q8 = q8env != "0" and (q8env == "2" or k == 4)
     return (f"gsa::nw_kscore_kernel<{mode}, {'true' if q8 else 'false'}, {k}> ({mname})" if krow else
             f"gsa::nw_strip_kernel<4,{mode}> ({mname}, strip kernel)")
 

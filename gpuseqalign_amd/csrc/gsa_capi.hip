@@ -369,12 +369,12 @@ int score_ag_strip(gsa_ctx* ctx, const int32_t* seqY, int64_t R, const int32_t* 
     // a linear gap (gapo == gape) runs the step without E' and F' (d = 0)
     const int mode = local ? (gapo == gape ? gsa::kModeScoreSWL : gsa::kModeScoreSW)
                            : (gapo == gape ? gsa::kModeScoreAGL : gsa::kModeScoreAG);
-    // linear modes read the int8 column profile where its LDS fits (the instance declines a table
-    // outside int8 and the int16 instance behind it runs): 50k SW-LG 3.87 -> 3.82 ms; the affine step
-    // is slower with it (NW-AG 4.20 -> 4.38 ms: the byte extraction costs more than the halved reads
-    // save there), so affine modes keep the int16 profile.  GSA_KROW_Q8=0 / 2: int16 / int8 always
+    // the int8 column profile where its LDS fits (the instance declines a table outside int8 and the
+    // int16 instance behind it runs) for the 4-rows-per-lane geometry (NW-LG): 50k 2.52 -> 2.46 ms;
+    // at 2 rows per lane the int16 profile is faster (SW-LG 3.71 -> 3.42 ms, NW-AG 4.16 -> 3.87;
+    // profiles/r04_score_k.txt).  GSA_KROW_Q8=0 / 2: int16 / int8 always
     const int q8env = env_int("GSA_KROW_Q8", 1);
-    a.q8 = (q8env != 0 && (q8env == 2 || gapo == gape) && gsa::krow_score_lds_bytes(substsz, true) <= (size_t)ctx->lds_max) ? 1 : 0;
+    a.q8 = (q8env != 0 && (q8env == 2 || scoreK == 4) && gsa::krow_score_lds_bytes(substsz, true) <= (size_t)ctx->lds_max) ? 1 : 0;
     a.q8flag = ctx->ctl + 2;
     if ((e = krow ? gsa::launch_krow_score(a, mode, scoreK, grid, st) : gsa::launch_strip_fill(a, mode, grid, st)) != hipSuccess)
         return fail(ctx, e, GSA_ERROR_KERNEL_FAILURE);

@@ -63,7 +63,7 @@ def test_score_kernel_label(monkeypatch):
     monkeypatch.delenv("GSA_KROW_Q8", raising=False)
     monkeypatch.delenv("GSA_SCORE_K", raising=False)
     assert bench.score_kernel_name(-11, -1, False).startswith("gsa::nw_kscore_kernel<3, false, 2>")
-    assert bench.score_kernel_name(-11, -11, True).startswith("gsa::nw_kscore_kernel<5, true, 2>")
+    assert bench.score_kernel_name(-11, -11, True).startswith("gsa::nw_kscore_kernel<5, false, 2>")
     assert bench.score_kernel_name(-11, -11, False).startswith("gsa::nw_kscore_kernel<6, true, 4>")
     monkeypatch.setenv("GSA_SCORE_KERNEL", "strip")
     assert "nw_strip_kernel" in bench.score_kernel_name(-11, -1, False)
