@@ -48,5 +48,7 @@ hipError_t launch_full_fused(const StripArgs& a, int ns, int waves, int grid, hi
 // int8-profile instance (values in [-127, 127]) with the int16 one behind it.
 size_t krow_score_lds_bytes(int substsz, bool q8 = false);
 hipError_t launch_krow_score(const StripArgs& a, int mode, int k, int grid, hipStream_t stream);
+// (the affine modes' instances, in nw_kscore_ag.hip; called by launch_krow_score)
+hipError_t launch_krow_score_affine(const StripArgs& a, int mode, int k, int grid, hipStream_t stream);
 
 }  // namespace gsa

@@ -1799,24 +1799,36 @@ hipError_t launch_ks(const StripArgs& a, int grid, hipStream_t stream)
 
 }  // namespace
 
-#if defined(GSA_KROW_SCORE)
+#if defined(GSA_KROW_SCORE) && defined(GSA_KSCORE_AFFINE)
+// the affine modes (nw_kscore_ag.hip: its own translation unit, built with the iterative ILP
+// scheduler: 50k NW-AG 3.86 -> 3.73 ms, profiles/r04_score_k.txt)
+hipError_t launch_krow_score_affine(const StripArgs& a, int mode, int k, int grid, hipStream_t stream)
+{
+    if (k == 2)
+    {
+        if (mode == kModeScoreAG) return launch_ks<kModeScoreAG, 2>(a, grid, stream);
+        if (mode == kModeScoreSW) return launch_ks<kModeScoreSW, 2>(a, grid, stream);
+        return hipErrorInvalidValue;
+    }
+    if (mode == kModeScoreAG) return launch_ks<kModeScoreAG, 4>(a, grid, stream);
+    if (mode == kModeScoreSW) return launch_ks<kModeScoreSW, 4>(a, grid, stream);
+    return hipErrorInvalidValue;
+}
+#elif defined(GSA_KROW_SCORE)
 // progress words (256 B) and the NW result cell's scratch (64 ints)
 size_t krow_score_lds_bytes(int substsz, bool q8) { return (size_t)ks_layout(substsz, q8).flags + 512; }
 
 hipError_t launch_krow_score(const StripArgs& a, int mode, int k, int grid, hipStream_t stream)
 {
     if (a.nPairs != 1 || grid <= 0 || (k != 2 && k != 4)) return hipErrorInvalidValue;
+    if (mode == kModeScoreAG || mode == kModeScoreSW) return launch_krow_score_affine(a, mode, k, grid, stream);
     if (k == 2)
     {
-        if (mode == kModeScoreAG) return launch_ks<kModeScoreAG, 2>(a, grid, stream);
         if (mode == kModeScoreAGL) return launch_ks<kModeScoreAGL, 2>(a, grid, stream);
-        if (mode == kModeScoreSW) return launch_ks<kModeScoreSW, 2>(a, grid, stream);
         if (mode == kModeScoreSWL) return launch_ks<kModeScoreSWL, 2>(a, grid, stream);
         return hipErrorInvalidValue;
     }
-    if (mode == kModeScoreAG) return launch_ks<kModeScoreAG, 4>(a, grid, stream);
     if (mode == kModeScoreAGL) return launch_ks<kModeScoreAGL, 4>(a, grid, stream);
-    if (mode == kModeScoreSW) return launch_ks<kModeScoreSW, 4>(a, grid, stream);
     if (mode == kModeScoreSWL) return launch_ks<kModeScoreSWL, 4>(a, grid, stream);
     return hipErrorInvalidValue;
 }
