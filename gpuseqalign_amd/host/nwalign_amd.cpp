@@ -153,38 +153,33 @@ NwStat runSlot(const char* slot, const NwAlgParams& pr, NwAlgInput& nw, NwAlgRes
 }  // namespace
 
 // ---- the parameter contract of the reference's slots ---------------------------------------
-// Each reference slot reads its own parameters and returns errorInvalidValue for a value its
+// Each reference slot reads its own parameters with pr.at() inside a try block, so a parameter
+// the file does not list throws and the slot returns errorInvalidValue, and so does a value its
 // rules reject (nwalign_gpu1_ml_diag.cu:82-93, gpu2:125-141, gpu3:297-311, gpu4:292-310,
-// gpu5:322-333, gpu6:303-321, gpu7_mlsp:304-320, gpu8:325-340, gpu9:382-414).  The rules are
-// kept as written, with the reference's units: a warp is kParamWarp = 32 threads (the unit its
-// parameter files are tuned in, param_best.json:1, an RTX 3090), a block at most 1024 threads.
-// A parameter the file does not list is not required: the engine's geometry does not need it.
+// gpu5:322-333, gpu6:303-321, gpu7_mlsp:305-320, gpu8:325-340, gpu9:382-414).  Both are kept
+// for the Gpu1..9 names: every parameter the reference slot reads is required.  The rules use
+// the reference's units: a warp is kParamWarp = 32 threads (the unit its parameter files are
+// tuned in, param_best.json:1, an RTX 3090), a block at most 1024 threads.  This engine's own
+// NwAlign_Amd_Strip_* slots have defaults (tileBx 256) and need no parameter.
 // The sparse slots' tile width maps to the engine's nearest (a multiple of 16, >= 64):
 //   gpu7/gpu8: tileBx;
 //   gpu9: the reference's derived width, tileBx = k*subtileBx - (tileBy - 1) with tileBy =
 //         subtileRows*32 and k = ceil((subtileCols*subtileBx + tileBy - 1) / subtileBx) (:389-398);
-//   this engine's slots (and gpu9 given "tileBx" directly): tileBx itself, which must then be a
-//         multiple of 16 and >= 64.
+//   this engine's slots: tileBx itself, which must then be a multiple of 16 and >= 64.
 // The tile height is the engine's 1024 whatever the slot asks (gsa_sparse_tile_by).
 NwStat slotGeometry(const std::string& slot, const NwAlgParams& pr, SlotGeometry& out)
 {
     constexpr int kParamWarp = 32, kMaxThreads = 1024;
-    const auto opt = [&](const char* n, int& v) {
-        if (!pr.has(n)) return false;
-        v = pr.at(n).curr();
-        return true;
-    };
+    // pr.at() throws std::out_of_range for a missing name, caught below as the reference does
+    const auto req = [&](const char* n) { return (long long)pr.at(n).curr(); };
     const auto threads = [&](const char* n) {
-        int v = 0;
-        return !opt(n, v) || (v >= kParamWarp && v <= kMaxThreads);
+        const long long v = req(n);
+        return v >= kParamWarp && v <= kMaxThreads;
     };
-    const auto atLeast1 = [&](const char* n) {
-        int v = 0;
-        return !opt(n, v) || v >= 1;
-    };
+    const auto atLeast1 = [&](const char* n) { return req(n) >= 1; };
     const auto warpMultiple = [&](const char* n) {
-        int v = 0;
-        return !opt(n, v) || (v >= 1 && v % kParamWarp == 0);
+        const long long v = req(n);
+        return v >= 1 && v % kParamWarp == 0;
     };
     const auto nearest16 = [](long long w) { return (int)std::max<long long>(64, ((w + 8) / 16) * 16); };
     out = SlotGeometry {};
@@ -193,30 +188,36 @@ NwStat slotGeometry(const std::string& slot, const NwAlgParams& pr, SlotGeometry
     {
         if (slot == "NwAlign_Gpu1_Ml_Diag") return threads("threadsPerBlock") ? NwStat::success : bad;
         if (slot == "NwAlign_Gpu2_Ml_DiagRow2Pass")
-            return atLeast1("tileBx") && atLeast1("tileBy") && threads("threadsPerBlock") ? NwStat::success : bad;
-        if (slot == "NwAlign_Gpu3_Ml_DiagDiag") return threads("threadsPerBlockA") && atLeast1("tileBx") ? NwStat::success : bad;
+        {
+            const bool ok = atLeast1("tileBx") && atLeast1("tileBy");
+            return ok && threads("threadsPerBlock") ? NwStat::success : bad;
+        }
+        if (slot == "NwAlign_Gpu3_Ml_DiagDiag")
+        {
+            const bool ok = threads("threadsPerBlockA");
+            return ok && atLeast1("tileBx") ? NwStat::success : bad;
+        }
         if (slot == "NwAlign_Gpu4_Ml_DiagDiag2Pass" || slot == "NwAlign_Gpu6_Coop_DiagDiag2Pass")
-            return warpMultiple("tileAx") && atLeast1("tileAy") && atLeast1("tileBx") ? NwStat::success : bad;
+        {
+            // all three are read before any is checked (gpu4:294-296)
+            const long long ax = req("tileAx"), ay = req("tileAy"), bx = req("tileBx");
+            return ax >= 1 && ay >= 1 && bx >= 1 && warpMultiple("tileAx") ? NwStat::success : bad;
+        }
         if (slot == "NwAlign_Gpu5_Coop_DiagDiag") return atLeast1("tileAx") ? NwStat::success : bad;
         if (slot == "NwAlign_Amd_Strip_Full") return NwStat::success;
         out.sparse = true;
-        int v = 256;
         if (slot == "NwAlign_Gpu7_Mlsp_DiagDiag" || slot == "NwAlign_Gpu8_Mlsp_DiagDiag")
         {
-            if (!threads("threadsPerBlockA") || !atLeast1("warpDivFactorB") || !atLeast1("tileBx")) return bad;
-            if (opt("tileBx", v)) v = nearest16(v);
-            out.tileBx = v;
+            const long long tpb = req("threadsPerBlockA"), bx = req("tileBx"), wdf = req("warpDivFactorB");
+            if (tpb < kParamWarp || tpb > kMaxThreads || bx < 1 || wdf < 1) return bad;
+            out.tileBx = nearest16(bx);
             return NwStat::success;
         }
-        const bool gpu9 = slot == "NwAlign_Gpu9_Mlsp_DiagDiagDiag";
-        if (!gpu9 && slot != "NwAlign_Amd_Strip_Mlsp" && slot != "NwAlign_Amd_Strip_Mlsppt") return bad;
-        const int nSub = (int)pr.has("subtileRows") + (int)pr.has("subtileCols") + (int)pr.has("subtileBx");
-        if (gpu9 && nSub > 0)
+        if (slot == "NwAlign_Gpu9_Mlsp_DiagDiagDiag")
         {
-            if (nSub != 3 || pr.has("tileBx") || !threads("threadsPerBlockA")) return bad;
-            const long long rows = pr.at("subtileRows").curr(), cols = pr.at("subtileCols").curr();
-            const long long sbx = pr.at("subtileBx").curr();
-            if (rows < 1 || cols < 1 || sbx < 1) return bad;
+            const long long tpb = req("threadsPerBlockA"), rows = req("subtileRows"), cols = req("subtileCols");
+            const long long sbx = req("subtileBx");
+            if (rows < 1 || cols < 1 || sbx < 1 || tpb < kParamWarp || tpb > kMaxThreads) return bad;
             const long long tileBy = rows * kParamWarp;
             const long long k = (cols * sbx + tileBy - 1 + sbx - 1) / sbx;
             const long long tileBx = k * sbx - (tileBy - 1);
@@ -224,8 +225,13 @@ NwStat slotGeometry(const std::string& slot, const NwAlgParams& pr, SlotGeometry
             out.tileBx = nearest16(tileBx);
             return NwStat::success;
         }
-        if (!threads("threadsPerBlockA")) return bad;
-        if (opt("tileBx", v) && (v < 64 || v % 16 != 0)) return bad;
+        if (slot != "NwAlign_Amd_Strip_Mlsp" && slot != "NwAlign_Amd_Strip_Mlsppt") return bad;
+        int v = 256;
+        if (pr.has("tileBx"))
+        {
+            v = pr.at("tileBx").curr();
+            if (v < 64 || v % 16 != 0) return bad;
+        }
         out.tileBx = v;
         return NwStat::success;
     }

@@ -6,6 +6,7 @@
 #include <cstdio>
 #include <map>
 #include <thread>
+#include <vector>
 
 #include "nw_host.hpp"
 
@@ -56,24 +57,53 @@ int main()
         {"NwAlign_Gpu7_Mlsp_DiagDiag", params({{"threadsPerBlockA", 96}, {"tileBx", 70}, {"warpDivFactorB", 1}}), NwStat::success, 64},
         {"NwAlign_Gpu8_Mlsp_DiagDiag", params({{"threadsPerBlockA", 160}, {"tileBx", 76}, {"warpDivFactorB", 1}}), NwStat::success, 80},
         {"NwAlign_Gpu9_Mlsp_DiagDiagDiag", params({{"threadsPerBlockA", 128}, {"subtileRows", 4}, {"subtileCols", 4}, {"subtileBx", 48}}), NwStat::success, 208},
-        // this engine's own form and defaults
-        {"NwAlign_Gpu9_Mlsp_DiagDiagDiag", params({{"tileBx", 512}}), NwStat::success, 512},
-        {"NwAlign_Gpu9_Mlsp_DiagDiagDiag", params({}), NwStat::success, 256},
-        {"NwAlign_Amd_Strip_Mlsp", params({{"tileBx", 128}}), NwStat::success, 128},
-        {"NwAlign_Gpu3_Ml_DiagDiag", params({}), NwStat::success, 0},
+        // this engine's own slots: tileBx with a default of 256
+        {"NwAlign_Amd_Strip_Mlsp", params({{"tileBx", 512}}), NwStat::success, 512},
+        {"NwAlign_Amd_Strip_Mlsp", params({}), NwStat::success, 256},
+        {"NwAlign_Amd_Strip_Mlsppt", params({{"tileBx", 128}}), NwStat::success, 128},
+        {"NwAlign_Amd_Strip_Full", params({}), NwStat::success, 0},
         // rejected as the reference rejects them
-        {"NwAlign_Gpu9_Mlsp_DiagDiagDiag", params({{"tileBx", 100}}), NwStat::errorInvalidValue, 0},
+        {"NwAlign_Amd_Strip_Mlsp", params({{"tileBx", 100}}), NwStat::errorInvalidValue, 0},
         {"NwAlign_Amd_Strip_Mlsppt", params({{"tileBx", 48}}), NwStat::errorInvalidValue, 0},
-        {"NwAlign_Gpu9_Mlsp_DiagDiagDiag", params({{"subtileRows", 4}, {"subtileCols", 4}, {"subtileBx", 16}}), NwStat::errorInvalidValue, 0},
-        {"NwAlign_Gpu9_Mlsp_DiagDiagDiag", params({{"subtileRows", 4}, {"subtileBx", 48}}), NwStat::errorInvalidValue, 0},
+        {"NwAlign_Gpu9_Mlsp_DiagDiagDiag", params({{"threadsPerBlockA", 128}, {"subtileRows", 4}, {"subtileCols", 4}, {"subtileBx", 16}}), NwStat::errorInvalidValue, 0},
         {"NwAlign_Gpu9_Mlsp_DiagDiagDiag", params({{"threadsPerBlockA", 2048}, {"subtileRows", 1}, {"subtileCols", 1}, {"subtileBx", 64}}), NwStat::errorInvalidValue, 0},
         {"NwAlign_Gpu7_Mlsp_DiagDiag", params({{"threadsPerBlockA", 96}, {"tileBx", 0}, {"warpDivFactorB", 1}}), NwStat::errorInvalidValue, 0},
-        {"NwAlign_Gpu8_Mlsp_DiagDiag", params({{"threadsPerBlockA", 16}, {"tileBx", 76}}), NwStat::errorInvalidValue, 0},
+        {"NwAlign_Gpu8_Mlsp_DiagDiag", params({{"threadsPerBlockA", 16}, {"tileBx", 76}, {"warpDivFactorB", 1}}), NwStat::errorInvalidValue, 0},
         {"NwAlign_Gpu4_Ml_DiagDiag2Pass", params({{"tileAx", 100}, {"tileAy", 32}, {"tileBx", 52}}), NwStat::errorInvalidValue, 0},
         {"NwAlign_Gpu1_Ml_Diag", params({{"threadsPerBlock", 2000}}), NwStat::errorInvalidValue, 0},
         {"NwAlign_Gpu5_Coop_DiagDiag", params({{"tileAx", -1}}), NwStat::errorInvalidValue, 0},
     };
-    for (const Case& c : cases)
+    // a parameter the reference slot reads with pr.at() and the file does not list: the slot throws
+    // and returns errorInvalidValue (nwalign_gpu9_mlsp_diagdiagdiag.cu:384-387,411-414, gpu3:299-300,
+    // gpu7:307-309, gpu8:327-329 and the others); every required name is dropped in turn from the
+    // slot's param_best.json entry
+    std::vector<Case> all(std::begin(cases), std::end(cases));
+    const std::vector<std::pair<const char*, std::vector<std::pair<const char*, int>>>> best = {
+        {"NwAlign_Gpu1_Ml_Diag", {{"threadsPerBlock", 64}}},
+        {"NwAlign_Gpu2_Ml_DiagRow2Pass", {{"tileBx", 8}, {"tileBy", 4}, {"threadsPerBlock", 64}}},
+        {"NwAlign_Gpu3_Ml_DiagDiag", {{"threadsPerBlockA", 96}, {"tileBx", 54}}},
+        {"NwAlign_Gpu4_Ml_DiagDiag2Pass", {{"tileAx", 384}, {"tileAy", 32}, {"tileBx", 52}}},
+        {"NwAlign_Gpu5_Coop_DiagDiag", {{"tileAx", 52}}},
+        {"NwAlign_Gpu6_Coop_DiagDiag2Pass", {{"tileAx", 192}, {"tileAy", 128}, {"tileBx", 66}}},
+        {"NwAlign_Gpu7_Mlsp_DiagDiag", {{"threadsPerBlockA", 96}, {"tileBx", 70}, {"warpDivFactorB", 1}}},
+        {"NwAlign_Gpu8_Mlsp_DiagDiag", {{"threadsPerBlockA", 160}, {"tileBx", 76}, {"warpDivFactorB", 1}}},
+        {"NwAlign_Gpu9_Mlsp_DiagDiagDiag", {{"threadsPerBlockA", 128}, {"subtileRows", 4}, {"subtileCols", 4}, {"subtileBx", 48}}},
+    };
+    int missingCases = 0;
+    for (const auto& [slot, kv] : best)
+    {
+        all.push_back({slot, params({}), NwStat::errorInvalidValue, 0});
+        for (size_t drop = 0; drop < kv.size(); ++drop)
+        {
+            NwAlgParams p;
+            for (size_t i = 0; i < kv.size(); ++i)
+                if (i != drop) p.params.push_back({kv[i].first, NwAlgParam {{kv[i].second}, 0}});
+            all.push_back({slot, p, NwStat::errorInvalidValue, 0});
+            ++missingCases;
+        }
+    }
+    if (missingCases != 23) { std::printf("missing-parameter cases: %d, want 23\n", missingCases); ++bad; }
+    for (const Case& c : all)
     {
         SlotGeometry geo;
         const NwStat st = slotGeometry(c.slot, c.pr, geo);

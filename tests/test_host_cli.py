@@ -77,13 +77,13 @@ def test_dry_run_ranges_and_default_pairs(gsa_nw, tmp_path):
 
 def test_param_combinations(gsa_nw, tmp_path):
     pj = tmp_path / "params.json"
-    pj.write_text('// comment allowed\n{"NwAlign_Gpu9_Mlsp_DiagDiagDiag": {"tileBx": [64, 128, 256], "x": [1, 2]},\n'
-                  ' "NwAlign_Gpu3_Ml_DiagDiag": {}}')
+    pj.write_text('// comment allowed\n{"NwAlign_Amd_Strip_Mlsp": {"tileBx": [64, 128, 256], "x": [1, 2]},\n'
+                  ' "NwAlign_Gpu3_Ml_DiagDiag": {"threadsPerBlockA": [96], "tileBx": [54]}}')
     r = run(gsa_nw, "-b", os.path.join(RES, "subst.json"), "-r", str(pj), "-s", os.path.join(RES, "seq_generated.fa"),
             "--dryRun")
     assert r.returncode == 0, r.stderr
     combos = {l.split()[1]: int(l.split()[3]) for l in r.stdout.splitlines() if l.startswith("alg ")}
-    assert combos == {"NwAlign_Gpu9_Mlsp_DiagDiagDiag": 6, "NwAlign_Gpu3_Ml_DiagDiag": 1}
+    assert combos == {"NwAlign_Amd_Strip_Mlsp": 6, "NwAlign_Gpu3_Ml_DiagDiag": 1}
 
 
 @pytest.mark.parametrize("content,what", [
@@ -126,15 +126,19 @@ def test_known_answers_end_to_end(gsa_nw, tmp_path):
     pf = tmp_path / "pairs.txt"
     pf.write_text("".join(c["pair"] + "\n" for c in known["cases"][:5]))
     pj = tmp_path / "params.json"
-    pj.write_text('{"NwAlign_Gpu3_Ml_DiagDiag": {}, "NwAlign_Gpu9_Mlsp_DiagDiagDiag": {"tileBx": [256, 64]},'
-                  ' "NwAlign_Amd_Strip_Mlsppt": {"tileBx": [128]}}')
+    # the reference's slots with their param_best.json entries (every parameter they read is
+    # required), this engine's slots with their own tile widths
+    pj.write_text('{"NwAlign_Gpu3_Ml_DiagDiag": {"threadsPerBlockA": [96], "tileBx": [54]},'
+                  ' "NwAlign_Gpu9_Mlsp_DiagDiagDiag": {"threadsPerBlockA": [128], "subtileRows": [4],'
+                  ' "subtileCols": [4], "subtileBx": [48]},'
+                  ' "NwAlign_Amd_Strip_Mlsp": {"tileBx": [256, 64]}, "NwAlign_Amd_Strip_Mlsppt": {"tileBx": [128]}}')
     out = tmp_path / "res.tsv"
     r = run(gsa_nw, "-b", os.path.join(RES, "subst.json"), "-r", str(pj), "-s", os.path.join(RES, "seq_generated.fa"),
             "-p", str(pf), "-o", str(out), "--fCalcScoreHash", "--fCalcTrace", "--warmupPerAlign", "1",
             "--samplesPerAlign", "2")
     assert r.returncode == 0, r.stderr
     rows = list(csv.DictReader(open(out), delimiter="\t"))
-    assert len(rows) == 5 * 4
+    assert len(rows) == 5 * 5
     by = {}
     for row in rows:
         assert row["err_step"] == "0" and row["nw_stat"] == "0"
