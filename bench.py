@@ -419,6 +419,61 @@ def bench_config5(dev, eng, steps, warmup, cpu_sample, rank, world):
             "modes": out}
 
 
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def launch_ranks(gpus):
+    """--gpus N and the process layout, settled before any GPU call.  Under a launcher (WORLD_SIZE
+    set) the launcher's world must equal --gpus, else exit 2: a line must never say N GPUs for a
+    different number of ranks.  Without one, --gpus N > 1 starts N ranks itself, one process per
+    GPU, through torch.distributed.run on 127.0.0.1 (a child process: this one never initialises
+    the GPU), and returns the child's exit code.  None: go on as this rank."""
+    if gpus < 1:
+        print(f"bench.py: --gpus {gpus} < 1", file=sys.stderr)
+        return 2
+    ws = os.environ.get("WORLD_SIZE")
+    if ws is not None:
+        if int(ws) != gpus:
+            print(f"bench.py: --gpus {gpus} but WORLD_SIZE={ws}: the launcher started a different number of ranks",
+                  file=sys.stderr)
+            return 2
+        return None
+    if gpus == 1:
+        return None
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+def ranks_probe():
+    """--ranks-probe: the ranks this invocation runs, gathered over gloo (CPU only), one JSON line
+    from rank 0 with the same n_gpus the bench line would carry."""
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    ranks = [rank]
+    if world > 1:
+        dist.init_process_group("gloo")
+        t = torch.tensor([rank, int(os.environ.get("LOCAL_RANK", "0")), os.getpid()], dtype=torch.int64)
+        lst = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(lst, t)
+        ranks = [int(v[0]) for v in lst]
+        pids = len({int(v[2]) for v in lst})
+        dist.destroy_process_group()
+    else:
+        pids = 1
+    if rank == 0:
+        print(json.dumps({"probe": True, "n_gpus": gpu_fields(world)["n_gpus"], "world": world, "ranks": ranks,
+                          "processes": pids}), flush=True)
+    return 0
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -432,10 +487,18 @@ def main():
     ap.add_argument("--full-batch-pairs", type=int, default=64, help="0 = skip the full-matrix batch field")
     ap.add_argument("--no-config5", action="store_true", help="skip the configs[4] score-only field")
     ap.add_argument("--config5-cpu-sample", type=int, default=50000, help="n x n prefix for the config-5 CPU leg")
+    ap.add_argument("--ranks-probe", action="store_true",
+                    help="test aid: start the ranks (gloo), gather them and print the n_gpus/ranks line; no GPU")
     a = ap.parse_args()
+
+    code = launch_ranks(a.gpus)  # before anything touches the GPU
+    if code is not None:
+        sys.exit(code)
 
     import torch
     import torch.distributed as dist
+    if a.ranks_probe:
+        sys.exit(ranks_probe())
     import gpuseqalign_amd as gsa
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
