@@ -317,8 +317,9 @@ def bench_full_batch(world, rank, local, n_pairs):
     from gpuseqalign_amd import shard
     pairs = shard.synthetic_batch(n_pairs, 18000, 22000, seed0=1000)
     sub = subst_blosum62()
+    tm = {}
     rep = shard.shard_align(pairs, sub, -11, shard.gpu_batch_align(device=local, mode="full", warmup=1, repeats=3,
-                                                                out_budget_bytes=int(0.9 * 140e9)),
+                                                                out_budget_bytes=int(0.9 * 140e9), timing=tm),
                             device=f"cuda:{local}" if world > 1 and not REHEARSE else None)
     gold = load_golden("config4_pairs.json")
     costs = [r.align_cost for r in rep.results]
@@ -334,7 +335,25 @@ def bench_full_batch(world, rank, local, n_pairs):
             "hbm_write_GBps": round(gbps * world, 1), "hbm_frac": round(gbps / PEAK_HBM_GBPS, 4),
             "bound": "hbm (4 B written per cell; MI355X 8 TB/s spec)",
             "pmc_write_over_algorithmic": pmc_write_ratio(n_pairs, full_kernel_name(False)),
+            "passes": pass_fields(tm, out_bytes / world),
             "pairs": n_pairs, "pairs_matching_golden": match}
+
+
+def pass_fields(tm, rank_bytes):
+    """This rank's last timed launch, pass by pass (HIP events on the launch stream,
+    gsa_last_full_timing), and pass 2's effective shader clock (per-workgroup s_memtime /
+    s_memrealtime): pass 2 alone is HBM-write bound, and its rate follows the clock the box runs."""
+    if not tm:
+        return None
+    out = dict(tm)
+    p1, p2 = tm.get("pass1_ms"), tm.get("pass2_ms")
+    if p2:
+        out["pass2_write_GBps"] = round(rank_bytes / (p2 * 1e-3) / 1e9, 1)
+        out["pass2_hbm_frac"] = round(rank_bytes / (p2 * 1e-3) / 1e9 / PEAK_HBM_GBPS, 4)
+    if p1 is not None and p2:
+        out["pass1_share"] = round(p1 / (p1 + p2), 4)
+    out["nominal_clock_ghz"] = CLOCK_GHZ
+    return out
 
 
 def pmc_write_ratio(n_pairs, kernel):

@@ -92,6 +92,13 @@ class MemStats(ctypes.Structure):
         return {k: int(getattr(self, k)) for k, _ in self._fields_}
 
 
+class FullTiming(ctypes.Structure):
+    """gsa_full_timing (include/gsa.h): pass times and pass 2's effective shader clock."""
+    _fields_ = [("pass1_ms", ctypes.c_float), ("pass2_ms", ctypes.c_float),
+                ("clock_ghz_median", ctypes.c_float), ("clock_ghz_mean", ctypes.c_float),
+                ("workgroups", ctypes.c_int64), ("fused", ctypes.c_int32), ("pad", ctypes.c_int32)]
+
+
 class ScoreResult(ctypes.Structure):
     """gsa_score_result (include/gsa.h)."""
     _fields_ = [("score", ctypes.c_int32), ("i_end", ctypes.c_int64), ("j_end", ctypes.c_int64),
@@ -113,6 +120,8 @@ SIGNATURES = {
     "gsa_version": (ctypes.c_char_p, []),
     "gsa_debug_stamps": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64)]),
     "gsa_set_lap_callback": (ctypes.c_int, [_vp, _vp, _vp]),
+    "gsa_set_full_timing": (ctypes.c_int, [_vp, _i32]),
+    "gsa_last_full_timing": (ctypes.c_int, [_vp, ctypes.POINTER(FullTiming)]),
     "gsa_sparse_tile_by": (_i32, []),
     "gsa_sparse_geometry": (ctypes.c_int, [_i32, _i32, _i32, ctypes.POINTER(SparseGeom)]),
     "gsa_fill_full_dev": (ctypes.c_int, [_vp, _vp, _i32, _vp, _i32, _vp, _i32, _i32, _vp, _vp]),
@@ -353,6 +362,21 @@ class Engine:
         if n.value:
             self._check(lib().gsa_debug_stamps(self._h, out.ctypes.data, n.value, ctypes.byref(n)), "gsa_debug_stamps")
         return out
+
+    def set_full_timing(self, on: bool = True):
+        """Events around the passes of every two-pass full fill and pass 2's clock stamps
+        (gsa_set_full_timing; a measurement aid)."""
+        self._check(lib().gsa_set_full_timing(self._h, 1 if on else 0), "gsa_set_full_timing")
+
+    def last_full_timing(self) -> dict:
+        """The last timed full fill (gsa_last_full_timing): pass1_ms, pass2_ms (HIP events; a fused
+        fill: pass1_ms None, the launch in pass2_ms), pass 2's effective clock in GHz (median over
+        workgroups and cycle-weighted mean of s_memtime / s_memrealtime), waits for that fill."""
+        t = FullTiming()
+        self._check(lib().gsa_last_full_timing(self._h, ctypes.byref(t)), "gsa_last_full_timing")
+        f = lambda v: None if v < 0 else round(float(v), 4)
+        return {"pass1_ms": f(t.pass1_ms), "pass2_ms": f(t.pass2_ms), "clock_ghz_median": f(t.clock_ghz_median),
+                "clock_ghz_mean": f(t.clock_ghz_mean), "clock_workgroups": int(t.workgroups), "fused": bool(t.fused)}
 
     def set_lap_callback(self, fn: Optional[Callable[[str], None]]):
         """fn(lap_name) at every phase boundary of the host-buffer entry points (align_full,

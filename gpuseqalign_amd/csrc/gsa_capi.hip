@@ -71,6 +71,14 @@ struct gsa_ctx
     // GSA_STAMPS=1: the fused fill's stamps of the last launch (gsa_debug_stamps)
     unsigned long long* stamps = nullptr;
     size_t stamps_cap = 0, stamps_n = 0;
+    hipStream_t stamps_stream = nullptr;  // the stream of the launch that wrote them
+    // gsa_set_full_timing: events around the passes of the last two-pass full fill and the
+    // expansion's per-workgroup clock stamps
+    bool timing = false;
+    hipEvent_t pev[3] = {nullptr, nullptr, nullptr};
+    unsigned long long* clk = nullptr;
+    size_t clk_cap = 0, clk_n = 0;
+    int timing_state = 0;  // 0 none, 1 two launches (events + stamps), 2 fused (one launch)
     void* expin[kStage] = {nullptr, nullptr, nullptr, nullptr};
     size_t expin_cap[kStage] = {0, 0, 0, 0};
     hipEvent_t expin_ev[kStage] = {nullptr, nullptr, nullptr, nullptr};
@@ -615,6 +623,9 @@ int enqueue_batch(gsa_ctx* ctx, int mode, int npairs, const gsa_pair_dev* pairs,
                 if (ctx->stamps_cap < n)
                 {
                     if (ctx->stamps) (void)hipFree(ctx->stamps);
+    if (ctx->clk) (void)hipFree(ctx->clk);
+    for (hipEvent_t ev : ctx->pev)
+        if (ev) (void)hipEventDestroy(ev);
                     ctx->stamps = nullptr;
                     ctx->stamps_cap = 0;
                     if ((e = hipMalloc(&ctx->stamps, n * sizeof(unsigned long long))) != hipSuccess)
@@ -625,6 +636,7 @@ int enqueue_batch(gsa_ctx* ctx, int mode, int npairs, const gsa_pair_dev* pairs,
                     return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
                 a.stamps = ctx->stamps;
                 ctx->stamps_n = n;
+                ctx->stamps_stream = st;
             }
         }
         a.xdone = ctx->xdone;
@@ -651,6 +663,11 @@ int enqueue_fill(gsa_ctx* ctx, int mode, const int32_t* seqY, int32_t adjrows, c
     gsa_pair_dev p {seqY, adjrows, seqX, adjcols, score, hrow, hcol};
     return enqueue_batch(ctx, mode, 1, &p, subst, substsz, gapo, tileBx, st, done, ptChunk, ld);
 }
+
+// enqueue_full_twopass's answer when its pass-1 scratch (header rows and columns plus every 64th
+// row, ~2 % of the matrix) does not fit next to the caller's matrix: enqueue_full then runs the
+// one-pass lane fill, which needs no scratch
+constexpr int kNoScratch = -1000;
 
 // Full fills in two passes (nw_expand.h): pass 1 = the K-rows sparse fill of every pair with tile
 // width kExpTW, which also keeps rows 64m (XR instance), into the context's scratch; pass 2 =
@@ -740,7 +757,10 @@ int enqueue_full_twopass(gsa_ctx* ctx, int npairs, const gsa_pair_dev* pairs, co
         ctx->exbuf = nullptr;
         ctx->excap = 0;
         if ((e = hipMalloc(&ctx->exbuf, std::max<size_t>(bytes, 256))) != hipSuccess)
-            return fail(ctx, e, GSA_ERROR_MEMORY_ALLOCATION);
+        {
+            (void)hipGetLastError();  // the caller falls back to the one-pass lane fill
+            return kNoScratch;
+        }
         ctx->excap = std::max<size_t>(bytes, 256);
     }
     char* base = (char*)ctx->exbuf;
@@ -814,13 +834,44 @@ int enqueue_full_twopass(gsa_ctx* ctx, int npairs, const gsa_pair_dev* pairs, co
     xa.mt = xmt;
     // fused batches: GSA_FUSED_P1 workgroups take the pass-1 tickets first (a single pair: all)
     const FusedLaunch fl {&xa, ns, fusedW, npairs == 1 ? (1 << 30) : std::max(1, env_int("GSA_FUSED_P1", 128))};
+    // gsa_set_full_timing: events before pass 1, between the passes and after pass 2, and the
+    // expansion's clock stamps (one per workgroup)
+    const bool timed = ctx->timing;
+    ctx->timing_state = 0;
+    if (timed && !fused && xGrid == 0)
+    {
+        if (ctx->clk_cap < (size_t)tasks || !ctx->clk)
+        {
+            if (ctx->clk) (void)hipFree(ctx->clk);
+            ctx->clk = nullptr;
+            ctx->clk_cap = 0;
+            if ((e = hipMalloc(&ctx->clk, (size_t)std::max<long long>(tasks, 1024) * 8)) != hipSuccess)
+                return fail(ctx, e, GSA_ERROR_MEMORY_ALLOCATION);
+            ctx->clk_cap = (size_t)std::max<long long>(tasks, 1024);
+        }
+        xa.clk = ctx->clk;
+        ctx->clk_n = (size_t)tasks;
+    }
+    if (timed && (e = hipEventRecord(ctx->pev[0], st)) != hipSuccess) return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
     int s = enqueue_batch(ctx, gsa::kModeSparse, npairs, p1.data(), subst, substsz, gapo, gsa::kExpHB, st, nullptr, 0,
                           nullptr, rows.data(), fused ? &fl : nullptr);
-    if (s != GSA_SUCCESS || fused) return s;
+    if (s != GSA_SUCCESS) return s;
+    if (fused)
+    {
+        if (timed && (e = hipEventRecord(ctx->pev[2], st)) != hipSuccess) return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
+        ctx->timing_state = timed ? 2 : 0;
+        return s;
+    }
+    if (timed && (e = hipEventRecord(ctx->pev[1], st)) != hipSuccess) return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
     xa.counter = ctx->ctl + 4;
     if (xGrid > 0 && (e = hipMemsetAsync(xa.counter, 0, 4, st)) != hipSuccess) return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
     if ((e = gsa::launch_expand(xa, st, xWaves, xGrid)) != hipSuccess) return fail(ctx, e, GSA_ERROR_KERNEL_FAILURE);
     note_launch(ctx);
+    if (timed)
+    {
+        if ((e = hipEventRecord(ctx->pev[2], st)) != hipSuccess) return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
+        ctx->timing_state = 1;
+    }
     return GSA_SUCCESS;
 }
 
@@ -830,6 +881,19 @@ bool full_twopass(int)
 {
     const char* e = std::getenv("GSA_FULL_KERNEL");
     return !(e && std::strcmp(e, "lane") == 0);
+}
+
+// every full fill: the two-pass fill, or the lane fill (GSA_FULL_KERNEL=lane, or no room for the
+// two-pass scratch); lds: row pitches (null: unpadded)
+int enqueue_full(gsa_ctx* ctx, int npairs, const gsa_pair_dev* pairs, const int32_t* lds, const int32_t* subst,
+                 int32_t substsz, int32_t gapo, hipStream_t st)
+{
+    if (full_twopass(npairs))
+    {
+        const int s = enqueue_full_twopass(ctx, npairs, pairs, lds, subst, substsz, gapo, st);
+        if (s != kNoScratch) return s;
+    }
+    return enqueue_batch(ctx, gsa::kModeFull, npairs, pairs, subst, substsz, gapo, 0, st, nullptr, 0, lds);
 }
 
 }  // namespace
@@ -845,11 +909,64 @@ int gsa_debug_stamps(gsa_ctx* ctx, uint64_t* out, int64_t cap, int64_t* n)
     if (!ctx || !n) return GSA_ERROR_INVALID_VALUE;
     *n = (int64_t)ctx->stamps_n;
     if (ctx->stamps_n == 0 || !out) return GSA_SUCCESS;
-    if (cap < (int64_t)ctx->stamps_n) return GSA_ERROR_MEMORY_ALLOCATION;
+    if (cap < (int64_t)ctx->stamps_n) return GSA_ERROR_INVALID_VALUE;
     hipError_t e = hipSetDevice(ctx->device);
-    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stamps_stream);  // the launch's stream only
     if (e == hipSuccess) e = hipMemcpy(out, ctx->stamps, ctx->stamps_n * sizeof(uint64_t), hipMemcpyDeviceToHost);
     return e == hipSuccess ? GSA_SUCCESS : fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
+}
+
+int gsa_set_full_timing(gsa_ctx* ctx, int32_t on)
+{
+    if (!ctx) return GSA_ERROR_INVALID_VALUE;
+    if (on && !ctx->pev[0])
+    {
+        hipError_t e = hipSetDevice(ctx->device);
+        for (int k = 0; k < 3 && e == hipSuccess; ++k) e = hipEventCreate(&ctx->pev[k]);
+        if (e != hipSuccess) return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
+    }
+    ctx->timing = on != 0;
+    ctx->timing_state = 0;
+    return GSA_SUCCESS;
+}
+
+int gsa_last_full_timing(gsa_ctx* ctx, gsa_full_timing* out)
+{
+    if (!ctx || !out) return GSA_ERROR_INVALID_VALUE;
+    std::memset(out, 0, sizeof(*out));
+    out->pass1_ms = out->pass2_ms = -1.f;
+    out->clock_ghz_median = out->clock_ghz_mean = -1.f;
+    if (ctx->timing_state == 0) return GSA_ERROR_INVALID_VALUE;  // no timed full fill since timing was set
+    hipError_t e = hipSetDevice(ctx->device);
+    if (e == hipSuccess) e = hipEventSynchronize(ctx->pev[2]);
+    if (e != hipSuccess) return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
+    out->fused = ctx->timing_state == 2;
+    if (out->fused) return hipEventElapsedTime(&out->pass2_ms, ctx->pev[0], ctx->pev[2]) == hipSuccess
+                               ? GSA_SUCCESS : GSA_ERROR_CUDA_GENERAL;
+    if (hipEventElapsedTime(&out->pass1_ms, ctx->pev[0], ctx->pev[1]) != hipSuccess ||
+        hipEventElapsedTime(&out->pass2_ms, ctx->pev[1], ctx->pev[2]) != hipSuccess)
+        return GSA_ERROR_CUDA_GENERAL;
+    if (ctx->clk_n == 0) return GSA_SUCCESS;
+    std::vector<unsigned long long> v(ctx->clk_n);
+    if ((e = hipMemcpy(v.data(), ctx->clk, v.size() * 8, hipMemcpyDeviceToHost)) != hipSuccess)
+        return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
+    std::vector<float> ghz;
+    ghz.reserve(v.size());
+    double cyc = 0, ticks = 0;
+    for (unsigned long long w : v)
+    {
+        const double c = (double)(uint32_t)w, t = (double)(uint32_t)(w >> 32);
+        if (t < 100) continue;  // under 1 us: too short to resolve
+        ghz.push_back((float)(c / t * 0.1));
+        cyc += c;
+        ticks += t;
+    }
+    out->workgroups = (int64_t)ghz.size();
+    if (ghz.empty()) return GSA_SUCCESS;
+    std::nth_element(ghz.begin(), ghz.begin() + ghz.size() / 2, ghz.end());
+    out->clock_ghz_median = ghz[ghz.size() / 2];
+    out->clock_ghz_mean = (float)(cyc / ticks * 0.1);
+    return GSA_SUCCESS;
 }
 
 int gsa_ctx_create(int device, gsa_ctx** out)
@@ -976,19 +1093,15 @@ int gsa_fill_full_dev(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, const 
     if (!ctx || !score) return GSA_ERROR_INVALID_VALUE;
     int s = check_inputs(adjrows, adjcols, substsz);
     if (s != GSA_SUCCESS) return s;
-    if (full_twopass(1))
-    {
-        gsa_pair_dev p {seqY, adjrows, seqX, adjcols, score, nullptr, nullptr};
-        return enqueue_full_twopass(ctx, 1, &p, nullptr, subst, substsz, gapo, pick_stream(ctx, stream));
-    }
-    return enqueue_fill(ctx, gsa::kModeFull, seqY, adjrows, seqX, adjcols, subst, substsz, gapo, score, 0, nullptr,
-                        nullptr, pick_stream(ctx, stream));
+    gsa_pair_dev p {seqY, adjrows, seqX, adjcols, score, nullptr, nullptr};
+    return enqueue_full(ctx, 1, &p, nullptr, subst, substsz, gapo, pick_stream(ctx, stream));
 }
 
 int32_t gsa_full_pitch(int32_t adjcols)
 {
     if (adjcols < 1) return 0;
-    return (int32_t)(32 * (((int64_t)adjcols - 1 + 31) / 32) + 1);
+    const int64_t ld = 32 * (((int64_t)adjcols - 1 + 31) / 32) + 1;
+    return ld > INT32_MAX ? 0 : (int32_t)ld;  // no pitch fits int32 past 2^31 - 32 columns
 }
 
 int32_t gsa_full_base_offset(void) { return 31; }
@@ -1001,13 +1114,8 @@ int gsa_fill_full_pitched_dev(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows
     int s = check_inputs(adjrows, adjcols, substsz);
     if (s != GSA_SUCCESS) return s;
     if (ld < adjcols) return GSA_ERROR_INVALID_VALUE;
-    if (full_twopass(1))
-    {
-        gsa_pair_dev p {seqY, adjrows, seqX, adjcols, score, nullptr, nullptr};
-        return enqueue_full_twopass(ctx, 1, &p, &ld, subst, substsz, gapo, pick_stream(ctx, stream));
-    }
-    return enqueue_fill(ctx, gsa::kModeFull, seqY, adjrows, seqX, adjcols, subst, substsz, gapo, score, 0, nullptr,
-                        nullptr, pick_stream(ctx, stream), nullptr, 0, &ld);
+    gsa_pair_dev p {seqY, adjrows, seqX, adjcols, score, nullptr, nullptr};
+    return enqueue_full(ctx, 1, &p, &ld, subst, substsz, gapo, pick_stream(ctx, stream));
 }
 
 int gsa_fill_sparse_dev(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, const int32_t* seqX, int32_t adjcols,
@@ -1025,17 +1133,14 @@ int gsa_fill_full_batch_dev(gsa_ctx* ctx, int32_t npairs, const gsa_pair_dev* pa
                             int32_t substsz, int32_t gapo, void* stream)
 {
     if (!ctx) return GSA_ERROR_INVALID_VALUE;
-    if (full_twopass(npairs)) return enqueue_full_twopass(ctx, npairs, pairs, nullptr, subst, substsz, gapo, pick_stream(ctx, stream));
-    return enqueue_batch(ctx, gsa::kModeFull, npairs, pairs, subst, substsz, gapo, 0, pick_stream(ctx, stream));
+    return enqueue_full(ctx, npairs, pairs, nullptr, subst, substsz, gapo, pick_stream(ctx, stream));
 }
 
 int gsa_fill_full_batch_pitched_dev(gsa_ctx* ctx, int32_t npairs, const gsa_pair_dev* pairs, const int32_t* lds,
                                     const int32_t* subst, int32_t substsz, int32_t gapo, void* stream)
 {
     if (!ctx || !lds) return GSA_ERROR_INVALID_VALUE;
-    if (full_twopass(npairs)) return enqueue_full_twopass(ctx, npairs, pairs, lds, subst, substsz, gapo, pick_stream(ctx, stream));
-    return enqueue_batch(ctx, gsa::kModeFull, npairs, pairs, subst, substsz, gapo, 0, pick_stream(ctx, stream), nullptr,
-                         0, lds);
+    return enqueue_full(ctx, npairs, pairs, lds, subst, substsz, gapo, pick_stream(ctx, stream));
 }
 
 int gsa_fill_sparse_batch_dev(gsa_ctx* ctx, int32_t npairs, const gsa_pair_dev* pairs, const int32_t* subst,

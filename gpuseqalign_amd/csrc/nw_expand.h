@@ -75,6 +75,9 @@ struct ExpandArgs
     // persistent launches: workgroups claim tasks from *counter (zeroed before the launch)
     unsigned* counter;
     int mt;  // tiles per wave per task: a task is waves x 64 x mt rows of one tile column
+    // measurement (gsa_set_full_timing): per workgroup, wave 0's s_memtime cycles (low word) and
+    // s_memrealtime ticks (100 MHz, high word) from its start to its end; null = off
+    unsigned long long* clk;
 };
 
 size_t expand_lds_bytes(int substsz, int waves);

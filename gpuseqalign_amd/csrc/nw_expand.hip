@@ -36,6 +36,15 @@ __global__ void __launch_bounds__(64 * WAVES, 4) nw_expand_kernel(ExpandArgs a)
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     const int task = blockIdx.x;
+    // effective clock (gsa_set_full_timing): s_memtime counts shader cycles, s_memrealtime 100 MHz
+    // ticks; both scalar reads, waited for here, before any LDS traffic of the task
+    uint64_t c0 = 0, r0 = 0;
+    if (a.clk && w == 0)
+    {
+        c0 = __builtin_amdgcn_s_memtime();
+        r0 = __builtin_amdgcn_s_memrealtime();
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+    }
     int lo = 0, tt = -1;
     if (a.sched)
     {
@@ -57,6 +66,12 @@ __global__ void __launch_bounds__(64 * WAVES, 4) nw_expand_kernel(ExpandArgs a)
     const ExpandPair d = ex_desc(a.pairs + lo);
     if (tt < 0) tt = task - d.taskBase;
     ex_task<WAVES>(a, d, tt, w, lane);
+    if (a.clk && w == 0)
+    {
+        const uint64_t c1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        if (lane == 0) G(a.clk)[task] = (uint64_t)(uint32_t)(c1 - c0) | ((uint64_t)(uint32_t)(r1 - r0) << 32);
+    }
 }
 
 template <int WAVES>

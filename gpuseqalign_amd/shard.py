@@ -131,7 +131,8 @@ def shard_align(pairs: List[Tuple[np.ndarray, np.ndarray]], subst: Optional[np.n
 
 
 def gpu_batch_align(device: int = 0, mode: str = "sparse", tileBx: int = 256, repeats: int = 1,
-                    out_budget_bytes: Optional[int] = None, warmup: int = 0, pitched: bool = True) -> AlignBatchFn:
+                    out_budget_bytes: Optional[int] = None, warmup: int = 0, pitched: bool = True,
+                    timing: Optional[dict] = None) -> AlignBatchFn:
     """The GPU `align_batch` of one rank: inputs uploaded before the timed region, then the
     rank's pairs in as few persistent launches as the output memory allows (one launch for
     the whole share when it fits `out_budget_bytes`, default 60 % of free HBM): the launch's
@@ -140,7 +141,9 @@ def gpu_batch_align(device: int = 0, mode: str = "sparse", tileBx: int = 256, re
     the reference's mlsp align functions, nwalign_gpu9_mlsp_diagdiagdiag.cu:713-716).
     pitched (full mode): each matrix in the engine's fastest device layout (gsa_full_pitch row
     pitch, cell (1, 0) on a 128-byte boundary), as the reference keeps its device matrix padded
-    (nwalign_gpu3_ml_diagdiag.cu:315-325); False: unpadded adjrows x adjcols."""
+    (nwalign_gpu3_ml_diagdiag.cu:315-325); False: unpadded adjrows x adjcols.
+    timing (full mode): a dict that receives the last launch's pass times and pass 2's effective
+    clock (Engine.last_full_timing; the events are recorded in every launch, read once at the end)."""
     import torch
     from . import Engine, sparse_geometry, sparse_align_cost, SparseResult, full_pitch, full_base_offset
 
@@ -202,6 +205,8 @@ def gpu_batch_align(device: int = 0, mode: str = "sparse", tileBx: int = 256, re
             descs.append((d, [lds[j] for j in c] if pit else None))
             # chunk c's pairs are consecutive, so their slices of keepflat are one range
             gathers.append((torch.from_numpy(np.concatenate(gi)).to(dev), keepflat[kbase[c[0]]:kbase[c[-1] + 1]]))
+        if timing is not None and mode != "sparse":
+            eng.set_full_timing(True)
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
         for it in range(max(0, warmup) + max(1, repeats)):
@@ -219,6 +224,8 @@ def gpu_batch_align(device: int = 0, mode: str = "sparse", tileBx: int = 256, re
         eng.sync(stream.cuda_stream)
         torch.cuda.synchronize(dev)
         secs = (time.perf_counter() - t0) / max(1, repeats)
+        if timing is not None and mode != "sparse":
+            timing.update(eng.last_full_timing())
         costs = []
         for j, g in enumerate(geoms):
             v = keep[j].cpu().numpy()

@@ -181,8 +181,27 @@ int gsa_align_sparse_pt(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, cons
 /* Measurement aid, not part of the reference's interface: with GSA_STAMPS=1 in the environment a
  * fused full fill records s_memrealtime stamps (100 MHz): [start, end] per pass-1
  * strip, then [claimed, ready, done] per expansion task.  Copies the last such launch's *n stamps
- * into out (cap >= *n; out may be null to query *n); synchronizes the device. */
+ * into out (cap >= *n, else errorInvalidValue; out may be null to query *n); synchronizes the stream
+ * that launch ran on. */
 int gsa_debug_stamps(gsa_ctx* ctx, uint64_t* out, int64_t cap, int64_t* n);
+
+/* Measurement aid, not part of the reference's interface: with timing on, every two-pass full fill
+ * (gsa_fill_full*_dev) records HIP events before pass 1, between the passes and
+ * after pass 2 on its stream, and pass 2's workgroups record their shader cycles (s_memtime) and
+ * 100 MHz ticks (s_memrealtime) from start to end.  gsa_last_full_timing waits for the last such
+ * fill and returns the pass times and the effective shader clock over pass 2's workgroups (median
+ * and cycle-weighted mean), so a slow box shows as a low clock.  A fused fill (one launch) has
+ * pass1_ms = -1, its whole time in pass2_ms and no clock.  errorInvalidValue: no timed fill. */
+typedef struct gsa_full_timing
+{
+    float pass1_ms, pass2_ms;
+    float clock_ghz_median, clock_ghz_mean;
+    int64_t workgroups;  /* pass-2 workgroups whose clock was resolved (>= 1 us) */
+    int32_t fused;
+    int32_t pad;
+} gsa_full_timing;
+int gsa_set_full_timing(gsa_ctx* ctx, int32_t on);
+int gsa_last_full_timing(gsa_ctx* ctx, gsa_full_timing* out);
 
 /* ---- consumers (host), the reference's L4 ----------------------------------------- */
 /* NwHash1_Plain (src/nwtrace1_plain.cpp:133-154). */

@@ -242,9 +242,10 @@ def test_full_fill_pitched(engine, golden, R, C, pad, off):
 def test_full_pitch_contract(engine):
     """gsa_full_pitch: the smallest ld >= adjcols with ld = 1 (mod 32); a pitch below adjcols is
     rejected with errorInvalidValue."""
-    for ac in (1, 2, 32, 33, 34, 64, 65, 10001, 20001, 20032):
+    for ac in (1, 2, 32, 33, 34, 64, 65, 10001, 20001, 20032, 2**31 - 31):
         ld = gsa.full_pitch(ac)
         assert ld >= ac and ld % 32 == 1 and ld - 32 < ac
+    assert gsa.full_pitch(2**31 - 30) == 0 and gsa.full_pitch(2**31 - 1) == 0  # past int32: no pitch
     assert gsa.full_base_offset() == 31
     import torch
     dev = torch.device("cuda:0")
@@ -254,13 +255,18 @@ def test_full_pitch_contract(engine):
     assert ei.value.stat == gsa.NwStat.errorInvalidValue
 
 
+@pytest.mark.parametrize("pair", ["0", "1"])
 @pytest.mark.parametrize("ns", ["2", "4", "8"])
-def test_full_batch_pitched(engine, golden, ns, monkeypatch):
-    """A batched launch into pitched matrices (gsa_fill_full_batch_pitched_dev), every cell of
-    every pair against the oracle."""
+def test_full_batch_pitched(engine, golden, ns, pair, monkeypatch):
+    """The one-pass lane fill's batch path (GSA_FULL_KERNEL=lane; batches default to the two-pass
+    fill, covered by test_twopass_tables_and_batches) into pitched matrices
+    (gsa_fill_full_batch_pitched_dev) and unpadded ones (shard.gpu_batch_align), with and without
+    paired stores (GSA_LANE_PAIR; NS != 4 always pairs): every cell of every pair against the oracle."""
     import torch
     from gpuseqalign_amd import shard
+    monkeypatch.setenv("GSA_FULL_KERNEL", "lane")
     monkeypatch.setenv("GSA_LANE_NS", ns)
+    monkeypatch.setenv("GSA_LANE_PAIR", pair)
     pairs = [random_pair(r, c, 11 * r + c) for r, c in ((700, 900), (1, 5), (1500, 333), (257, 2049), (64, 64))]
     dev = torch.device("cuda:0")
     s = torch.from_numpy(golden.blosum62).to(dev)
