@@ -96,7 +96,7 @@ class FullTiming(ctypes.Structure):
     """gsa_full_timing (include/gsa.h): pass times and pass 2's effective shader clock."""
     _fields_ = [("pass1_ms", ctypes.c_float), ("pass2_ms", ctypes.c_float),
                 ("clock_ghz_median", ctypes.c_float), ("clock_ghz_mean", ctypes.c_float),
-                ("workgroups", ctypes.c_int64), ("fused", ctypes.c_int32), ("pad", ctypes.c_int32)]
+                ("workgroups", ctypes.c_int64), ("fused", ctypes.c_int32), ("groups", ctypes.c_int32)]
 
 
 class ScoreResult(ctypes.Structure):
@@ -376,7 +376,8 @@ class Engine:
         self._check(lib().gsa_last_full_timing(self._h, ctypes.byref(t)), "gsa_last_full_timing")
         f = lambda v: None if v < 0 else round(float(v), 4)
         return {"pass1_ms": f(t.pass1_ms), "pass2_ms": f(t.pass2_ms), "clock_ghz_median": f(t.clock_ghz_median),
-                "clock_ghz_mean": f(t.clock_ghz_mean), "clock_workgroups": int(t.workgroups), "fused": bool(t.fused)}
+                "clock_ghz_mean": f(t.clock_ghz_mean), "clock_workgroups": int(t.workgroups), "fused": bool(t.fused),
+                "pipelined_groups": int(t.groups)}
 
     def set_lap_callback(self, fn: Optional[Callable[[str], None]]):
         """fn(lap_name) at every phase boundary of the host-buffer entry points (align_full,

@@ -78,7 +78,12 @@ struct gsa_ctx
     hipEvent_t pev[3] = {nullptr, nullptr, nullptr};
     unsigned long long* clk = nullptr;
     size_t clk_cap = 0, clk_n = 0;
-    int timing_state = 0;  // 0 none, 1 two launches (events + stamps), 2 fused (one launch)
+    int timing_state = 0;  // 0 none, 1 two launches (events + stamps), 2 fused (one launch), 3 pipelined
+    int timing_groups = 0;
+    // the pipelined full batch: pass 1 of pair groups 1.. on a stream of its own, one event per group
+    hipStream_t p1stream = nullptr;
+    static constexpr int kMaxGroups = 16;
+    hipEvent_t pipe_ev[kMaxGroups + 1] = {};
     void* expin[kStage] = {nullptr, nullptr, nullptr, nullptr};
     size_t expin_cap[kStage] = {0, 0, 0, 0};
     hipEvent_t expin_ev[kStage] = {nullptr, nullptr, nullptr, nullptr};
@@ -428,7 +433,8 @@ struct FusedLaunch
 // tickets of all pairs (pair-major).  `pairs` holds device pointers.
 int enqueue_batch(gsa_ctx* ctx, int mode, int npairs, const gsa_pair_dev* pairs, const int32_t* subst, int32_t substsz,
                   int32_t gapo, int32_t tileBx, hipStream_t st, unsigned long long* done = nullptr, int ptChunk = 0,
-                  const int32_t* lds = nullptr, int* const* rows64 = nullptr, const FusedLaunch* fused = nullptr)
+                  const int32_t* lds = nullptr, int* const* rows64 = nullptr, const FusedLaunch* fused = nullptr,
+                  bool co = false)
 {
     if (npairs < 1 || !pairs || !subst) return GSA_ERROR_INVALID_VALUE;
     if (substsz < 1 || substsz > 32) return GSA_ERROR_INVALID_VALUE;  // LDS profile holds <= 32 letters
@@ -454,6 +460,7 @@ int enqueue_batch(gsa_ctx* ctx, int mode, int npairs, const gsa_pair_dev* pairs,
     {
         krowK = 4;
         krowNS = fused ? fused->ns : env_int("GSA_KROW_NS", (npairs > 1 && !fitsChip) ? 8 : 4) == 8 ? 8 : 4;
+        if (co) krowK = krowNS = 2;  // the pipelined batch's co-resident instance
     }
     // mlsppt flags one ticket per tile row: only the geometry whose ticket is one tile row
     if (!gsa::krow_ok(krowNS, krowK) || (done && gsa::krow_ticket_rows(krowNS, krowK) != gsa::kSparseTileBy))
@@ -624,6 +631,9 @@ int enqueue_batch(gsa_ctx* ctx, int mode, int npairs, const gsa_pair_dev* pairs,
                 {
                     if (ctx->stamps) (void)hipFree(ctx->stamps);
     if (ctx->clk) (void)hipFree(ctx->clk);
+    for (hipEvent_t ev : ctx->pipe_ev)
+        if (ev) (void)hipEventDestroy(ev);
+    if (ctx->p1stream) (void)hipStreamDestroy(ctx->p1stream);
     for (hipEvent_t ev : ctx->pev)
         if (ev) (void)hipEventDestroy(ev);
                     ctx->stamps = nullptr;
@@ -645,8 +655,11 @@ int enqueue_batch(gsa_ctx* ctx, int mode, int npairs, const gsa_pair_dev* pairs,
     if (e != hipSuccess) return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
     // one pair: one workgroup per CU (its tickets are a chain); a batch: all resident slots
     int grid = (npairs == 1) ? std::max(1, std::min((int)tickets, ctx->cu_count)) : 0;
+    // (the co-resident pass 1: one workgroup per CU, beside an expansion workgroup)
+    if (co) grid = std::max(1, std::min((int)tickets, ctx->cu_count));
     e = lane     ? gsa::launch_lane_fill(a, a.ns, grid, st)
         : fused  ? gsa::launch_full_fused(a, fused->ns, fused->waves, 0, st)
+        : co     ? gsa::launch_krow_fill_co(a, grid, st)
         : rows64 ? gsa::launch_krow_fill_xr(a, krowNS, grid, st)
         : krow   ? gsa::launch_krow_fill(a, krowNS, krowK, 0, grid, st)
                  : gsa::launch_strip_fill(a, mode, grid, st);
@@ -669,6 +682,268 @@ int enqueue_fill(gsa_ctx* ctx, int mode, const int32_t* seqY, int32_t adjrows, c
 // one-pass lane fill, which needs no scratch
 constexpr int kNoScratch = -1000;
 
+// The pipelined full batch: the pairs in G groups (sizes dealt longest first, snake order); group 0's
+// pass 1 runs alone on the whole chip (the XR instance the batch would use), then group g's expansion
+// (persistent 12-wave workgroups, one per CU: 87 KB of LDS, 12 of 16 wave slots) runs on `st` while
+// group g+1's pass 1 runs on the context's p1stream in 4-wave (2, 2) workgroups that fit beside it
+// (74 KB, 4 slots): pass 2 is bound by each CU's store path with its VALU ~15 % busy, so pass 1
+// takes issue slots the expansion leaves idle instead of whole CUs (a CU split or two-stream
+// pipeline of the 16-wave expansion was 15-27 % slower, profiles/r04_probe_q.txt).  Expansion g
+// waits for pass 1 of group g by an event; the kernels never wait on each other inside a launch.
+int enqueue_full_pipelined(gsa_ctx* ctx, int npairs, const gsa_pair_dev* pairs, const int32_t* lds,
+                           const int32_t* subst, int32_t substsz, int32_t gapo, hipStream_t st, int groups)
+{
+    constexpr int kXW = 12;  // expansion waves per workgroup
+    const int G = std::max(2, std::min(groups, std::min(npairs, gsa_ctx::kMaxGroups)));
+    // groups: pairs by cells, dealt in snake order so the groups' cells are even
+    std::vector<int> ord((size_t)npairs);
+    for (int p = 0; p < npairs; ++p) ord[(size_t)p] = p;
+    auto cells = [&](int p) { return (long long)(pairs[p].adjrows - 1) * (long long)(pairs[p].adjcols - 1); };
+    std::stable_sort(ord.begin(), ord.end(), [&](int x, int y) { return cells(x) > cells(y); });
+    std::vector<std::vector<int>> grp((size_t)G);
+    for (int k = 0; k < npairs; ++k)
+    {
+        const int r = k / G, c = k % G;
+        grp[(size_t)((r & 1) ? G - 1 - c : c)].push_back(ord[(size_t)k]);
+    }
+    // per pair: pass-1 geometry (group 0: the batch's XR instance, (8, 4) or (4, 4); others (2, 2)),
+    // scratch offsets, expansion descriptor
+    long long g0Rows = 0;
+    for (int p : grp[0]) g0Rows += std::max(1, (pairs[p].adjrows - 1 + gsa::kSparseTileBy - 1) / gsa::kSparseTileBy);
+    const int ns0 = (grp[0].size() > 1 && g0Rows > (long long)std::max(1, ctx->cu_count)) ? 8 : 4;
+    std::vector<size_t> off((size_t)npairs * 3);
+    std::vector<gsa::ExpandPair> ex((size_t)npairs);
+    std::vector<int> grpOf((size_t)npairs);
+    for (int g = 0; g < G; ++g)
+        for (int p : grp[(size_t)g]) grpOf[(size_t)p] = g;
+    size_t bytes = 0;
+    auto take = [&](size_t b) {
+        const size_t o = bytes;
+        bytes += (b + 255) & ~(size_t)255;
+        return o;
+    };
+    std::vector<long long> granG((size_t)G, 0), tasksG((size_t)G, 0);
+    for (int p = 0; p < npairs; ++p)
+    {
+        const gsa_pair_dev& in = pairs[p];
+        if (in.adjrows < 2 || in.adjcols < 2 || !in.seqY || !in.seqX || !in.score) return GSA_ERROR_INVALID_VALUE;
+        const long long ld = lds ? lds[p] : in.adjcols;
+        if (ld < in.adjcols) return GSA_ERROR_INVALID_VALUE;
+        gsa_sparse_geom geom;
+        int s = gsa_sparse_geometry(in.adjrows, in.adjcols, gsa::kExpHB, &geom);
+        if (s != GSA_SUCCESS) return s;
+        const int g = grpOf[(size_t)p];
+        const int ns = g == 0 ? ns0 : 2, k = g == 0 ? 4 : 2;
+        const int Cp = geom.tileHdrMatCols * gsa::kExpHB;
+        const long long tickets = gsa::krow_tickets(geom.tileHdrMatRows, ns, k);
+        const long long nrows = tickets * ns * k;  // rows 64m written by pass 1, m = 1 .. nrows
+        granG[(size_t)g] += tickets * gsa::gran_stride(Cp);
+        off[3 * p] = take((size_t)geom.hrowElems * 4);
+        off[3 * p + 1] = take((size_t)geom.hcolElems * 4);
+        off[3 * p + 2] = take((size_t)(nrows * gsa::rows64_pitch(Cp)) * 4);
+        gsa::ExpandPair& e = ex[(size_t)p];
+        std::memset(&e, 0, sizeof(e));
+        e.seqY = in.seqY;
+        e.seqX = in.seqX;
+        e.R = in.adjrows - 1;
+        e.C = in.adjcols - 1;
+        e.score = in.score;
+        e.ld = ld;
+        e.rpitch = gsa::rows64_pitch(Cp);
+        e.tcols = geom.tileHdrMatCols;
+        e.colTiles = std::max(1, (e.C + gsa::kExpTW - 1) / gsa::kExpTW);
+        e.lastSplit = e.C - (e.colTiles - 1) * gsa::kExpTW > gsa::kExpHB ? 1 : 0;
+        e.colTiles += e.lastSplit;
+        e.rowChunks = std::max(1, (e.R + kXW * gsa::kExpRows - 1) / (kXW * gsa::kExpRows));
+        e.taskBase = (int)tasksG[(size_t)g];
+        tasksG[(size_t)g] += (long long)e.colTiles * e.rowChunks;
+        if (tasksG[(size_t)g] > (1ll << 30) || tickets > (1ll << 30)) return GSA_ERROR_INVALID_VALUE;
+    }
+    hipError_t e = hipSetDevice(ctx->device);
+    if (e != hipSuccess) return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
+    if (ctx->excap < bytes || !ctx->exbuf)
+    {
+        if (ctx->exbuf) (void)hipFree(ctx->exbuf);
+        ctx->exbuf = nullptr;
+        ctx->excap = 0;
+        if ((e = hipMalloc(&ctx->exbuf, std::max<size_t>(bytes, 256))) != hipSuccess)
+        {
+            (void)hipGetLastError();
+            return kNoScratch;
+        }
+        ctx->excap = std::max<size_t>(bytes, 256);
+    }
+    if (!ctx->p1stream && (e = hipStreamCreateWithFlags(&ctx->p1stream, hipStreamNonBlocking)) != hipSuccess)
+        return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
+    for (int g = 0; g <= G; ++g)
+        if (!ctx->pipe_ev[g] && (e = hipEventCreateWithFlags(&ctx->pipe_ev[g], hipEventDisableTiming)) != hipSuccess)
+            return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
+    // buffers every launch of the pipeline shares, sized once up front (no reallocation while a launch
+    // on the other stream may use them): granules, pass-1 descriptors, expansion descriptors
+    long long granMax = 0, tasksMax = 0;
+    size_t unitsMax = 0;
+    for (int g = 0; g < G; ++g)
+    {
+        granMax = std::max(granMax, granG[(size_t)g]);
+        tasksMax = std::max(tasksMax, tasksG[(size_t)g]);
+        unitsMax = std::max(unitsMax, grp[(size_t)g].size());
+    }
+    int s = ensure_gran(ctx, (size_t)std::max<long long>(granMax, 1), st);
+    if (s != GSA_SUCCESS) return s;
+    // pass-1 descriptors + the round-robin schedule (2 ints per ticket) of the largest group
+    {
+        long long schedMax = 0;
+        for (int g = 0; g < G; ++g)
+        {
+            long long t = 0;
+            for (int p : grp[(size_t)g])
+            {
+                gsa_sparse_geom geom;
+                (void)gsa_sparse_geometry(pairs[p].adjrows, pairs[p].adjcols, gsa::kExpHB, &geom);
+                t += gsa::krow_tickets(geom.tileHdrMatRows, g == 0 ? ns0 : 2, g == 0 ? 4 : 2);
+            }
+            schedMax = std::max(schedMax, t);
+        }
+        const size_t schedUnits = ((size_t)schedMax * 2 * sizeof(int) + sizeof(gsa::PairDesc) - 1) / sizeof(gsa::PairDesc);
+        if ((s = ensure_desc(ctx, unitsMax + schedUnits)) != GSA_SUCCESS) return s;
+    }
+    const size_t descBytesMax = (unitsMax * sizeof(gsa::ExpandPair) + 15) & ~(size_t)15;
+    const size_t exBytesMax = descBytesMax + (size_t)tasksMax * 2 * sizeof(int);
+    if (ctx->exdesc_cap < exBytesMax || !ctx->exdesc)
+    {
+        if (ctx->exdesc) (void)hipFree(ctx->exdesc);
+        ctx->exdesc = nullptr;
+        ctx->exdesc_cap = 0;
+        if ((e = hipMalloc(&ctx->exdesc, std::max<size_t>(exBytesMax, 4096))) != hipSuccess)
+            return fail(ctx, e, GSA_ERROR_MEMORY_ALLOCATION);
+        ctx->exdesc_cap = std::max<size_t>(exBytesMax, 4096);
+    }
+    if (ctx->timing)
+    {
+        const size_t n = (size_t)std::max(1, ctx->cu_count);
+        if (ctx->clk_cap < n || !ctx->clk)
+        {
+            if (ctx->clk) (void)hipFree(ctx->clk);
+            ctx->clk = nullptr;
+            ctx->clk_cap = 0;
+            if ((e = hipMalloc(&ctx->clk, std::max<size_t>(n, 1024) * 8)) != hipSuccess)
+                return fail(ctx, e, GSA_ERROR_MEMORY_ALLOCATION);
+            ctx->clk_cap = std::max<size_t>(n, 1024);
+        }
+    }
+    ctx->timing_state = 0;
+    if (ctx->timing && (e = hipEventRecord(ctx->pev[0], st)) != hipSuccess) return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
+    char* base = (char*)ctx->exbuf;
+    // pass 1 of group g on stream sp (group 0: the caller's stream, alone on the chip)
+    auto pass1 = [&](int g, hipStream_t sp) {
+        const std::vector<int>& gp = grp[(size_t)g];
+        std::vector<gsa_pair_dev> p1(gp.size());
+        std::vector<int*> rows(gp.size());
+        for (size_t i = 0; i < gp.size(); ++i)
+        {
+            const int p = gp[i];
+            p1[i] = pairs[p];
+            p1[i].score = nullptr;
+            p1[i].tileHrowMat = (int32_t*)(base + off[3 * p]);
+            p1[i].tileHcolMat = (int32_t*)(base + off[3 * p + 1]);
+            rows[i] = (int*)(base + off[3 * p + 2]);
+        }
+        return enqueue_batch(ctx, gsa::kModeSparse, (int)gp.size(), p1.data(), subst, substsz, gapo, gsa::kExpHB, sp,
+                             nullptr, 0, nullptr, rows.data(), nullptr, g > 0);
+    };
+    // the expansion of group g on the caller's stream: its descriptors (pair-relative task bases) and
+    // the round-robin task schedule, staged through a pinned slot
+    auto pass2 = [&](int g) {
+        const std::vector<int>& gp = grp[(size_t)g];
+        std::vector<gsa::ExpandPair> xd(gp.size());
+        for (size_t i = 0; i < gp.size(); ++i)
+        {
+            const int p = gp[i];
+            xd[i] = ex[(size_t)p];
+            xd[i].rows64 = (const int*)(base + off[3 * p + 2]);
+            xd[i].hcol = (const int*)(base + off[3 * p + 1]);
+        }
+        std::vector<int> xs;
+        if (gp.size() > 1)
+        {
+            std::vector<int> o(gp.size());
+            for (size_t i = 0; i < gp.size(); ++i) o[i] = (int)i;
+            auto ntask = [&](int i) { return xd[(size_t)i].colTiles * xd[(size_t)i].rowChunks; };
+            std::stable_sort(o.begin(), o.end(), [&](int x, int y) { return ntask(x) > ntask(y); });
+            for (int j = 0; j < ntask(o[0]); ++j)
+                for (int i : o)
+                {
+                    if (ntask(i) <= j) break;
+                    xs.push_back(i);
+                    xs.push_back(j);
+                }
+        }
+        const size_t descBytes = (xd.size() * sizeof(gsa::ExpandPair) + 15) & ~(size_t)15;
+        const size_t exBytes = descBytes + xs.size() * sizeof(int);
+        const int slot = ctx->expin_next;
+        ctx->expin_next = (slot + 1) % gsa_ctx::kStage;
+        hipError_t er = hipSuccess;
+        if (ctx->expin_used[slot] && (er = hipEventSynchronize(ctx->expin_ev[slot])) != hipSuccess)
+            return fail(ctx, er, GSA_ERROR_CUDA_GENERAL);
+        if (ctx->expin_cap[slot] < exBytes)
+        {
+            if (ctx->expin[slot]) (void)hipHostFree(ctx->expin[slot]);
+            ctx->expin[slot] = nullptr;
+            ctx->expin_cap[slot] = 0;
+            if ((er = hipHostMalloc(&ctx->expin[slot], exBytes)) != hipSuccess) return fail(ctx, er, GSA_ERROR_MEMORY_ALLOCATION);
+            ctx->expin_cap[slot] = exBytes;
+        }
+        std::memcpy(ctx->expin[slot], xd.data(), xd.size() * sizeof(gsa::ExpandPair));
+        if (!xs.empty()) std::memcpy((char*)ctx->expin[slot] + descBytes, xs.data(), xs.size() * sizeof(int));
+        er = hipMemcpyAsync(ctx->exdesc, ctx->expin[slot], exBytes, hipMemcpyHostToDevice, st);
+        if (er == hipSuccess) er = hipEventRecord(ctx->expin_ev[slot], st);
+        if (er != hipSuccess) return fail(ctx, er, GSA_ERROR_MEMORY_TRANSFER);
+        ctx->expin_used[slot] = true;
+        gsa::ExpandArgs xa {};
+        xa.subst = subst;
+        xa.substsz = substsz;
+        xa.g = gapo;
+        xa.pairs = (const gsa::ExpandPair*)ctx->exdesc;
+        xa.nPairs = (int)xd.size();
+        xa.nTasks = (int)tasksG[(size_t)g];
+        xa.sched = xs.empty() ? nullptr : (const int*)((char*)ctx->exdesc + descBytes);
+        xa.knob = env_int("GSA_EXPAND_KNOB", 0);
+        xa.mt = 1;
+        xa.counter = ctx->ctl + 4;
+        if (ctx->timing && g == G - 1)
+        {
+            xa.clk = ctx->clk;
+            ctx->clk_n = (size_t)std::min(ctx->cu_count, xa.nTasks);
+        }
+        if ((er = hipMemsetAsync(xa.counter, 0, 4, st)) != hipSuccess) return fail(ctx, er, GSA_ERROR_MEMORY_TRANSFER);
+        if ((er = gsa::launch_expand(xa, st, kXW, ctx->cu_count)) != hipSuccess) return fail(ctx, er, GSA_ERROR_KERNEL_FAILURE);
+        note_launch(ctx);
+        return (int)GSA_SUCCESS;
+    };
+    if ((s = pass1(0, st)) != GSA_SUCCESS) return s;
+    if (ctx->timing && (e = hipEventRecord(ctx->pev[1], st)) != hipSuccess) return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
+    // the side stream starts behind everything on st so far (inputs, granule clear, pass 1 of group 0)
+    if ((e = hipEventRecord(ctx->pipe_ev[0], st)) != hipSuccess || (e = hipStreamWaitEvent(ctx->p1stream, ctx->pipe_ev[0], 0)) != hipSuccess)
+        return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
+    for (int g = 1; g < G; ++g)
+    {
+        if ((s = pass1(g, ctx->p1stream)) != GSA_SUCCESS) return s;
+        if ((e = hipEventRecord(ctx->pipe_ev[g], ctx->p1stream)) != hipSuccess) return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
+    }
+    for (int g = 0; g < G; ++g)
+    {
+        if (g > 0 && (e = hipStreamWaitEvent(st, ctx->pipe_ev[g], 0)) != hipSuccess) return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
+        if ((s = pass2(g)) != GSA_SUCCESS) return s;
+    }
+    if (ctx->timing)
+    {
+        if ((e = hipEventRecord(ctx->pev[2], st)) != hipSuccess) return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
+        ctx->timing_state = 3;
+        ctx->timing_groups = G;
+    }
+    return GSA_SUCCESS;
+}
+
 // Full fills in two passes (nw_expand.h): pass 1 = the K-rows sparse fill of every pair with tile
 // width kExpTW, which also keeps rows 64m (XR instance), into the context's scratch; pass 2 =
 // every 64-row x kExpTW tile of every matrix recomputed from its top row and left column at once.
@@ -690,6 +965,11 @@ int enqueue_full_twopass(gsa_ctx* ctx, int npairs, const gsa_pair_dev* pairs, co
     bool interior = true;
     for (int p = 0; p < npairs; ++p) interior = interior && pairs[p].adjrows > 1 && pairs[p].adjcols > 1;
     const bool fused = interior && (npairs == 1 ? fusedMode >= 1 : fusedMode >= 2);
+    // batches that overfill the chip: pass 1 pipelined beside the expansion (enqueue_full_pipelined),
+    // GSA_FULL_PIPE groups (default 4; 0 or 1: two launches)
+    const int pipeG = env_int("GSA_FULL_PIPE", (npairs >= 8 && !fitsChip) ? 4 : 0);
+    if (!fused && interior && npairs > 1 && pipeG >= 2)
+        return enqueue_full_pipelined(ctx, npairs, pairs, lds, subst, substsz, gapo, st, pipeG);
     // two launches: pass 2 one workgroup of kExpWaves waves per task, or (GSA_EXPAND_GRID > 0)
     // that many persistent workgroups of GSA_EXPAND_WAVES (8, 12, 16) waves
     const int xGrid = fused ? 0 : std::max(0, env_int("GSA_EXPAND_GRID", 0));
@@ -843,6 +1123,9 @@ int enqueue_full_twopass(gsa_ctx* ctx, int npairs, const gsa_pair_dev* pairs, co
         if (ctx->clk_cap < (size_t)tasks || !ctx->clk)
         {
             if (ctx->clk) (void)hipFree(ctx->clk);
+    for (hipEvent_t ev : ctx->pipe_ev)
+        if (ev) (void)hipEventDestroy(ev);
+    if (ctx->p1stream) (void)hipStreamDestroy(ctx->p1stream);
             ctx->clk = nullptr;
             ctx->clk_cap = 0;
             if ((e = hipMalloc(&ctx->clk, (size_t)std::max<long long>(tasks, 1024) * 8)) != hipSuccess)
@@ -941,6 +1224,7 @@ int gsa_last_full_timing(gsa_ctx* ctx, gsa_full_timing* out)
     if (e == hipSuccess) e = hipEventSynchronize(ctx->pev[2]);
     if (e != hipSuccess) return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
     out->fused = ctx->timing_state == 2;
+    out->groups = ctx->timing_state == 3 ? ctx->timing_groups : 0;
     if (out->fused) return hipEventElapsedTime(&out->pass2_ms, ctx->pev[0], ctx->pev[2]) == hipSuccess
                                ? GSA_SUCCESS : GSA_ERROR_CUDA_GENERAL;
     if (hipEventElapsedTime(&out->pass1_ms, ctx->pev[0], ctx->pev[1]) != hipSuccess ||

@@ -93,6 +93,13 @@ __global__ void __launch_bounds__(64 * WAVES, 4) nw_expand_persist_kernel(Expand
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     const uint32_t word = ex_word(a.substsz, WAVES);
+    uint64_t c0 = 0, r0 = 0;  // effective clock over the workgroup's life (gsa_set_full_timing)
+    if (a.clk && w == 0)
+    {
+        c0 = __builtin_amdgcn_s_memtime();
+        r0 = __builtin_amdgcn_s_memrealtime();
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+    }
     for (;;)
     {
         __syncthreads();
@@ -121,6 +128,12 @@ __global__ void __launch_bounds__(64 * WAVES, 4) nw_expand_persist_kernel(Expand
         const ExpandPair d = ex_desc(a.pairs + lo);
         if (tt < 0) tt = task - d.taskBase;
         ex_task<WAVES>(a, d, tt, w, lane);
+    }
+    if (a.clk && w == 0)
+    {
+        const uint64_t c1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        if (lane == 0) G(a.clk)[blockIdx.x] = (uint64_t)(uint32_t)(c1 - c0) | ((uint64_t)(uint32_t)(r1 - r0) << 32);
     }
 }
 

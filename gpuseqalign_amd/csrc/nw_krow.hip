@@ -279,12 +279,14 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
     for (int k = 0; k < K; ++k) H[k] = 0;
     int lt[kBlk];  // lane 63's hand-off values of the last block (H[K-1] of columns t-64)
     // XR: byte address of block 0's segment of this lane's row 64m (lanes 16j - 1 only)
+    // (lanes (64/K) j - 1, j = 1 .. K, hold the strip's rows 64 j - 1 as their last row)
+    constexpr int kXL = 64 / K;  // lanes per 64 rows
     uint64_t xrBase = 0;
     if constexpr (PT >= 2)
     {
-        const int j = (lane + 1) >> 4;
-        const long long m = (long long)(K * NS) * tk + 4ll * w + j;  // a ticket holds 64 K NS rows
-        xrBase = (uint64_t)(uintptr_t)a.rows64 + 4ull * (uint64_t)((m - 1) * a.rpitch + kRowsPad - 16 * j);
+        const int j = (lane + 1) / kXL;
+        const long long m = (long long)(K * NS) * tk + (long long)K * w + j;  // a ticket holds 64 K NS rows
+        xrBase = (uint64_t)(uintptr_t)a.rows64 + 4ull * (uint64_t)((m - 1) * a.rpitch + kRowsPad - kXL * j);
     }
     // hand-off of block bb: lane 63's 16 values, then the progress word
     auto handoff = [&](int bb) {
@@ -307,9 +309,10 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
         }
         if constexpr (PT >= 2)
         {
-            // XR: lanes 16j - 1 (j = 1..4) hold row r0 + 64j - 1 = 64m, m = K NS tk + 4 w + j; their
-            // values of the block are columns 16(bb - j) .. +15 (shifted), one 64-byte row segment
-            // each (columns < 0 fall in the row buffer's left pad)
+            // XR: lanes 16j - 1 (K = 4; 32j - 1 for K = 2) hold row r0 + 64j - 1 = 64m, m = K NS tk
+            // + K w + j; their values of the block are columns 16 bb - 16j .. +15 (16 bb - 32j for
+            // K = 2; shifted), one 64-byte row segment each (columns < 0 fall in the row buffer's
+            // left pad)
             const uint64_t addr = xrBase + 64ull * (uint64_t)bb;
             uint64_t sv;
             // fused fill: write-through (sc1) stores, read by other workgroups of the launch
@@ -322,7 +325,8 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
                  "global_store_dwordx4 %2, %6, off offset:48" MOD "\n"                                  \
                  "s_mov_b64 exec, %0"                                                                    \
                  : "=&s"(sv)                                                                             \
-                 : "s"(0x8000800080008000ull), "v"(addr), "v"(int4v {lt[0], lt[1], lt[2], lt[3]}),       \
+                 : "s"(K == 4 ? 0x8000800080008000ull : 0x8000000080000000ull), "v"(addr),              \
+                   "v"(int4v {lt[0], lt[1], lt[2], lt[3]}),                                              \
                    "v"(int4v {lt[4], lt[5], lt[6], lt[7]}), "v"(int4v {lt[8], lt[9], lt[10], lt[11]}),   \
                    "v"(int4v {lt[12], lt[13], lt[14], lt[15]})                                           \
                  : "memory")
@@ -925,10 +929,12 @@ __device__ __forceinline__ PairDesc kr_desc(const PairDesc* p)
 
 // waves per workgroup: NS strips, the loader (split into a feeder and a profiler wave when the SIMDs
 // have room: NS <= 4), the drain
-template <int NS>
-constexpr bool kr_split() { return NS <= 4; }
-template <int NS>
-constexpr int kr_waves() { return NS + 2 + (kr_split<NS>() ? 1 : 0); }
+// (PT = 4, the pipelined full batch's pass 1, keeps one loader wave: its 4-wave workgroup fits the
+// wave slots an expansion workgroup leaves on the CU)
+template <int NS, int PT = 0>
+constexpr bool kr_split() { return NS <= 4 && PT != 4; }
+template <int NS, int PT = 0>
+constexpr int kr_waves() { return NS + 2 + (kr_split<NS, PT>() ? 1 : 0); }
 
 // Q8: the int8-profile instance.  It declines a table with some s - 2g outside int8 (every
 // workgroup exits before taking a ticket and the launch's word in a.q8flag is set to its epoch);
@@ -936,7 +942,7 @@ constexpr int kr_waves() { return NS + 2 + (kr_split<NS>() ? 1 : 0); }
 // profiles in one kernel (a uniform branch, or the int16 path out of line) cost the int8 path its
 // code generation: 5.49 / 5.75 ms against 5.30 for the int8 instance alone.
 template <int NS, int K, int LW, int PT, bool Q8>
-__global__ void __launch_bounds__(64 * kr_waves<NS>()) nw_krow_kernel(StripArgs a)
+__global__ void __launch_bounds__((64 * kr_waves<NS, PT>()), (PT == 4 ? 4 : 1)) nw_krow_kernel(StripArgs a)
 {
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
@@ -944,7 +950,7 @@ __global__ void __launch_bounds__(64 * kr_waves<NS>()) nw_krow_kernel(StripArgs 
     // the int16 fallback behind an int8 launch: nothing to do unless that launch declined the table
     if (!Q8 && a.q8 == 2 && __hip_atomic_load(a.q8flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != a.epoch) return;
     bool bad = false, bad8 = false;
-    for (int k = threadIdx.x; k < a.substsz * kSubRow; k += 64 * kr_waves<NS>())
+    for (int k = threadIdx.x; k < a.substsz * kSubRow; k += 64 * kr_waves<NS, PT>())
     {
         const int x = k / kSubRow, yy = k % kSubRow;
         const int v = yy < a.substsz ? G(a.subst)[yy * a.substsz + x] - 2 * a.g : 0;
@@ -1018,8 +1024,8 @@ __global__ void __launch_bounds__(64 * kr_waves<NS>()) nw_krow_kernel(StripArgs 
         if (w == NS + 1)
             kr_drain<NS, K, LW, PT>(pa, L, tk, lane);
         else if (w == NS)
-            kr_loader<NS, K, LW, kr_split<NS>() ? 1 : 0, Q8>(pa, L, tk, lane);
-        else if (kr_split<NS>() && w == NS + 2)
+            kr_loader<NS, K, LW, kr_split<NS, PT>() ? 1 : 0, Q8>(pa, L, tk, lane);
+        else if (kr_split<NS, PT>() && w == NS + 2)
             kr_loader<NS, K, LW, 2, Q8>(pa, L, tk, lane);
         else
         {
@@ -1040,14 +1046,14 @@ hipError_t launch_kr1(const StripArgs& a, int grid, hipStream_t stream, bool foo
     if (grid <= 0)
     {
         int per_cu = 0, dev = 0, cus = 0;
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)kern, 64 * kr_waves<NS>(), lds);
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)kern, 64 * kr_waves<NS, PT>(), lds);
         if (e == hipSuccess) e = hipGetDevice(&dev);
         if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
         if (e != hipSuccess) return e;
         grid = std::max(1, std::min(a.nTicketsTotal, std::max(1, per_cu) * cus));
     }
-    if (foot && (e = record_foot((const void*)kern, lds, 64 * kr_waves<NS>(), grid)) != hipSuccess) return e;
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * kr_waves<NS>()), lds, stream, a);
+    if (foot && (e = record_foot((const void*)kern, lds, 64 * kr_waves<NS, PT>(), grid)) != hipSuccess) return e;
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * kr_waves<NS, PT>()), lds, stream, a);
     return hipGetLastError();
 }
 
@@ -2080,6 +2086,17 @@ hipError_t launch_full_fused(const StripArgs& a, int ns, int waves, int grid, hi
     if (ns == 4 && waves == 8) return launch_fused<4, 8>(a, grid, stream);
     if (ns == 8 && waves == 12) return launch_fused<8, 12>(a, grid, stream);
     return hipErrorInvalidValue;
+}
+#elif defined(GSA_KROW_CO)
+// nw_krowco.hip: pass 1 of the pipelined full batch (gsa_capi.hip enqueue_full_twopass): the XR
+// fill on (2, 2) tickets (256 rows; a 512-column profile ring) in 4-wave workgroups of at most 128
+// VGPRs and 74 KB of LDS, which fit beside a 12-wave expansion workgroup of the previous pair group
+// on every CU (16 wave slots, 160 KB of LDS)
+size_t krow_co_lds_bytes(int substsz, bool q8) { return (size_t)kr_layout(2, 512, substsz, q8).flags + 256; }
+
+hipError_t launch_krow_fill_co(const StripArgs& a, int grid, hipStream_t stream)
+{
+    return launch_kr<2, 2, 512, 4>(a, grid, stream);
 }
 #elif defined(GSA_KROW_BATCH8)
 // nw_krow8.hip: the 8-strip batch instance in a translation unit of its own, so it can be built

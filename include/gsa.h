@@ -191,14 +191,17 @@ int gsa_debug_stamps(gsa_ctx* ctx, uint64_t* out, int64_t cap, int64_t* n);
  * 100 MHz ticks (s_memrealtime) from start to end.  gsa_last_full_timing waits for the last such
  * fill and returns the pass times and the effective shader clock over pass 2's workgroups (median
  * and cycle-weighted mean), so a slow box shows as a low clock.  A fused fill (one launch) has
- * pass1_ms = -1, its whole time in pass2_ms and no clock.  errorInvalidValue: no timed fill. */
+ * pass1_ms = -1, its whole time in pass2_ms and no clock.  A pipelined batch (groups > 0: pass 1 of
+ * pair group g + 1 beside the expansion of group g) has group 0's pass 1 (alone on the chip) in
+ * pass1_ms, everything after it in pass2_ms and the clock of its last expansion launch.
+ * errorInvalidValue: no timed fill. */
 typedef struct gsa_full_timing
 {
     float pass1_ms, pass2_ms;
     float clock_ghz_median, clock_ghz_mean;
     int64_t workgroups;  /* pass-2 workgroups whose clock was resolved (>= 1 us) */
     int32_t fused;
-    int32_t pad;
+    int32_t groups;  /* pipelined batch: pair groups (0: not pipelined) */
 } gsa_full_timing;
 int gsa_set_full_timing(gsa_ctx* ctx, int32_t on);
 int gsa_last_full_timing(gsa_ctx* ctx, gsa_full_timing* out);
