@@ -326,6 +326,7 @@ def bench_full_batch(world, rank, local, n_pairs):
     match = None if gold is None else sum(int(a == b) for a, b in zip(costs, gold["align_cost"][:n_pairs]))
     out_bytes = 4.0 * sum(len(y) * len(x) for y, x in pairs)
     gbps = out_bytes / rep.elapsed_s / 1e9
+    box = box_write_rate(local)
     return {"workload": f"{n_pairs} NW-LG pairs of BASELINE configs[3] (18-22k, seeds 1000+k) as FULL int32 score "
                         f"matrices ({out_bytes / 1e9:.1f} GB), one persistent launch, LPT-sharded over {world} rank(s) "
                         "(1 untimed + 3 timed launches; seconds per launch)",
@@ -336,7 +337,37 @@ def bench_full_batch(world, rank, local, n_pairs):
             "bound": "hbm (4 B written per cell; MI355X 8 TB/s spec)",
             "pmc_write_over_algorithmic": pmc_write_ratio(n_pairs, full_kernel_name(False)),
             "passes": pass_fields(tm, out_bytes / world),
+            "box_fill": box,
+            "over_box_fill": round(gbps / box["GBps"], 4) if box and "GBps" in box else None,
             "pairs": n_pairs, "pairs_matching_golden": match}
+
+
+def box_write_rate(local, gib=16, reps=5):
+    """What this box's HBM takes in plain writes: torch fill_ of a 16 GiB int32 buffer (the runtime's
+    fill kernel, 16-byte stores, every CU), best of 5.  The full batch's rate over this one separates
+    the kernel from the box: the same build's pass 2 ran 18.8 ms on one box and 25.3 on another at a
+    higher shader clock (profiles/r05_pipe_ab.txt)."""
+    import torch
+    try:
+        dev = torch.device("cuda", local)
+        buf = torch.empty(gib * (1 << 28), dtype=torch.int32, device=dev)
+        buf.fill_(1)
+        torch.cuda.synchronize(dev)
+        best = None
+        for _ in range(reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            buf.fill_(7)
+            e1.record()
+            e1.synchronize()
+            ms = e0.elapsed_time(e1)
+            best = ms if best is None else min(best, ms)
+        del buf
+        torch.cuda.empty_cache()
+        return {"what": f"torch fill_ of {gib} GiB int32, best of {reps}", "ms": round(best, 4),
+                "GBps": round(gib * (1 << 30) / (best * 1e-3) / 1e9, 1)}
+    except Exception as ex:  # (no room: the field is left out)
+        return {"error": str(ex)[:120]}
 
 
 def pass_fields(tm, rank_bytes):

@@ -965,9 +965,12 @@ int enqueue_full_twopass(gsa_ctx* ctx, int npairs, const gsa_pair_dev* pairs, co
     bool interior = true;
     for (int p = 0; p < npairs; ++p) interior = interior && pairs[p].adjrows > 1 && pairs[p].adjcols > 1;
     const bool fused = interior && (npairs == 1 ? fusedMode >= 1 : fusedMode >= 2);
-    // batches that overfill the chip: pass 1 pipelined beside the expansion (enqueue_full_pipelined),
-    // GSA_FULL_PIPE groups (default 4; 0 or 1: two launches)
-    const int pipeG = env_int("GSA_FULL_PIPE", (npairs >= 8 && !fitsChip) ? 4 : 0);
+    // GSA_FULL_PIPE = G >= 2: pass 1 pipelined beside the expansion in G pair groups
+    // (enqueue_full_pipelined).  Measured slower, so off by default: the 12-wave expansion that leaves
+    // room for pass 1 is 14 % slower than the 16-wave one alone, and the co-resident pass 1 costs it
+    // more than the 3.9 ms it hides (64 x 20k: 29.5 ms two launches vs 30.1-38 ms at G = 2-8 on one
+    // box, 25.0 vs 30.1 on another; profiles/r05_pipe_ab.txt)
+    const int pipeG = env_int("GSA_FULL_PIPE", 0);
     if (!fused && interior && npairs > 1 && pipeG >= 2)
         return enqueue_full_pipelined(ctx, npairs, pairs, lds, subst, substsz, gapo, st, pipeG);
     // two launches: pass 2 one workgroup of kExpWaves waves per task, or (GSA_EXPAND_GRID > 0)

@@ -9,6 +9,10 @@
 
 #include "nw_expand.h"
 
+#ifndef GSA_EXPAND_PROBE
+#define GSA_EXPAND_PROBE 0  // diagnostic builds only (tools/r05_xprobe.sh)
+#endif
+
 namespace gsa {
 namespace xdev {
 
@@ -118,6 +122,9 @@ __device__ __forceinline__ void ex_tile(const ExpandArgs& a, const ExpandPair& d
 #pragma unroll
     for (int u = 0; u < kBlk; ++u) qA[u] = lds_ld(qrow + 4u * (uint32_t)(u - lane));
     int H = lb, U = lb;
+#if GSA_EXPAND_PROBE == 2
+    int sink = 0;
+#endif
     int tE[kBlk];  // the even block's transposed values, stored with the odd block's
     bool held = false;
 #pragma unroll
@@ -140,7 +147,12 @@ __device__ __forceinline__ void ex_tile(const ExpandArgs& a, const ExpandPair& d
         {
             const int up = shr1z(H) + hc[u >> 2][u & 3];
             const int t1 = U + qc[u];
+#if GSA_EXPAND_PROBE == 1
+            // diagnostic build (tools/r05_xprobe.sh): no recurrence, one add per cell (results wrong)
+            int h = t1;
+#else
             int h = max(max(t1, up), H + g);
+#endif
             if constexpr (RAMP) h = (lane >= kBlk * b + u) ? lb : h;  // column <= cb: the left boundary
             U = up;
             H = h;
@@ -173,7 +185,13 @@ __device__ __forceinline__ void ex_tile(const ExpandArgs& a, const ExpandPair& d
         auto interior = [&](int bb) { return kBlk * bb - 63 >= 1 && kBlk * bb + kBlk - 1 <= cols && r0 + 63 <= d.R; };
         auto store4 = [&](int bb, int k, const int (&v)[kBlk]) {
             const gptr<int> ub = G(d.score) + ((ptrdiff_t)(r0 + 16 * k) * d.ld - 16 * k + kBlk * bb + cb);
+#if GSA_EXPAND_PROBE == 2
+            // diagnostic build: interior stores only into one line per wave (results wrong)
+            sink ^= v[4 * k] ^ v[4 * k + 1] ^ v[4 * k + 2] ^ v[4 * k + 3];
+            (void)ub;
+#else
             *(gptr<int4a>)(ub + xoff) = int4a {v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]};
+#endif
         };
         if (!RAMP && (b & 1) == 0 && b + 1 < NB && interior(b) && interior(b + 1))
         {
@@ -232,6 +250,9 @@ __device__ __forceinline__ void ex_tile(const ExpandArgs& a, const ExpandPair& d
         block(b, qA, qB, F());
         if (b + 1 < NB) block(b + 1, qB, qA, F());
     }
+#if GSA_EXPAND_PROBE == 2
+    if (sink == 0x7fffffff) G(d.score)[0] = sink;
+#endif
 }
 
 
