@@ -1233,16 +1233,15 @@ __device__ __forceinline__ void ks_strip(const StripArgs& a, const KsLds& L, int
     const uint32_t c_out = L.flags + kr_cons(w + 1);
     const uint32_t f_xo = L.flags + kFXo;
     const int NB = (Cp + 65 + kBlk - 1) / kBlk;
-    auto ok = [&](int pin, int pco, int pxo, int b, int look = 0) {
-        return pin >= kBlk * (b + look) + 64 + kBlk && pco >= kBlk * (b + look) + kBlk - kRing &&
-               (w != 0 || pxo >= kBlk * (b + look) + 2 * kBlk);
+    auto ok = [&](int pin, int pco, int pxo, int b) {
+        return pin >= kBlk * b + 64 + kBlk && pco >= kBlk * b + kBlk - kRing && (w != 0 || pxo >= kBlk * b + 2 * kBlk);
     };
-    auto spin = [&](int b, int look = 0) {
+    auto spin = [&](int b) {
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
         for (int it = 1;; ++it)
         {
             const int pin = flag_ld(f_in), pco = flag_ld(c_out), pxo = (w == 0) ? flag_ld(f_xo) : 0;
-            if (ok(pin, pco, pxo, b, look)) return true;
+            if (ok(pin, pco, pxo, b)) return true;
             __builtin_amdgcn_s_sleep(1);
             if (__builtin_amdgcn_s_memrealtime() - t0 > a.spin || ((it & 31) == 0 && err_set(a)))
             {
@@ -1260,66 +1259,6 @@ __device__ __forceinline__ void ks_strip(const StripArgs& a, const KsLds& L, int
         hc[j] = int4v {0, 0, 0, 0};
         hf[j] = int4v {0, 0, 0, 0};
     }
-#if GSA_KROW_SYNC2
-    // block b+1's halos, read with block b's (the odd block then reads none)
-    int4v hc2[kHalo], hf2[kHalo];
-#pragma unroll
-    for (int j = 0; j < kHalo; ++j)
-    {
-        hc2[j] = int4v {0, 0, 0, 0};
-        hf2[j] = int4v {0, 0, 0, 0};
-    }
-    auto halo_load2 = [&](int b) {
-        const uint32_t hb = ring_in + 4u * (uint32_t)((kBlk * b + 64) & (kRing - 1));
-        uint64_t sv;
-        if constexpr (AG)
-            asm volatile(
-                "s_mov_b64 %16, exec\n"
-                "s_mov_b64 exec, 1\n"
-                "ds_read_b128 %0, %17\n"
-                "ds_read_b128 %1, %17 offset:16\n"
-                "ds_read_b128 %2, %17 offset:32\n"
-                "ds_read_b128 %3, %17 offset:48\n"
-                "ds_read_b128 %4, %17 offset:64\n"
-                "ds_read_b128 %5, %17 offset:80\n"
-                "ds_read_b128 %6, %17 offset:96\n"
-                "ds_read_b128 %7, %17 offset:112\n"
-                "ds_read_b128 %8, %17 offset:%18\n"
-                "ds_read_b128 %9, %17 offset:%19\n"
-                "ds_read_b128 %10, %17 offset:%20\n"
-                "ds_read_b128 %11, %17 offset:%21\n"
-                "ds_read_b128 %12, %17 offset:%22\n"
-                "ds_read_b128 %13, %17 offset:%23\n"
-                "ds_read_b128 %14, %17 offset:%24\n"
-                "ds_read_b128 %15, %17 offset:%25\n"
-                "s_mov_b64 exec, %16\n"
-                "s_waitcnt lgkmcnt(0)"
-                : "+v"(hc[0]), "+v"(hc[1]), "+v"(hc[2]), "+v"(hc[3]), "+v"(hc2[0]), "+v"(hc2[1]), "+v"(hc2[2]),
-                  "+v"(hc2[3]), "+v"(hf[0]), "+v"(hf[1]), "+v"(hf[2]), "+v"(hf[3]), "+v"(hf2[0]), "+v"(hf2[1]),
-                  "+v"(hf2[2]), "+v"(hf2[3]), "=&s"(sv)
-                : "v"(hb), "n"(kRing2Off), "n"(kRing2Off + 16), "n"(kRing2Off + 32), "n"(kRing2Off + 48),
-                  "n"(kRing2Off + 64), "n"(kRing2Off + 80), "n"(kRing2Off + 96), "n"(kRing2Off + 112)
-                : "memory");
-        else
-            asm volatile(
-                "s_mov_b64 %8, exec\n"
-                "s_mov_b64 exec, 1\n"
-                "ds_read_b128 %0, %9\n"
-                "ds_read_b128 %1, %9 offset:16\n"
-                "ds_read_b128 %2, %9 offset:32\n"
-                "ds_read_b128 %3, %9 offset:48\n"
-                "ds_read_b128 %4, %9 offset:64\n"
-                "ds_read_b128 %5, %9 offset:80\n"
-                "ds_read_b128 %6, %9 offset:96\n"
-                "ds_read_b128 %7, %9 offset:112\n"
-                "s_mov_b64 exec, %8\n"
-                "s_waitcnt lgkmcnt(0)"
-                : "+v"(hc[0]), "+v"(hc[1]), "+v"(hc[2]), "+v"(hc[3]), "+v"(hc2[0]), "+v"(hc2[1]), "+v"(hc2[2]),
-                  "+v"(hc2[3]), "=&s"(sv)
-                : "v"(hb)
-                : "memory");
-    };
-#endif
     auto halo_load = [&](int b) {
         const uint32_t hb = ring_in + 4u * (uint32_t)((kBlk * b + 64) & (kRing - 1));
         uint64_t sv;
@@ -1404,74 +1343,7 @@ __device__ __forceinline__ void ks_strip(const StripArgs& a, const KsLds& L, int
     const bool hasR = !SW && rR >= 0 && rR < 64 * K;
     const int laneR = rR / K, kR = rR % K, tStar = a.C + laneR;
     int lt[kBlk], lf[kBlk];  // lane 63's hand-off values of the last block (Hgo', F' of columns t-64)
-#if GSA_KROW_SYNC2
-    int lt2[kBlk], lf2[kBlk];  // ... of the even block before it (GSA_KROW_SYNC2)
-#endif
-    auto handoff = [&](int bb, auto parT) {
-        constexpr int PAR = decltype(parT)::value;
-#if GSA_KROW_SYNC2
-        if (PAR == 0 && bb + 1 < NB)
-        {
-            // the even block's values wait for the odd block's hand-off
-#pragma unroll
-            for (int e = 0; e < kBlk; ++e)
-            {
-                lt2[e] = lt[e];
-                if constexpr (AG) lf2[e] = lf[e];
-            }
-            return;
-        }
-        if (PAR == 1)
-        {
-            const uint32_t eb = ring_out + 4u * (uint32_t)((kBlk * (bb - 1)) & (kRing - 1));
-            uint64_t sv;
-            asm volatile(
-                "s_mov_b64 %0, exec\n"
-                "s_mov_b64 exec, %1\n"
-                "ds_write_b128 %2, %3\n"
-                "ds_write_b128 %2, %4 offset:16\n"
-                "ds_write_b128 %2, %5 offset:32\n"
-                "ds_write_b128 %2, %6 offset:48\n"
-                "ds_write_b128 %2, %7 offset:64\n"
-                "ds_write_b128 %2, %8 offset:80\n"
-                "ds_write_b128 %2, %9 offset:96\n"
-                "ds_write_b128 %2, %10 offset:112\n"
-                "s_mov_b64 exec, %0"
-                : "=&s"(sv)
-                : "s"(1ull << 63), "v"(eb), "v"(int4v {lt2[0], lt2[1], lt2[2], lt2[3]}),
-                  "v"(int4v {lt2[4], lt2[5], lt2[6], lt2[7]}), "v"(int4v {lt2[8], lt2[9], lt2[10], lt2[11]}),
-                  "v"(int4v {lt2[12], lt2[13], lt2[14], lt2[15]}), "v"(int4v {lt[0], lt[1], lt[2], lt[3]}),
-                  "v"(int4v {lt[4], lt[5], lt[6], lt[7]}), "v"(int4v {lt[8], lt[9], lt[10], lt[11]}),
-                  "v"(int4v {lt[12], lt[13], lt[14], lt[15]})
-                : "memory");
-            if constexpr (AG)
-                asm volatile(
-                    "s_mov_b64 %0, exec\n"
-                    "s_mov_b64 exec, %1\n"
-                    "ds_write_b128 %2, %3 offset:%11\n"
-                    "ds_write_b128 %2, %4 offset:%12\n"
-                    "ds_write_b128 %2, %5 offset:%13\n"
-                    "ds_write_b128 %2, %6 offset:%14\n"
-                    "ds_write_b128 %2, %7 offset:%15\n"
-                    "ds_write_b128 %2, %8 offset:%16\n"
-                    "ds_write_b128 %2, %9 offset:%17\n"
-                    "ds_write_b128 %2, %10 offset:%18\n"
-                    "s_mov_b64 exec, %0"
-                    : "=&s"(sv)
-                    : "s"(1ull << 63), "v"(eb), "v"(int4v {lf2[0], lf2[1], lf2[2], lf2[3]}),
-                      "v"(int4v {lf2[4], lf2[5], lf2[6], lf2[7]}), "v"(int4v {lf2[8], lf2[9], lf2[10], lf2[11]}),
-                      "v"(int4v {lf2[12], lf2[13], lf2[14], lf2[15]}), "v"(int4v {lf[0], lf[1], lf[2], lf[3]}),
-                      "v"(int4v {lf[4], lf[5], lf[6], lf[7]}), "v"(int4v {lf[8], lf[9], lf[10], lf[11]}),
-                      "v"(int4v {lf[12], lf[13], lf[14], lf[15]}), "n"(kRing2Off), "n"(kRing2Off + 16),
-                      "n"(kRing2Off + 32), "n"(kRing2Off + 48), "n"(kRing2Off + 64), "n"(kRing2Off + 80),
-                      "n"(kRing2Off + 96), "n"(kRing2Off + 112)
-                    : "memory");
-            flag_st2(f_out, bb + 1 == NB ? kBig : kBlk * bb + kBlk, kBlk * bb + 64 + kBlk);
-            return;
-        }
-#else
-        (void)PAR;
-#endif
+    auto handoff = [&](int bb) {
         const uint32_t eb = ring_out + 4u * (uint32_t)((kBlk * bb) & (kRing - 1));
         uint64_t sv;
         if constexpr (AG)
@@ -1511,22 +1383,7 @@ __device__ __forceinline__ void ks_strip(const StripArgs& a, const KsLds& L, int
     };
     int rpin = 0, rpco = 0, rpxo = 0, rsink = 0;
 
-    auto block = [&](int b, int (&qc)[K][kQD], int (&qn)[K][kQD], auto parT) {
-        constexpr int PAR = decltype(parT)::value;  // b & 1
-#if GSA_KROW_SYNC2
-        if constexpr (PAR == 0)
-        {
-            const int pin = __builtin_amdgcn_readfirstlane(rpin), pco = __builtin_amdgcn_readfirstlane(rpco);
-            const int pxo = (w == 0) ? __builtin_amdgcn_readfirstlane(rpxo) : 0;
-            asm volatile("" ::"v"(rpin), "v"(rpco), "v"(rpxo), "v"(rsink));
-            if (!ok(pin, pco, pxo, b, 1) && !spin(b, 1)) return false;
-            halo_load2(b);
-        }
-        int4v* const hcur = PAR ? hc2 : hc;
-        int4v* const hfur = PAR ? hf2 : hf;
-#else
-        auto& hcur = hc;
-        auto& hfur = hf;
+    auto block = [&](int b, int (&qc)[K][kQD], int (&qn)[K][kQD]) {
         {
             const int pin = __builtin_amdgcn_readfirstlane(rpin), pco = __builtin_amdgcn_readfirstlane(rpco);
             const int pxo = (w == 0) ? __builtin_amdgcn_readfirstlane(rpxo) : 0;
@@ -1534,7 +1391,6 @@ __device__ __forceinline__ void ks_strip(const StripArgs& a, const KsLds& L, int
             if (!ok(pin, pco, pxo, b) && !spin(b)) return false;
         }
         halo_load(b);
-#endif
         const uint32_t pn = q_off(b + 1);
         int va[SW ? 1 : K][SW ? 1 : kBlk];  // NW: the block's Hgo' (result cell)
         int zz[SW ? kBlk + K : 1];          // SW: row 0's floor at steps 0 .. 19 of the block
@@ -1547,8 +1403,8 @@ __device__ __forceinline__ void ks_strip(const StripArgs& a, const KsLds& L, int
 #pragma unroll
         for (int u = 0; u < kBlk; ++u)
         {
-            const int upH = shr1z(H[K - 1]) + hcur[u >> 2][u & 3];
-            const int upF = AG ? shr1z(FD) + hfur[u >> 2][u & 3] : 0;
+            const int upH = shr1z(H[K - 1]) + hc[u >> 2][u & 3];
+            const int upF = AG ? shr1z(FD) + hf[u >> 2][u & 3] : 0;
             int nh[K], ne[K], h[K];
             int f = 0;
 #pragma unroll
@@ -1599,7 +1455,7 @@ __device__ __forceinline__ void ks_strip(const StripArgs& a, const KsLds& L, int
                 if constexpr (!SW) va[k][u] = nh[k];
             }
             if constexpr (AG) FD = f;
-            if (u == kBlk - 2 && (!GSA_KROW_SYNC2 || PAR == 1))
+            if (u == kBlk - 2)
             {
                 asm volatile("" ::: "memory");
                 const int2v lo = *(const int2v*)(krsm + f_in), hi = *(const int2v*)(krsm + f_in + 16u);
@@ -1610,7 +1466,7 @@ __device__ __forceinline__ void ks_strip(const StripArgs& a, const KsLds& L, int
                 rsink = hi.x;
             }
         }
-        handoff(b, parT);
+        handoff(b);
         if constexpr (SW)
         {
             // fold the block's best per row: score = key >> 4 - k |ge|, first step 15 - key & 15
@@ -1650,9 +1506,9 @@ __device__ __forceinline__ void ks_strip(const StripArgs& a, const KsLds& L, int
     if constexpr (SW) wv = 15u - 16u * (uint32_t)z0;
     for (int b = 0; b < NB; b += 2)
     {
-        if (!block(b, qA, qB, std::integral_constant<int, 0>())) return;
+        if (!block(b, qA, qB)) return;
         if (b + 1 >= NB) break;
-        if (!block(b + 1, qB, qA, std::integral_constant<int, 1>())) return;
+        if (!block(b + 1, qB, qA)) return;
     }
     if constexpr (SW)
     {
