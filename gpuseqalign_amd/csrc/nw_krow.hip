@@ -93,13 +93,6 @@ constexpr uint32_t kFCap = 160;
 
 extern __shared__ __attribute__((aligned(16))) char krsm[];
 
-// GSA_KROW_SYNC2 = 1: strips synchronise every second block -- the progress check, the halo read
-// (32 elements) and the hand-off (32 elements + the progress word) once per 32 steps, the step,
-// profile and capture per 16-step block as before (kr_strip)
-#ifndef GSA_KROW_SYNC2
-#define GSA_KROW_SYNC2 0
-#endif
-
 
 typedef int int4v __attribute__((ext_vector_type(4)));
 typedef int int2v __attribute__((ext_vector_type(2)));
@@ -210,19 +203,17 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
 
     // block b needs its halo (ring elements 16b+64 .. 16b+79), room in ring_out for elements
     // 16b .. 16b+15, and (strip 0; the others trail it) the profile of block b+1 (columns < 16b+32)
-    // look = 1: blocks b and b+1 at once (GSA_KROW_SYNC2)
-    auto ok = [&](int pin, int pco, int pxo, int b, int look = 0) {
-        return pin >= kBlk * (b + look) + 64 + kBlk && pco >= kBlk * (b + look) + kBlk - kRing &&
-               (w != 0 || pxo >= kBlk * (b + look) + 2 * kBlk);
+    auto ok = [&](int pin, int pco, int pxo, int b) {
+        return pin >= kBlk * b + 64 + kBlk && pco >= kBlk * b + kBlk - kRing && (w != 0 || pxo >= kBlk * b + 2 * kBlk);
     };
     // the error word is a global load, which waits for this wave's outstanding header stores
     // (vmcnt retires in order): polled once per 32 LDS polls
-    auto spin = [&](int b, int look = 0) {
+    auto spin = [&](int b) {
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
         for (int it = 1;; ++it)
         {
             const int pin = flag_ld(f_in), pco = flag_ld(c_out), pxo = (w == 0) ? flag_ld(f_xo) : 0;
-            if (ok(pin, pco, pxo, b, look)) return true;
+            if (ok(pin, pco, pxo, b)) return true;
             __builtin_amdgcn_s_sleep(1);
             if (__builtin_amdgcn_s_memrealtime() - t0 > a.spin || ((it & 31) == 0 && err_set(a)))
             {
@@ -235,32 +226,6 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
     int4v hc[kHalo];
 #pragma unroll
     for (int j = 0; j < kHalo; ++j) hc[j] = int4v {0, 0, 0, 0};
-#if GSA_KROW_SYNC2
-    int4v hc2[kHalo];  // block b+1's halo, read with block b's
-#pragma unroll
-    for (int j = 0; j < kHalo; ++j) hc2[j] = int4v {0, 0, 0, 0};
-    auto halo_load2 = [&](int b) {
-        const uint32_t hb = ring_in + 4u * (uint32_t)((kBlk * b + 64) & (kRing - 1));
-        uint64_t sv;
-        asm volatile(
-            "s_mov_b64 %8, exec\n"
-            "s_mov_b64 exec, 1\n"
-            "ds_read_b128 %0, %9\n"
-            "ds_read_b128 %1, %9 offset:16\n"
-            "ds_read_b128 %2, %9 offset:32\n"
-            "ds_read_b128 %3, %9 offset:48\n"
-            "ds_read_b128 %4, %9 offset:64\n"
-            "ds_read_b128 %5, %9 offset:80\n"
-            "ds_read_b128 %6, %9 offset:96\n"
-            "ds_read_b128 %7, %9 offset:112\n"
-            "s_mov_b64 exec, %8\n"
-            "s_waitcnt lgkmcnt(0)"
-            : "+v"(hc[0]), "+v"(hc[1]), "+v"(hc[2]), "+v"(hc[3]), "+v"(hc2[0]), "+v"(hc2[1]), "+v"(hc2[2]),
-              "+v"(hc2[3]), "=&s"(sv)
-            : "v"(hb)
-            : "memory");
-    };
-#endif
     auto halo_load = [&](int b) {
         {
             // lane 0 alone (exec set and restored inside the asm: no divergent branch in the
@@ -313,9 +278,6 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
 #pragma unroll
     for (int k = 0; k < K; ++k) H[k] = 0;
     int lt[kBlk];  // lane 63's hand-off values of the last block (H[K-1] of columns t-64)
-#if GSA_KROW_SYNC2
-    int lt2[kBlk];  // ... of the even block before it, handed off with it
-#endif
     // XR: byte address of block 0's segment of this lane's row 64m (lanes 16j - 1 only)
     // (lanes (64/K) j - 1, j = 1 .. K, hold the strip's rows 64 j - 1 as their last row)
     constexpr int kXL = 64 / K;  // lanes per 64 rows
@@ -326,44 +288,8 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
         const long long m = (long long)(K * NS) * tk + (long long)K * w + j;  // a ticket holds 64 K NS rows
         xrBase = (uint64_t)(uintptr_t)a.rows64 + 4ull * (uint64_t)((m - 1) * a.rpitch + kRowsPad - kXL * j);
     }
-    // hand-off of block bb: lane 63's 16 values, then the progress word.  (GSA_KROW_SYNC2: an even
-    // block keeps its values for the odd block after it, which writes both blocks' 32 and the word)
-    auto handoff = [&](int bb, auto parT) {
-        constexpr int PAR = decltype(parT)::value;
-#if GSA_KROW_SYNC2
-        if (PAR == 0 && bb + 1 < NB)
-        {
-#pragma unroll
-            for (int e = 0; e < kBlk; ++e) lt2[e] = lt[e];
-        }
-        else if (PAR == 1)
-        {
-            const uint32_t eb = ring_out + 4u * (uint32_t)((kBlk * (bb - 1)) & (kRing - 1));
-            uint64_t sv;
-            asm volatile(
-                "s_mov_b64 %0, exec\n"
-                "s_mov_b64 exec, %1\n"
-                "ds_write_b128 %2, %3\n"
-                "ds_write_b128 %2, %4 offset:16\n"
-                "ds_write_b128 %2, %5 offset:32\n"
-                "ds_write_b128 %2, %6 offset:48\n"
-                "ds_write_b128 %2, %7 offset:64\n"
-                "ds_write_b128 %2, %8 offset:80\n"
-                "ds_write_b128 %2, %9 offset:96\n"
-                "ds_write_b128 %2, %10 offset:112\n"
-                "s_mov_b64 exec, %0"
-                : "=&s"(sv)
-                : "s"(1ull << 63), "v"(eb), "v"(int4v {lt2[0], lt2[1], lt2[2], lt2[3]}),
-                  "v"(int4v {lt2[4], lt2[5], lt2[6], lt2[7]}), "v"(int4v {lt2[8], lt2[9], lt2[10], lt2[11]}),
-                  "v"(int4v {lt2[12], lt2[13], lt2[14], lt2[15]}), "v"(int4v {lt[0], lt[1], lt[2], lt[3]}),
-                  "v"(int4v {lt[4], lt[5], lt[6], lt[7]}), "v"(int4v {lt[8], lt[9], lt[10], lt[11]}),
-                  "v"(int4v {lt[12], lt[13], lt[14], lt[15]})
-                : "memory");
-        }
-        else
-#else
-        (void)PAR;
-#endif
+    // hand-off of block bb: lane 63's 16 values, then the progress word
+    auto handoff = [&](int bb) {
         {
             // lane 63 alone (exec set and restored inside the asm)
             const uint32_t eb = ring_out + 4u * (uint32_t)((kBlk * bb) & (kRing - 1));
@@ -412,10 +338,7 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
         }
         // {prog[w+1], cons[w]}: block bb's 16 elements handed off; ring_in elements < 16bb+80
         // (block bb's halo, read at its start) no longer needed
-#if GSA_KROW_SYNC2
-        if (PAR == 1 || bb + 1 == NB)
-#endif
-            flag_st2(f_out, bb + 1 == NB ? kBig : kBlk * bb + kBlk, kBlk * bb + 64 + kBlk);
+        flag_st2(f_out, bb + 1 == NB ? kBig : kBlk * bb + kBlk, kBlk * bb + 64 + kBlk);
     };
     int rpin = 0, rpco = 0, rpxo = 0;  // progress words read in mid-block, checked at the next block
     int rsink = 0;                     // the read's 4th dword (unused)
@@ -442,23 +365,9 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
 
     // One body for blocks with and without a header-column capture (cap, uniform): separate
     // bodies get different register assignments and ~100 v_mov per block to reconcile them.
-    auto block = [&](int b, int (&qc)[K][kQD], int (&qn)[K][kQD], auto rampT, bool cap, auto parT) {
+    auto block = [&](int b, int (&qc)[K][kQD], int (&qn)[K][kQD], auto rampT, bool cap) {
         constexpr bool RAMP = decltype(rampT)::value;
         constexpr bool CAP = !RAMP;  // ramp blocks hold no boundary (tBx >= 64)
-        constexpr int PAR = decltype(parT)::value;  // b & 1
-#if GSA_KROW_SYNC2
-        if constexpr (PAR == 0)
-        {
-            // blocks b and b+1: both halos, room for both hand-offs, the profile of b+2
-            const int pin = __builtin_amdgcn_readfirstlane(rpin), pco = __builtin_amdgcn_readfirstlane(rpco);
-            const int pxo = (w == 0) ? __builtin_amdgcn_readfirstlane(rpxo) : 0;
-            asm volatile("" ::"v"(rpin), "v"(rpco), "v"(rpxo), "v"(rsink));
-            if (!ok(pin, pco, pxo, b, 1) && !spin(b, 1)) return false;
-            halo_load2(b);
-        }
-        int4v* const hcur = PAR ? hc2 : hc;
-#else
-        auto& hcur = hc;
         {
             const int pin = __builtin_amdgcn_readfirstlane(rpin), pco = __builtin_amdgcn_readfirstlane(rpco);
             const int pxo = (w == 0) ? __builtin_amdgcn_readfirstlane(rpxo) : 0;
@@ -470,14 +379,13 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
             if (!ok(pin, pco, pxo, b) && !spin(b)) return false;
         }
         halo_load(b);
-#endif
         const uint32_t pn = q_off(b + 1);
         int va[CAP ? K : 1][CAP ? kBlk : 1];
 #pragma unroll
         for (int u = 0; u < kBlk; ++u)
         {
             int nh[K];
-            const int up = shr1z(H[K - 1]) + hcur[u >> 2][u & 3];
+            const int up = shr1z(H[K - 1]) + hc[u >> 2][u & 3];
             nh[0] = max3i(D + qv(qc, 0, u), up, H[0]);
 #pragma unroll
             for (int k = 1; k < K; ++k) nh[k] = max3i(H[k - 1] + qv(qc, k, u), nh[k - 1], H[k]);
@@ -503,7 +411,7 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
             // read late (step 14): the fresher the words, the rarer the spin at the next block
             // start, where a strip that trails the one above at the minimum lag ends up each block
             // (steps 8 / 12 / 14: 100k 5.95 / 5.97 / 5.87 ms)
-            if (u == kBlk - 2 && (!GSA_KROW_SYNC2 || PAR == 1))
+            if (u == kBlk - 2)
             {
                 // slot w-1 {prog[w], cons[w-1] | xo} and slot w+1 {prog[w+2], cons[w+1]}: one
                 // ds_read2_b64 (plain loads, kept in place by the memory clobbers around them)
@@ -519,7 +427,7 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
         // the block's hand-off at its end (the next strip sees it a block earlier than when it is
         // written behind the next block's halo reads: measured 1 % faster at 100k, slightly slower
         // per block)
-        handoff(b, parT);
+        handoff(b);
         if constexpr (fx && !RAMP)
             if ((b & 15) == 15)
             {
@@ -595,20 +503,18 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
     auto advance = [&](int b) { return b >= nbb && jb < tcols && capRows; };
     using T = std::integral_constant<bool, true>;
     using F = std::integral_constant<bool, false>;
-    using P0 = std::integral_constant<int, 0>;
-    using P1 = std::integral_constant<int, 1>;
     constexpr int kRampBlocks = 64 / kBlk;  // columns <= 0 occur only in the first 64 steps
     int b = 0;
     for (; b < kRampBlocks; b += 2)
     {
-        if (!block(b, qA, qB, T(), false, P0())) return;
-        if (!block(b + 1, qB, qA, T(), false, P1())) return;
+        if (!block(b, qA, qB, T(), false)) return;
+        if (!block(b + 1, qB, qA, T(), false)) return;
     }
     for (; b < NB; b += 2)
     {
-        if (!block(b, qA, qB, F(), advance(b), P0())) return;
+        if (!block(b, qA, qB, F(), advance(b))) return;
         if (b + 1 >= NB) break;
-        if (!block(b + 1, qB, qA, F(), advance(b + 1), P1())) return;
+        if (!block(b + 1, qB, qA, F(), advance(b + 1))) return;
     }
     if (pt)
     {
