@@ -18,6 +18,7 @@
 #include <vector>
 
 #include "../../include/gsa.h"
+#include "nw_bidi.h"
 #include "nw_check.h"
 #include "nw_lane.h"
 #include "nw_expand.h"
@@ -80,6 +81,10 @@ struct gsa_ctx
     size_t clk_cap = 0, clk_n = 0;
     int timing_state = 0;  // 0 none, 1 two launches (events + stamps), 2 fused (one launch), 3 pipelined
     int timing_groups = 0;
+    // score-only NW from both ends (score_bidi): tap rows, reversed sequences, the second launch's
+    // control words and results
+    int* bidi = nullptr;
+    size_t bidi_cap = 0;  // ints
     // the pipelined full batch: pass 1 of pair groups 1.. on a stream of its own, one event per group
     hipStream_t p1stream = nullptr;
     static constexpr int kMaxGroups = 16;
@@ -320,6 +325,139 @@ int sw_idx_bits(int64_t R, int64_t C)
     return n ? 64 - __builtin_clzll(n) : 1;
 }
 
+// Score-only NW from both ends (nw_bidi.h): a single pair's wavefront time is (C + strips x lag)
+// steps, and at 50k the strips' fill-in is ~45 % of it; the top half (rows 1..m) forward and the
+// bottom half reversed (rows R..m+1 of the reversed pair) run at the same time on other CUs, each
+// with half the strips, and one workgroup combines the two rows where they meet.  m = K floor(R/2K)
+// so that row m of the top and row R - m of the reversed bottom are both a lane's last row (the
+// strips' tap, StripArgs::tapRow); R % K != 0 takes the one-direction path.
+constexpr int kScoreTooLargeB = -1001;
+int score_bidi(gsa_ctx* ctx, const int32_t* seqY, int64_t R, const int32_t* seqX, int64_t C, const int32_t* subst,
+               int32_t substsz, int32_t gapo, int32_t gape, int scoreK, gsa_score_result* out, hipStream_t st)
+{
+    const int K = scoreK;
+    const int64_t TR = (int64_t)(64 * K) * gsa::kSparseNS;
+    const int64_t m = (int64_t)K * (R / (2 * K)), mb = R - m;
+    const int64_t tkTop = (m + TR - 1) / TR, tkBot = (mb + TR - 1) / TR;
+    const bool affine = gapo != gape;
+    const size_t tapLen = (size_t)gsa::kTapPad + (size_t)C + 160;
+    // layout (ints): 4 tap rows, reversed Y (mb + 1), reversed X (C + 1), control: [0] result,
+    // [16..] the bottom launch's ticket / q8flag words, [32..] its 8 result words (64-bit)
+    const size_t oRY = 4 * tapLen, oRX = oRY + (size_t)mb + 1, oCtl = (oRX + (size_t)C + 1 + 63) & ~(size_t)63;
+    const size_t need = oCtl + 64;
+    hipError_t e;
+    if (ctx->bidi_cap < need || !ctx->bidi)
+    {
+        if (ctx->bidi) (void)hipFree(ctx->bidi);
+        ctx->bidi = nullptr;
+        ctx->bidi_cap = 0;
+        if ((e = hipMalloc(&ctx->bidi, need * sizeof(int))) != hipSuccess) return fail(ctx, e, GSA_ERROR_MEMORY_ALLOCATION);
+        ctx->bidi_cap = need;
+    }
+    if (!ctx->p1stream && (e = hipStreamCreateWithFlags(&ctx->p1stream, hipStreamNonBlocking)) != hipSuccess)
+        return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
+    for (int g = 0; g < 2; ++g)
+        if (!ctx->pipe_ev[g] && (e = hipEventCreateWithFlags(&ctx->pipe_ev[g], hipEventDisableTiming)) != hipSuccess)
+            return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
+    if (!ctx->sctl && (e = hipMalloc(&ctx->sctl, 64)) != hipSuccess) return fail(ctx, e, GSA_ERROR_MEMORY_ALLOCATION);
+    int* tapTH = ctx->bidi;
+    int* tapTF = tapTH + tapLen;
+    int* tapBH = tapTF + tapLen;
+    int* tapBF = tapBH + tapLen;
+    int* ry = ctx->bidi + oRY;
+    int* rx = ctx->bidi + oRX;
+    int* ctl = ctx->bidi + oCtl;
+    unsigned long long* bsctl = (unsigned long long*)(ctl + 32);
+    // descriptors of both halves, granules of both (two arrays each)
+    int s = ensure_desc(ctx, 2);
+    if (s != GSA_SUCCESS) return s;
+    const size_t granT = (size_t)tkTop * (size_t)gsa::gran_stride((int)C);
+    const size_t granB = (size_t)tkBot * (size_t)gsa::gran_stride((int)C);
+    if ((s = ensure_gran(ctx, 2 * (granT + granB), st)) != GSA_SUCCESS) return s;
+    gsa::PairDesc d[2];
+    std::memset(d, 0, sizeof(d));
+    d[0].seqY = seqY;
+    d[0].seqX = seqX;
+    d[0].R = (int)m;
+    d[0].nTickets = (int)tkTop;
+    d[1].seqY = ry;
+    d[1].seqX = rx;
+    d[1].R = (int)mb;
+    d[1].nTickets = (int)tkBot;
+    for (int h = 0; h < 2; ++h) d[h].C = d[h].Cp = (int)C;
+    (void)hipEventRecord(ctx->ev0, st);
+    if ((e = hipMemcpyAsync(ctx->desc, d, sizeof(d), hipMemcpyHostToDevice, st)) != hipSuccess)
+        return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
+    if ((e = gsa::launch_reverse(seqY, (int)m + 1, (int)R, ry, st)) != hipSuccess ||
+        (e = gsa::launch_reverse(seqX, 1, (int)C, rx, st)) != hipSuccess)
+        return fail(ctx, e, GSA_ERROR_KERNEL_FAILURE);
+    if ((e = hipMemsetAsync(ctx->ctl, 0, 4, st)) != hipSuccess || (e = hipMemsetAsync(ctx->sctl, 0, 32, st)) != hipSuccess ||
+        (e = hipMemsetAsync(ctl, 0, 64 * sizeof(int), st)) != hipSuccess)
+        return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
+    const int mode = affine ? gsa::kModeScoreAG : gsa::kModeScoreAGL;
+    const int q8env = env_int("GSA_KROW_Q8", 1);
+    const int q8 = (q8env != 0 && (q8env == 2 || K == 4) && gsa::krow_score_lds_bytes(substsz, true) <= (size_t)ctx->lds_max) ? 1 : 0;
+    auto args = [&](int h) {
+        gsa::StripArgs a;
+        std::memset(&a, 0, sizeof(a));
+        a.subst = subst;
+        a.substsz = substsz;
+        a.g = gapo;
+        a.go = gapo;
+        a.ge = gape;
+        a.ns = gsa::kSparseNS;
+        a.pairs = ctx->desc + h;
+        a.nPairs = 1;
+        a.nTicketsTotal = (int)(h == 0 ? tkTop : tkBot);
+        a.gran = ctx->gran + (h == 0 ? 0 : 2 * granT);
+        a.gran2 = a.gran + (h == 0 ? granT : granB);
+        a.ticket = h == 0 ? ctx->ctl : (unsigned*)ctl + 16;
+        a.q8flag = h == 0 ? ctx->ctl + 2 : (unsigned*)ctl + 17;
+        a.err = (unsigned*)((h == 0 ? ctx->sctl : bsctl) + 3);
+        a.agResult = (int*)(h == 0 ? ctx->sctl : bsctl);
+        a.swBest = (h == 0 ? ctx->sctl : bsctl) + 1;
+        a.spin = ctx->spin_ticks;
+        a.idxBits = sw_idx_bits(h == 0 ? m : mb, C);
+        a.epoch = ++ctx->epoch;
+        if (a.epoch == 0) a.epoch = ++ctx->epoch;
+        a.q8 = q8;
+        a.tapRow = (int)(h == 0 ? m : mb);
+        a.tapH = h == 0 ? tapTH : tapBH;
+        a.tapF = h == 0 ? tapTF : tapBF;
+        return a;
+    };
+    const gsa::StripArgs top = args(0), bot = args(1);
+    // the bottom half on the side stream, behind everything on st so far
+    if ((e = hipEventRecord(ctx->pipe_ev[0], st)) != hipSuccess || (e = hipStreamWaitEvent(ctx->p1stream, ctx->pipe_ev[0], 0)) != hipSuccess)
+        return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
+    if ((e = gsa::launch_krow_score(bot, mode, K, std::max(1, std::min((int)tkBot, ctx->cu_count)), ctx->p1stream)) != hipSuccess)
+        return fail(ctx, e, GSA_ERROR_KERNEL_FAILURE);
+    if ((e = hipEventRecord(ctx->pipe_ev[1], ctx->p1stream)) != hipSuccess) return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
+    if ((e = gsa::launch_krow_score(top, mode, K, std::max(1, std::min((int)tkTop, ctx->cu_count)), st)) != hipSuccess)
+        return fail(ctx, e, GSA_ERROR_KERNEL_FAILURE);
+    note_launch(ctx);
+    if ((e = hipStreamWaitEvent(st, ctx->pipe_ev[1], 0)) != hipSuccess) return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
+    if ((e = gsa::launch_bidi_combine(tapTH, tapTF, tapBH, tapBF, (int)m, (int)mb, (int)C, gapo, gape, affine, ctl, st)) !=
+        hipSuccess)
+        return fail(ctx, e, GSA_ERROR_KERNEL_FAILURE);
+    (void)hipEventRecord(ctx->ev1, st);
+    unsigned long long rt[4] = {0, 0, 0, 0}, rb[4] = {0, 0, 0, 0};
+    int res = 0;
+    if ((e = hipMemcpyAsync(rt, ctx->sctl, sizeof(rt), hipMemcpyDeviceToHost, st)) != hipSuccess ||
+        (e = hipMemcpyAsync(rb, bsctl, sizeof(rb), hipMemcpyDeviceToHost, st)) != hipSuccess ||
+        (e = hipMemcpyAsync(&res, ctl, sizeof(int), hipMemcpyDeviceToHost, st)) != hipSuccess ||
+        (e = hipStreamSynchronize(st)) != hipSuccess)
+        return fail(ctx, e, GSA_ERROR_KERNEL_FAILURE);
+    (void)hipEventElapsedTime(&out->calc_kernel_ms, ctx->ev0, ctx->ev1);
+    const unsigned et = (unsigned)rt[3], eb = (unsigned)rb[3];
+    if (et == 2u || eb == 2u) return kScoreTooLargeB;  // a value outside int16: the row scan
+    if (et != 0 || eb != 0) return GSA_ERROR_KERNEL_FAILURE;
+    out->score = res;
+    out->i_end = R;
+    out->j_end = C;
+    return GSA_SUCCESS;
+}
+
 int score_ag_strip(gsa_ctx* ctx, const int32_t* seqY, int64_t R, const int32_t* seqX, int64_t C, const int32_t* subst,
                    int32_t substsz, int32_t gapo, int32_t gape, int32_t local, gsa_score_result* out, hipStream_t st)
 {
@@ -337,6 +475,14 @@ int score_ag_strip(gsa_ctx* ctx, const int32_t* seqY, int64_t R, const int32_t* 
     const int64_t TR = krow ? (int64_t)(64 * scoreK) * gsa::kSparseNS : (int64_t)gsa::kWaveRows * gsa::kSparseNS;
     const int64_t tickets = (R + TR - 1) / TR;
     if (tickets > (1ll << 30) || C > (1ll << 30)) return GSA_ERROR_INVALID_VALUE;
+    // NW from both ends (score_bidi) when each half keeps >= 4 tickets (GSA_SCORE_BIDI: 0 never, 2 any
+    // size, for tests)
+    const int bidi = env_int("GSA_SCORE_BIDI", 1);
+    if (krow && !local && bidi != 0 && R % scoreK == 0 && R >= 2 * scoreK && (bidi == 2 || R >= 8 * TR))
+    {
+        const int sb = score_bidi(ctx, seqY, R, seqX, C, subst, substsz, gapo, gape, scoreK, out, st);
+        return sb == kScoreTooLargeB ? kScoreTooLarge : sb;
+    }
     gsa::StripArgs a;
     std::memset(&a, 0, sizeof(a));
     a.subst = subst;
@@ -631,6 +777,7 @@ int enqueue_batch(gsa_ctx* ctx, int mode, int npairs, const gsa_pair_dev* pairs,
                 {
                     if (ctx->stamps) (void)hipFree(ctx->stamps);
     if (ctx->clk) (void)hipFree(ctx->clk);
+    if (ctx->bidi) (void)hipFree(ctx->bidi);
     for (hipEvent_t ev : ctx->pipe_ev)
         if (ev) (void)hipEventDestroy(ev);
     if (ctx->p1stream) (void)hipStreamDestroy(ctx->p1stream);

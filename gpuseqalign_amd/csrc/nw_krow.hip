@@ -1108,9 +1108,10 @@ __host__ __device__ inline KsLds ks_layout(int substsz, bool q8 = false)
     return L;
 }
 
-// strip wave (NS = 4): 64 K rows, K (4, or 2) per lane
-template <int MODE, bool Q8, int K>
-__device__ __forceinline__ void ks_strip(const StripArgs& a, const KsLds& L, int tk, int w, int lane)
+// strip wave (NS = 4): 64 K rows, K (4, or 2) per lane.  TAP: lane tapLane's last row is a.tapRow,
+// stored block by block (score_bidi)
+template <int MODE, bool Q8, int K, bool TAP = false>
+__device__ __forceinline__ void ks_strip(const StripArgs& a, const KsLds& L, int tk, int w, int lane, int tapLane = 0)
 {
     constexpr int NS = kKrowNSDefault, LW = 1024;
     constexpr bool AG = !is_lin_mode(MODE);  // E' and F' carried
@@ -1288,6 +1289,15 @@ __device__ __forceinline__ void ks_strip(const StripArgs& a, const KsLds& L, int
         flag_st2(f_out, bb + 1 == NB ? kBig : kBlk * bb + kBlk, kBlk * bb + 64 + kBlk);
     };
     int rpin = 0, rpco = 0, rpxo = 0, rsink = 0;
+    // TAP: byte address of block 0's 16 values of the tap row (lane tapLane: lt[u] and lf[u] are
+    // columns 16 b + u - 1 - lane of its last row)
+    uint64_t tapB = 0, tapBF = 0;
+    if constexpr (TAP)
+    {
+        tapB = (uint64_t)(uintptr_t)a.tapH + 4ull * (uint64_t)(kTapPad - 1 - lane);
+        tapBF = (uint64_t)(uintptr_t)a.tapF + 4ull * (uint64_t)(kTapPad - 1 - lane);
+    }
+    const uint64_t tapMask = 1ull << (tapLane & 63);
 
     auto block = [&](int b, int (&qc)[K][kQD], int (&qn)[K][kQD]) {
         {
@@ -1373,6 +1383,36 @@ __device__ __forceinline__ void ks_strip(const StripArgs& a, const KsLds& L, int
             }
         }
         handoff(b);
+        if constexpr (TAP)
+        {
+            // the tap lane alone (exec set and restored inside the asm), 64 B per row per block
+            uint64_t sv;
+            asm volatile("s_mov_b64 %0, exec\n"
+                         "s_mov_b64 exec, %1\n"
+                         "global_store_dwordx4 %2, %3, off\n"
+                         "global_store_dwordx4 %2, %4, off offset:16\n"
+                         "global_store_dwordx4 %2, %5, off offset:32\n"
+                         "global_store_dwordx4 %2, %6, off offset:48\n"
+                         "s_mov_b64 exec, %0"
+                         : "=&s"(sv)
+                         : "s"(tapMask), "v"(tapB + 64ull * (uint64_t)b), "v"(int4v {lt[0], lt[1], lt[2], lt[3]}),
+                           "v"(int4v {lt[4], lt[5], lt[6], lt[7]}), "v"(int4v {lt[8], lt[9], lt[10], lt[11]}),
+                           "v"(int4v {lt[12], lt[13], lt[14], lt[15]})
+                         : "memory");
+            if constexpr (AG)
+                asm volatile("s_mov_b64 %0, exec\n"
+                             "s_mov_b64 exec, %1\n"
+                             "global_store_dwordx4 %2, %3, off\n"
+                             "global_store_dwordx4 %2, %4, off offset:16\n"
+                             "global_store_dwordx4 %2, %5, off offset:32\n"
+                             "global_store_dwordx4 %2, %6, off offset:48\n"
+                             "s_mov_b64 exec, %0"
+                             : "=&s"(sv)
+                             : "s"(tapMask), "v"(tapBF + 64ull * (uint64_t)b), "v"(int4v {lf[0], lf[1], lf[2], lf[3]}),
+                               "v"(int4v {lf[4], lf[5], lf[6], lf[7]}), "v"(int4v {lf[8], lf[9], lf[10], lf[11]}),
+                               "v"(int4v {lf[12], lf[13], lf[14], lf[15]})
+                             : "memory");
+        }
         if constexpr (SW)
         {
             // fold the block's best per row: score = key >> 4 - k |ge|, first step 15 - key & 15
@@ -1770,8 +1810,14 @@ __global__ void __launch_bounds__(64 * kr_waves<kKrowNSDefault>()) nw_kscore_ker
             ks_profile<Q8>(pa, L, lane);
         else
         {
+            // score_bidi's tap: the strip with a lane whose last row is a.tapRow (uniform)
+            const int r0 = tk * (64 * K * NS) + 64 * K * w + 1;
+            const int rt = a.tapRow - r0;
             __builtin_amdgcn_s_setprio(3);
-            ks_strip<MODE, Q8, K>(pa, L, tk, w, lane);
+            if (!is_sw_mode(MODE) && a.tapRow >= 0 && rt >= 0 && rt < 64 * K && (rt + 1) % K == 0)
+                ks_strip<MODE, Q8, K, !is_sw_mode(MODE)>(pa, L, tk, w, lane, (rt + 1) / K - 1);
+            else
+                ks_strip<MODE, Q8, K>(pa, L, tk, w, lane);
             __builtin_amdgcn_s_setprio(0);
         }
     }

@@ -118,7 +118,14 @@ struct StripArgs
     // [start, end] per pass-1 strip (global strip index; start = the ticket's start, before the
     // strip's first wait), then [claimed, ready, done] per expansion task; null otherwise
     unsigned long long* stamps;
+    // score-only NW from both ends (gsa_capi.hip score_bidi): the strip with a lane whose last row is
+    // tapRow stores that row's Hgo' (tapH) and, affine, F' (tapF), shifted as the hand-off holds
+    // them, at tap[kTapPad + column] for every column the lane computes; tapRow < 0: none
+    int* tapH;
+    int* tapF;
+    int tapRow;
 };
+constexpr int kTapPad = 128;  // tap row buffers: columns -kTapPad .. C + 79
 
 // Resource footprint of the last fill launched from this host thread: what the reference's
 // updateNwAlgPeakMemUsage (nwalign_shared.cpp:5-25) multiplies out -- kernel attributes

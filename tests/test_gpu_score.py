@@ -188,3 +188,60 @@ def test_profile_widths_and_stale_columns(engine, golden, monkeypatch, q8, k, go
         Y, X = random_pair(R, C, 11 * R + C)
         r = engine.score(Y, X, golden.blosum62, go, ge, local)
         assert (r["score"], r["i_end"], r["j_end"]) == oracle.score_ag(Y, X, golden.blosum62, go, ge, local), (R, C)
+
+
+@pytest.mark.parametrize("k", ["2", "4"])
+@pytest.mark.parametrize("q8", ["0", "1"])
+@pytest.mark.parametrize("go,ge,local", MODES)
+def test_score_both_ends(engine, golden, monkeypatch, k, q8, go, ge, local):
+    """NW from both ends (gsa_capi.hip score_bidi, nw_bidi.hip), forced at every size
+    (GSA_SCORE_BIDI=2; by default pairs whose halves keep >= 4 tickets): the top half's tap row m,
+    the reversed bottom half's row R - m and the combine.  Odd R (R % K != 0) and local modes keep the
+    one-direction kernel; both equal the oracle."""
+    import oracle
+    monkeypatch.setenv("GSA_SCORE_BIDI", "2")
+    monkeypatch.setenv("GSA_SCORE_K", k)
+    monkeypatch.setenv("GSA_KROW_Q8", q8)
+    for R, C in [(2, 1), (4, 5), (8, 300), (130, 1), (130, 700), (512, 64), (514, 1000), (1024, 1024), (1027, 900),
+                 (2052, 257), (4100, 3000)]:
+        Y, X = random_pair(R, C, 13 * R + C)
+        r = engine.score(Y, X, golden.blosum62, go, ge, local)
+        assert (r["score"], r["i_end"], r["j_end"]) == oracle.score_ag(Y, X, golden.blosum62, go, ge, local), (R, C)
+
+
+@pytest.mark.parametrize("k", ["2", "4"])
+@pytest.mark.parametrize("go,ge", [(-11, -11), (-11, -1), (-5, -2), (-3, -1)])
+@pytest.mark.parametrize("ins", [1, 7, 40, 300])
+def test_score_both_ends_gap_across_split(engine, golden, monkeypatch, k, go, ge, ins):
+    """A vertical gap that crosses the split row m = K floor(R / 2K): Y is X with ins letters
+    inserted around the middle, so the best path's gap spans rows m and m + 1 and pays its open once
+    (the combine's F + F^r - (go - ge) term); also a horizontal gap at the split (X longer)."""
+    import oracle
+    monkeypatch.setenv("GSA_SCORE_BIDI", "2")
+    monkeypatch.setenv("GSA_SCORE_K", k)
+    rng = np.random.default_rng(ins * 31 + int(k))
+    base = rng.integers(0, 20, 1200).astype(np.int32)
+    extra = rng.integers(0, 20, ins).astype(np.int32)
+    for cut in (600 - ins // 2, 600 - ins + 2, 600):
+        ycore = np.concatenate([base[:cut], extra, base[cut:]])
+        Y = np.concatenate([[0], ycore]).astype(np.int32)
+        X = np.concatenate([[0], base]).astype(np.int32)
+        for A, B in ((Y, X), (X, Y)):
+            A = A[:len(A) - (len(A) - 1) % int(k)]
+            r = engine.score(A, B, golden.blosum62, go, ge, False)
+            assert (r["score"], r["i_end"], r["j_end"]) == oracle.score_ag(A, B, golden.blosum62, go, ge, False), cut
+
+
+def test_score_both_ends_default_matches_one_direction(engine, golden, monkeypatch):
+    """The default switch (GSA_SCORE_BIDI=1: halves of >= 4 tickets) on a 20k related pair, NW-LG
+    and NW-AG, against the one-direction kernel (GSA_SCORE_BIDI=0) and the oracle's tiled restatement."""
+    import oracle
+    Y, X = related_pair(20000, 20100)
+    Y = Y[:len(Y) - (len(Y) - 1) % 4]  # R % K == 0: the split's rows are lanes' last rows
+    for go, ge in [(-11, -11), (-11, -1)]:
+        monkeypatch.setenv("GSA_SCORE_BIDI", "1")
+        r1 = engine.score(Y, X, golden.blosum62, go, ge, False)
+        monkeypatch.setenv("GSA_SCORE_BIDI", "0")
+        r0 = engine.score(Y, X, golden.blosum62, go, ge, False)
+        ref = oracle.score_ag(Y, X, golden.blosum62, go, ge, False, mt=True, blocksz=256, nthreads=8)
+        assert (r1["score"], r1["i_end"], r1["j_end"]) == (r0["score"], r0["i_end"], r0["j_end"]) == ref
