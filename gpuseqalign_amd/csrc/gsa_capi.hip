@@ -325,26 +325,26 @@ int sw_idx_bits(int64_t R, int64_t C)
     return n ? 64 - __builtin_clzll(n) : 1;
 }
 
-// Score-only NW from both ends (nw_bidi.h): a single pair's wavefront time is (C + strips x lag)
-// steps, and at 50k the strips' fill-in is ~45 % of it; the top half (rows 1..m) forward and the
-// bottom half reversed (rows R..m+1 of the reversed pair) run at the same time on other CUs, each
-// with half the strips, and one workgroup combines the two rows where they meet.  m = K floor(R/2K)
-// so that row m of the top and row R - m of the reversed bottom are both a lane's last row (the
-// strips' tap, StripArgs::tapRow); R % K != 0 takes the one-direction path.
+// Score-only NW from both ends (nw_bidi.h): a single pair's wavefront time is (C + strips x hop)
+// steps, and at 50k the strips' fill-in is ~30 % of it; the top half (rows 1..m) forward and the
+// bottom half reversed (rows R..m+1 of the reversed pair) run at the same time, each with half the
+// strips, as two pairs of one launch with their tickets interleaved, and a combine kernel takes the
+// best crossing of the rows where they meet.  m = K floor(R/2K), so that row m of the top and row
+// R - m of the reversed bottom are both a lane's last row (the strips' tap); R % K != 0 takes the
+// one-direction path.
 constexpr int kScoreTooLargeB = -1001;
 int score_bidi(gsa_ctx* ctx, const int32_t* seqY, int64_t R, const int32_t* seqX, int64_t C, const int32_t* subst,
-               int32_t substsz, int32_t gapo, int32_t gape, int scoreK, gsa_score_result* out, hipStream_t st)
+               int32_t substsz, int32_t gapo, int32_t gape, int K, gsa_score_result* out, hipStream_t st)
 {
-    const int K = scoreK;
     const int64_t TR = (int64_t)(64 * K) * gsa::kSparseNS;
     const int64_t m = (int64_t)K * (R / (2 * K)), mb = R - m;
     const int64_t tkTop = (m + TR - 1) / TR, tkBot = (mb + TR - 1) / TR;
     const bool affine = gapo != gape;
-    const size_t tapLen = (size_t)gsa::kTapPad + (size_t)C + 160;
-    // layout (ints): 4 tap rows, reversed Y (mb + 1), reversed X (C + 1), control: [0] result,
-    // [16..] the bottom launch's ticket / q8flag words, [32..] its 8 result words (64-bit)
-    const size_t oRY = 4 * tapLen, oRX = oRY + (size_t)mb + 1, oCtl = (oRX + (size_t)C + 1 + 63) & ~(size_t)63;
-    const size_t need = oCtl + 64;
+    const size_t tapLen = ((size_t)gsa::kTapPad + (size_t)C + 160 + 63) & ~(size_t)63;
+    // layout (ints): tap rows H, F of the top, then of the bottom; reversed Y (mb + 1), reversed X
+    // (C + 1), the combine's result
+    const size_t oRY = 4 * tapLen, oRX = oRY + (size_t)mb + 1, oRes = (oRX + (size_t)C + 1 + 63) & ~(size_t)63;
+    const size_t need = oRes + 64;
     hipError_t e;
     if (ctx->bidi_cap < need || !ctx->bidi)
     {
@@ -354,105 +354,85 @@ int score_bidi(gsa_ctx* ctx, const int32_t* seqY, int64_t R, const int32_t* seqX
         if ((e = hipMalloc(&ctx->bidi, need * sizeof(int))) != hipSuccess) return fail(ctx, e, GSA_ERROR_MEMORY_ALLOCATION);
         ctx->bidi_cap = need;
     }
-    if (!ctx->p1stream && (e = hipStreamCreateWithFlags(&ctx->p1stream, hipStreamNonBlocking)) != hipSuccess)
-        return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
-    for (int g = 0; g < 2; ++g)
-        if (!ctx->pipe_ev[g] && (e = hipEventCreateWithFlags(&ctx->pipe_ev[g], hipEventDisableTiming)) != hipSuccess)
-            return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
     if (!ctx->sctl && (e = hipMalloc(&ctx->sctl, 64)) != hipSuccess) return fail(ctx, e, GSA_ERROR_MEMORY_ALLOCATION);
-    int* tapTH = ctx->bidi;
-    int* tapTF = tapTH + tapLen;
-    int* tapBH = tapTF + tapLen;
-    int* tapBF = tapBH + tapLen;
+    int* tapH = ctx->bidi;
+    int* tapF = tapH + tapLen;  // half 1: + 2 tapLen
     int* ry = ctx->bidi + oRY;
     int* rx = ctx->bidi + oRX;
-    int* ctl = ctx->bidi + oCtl;
-    unsigned long long* bsctl = (unsigned long long*)(ctl + 32);
-    // descriptors of both halves, granules of both (two arrays each)
+    int* res = ctx->bidi + oRes;
     int s = ensure_desc(ctx, 2);
     if (s != GSA_SUCCESS) return s;
-    const size_t granT = (size_t)tkTop * (size_t)gsa::gran_stride((int)C);
-    const size_t granB = (size_t)tkBot * (size_t)gsa::gran_stride((int)C);
-    if ((s = ensure_gran(ctx, 2 * (granT + granB), st)) != GSA_SUCCESS) return s;
+    const size_t stride = (size_t)gsa::gran_stride((int)C);
+    const size_t granAll = (size_t)(tkTop + tkBot) * stride;
+    if ((s = ensure_gran(ctx, 2 * granAll, st)) != GSA_SUCCESS) return s;
     gsa::PairDesc d[2];
     std::memset(d, 0, sizeof(d));
     d[0].seqY = seqY;
     d[0].seqX = seqX;
     d[0].R = (int)m;
     d[0].nTickets = (int)tkTop;
+    d[0].granOff = 0;
     d[1].seqY = ry;
     d[1].seqX = rx;
     d[1].R = (int)mb;
     d[1].nTickets = (int)tkBot;
+    d[1].granOff = (long long)((size_t)tkTop * stride);
     for (int h = 0; h < 2; ++h) d[h].C = d[h].Cp = (int)C;
-    (void)hipEventRecord(ctx->ev0, st);
-    if ((e = hipMemcpyAsync(ctx->desc, d, sizeof(d), hipMemcpyHostToDevice, st)) != hipSuccess)
-        return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
-    if ((e = gsa::launch_reverse(seqY, (int)m + 1, (int)R, ry, st)) != hipSuccess ||
-        (e = gsa::launch_reverse(seqX, 1, (int)C, rx, st)) != hipSuccess)
-        return fail(ctx, e, GSA_ERROR_KERNEL_FAILURE);
-    if ((e = hipMemsetAsync(ctx->ctl, 0, 4, st)) != hipSuccess || (e = hipMemsetAsync(ctx->sctl, 0, 32, st)) != hipSuccess ||
-        (e = hipMemsetAsync(ctl, 0, 64 * sizeof(int), st)) != hipSuccess)
-        return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
     const int mode = affine ? gsa::kModeScoreAG : gsa::kModeScoreAGL;
     const int q8env = env_int("GSA_KROW_Q8", 1);
-    const int q8 = (q8env != 0 && (q8env == 2 || K == 4) && gsa::krow_score_lds_bytes(substsz, true) <= (size_t)ctx->lds_max) ? 1 : 0;
-    auto args = [&](int h) {
-        gsa::StripArgs a;
-        std::memset(&a, 0, sizeof(a));
-        a.subst = subst;
-        a.substsz = substsz;
-        a.g = gapo;
-        a.go = gapo;
-        a.ge = gape;
-        a.ns = gsa::kSparseNS;
-        a.pairs = ctx->desc + h;
-        a.nPairs = 1;
-        a.nTicketsTotal = (int)(h == 0 ? tkTop : tkBot);
-        a.gran = ctx->gran + (h == 0 ? 0 : 2 * granT);
-        a.gran2 = a.gran + (h == 0 ? granT : granB);
-        a.ticket = h == 0 ? ctx->ctl : (unsigned*)ctl + 16;
-        a.q8flag = h == 0 ? ctx->ctl + 2 : (unsigned*)ctl + 17;
-        a.err = (unsigned*)((h == 0 ? ctx->sctl : bsctl) + 3);
-        a.agResult = (int*)(h == 0 ? ctx->sctl : bsctl);
-        a.swBest = (h == 0 ? ctx->sctl : bsctl) + 1;
-        a.spin = ctx->spin_ticks;
-        a.idxBits = sw_idx_bits(h == 0 ? m : mb, C);
-        a.epoch = ++ctx->epoch;
-        if (a.epoch == 0) a.epoch = ++ctx->epoch;
-        a.q8 = q8;
-        a.tapRow = (int)(h == 0 ? m : mb);
-        a.tapH = h == 0 ? tapTH : tapBH;
-        a.tapF = h == 0 ? tapTF : tapBF;
-        return a;
-    };
-    const gsa::StripArgs top = args(0), bot = args(1);
-    // the bottom half on the side stream, behind everything on st so far
-    if ((e = hipEventRecord(ctx->pipe_ev[0], st)) != hipSuccess || (e = hipStreamWaitEvent(ctx->p1stream, ctx->pipe_ev[0], 0)) != hipSuccess)
-        return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
-    if ((e = gsa::launch_krow_score(bot, mode, K, std::max(1, std::min((int)tkBot, ctx->cu_count)), ctx->p1stream)) != hipSuccess)
-        return fail(ctx, e, GSA_ERROR_KERNEL_FAILURE);
-    if ((e = hipEventRecord(ctx->pipe_ev[1], ctx->p1stream)) != hipSuccess) return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
-    if ((e = gsa::launch_krow_score(top, mode, K, std::max(1, std::min((int)tkTop, ctx->cu_count)), st)) != hipSuccess)
+    const int q8 =
+        (q8env != 0 && (q8env == 2 || K == 4) && gsa::krow_score_lds_bytes(substsz, true) <= (size_t)ctx->lds_max) ? 1 : 0;
+    gsa::StripArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.subst = subst;
+    a.substsz = substsz;
+    a.g = gapo;
+    a.go = gapo;
+    a.ge = gape;
+    a.ns = gsa::kSparseNS;
+    a.pairs = ctx->desc;
+    a.nPairs = 2;
+    a.nTicketsTotal = (int)(tkTop + tkBot);
+    a.bidiTop = (int)tkTop;
+    a.gran = ctx->gran;
+    a.gran2 = ctx->gran + granAll;
+    a.ticket = ctx->ctl;
+    a.q8flag = ctx->ctl + 2;
+    a.err = (unsigned*)(ctx->sctl + 3);
+    a.agResult = (int*)ctx->sctl;
+    a.swBest = ctx->sctl + 1;
+    a.spin = ctx->spin_ticks;
+    a.idxBits = sw_idx_bits(R, C);
+    a.epoch = ++ctx->epoch;
+    if (a.epoch == 0) a.epoch = ++ctx->epoch;
+    a.q8 = q8;
+    a.tapRow = (int)m;
+    a.tapRowB = (int)mb;
+    a.tapH = tapH;
+    a.tapF = tapF;
+    a.tapStride = (int)(2 * tapLen);
+    (void)hipEventRecord(ctx->ev0, st);
+    if ((e = gsa::launch_bidi_prep(d[0], d[1], ctx->desc, seqY, (int)m, (int)R, seqX, (int)C, ry, rx, ctx->ctl, ctx->sctl,
+                                   res, st)) != hipSuccess ||
+        (e = gsa::launch_krow_score(a, mode, K, std::max(1, std::min((int)(tkTop + tkBot), ctx->cu_count)), st)) !=
+            hipSuccess)
         return fail(ctx, e, GSA_ERROR_KERNEL_FAILURE);
     note_launch(ctx);
-    if ((e = hipStreamWaitEvent(st, ctx->pipe_ev[1], 0)) != hipSuccess) return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
-    if ((e = gsa::launch_bidi_combine(tapTH, tapTF, tapBH, tapBF, (int)m, (int)mb, (int)C, gapo, gape, affine, ctl, st)) !=
-        hipSuccess)
+    if ((e = gsa::launch_bidi_combine(tapH, tapF, tapH + 2 * tapLen, tapF + 2 * tapLen, (int)m, (int)mb, (int)C, gapo,
+                                      gape, affine, res, st)) != hipSuccess)
         return fail(ctx, e, GSA_ERROR_KERNEL_FAILURE);
     (void)hipEventRecord(ctx->ev1, st);
-    unsigned long long rt[4] = {0, 0, 0, 0}, rb[4] = {0, 0, 0, 0};
-    int res = 0;
-    if ((e = hipMemcpyAsync(rt, ctx->sctl, sizeof(rt), hipMemcpyDeviceToHost, st)) != hipSuccess ||
-        (e = hipMemcpyAsync(rb, bsctl, sizeof(rb), hipMemcpyDeviceToHost, st)) != hipSuccess ||
-        (e = hipMemcpyAsync(&res, ctl, sizeof(int), hipMemcpyDeviceToHost, st)) != hipSuccess ||
+    unsigned long long rw[4] = {0, 0, 0, 0};
+    int score = 0;
+    if ((e = hipMemcpyAsync(rw, ctx->sctl, sizeof(rw), hipMemcpyDeviceToHost, st)) != hipSuccess ||
+        (e = hipMemcpyAsync(&score, res, sizeof(int), hipMemcpyDeviceToHost, st)) != hipSuccess ||
         (e = hipStreamSynchronize(st)) != hipSuccess)
         return fail(ctx, e, GSA_ERROR_KERNEL_FAILURE);
     (void)hipEventElapsedTime(&out->calc_kernel_ms, ctx->ev0, ctx->ev1);
-    const unsigned et = (unsigned)rt[3], eb = (unsigned)rb[3];
-    if (et == 2u || eb == 2u) return kScoreTooLargeB;  // a value outside int16: the row scan
-    if (et != 0 || eb != 0) return GSA_ERROR_KERNEL_FAILURE;
-    out->score = res;
+    const unsigned err = (unsigned)rw[3];
+    if (err == 2u) return kScoreTooLargeB;  // a value outside int16: the row scan
+    if (err != 0) return GSA_ERROR_KERNEL_FAILURE;
+    out->score = score;
     out->i_end = R;
     out->j_end = C;
     return GSA_SUCCESS;
@@ -475,12 +455,15 @@ int score_ag_strip(gsa_ctx* ctx, const int32_t* seqY, int64_t R, const int32_t* 
     const int64_t TR = krow ? (int64_t)(64 * scoreK) * gsa::kSparseNS : (int64_t)gsa::kWaveRows * gsa::kSparseNS;
     const int64_t tickets = (R + TR - 1) / TR;
     if (tickets > (1ll << 30) || C > (1ll << 30)) return GSA_ERROR_INVALID_VALUE;
-    // NW from both ends (score_bidi) when each half keeps >= 4 tickets (GSA_SCORE_BIDI: 0 never, 2 any
-    // size, for tests)
+    // NW from both ends (score_bidi) when each half keeps >= 4 tickets, at 2 rows per lane in both
+    // NW modes (its halves have half the strips, so the shorter block wins for NW-LG too: 50k 2.25 ->
+    // 2.11 ms, profiles/r05_bidi_ab.txt).  GSA_SCORE_BIDI: 0 never, 2 at any size (tests)
     const int bidi = env_int("GSA_SCORE_BIDI", 1);
-    if (krow && !local && bidi != 0 && R % scoreK == 0 && R >= 2 * scoreK && (bidi == 2 || R >= 8 * TR))
+    const int kb = kenv == 2 || kenv == 4 ? kenv : 2;
+    const int64_t TRb = (int64_t)(64 * kb) * gsa::kSparseNS;
+    if (krow && !local && bidi != 0 && R % kb == 0 && R >= 2 * kb && (bidi == 2 || R >= 8 * TRb))
     {
-        const int sb = score_bidi(ctx, seqY, R, seqX, C, subst, substsz, gapo, gape, scoreK, out, st);
+        const int sb = score_bidi(ctx, seqY, R, seqX, C, subst, substsz, gapo, gape, kb, out, st);
         return sb == kScoreTooLargeB ? kScoreTooLarge : sb;
     }
     gsa::StripArgs a;

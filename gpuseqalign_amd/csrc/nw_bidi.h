@@ -1,19 +1,26 @@
 // nw_bidi.h -- score-only NW from both ends (gsa_capi.hip score_bidi): the pair's top half runs
-// forward and its bottom half, reversed, runs forward at the same time on other CUs; each launch
-// taps the row where the halves meet (StripArgs::tapRow), and one workgroup combines the two rows.
+// forward and its bottom half, reversed, runs forward in the same launch on other CUs (tickets
+// interleaved, StripArgs::bidiTop); each half taps the row where the halves meet
+// (StripArgs::tapRow / tapRowB), and a combine kernel takes the best crossing.
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include "nw_strip.h"
+
 namespace gsa {
 
-// dst[0] = 0, dst[i] = src[last + 1 - i] for i = 1 .. last - first + 1 (a header element, then
-// src[first .. last] reversed)
-hipError_t launch_reverse(const int* src, int first, int last, int* dst, hipStream_t stream);
+// One launch before the fill: desc[0..1] = d0, d1; ry[0] = rx[0] = 0, ry[i] = seqY[R + 1 - i]
+// (i = 1 .. R - m: rows m+1 .. R reversed), rx[j] = seqX[C + 1 - j]; the launch's ticket word, its
+// 4 result / error words and the combine's output (-2^31) reset.
+hipError_t launch_bidi_prep(const PairDesc& d0, const PairDesc& d1, PairDesc* desc, const int* seqY, int m, int R,
+                            const int* seqX, int C, int* ry, int* rx, unsigned* ticket,
+                            unsigned long long* words, int* out, hipStream_t stream);
 
 // out[0] = max over j = 0 .. C of max(Ht(j) + Hb(C - j), Ft(j) + Fb(C - j) - (go - ge)) (affine), or
 // of Ht(j) + Hb(C - j) (linear), where the tapped rows hold shifted values (Hgo' = H - (i+j) ge +
 // (go - ge), F' = F - (i+j) ge) of row m (top, forward) and of row mb (bottom, reversed) at
-// tap[kTapPad + j]; column 0 is the gap border go + (i-1) ge
+// tap[kTapPad + j]; column 0 is the gap border go + (i-1) ge.  Many workgroups, each folding its
+// columns into out[0] with an atomic max (out[0] starts at -2^31, launch_bidi_prep).
 hipError_t launch_bidi_combine(const int* topH, const int* topF, const int* botH, const int* botF, int m, int mb,
                                int C, int go, int ge, bool affine, int* out, hipStream_t stream);
 

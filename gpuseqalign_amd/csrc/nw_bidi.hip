@@ -5,6 +5,7 @@
 // best suffix score from (m, j) (H^r) and the one that starts with a vertical gap (F^r), and a gap
 // that crosses the boundary pays its open once: score = max_j max(H + H^r, F + F^r - (go - ge)).
 #include <hip/hip_runtime.h>
+#include <limits.h>
 #include <stdint.h>
 
 #include "nw_bidi.h"
@@ -13,21 +14,32 @@
 namespace gsa {
 namespace {
 
-__global__ void reverse_kernel(const int* src, int first, int last, int* dst)
+__global__ void __launch_bounds__(256) bidi_prep_kernel(PairDesc d0, PairDesc d1, PairDesc* desc, const int* seqY,
+                                                        int m, int R, const int* seqX, int C, int* ry, int* rx,
+                                                        unsigned* ticket, unsigned long long* words, int* out)
 {
-    const int n = last - first + 1;
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i <= n; i += gridDim.x * blockDim.x)
-        dst[i] = i == 0 ? 0 : src[last + 1 - i];
+    const int t = blockIdx.x * blockDim.x + threadIdx.x, stride = gridDim.x * blockDim.x;
+    if (t == 0)
+    {
+        desc[0] = d0;
+        desc[1] = d1;
+        ticket[0] = 0;
+        for (int k = 0; k < 4; ++k) words[k] = 0;
+        out[0] = INT_MIN;
+    }
+    const int mb = R - m;
+    for (int i = t; i <= mb; i += stride) ry[i] = i == 0 ? 0 : seqY[R + 1 - i];
+    for (int j = t; j <= C; j += stride) rx[j] = j == 0 ? 0 : seqX[C + 1 - j];
 }
 
-__global__ void __launch_bounds__(1024) bidi_combine_kernel(const int* topH, const int* topF, const int* botH,
-                                                            const int* botF, int m, int mb, int C, int go, int ge,
-                                                            int affine, int* out)
+__global__ void __launch_bounds__(256) bidi_combine_kernel(const int* topH, const int* topF, const int* botH,
+                                                           const int* botF, int m, int mb, int C, int go, int ge,
+                                                           int affine, int* out)
 {
-    __shared__ long long red[1024];
+    __shared__ int red[256];
     const long long d = (long long)go - ge;
     long long best = -(1ll << 62);
-    for (int j = threadIdx.x; j <= C; j += blockDim.x)
+    for (int j = blockIdx.x * blockDim.x + threadIdx.x; j <= C; j += gridDim.x * blockDim.x)
     {
         const int jb = C - j;
         // H and F of the forward top at (m, j) and of the reversed bottom at (mb, jb), unshifted
@@ -50,30 +62,35 @@ __global__ void __launch_bounds__(1024) bidi_combine_kernel(const int* topH, con
         if (affine) v = max(v, ft + fb - d);
         best = max(best, v);
     }
-    red[threadIdx.x] = best;
+    // scores stay far inside int (the fill flags anything outside int16 / 2^26)
+    red[threadIdx.x] = (int)max(best, (long long)INT_MIN);
     __syncthreads();
     for (int s = blockDim.x / 2; s > 0; s >>= 1)
     {
         if ((int)threadIdx.x < s) red[threadIdx.x] = max(red[threadIdx.x], red[threadIdx.x + s]);
         __syncthreads();
     }
-    if (threadIdx.x == 0) out[0] = (int)red[0];
+    if (threadIdx.x == 0) atomicMax(out, red[0]);
 }
 
 }  // namespace
 
-hipError_t launch_reverse(const int* src, int first, int last, int* dst, hipStream_t stream)
+hipError_t launch_bidi_prep(const PairDesc& d0, const PairDesc& d1, PairDesc* desc, const int* seqY, int m, int R,
+                            const int* seqX, int C, int* ry, int* rx, unsigned* ticket,
+                            unsigned long long* words, int* out, hipStream_t stream)
 {
-    const int n = last - first + 2;
-    const int grid = (n + 255) / 256 < 1024 ? (n + 255) / 256 : 1024;
-    hipLaunchKernelGGL(reverse_kernel, dim3(grid > 0 ? grid : 1), dim3(256), 0, stream, src, first, last, dst);
+    const int n = (R - m > C ? R - m : C) + 1;
+    const int grid = (n + 255) / 256 < 512 ? (n + 255) / 256 : 512;
+    hipLaunchKernelGGL(bidi_prep_kernel, dim3(grid), dim3(256), 0, stream, d0, d1, desc, seqY, m, R, seqX, C, ry, rx,
+                       ticket, words, out);
     return hipGetLastError();
 }
 
 hipError_t launch_bidi_combine(const int* topH, const int* topF, const int* botH, const int* botF, int m, int mb,
                                int C, int go, int ge, bool affine, int* out, hipStream_t stream)
 {
-    hipLaunchKernelGGL(bidi_combine_kernel, dim3(1), dim3(1024), 0, stream, topH, topF, botH, botF, m, mb, C, go, ge,
+    const int grid = (C + 1 + 255) / 256 < 256 ? (C + 1 + 255) / 256 : 256;
+    hipLaunchKernelGGL(bidi_combine_kernel, dim3(grid), dim3(256), 0, stream, topH, topF, botH, botF, m, mb, C, go, ge,
                        affine ? 1 : 0, out);
     return hipGetLastError();
 }

@@ -1786,10 +1786,17 @@ __global__ void __launch_bounds__(64 * kr_waves<kKrowNSDefault>()) nw_kscore_ker
         __syncthreads();
         if (threadIdx.x == 0) lds_st(L.flags + kFTicket, err_set(a) ? a.nTicketsTotal : (int)atomicAdd(a.ticket, 1u));
         __syncthreads();
-        const int tk = __builtin_amdgcn_readfirstlane(lds_ld(L.flags + kFTicket));
-        if (tk >= a.nTicketsTotal) break;
-        // one pair (gsa_score): its descriptor
-        const PairDesc d = kr_desc(a.pairs);
+        const int tkg = __builtin_amdgcn_readfirstlane(lds_ld(L.flags + kFTicket));
+        if (tkg >= a.nTicketsTotal) break;
+        // one pair (gsa_score), or score_bidi's two halves with their tickets interleaved while both
+        // have some left (each half's tickets are still claimed in order)
+        int h = 0, tk = tkg;
+        if (a.bidiTop > 0)
+        {
+            h = tkg < 2 * a.bidiTop ? (tkg & 1) : 1;
+            tk = tkg < 2 * a.bidiTop ? (tkg >> 1) : tkg - a.bidiTop;
+        }
+        const PairDesc d = kr_desc(a.pairs + h);
         StripArgs pa = a;
         pa.seqY = d.seqY;
         pa.seqX = d.seqX;
@@ -1798,6 +1805,14 @@ __global__ void __launch_bounds__(64 * kr_waves<kKrowNSDefault>()) nw_kscore_ker
         pa.Cp = d.Cp;
         pa.nTickets = d.nTickets;
         pa.granStride = gran_stride(d.Cp);
+        pa.gran = a.gran + d.granOff;
+        pa.gran2 = a.gran2 + d.granOff;
+        if (h)
+        {
+            pa.tapRow = a.tapRowB;
+            pa.tapH = a.tapH + a.tapStride;
+            pa.tapF = a.tapF + a.tapStride;
+        }
         if (threadIdx.x < 32) lds_st(L.flags + 4u * threadIdx.x, 0);
         // rings: -inf, so columns no writer reaches (past C at the strips' ends) hold nothing larger
         for (int k = threadIdx.x; k < 2 * (NS + 1) * kRing; k += kThreads) lds_st(L.ring + 4u * k, kNegS);
@@ -1812,9 +1827,9 @@ __global__ void __launch_bounds__(64 * kr_waves<kKrowNSDefault>()) nw_kscore_ker
         {
             // score_bidi's tap: the strip with a lane whose last row is a.tapRow (uniform)
             const int r0 = tk * (64 * K * NS) + 64 * K * w + 1;
-            const int rt = a.tapRow - r0;
+            const int rt = pa.tapRow - r0;
             __builtin_amdgcn_s_setprio(3);
-            if (!is_sw_mode(MODE) && a.tapRow >= 0 && rt >= 0 && rt < 64 * K && (rt + 1) % K == 0)
+            if (!is_sw_mode(MODE) && pa.tapRow > 0 && rt >= 0 && rt < 64 * K && (rt + 1) % K == 0)
                 ks_strip<MODE, Q8, K, !is_sw_mode(MODE)>(pa, L, tk, w, lane, (rt + 1) / K - 1);
             else
                 ks_strip<MODE, Q8, K>(pa, L, tk, w, lane);
@@ -1872,7 +1887,8 @@ size_t krow_score_lds_bytes(int substsz, bool q8) { return (size_t)ks_layout(sub
 
 hipError_t launch_krow_score(const StripArgs& a, int mode, int k, int grid, hipStream_t stream)
 {
-    if (a.nPairs != 1 || grid <= 0 || (k != 2 && k != 4)) return hipErrorInvalidValue;
+    // one pair, or score_bidi's two halves (bidiTop > 0)
+    if (a.nPairs != (a.bidiTop > 0 ? 2 : 1) || grid <= 0 || (k != 2 && k != 4)) return hipErrorInvalidValue;
     if (mode == kModeScoreAG || mode == kModeScoreSW) return launch_krow_score_affine(a, mode, k, grid, stream);
     if (k == 2)
     {

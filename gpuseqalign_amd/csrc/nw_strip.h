@@ -120,10 +120,15 @@ struct StripArgs
     unsigned long long* stamps;
     // score-only NW from both ends (gsa_capi.hip score_bidi): the strip with a lane whose last row is
     // tapRow stores that row's Hgo' (tapH) and, affine, F' (tapF), shifted as the hand-off holds
-    // them, at tap[kTapPad + column] for every column the lane computes; tapRow < 0: none
+    // them, at tap[kTapPad + column] for every column the lane computes; tapRow <= 0: none.
+    // bidiTop > 0: one launch runs both halves, pairs[0] (bidiTop tickets) and pairs[1] (the rest),
+    // tickets interleaved; half 1 taps row tapRowB into tapH / tapF + tapStride
     int* tapH;
     int* tapF;
     int tapRow;
+    int tapRowB;
+    int tapStride;
+    int bidiTop;
 };
 constexpr int kTapPad = 128;  // tap row buffers: columns -kTapPad .. C + 79
 

@@ -62,9 +62,18 @@ def test_score_kernel_label(monkeypatch):
     monkeypatch.delenv("GSA_SCORE_KERNEL", raising=False)
     monkeypatch.delenv("GSA_KROW_Q8", raising=False)
     monkeypatch.delenv("GSA_SCORE_K", raising=False)
+    monkeypatch.delenv("GSA_SCORE_BIDI", raising=False)
     assert bench.score_kernel_name(-11, -1, False).startswith("gsa::nw_kscore_kernel<3, false, 2>")
     assert bench.score_kernel_name(-11, -11, True).startswith("gsa::nw_kscore_kernel<5, false, 2>")
+    # NW at 50k: both ends at 2 rows per lane; one direction for an odd R or a short pair
+    assert "both ends" in bench.score_kernel_name(-11, -1, False)
+    assert bench.score_kernel_name(-11, -11, False).startswith("gsa::nw_kscore_kernel<6, false, 2> (kModeScoreAGL, both")
+    assert bench.score_kernel_name(-11, -11, False, R=49999).startswith("gsa::nw_kscore_kernel<6, true, 4>")
+    assert bench.score_kernel_name(-11, -11, False, R=4000).startswith("gsa::nw_kscore_kernel<6, true, 4>")
+    assert "both ends" not in bench.score_kernel_name(-11, -11, True)
+    monkeypatch.setenv("GSA_SCORE_BIDI", "0")
     assert bench.score_kernel_name(-11, -11, False).startswith("gsa::nw_kscore_kernel<6, true, 4>")
+    monkeypatch.delenv("GSA_SCORE_BIDI")
     monkeypatch.setenv("GSA_SCORE_KERNEL", "strip")
     assert "nw_strip_kernel" in bench.score_kernel_name(-11, -1, False)
 
