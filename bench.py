@@ -404,11 +404,12 @@ def pmc_write_ratio(n_pairs, kernel):
 CFG5 = [("SW-LG", -11, -11, True), ("NW-AG", -11, -1, False)]
 
 
-def score_kernel_name(go, ge, local, substsz=25, R=50000):
+def score_kernel_name(go, ge, local, substsz=25, R=50000, C=50000):
     """The kernel gsa_score_dev runs (gsa_capi.hip score_dev_impl): the K-rows score kernel unless
     GSA_SCORE_KERNEL=strip, SW with ge > 0, or its LDS does not fit (a 25-letter table fits); the
     strip kernel's score modes otherwise (4 strips per workgroup).  NW on R rows, R a multiple of K
-    and each half >= 4 tickets: from both ends (score_bidi: two halves in one launch, K = 2)."""
+    and each half >= 4 tickets (or the same of C, transposed): from both ends (score_bidi: two
+    halves in one launch, K = 2)."""
     mode = (5 if go == ge else 4) if local else (6 if go == ge else 3)
     mname = (("kModeScoreSWL" if go == ge else "kModeScoreSW") if local else
              ("kModeScoreAGL" if go == ge else "kModeScoreAG"))
@@ -419,8 +420,8 @@ def score_kernel_name(go, ge, local, substsz=25, R=50000):
     k = int(kenv) if kenv in ("2", "4") else (4 if (not local and go == ge) else 2)
     bidi_env = os.environ.get("GSA_SCORE_BIDI", "1")
     kb = int(kenv) if kenv in ("2", "4") else 2
-    bidi = (krow and not local and bidi_env != "0" and R % kb == 0 and R >= 2 * kb
-            and (bidi_env == "2" or R >= 8 * 64 * kb * 4))
+    splits = lambda rows: rows % kb == 0 and rows >= 2 * kb and (bidi_env == "2" or rows >= 8 * 64 * kb * 4)
+    bidi = krow and not local and bidi_env != "0" and (splits(R) or splits(C))
     if bidi:
         k = kb
     q8env = os.environ.get("GSA_KROW_Q8", "1")
@@ -460,7 +461,7 @@ def bench_config5(dev, eng, steps, warmup, cpu_sample, rank, world):
         out[name] = {"value": round(R * C / kms / 1e6, 2), "unit": "GCUPS", "kernel_ms": round(kms, 4),
                      "ms_per_call": round(wall * 1e3, 4), "score": r["score"], "end": [r["i_end"], r["j_end"]],
                      "golden_match": ok, "gapo": go, "gape": ge, "local": local,
-                     "kernel": score_kernel_name(go, ge, local, R=R)}
+                     "kernel": score_kernel_name(go, ge, local, R=R, C=C)}
         if cpu_sample > 0 and rank == 0 and world == 1:
             import oracle
             ncpu, phys, quota, nproc = cpu_topology()

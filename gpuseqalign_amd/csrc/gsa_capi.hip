@@ -334,7 +334,8 @@ int sw_idx_bits(int64_t R, int64_t C)
 // one-direction path.
 constexpr int kScoreTooLargeB = -1001;
 int score_bidi(gsa_ctx* ctx, const int32_t* seqY, int64_t R, const int32_t* seqX, int64_t C, const int32_t* subst,
-               int32_t substsz, int32_t gapo, int32_t gape, int K, gsa_score_result* out, hipStream_t st)
+               int32_t substsz, int32_t gapo, int32_t gape, int K, bool transposed, gsa_score_result* out,
+               hipStream_t st)
 {
     const int64_t TR = (int64_t)(64 * K) * gsa::kSparseNS;
     const int64_t m = (int64_t)K * (R / (2 * K)), mb = R - m;
@@ -344,7 +345,8 @@ int score_bidi(gsa_ctx* ctx, const int32_t* seqY, int64_t R, const int32_t* seqX
     // layout (ints): tap rows H, F of the top, then of the bottom; reversed Y (mb + 1), reversed X
     // (C + 1), the combine's result
     const size_t oRY = 4 * tapLen, oRX = oRY + (size_t)mb + 1, oRes = (oRX + (size_t)C + 1 + 63) & ~(size_t)63;
-    const size_t need = oRes + 64;
+    const size_t oSub = oRes + 64;  // transposed: the table transposed
+    const size_t need = oSub + (size_t)substsz * (size_t)substsz;
     hipError_t e;
     if (ctx->bidi_cap < need || !ctx->bidi)
     {
@@ -360,6 +362,7 @@ int score_bidi(gsa_ctx* ctx, const int32_t* seqY, int64_t R, const int32_t* seqX
     int* ry = ctx->bidi + oRY;
     int* rx = ctx->bidi + oRX;
     int* res = ctx->bidi + oRes;
+    int* substT = transposed ? ctx->bidi + oSub : nullptr;
     int s = ensure_desc(ctx, 2);
     if (s != GSA_SUCCESS) return s;
     const size_t stride = (size_t)gsa::gran_stride((int)C);
@@ -384,7 +387,7 @@ int score_bidi(gsa_ctx* ctx, const int32_t* seqY, int64_t R, const int32_t* seqX
         (q8env != 0 && (q8env == 2 || K == 4) && gsa::krow_score_lds_bytes(substsz, true) <= (size_t)ctx->lds_max) ? 1 : 0;
     gsa::StripArgs a;
     std::memset(&a, 0, sizeof(a));
-    a.subst = subst;
+    a.subst = transposed ? substT : subst;
     a.substsz = substsz;
     a.g = gapo;
     a.go = gapo;
@@ -413,7 +416,7 @@ int score_bidi(gsa_ctx* ctx, const int32_t* seqY, int64_t R, const int32_t* seqX
     a.tapStride = (int)(2 * tapLen);
     (void)hipEventRecord(ctx->ev0, st);
     if ((e = gsa::launch_bidi_prep(d[0], d[1], ctx->desc, seqY, (int)m, (int)R, seqX, (int)C, ry, rx, ctx->ctl, ctx->sctl,
-                                   res, st)) != hipSuccess ||
+                                   res, subst, substsz, substT, st)) != hipSuccess ||
         (e = gsa::launch_krow_score(a, mode, K, std::max(1, std::min((int)(tkTop + tkBot), ctx->cu_count)), st)) !=
             hipSuccess)
         return fail(ctx, e, GSA_ERROR_KERNEL_FAILURE);
@@ -433,8 +436,8 @@ int score_bidi(gsa_ctx* ctx, const int32_t* seqY, int64_t R, const int32_t* seqX
     if (err == 2u) return kScoreTooLargeB;  // a value outside int16: the row scan
     if (err != 0) return GSA_ERROR_KERNEL_FAILURE;
     out->score = score;
-    out->i_end = R;
-    out->j_end = C;
+    out->i_end = transposed ? C : R;
+    out->j_end = transposed ? R : C;
     return GSA_SUCCESS;
 }
 
@@ -458,12 +461,17 @@ int score_ag_strip(gsa_ctx* ctx, const int32_t* seqY, int64_t R, const int32_t* 
     // NW from both ends (score_bidi) when each half keeps >= 4 tickets, at 2 rows per lane in both
     // NW modes (its halves have half the strips, so the shorter block wins for NW-LG too: 50k 2.25 ->
     // 2.11 ms, profiles/r05_bidi_ab.txt).  GSA_SCORE_BIDI: 0 never, 2 at any size (tests)
+    // A pair whose R is not a multiple of K but whose C is runs transposed (X down the rows, Y along
+    // them, the table transposed: the same global score, and gaps cost the same either way).
     const int bidi = env_int("GSA_SCORE_BIDI", 1);
     const int kb = kenv == 2 || kenv == 4 ? kenv : 2;
     const int64_t TRb = (int64_t)(64 * kb) * gsa::kSparseNS;
-    if (krow && !local && bidi != 0 && R % kb == 0 && R >= 2 * kb && (bidi == 2 || R >= 8 * TRb))
+    auto splits = [&](int64_t rows) { return rows % kb == 0 && rows >= 2 * kb && (bidi == 2 || rows >= 8 * TRb); };
+    if (krow && !local && bidi != 0 && (splits(R) || splits(C)))
     {
-        const int sb = score_bidi(ctx, seqY, R, seqX, C, subst, substsz, gapo, gape, kb, out, st);
+        const bool tr = !splits(R);
+        const int sb = tr ? score_bidi(ctx, seqX, C, seqY, R, subst, substsz, gapo, gape, kb, true, out, st)
+                          : score_bidi(ctx, seqY, R, seqX, C, subst, substsz, gapo, gape, kb, false, out, st);
         return sb == kScoreTooLargeB ? kScoreTooLarge : sb;
     }
     gsa::StripArgs a;

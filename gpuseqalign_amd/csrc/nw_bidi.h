@@ -11,10 +11,12 @@ namespace gsa {
 
 // One launch before the fill: desc[0..1] = d0, d1; ry[0] = rx[0] = 0, ry[i] = seqY[R + 1 - i]
 // (i = 1 .. R - m: rows m+1 .. R reversed), rx[j] = seqX[C + 1 - j]; the launch's ticket word, its
-// 4 result / error words and the combine's output (-2^31) reset.
+// 4 result / error words and the combine's output (-2^31) reset; substT non-null: substT[x][y] =
+// subst[y][x] (substsz x substsz; the pair transposed, when R is odd and C even).
 hipError_t launch_bidi_prep(const PairDesc& d0, const PairDesc& d1, PairDesc* desc, const int* seqY, int m, int R,
                             const int* seqX, int C, int* ry, int* rx, unsigned* ticket,
-                            unsigned long long* words, int* out, hipStream_t stream);
+                            unsigned long long* words, int* out, const int* subst, int substsz, int* substT,
+                            hipStream_t stream);
 
 // out[0] = max over j = 0 .. C of max(Ht(j) + Hb(C - j), Ft(j) + Fb(C - j) - (go - ge)) (affine), or
 // of Ht(j) + Hb(C - j) (linear), where the tapped rows hold shifted values (Hgo' = H - (i+j) ge +

@@ -16,7 +16,8 @@ namespace {
 
 __global__ void __launch_bounds__(256) bidi_prep_kernel(PairDesc d0, PairDesc d1, PairDesc* desc, const int* seqY,
                                                         int m, int R, const int* seqX, int C, int* ry, int* rx,
-                                                        unsigned* ticket, unsigned long long* words, int* out)
+                                                        unsigned* ticket, unsigned long long* words, int* out,
+                                                        const int* subst, int substsz, int* substT)
 {
     const int t = blockIdx.x * blockDim.x + threadIdx.x, stride = gridDim.x * blockDim.x;
     if (t == 0)
@@ -30,6 +31,8 @@ __global__ void __launch_bounds__(256) bidi_prep_kernel(PairDesc d0, PairDesc d1
     const int mb = R - m;
     for (int i = t; i <= mb; i += stride) ry[i] = i == 0 ? 0 : seqY[R + 1 - i];
     for (int j = t; j <= C; j += stride) rx[j] = j == 0 ? 0 : seqX[C + 1 - j];
+    if (substT)
+        for (int k = t; k < substsz * substsz; k += stride) substT[k] = subst[(k % substsz) * substsz + k / substsz];
 }
 
 __global__ void __launch_bounds__(256) bidi_combine_kernel(const int* topH, const int* topF, const int* botH,
@@ -77,12 +80,13 @@ __global__ void __launch_bounds__(256) bidi_combine_kernel(const int* topH, cons
 
 hipError_t launch_bidi_prep(const PairDesc& d0, const PairDesc& d1, PairDesc* desc, const int* seqY, int m, int R,
                             const int* seqX, int C, int* ry, int* rx, unsigned* ticket,
-                            unsigned long long* words, int* out, hipStream_t stream)
+                            unsigned long long* words, int* out, const int* subst, int substsz, int* substT,
+                            hipStream_t stream)
 {
     const int n = (R - m > C ? R - m : C) + 1;
     const int grid = (n + 255) / 256 < 512 ? (n + 255) / 256 : 512;
     hipLaunchKernelGGL(bidi_prep_kernel, dim3(grid), dim3(256), 0, stream, d0, d1, desc, seqY, m, R, seqX, C, ry, rx,
-                       ticket, words, out);
+                       ticket, words, out, subst, substsz, substT);
     return hipGetLastError();
 }
 

@@ -68,8 +68,9 @@ def test_score_kernel_label(monkeypatch):
     # NW at 50k: both ends at 2 rows per lane; one direction for an odd R or a short pair
     assert "both ends" in bench.score_kernel_name(-11, -1, False)
     assert bench.score_kernel_name(-11, -11, False).startswith("gsa::nw_kscore_kernel<6, false, 2> (kModeScoreAGL, both")
-    assert bench.score_kernel_name(-11, -11, False, R=49999).startswith("gsa::nw_kscore_kernel<6, true, 4>")
-    assert bench.score_kernel_name(-11, -11, False, R=4000).startswith("gsa::nw_kscore_kernel<6, true, 4>")
+    assert "both ends" in bench.score_kernel_name(-11, -11, False, R=49999)  # transposed
+    assert bench.score_kernel_name(-11, -11, False, R=49999, C=49999).startswith("gsa::nw_kscore_kernel<6, true, 4>")
+    assert bench.score_kernel_name(-11, -11, False, R=4000, C=4000).startswith("gsa::nw_kscore_kernel<6, true, 4>")
     assert "both ends" not in bench.score_kernel_name(-11, -11, True)
     monkeypatch.setenv("GSA_SCORE_BIDI", "0")
     assert bench.score_kernel_name(-11, -11, False).startswith("gsa::nw_kscore_kernel<6, true, 4>")

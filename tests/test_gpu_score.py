@@ -245,3 +245,23 @@ def test_score_both_ends_default_matches_one_direction(engine, golden, monkeypat
         r0 = engine.score(Y, X, golden.blosum62, go, ge, False)
         ref = oracle.score_ag(Y, X, golden.blosum62, go, ge, False, mt=True, blocksz=256, nthreads=8)
         assert (r1["score"], r1["i_end"], r1["j_end"]) == (r0["score"], r0["i_end"], r0["j_end"]) == ref
+
+
+@pytest.mark.parametrize("k", ["2", "4"])
+@pytest.mark.parametrize("go,ge", [(-11, -11), (-11, -1), (-4, -3)])
+def test_score_both_ends_transposed(engine, golden, monkeypatch, k, go, ge):
+    """R not a multiple of K but C one: the pair runs transposed from both ends (X down the rows, the
+    table transposed), on an asymmetric table so a missed transpose shows; R and C both off the
+    multiple keep one direction.  All equal the oracle, end cell (R, C)."""
+    import oracle
+    monkeypatch.setenv("GSA_SCORE_BIDI", "2")
+    monkeypatch.setenv("GSA_SCORE_K", k)
+    n = int(round(np.sqrt(golden.blosum62.size)))
+    rng = np.random.default_rng(int(k) * 7 + go)
+    sub = rng.integers(-7, 9, size=(n, n)).astype(np.int32)
+    assert not np.array_equal(sub, sub.T)
+    kk = int(k)
+    for R, C in [(kk * 300 + 1, kk * 400), (kk * 513 + 1, kk * 41), (kk * 77 + 1, kk * 900 + 1), (kk * 2 + 1, kk * 2)]:
+        Y, X = random_pair(R, C, 17 * R + C)
+        r = engine.score(Y, X, sub, go, ge, False)
+        assert (r["score"], r["i_end"], r["j_end"]) == oracle.score_ag(Y, X, sub, go, ge, False), (R, C)
