@@ -265,3 +265,35 @@ def test_score_both_ends_transposed(engine, golden, monkeypatch, k, go, ge):
         Y, X = random_pair(R, C, 17 * R + C)
         r = engine.score(Y, X, sub, go, ge, False)
         assert (r["score"], r["i_end"], r["j_end"]) == oracle.score_ag(Y, X, sub, go, ge, False), (R, C)
+
+
+def test_score_both_ends_random_shapes(engine, golden, monkeypatch):
+    """40 random NW shapes (R, C in 1..3000, either parity), random gap pairs and tables, forced from
+    both ends where the shape allows (GSA_SCORE_BIDI=2): equal to the oracle."""
+    import oracle
+    monkeypatch.setenv("GSA_SCORE_BIDI", "2")
+    n = int(round(np.sqrt(golden.blosum62.size)))
+    rng = np.random.default_rng(2024)
+    for case in range(40):
+        R, C = (int(v) for v in rng.integers(1, 3001, 2))
+        ge = -int(rng.integers(1, 6))
+        go = ge - int(rng.integers(0, 12))
+        sub = rng.integers(-8, 12, size=(n, n)).astype(np.int32)
+        Y, X = random_pair(R, C, 1000 + case)
+        r = engine.score(Y, X, sub, go, ge, False)
+        assert (r["score"], r["i_end"], r["j_end"]) == oracle.score_ag(Y, X, sub, go, ge, False), (case, R, C, go, ge)
+
+
+def test_score_both_ends_100k(engine, golden):
+    """100k x 100k NW-AG and NW-LG (default switch: from both ends) against the one-direction kernel."""
+    import os
+    from gpuseqalign_amd import formats as F
+    Y, X = F.synthetic_seq(100000, 300), F.synthetic_seq(100000, 301)
+    for go, ge in [(-11, -1), (-11, -11)]:
+        r1 = engine.score(Y, X, golden.blosum62, go, ge, False)
+        os.environ["GSA_SCORE_BIDI"] = "0"
+        try:
+            r0 = engine.score(Y, X, golden.blosum62, go, ge, False)
+        finally:
+            del os.environ["GSA_SCORE_BIDI"]
+        assert (r1["score"], r1["i_end"], r1["j_end"]) == (r0["score"], r0["i_end"], r0["j_end"])
