@@ -81,8 +81,8 @@ struct gsa_ctx
     size_t clk_cap = 0, clk_n = 0;
     int timing_state = 0;  // 0 none, 1 two launches (events + stamps), 2 fused (one launch), 3 pipelined
     int timing_groups = 0;
-    // score-only NW from both ends (score_bidi): tap rows, reversed sequences, the second launch's
-    // control words and results
+    // score-only NW from both ends (score_bidi): tap rows of both halves, the reversed sequences, the
+    // combine's result, the transposed table
     int* bidi = nullptr;
     size_t bidi_cap = 0;  // ints
     // the pipelined full batch: pass 1 of pair groups 1.. on a stream of its own, one event per group
@@ -241,12 +241,15 @@ int lane_ns()
 hipStream_t pick_stream(gsa_ctx*, void* stream) { return (hipStream_t)stream; }
 
 // Device bytes this context holds (scratch, hand-off granules, the host entry points' I/O buffers).
-// Units of the *_cap fields: bytes for tmoves, tdirs, tband and dcap; ints for sbnd and tlist.
+// Units of the *_cap fields: bytes for tmoves, tdirs, tband, dcap, excap and exdesc_cap; ints for
+// sbnd, tlist and bidi; 8-byte words for xdone, stamps and clk.
 long long held_bytes(const gsa_ctx* c)
 {
     long long b = 256 + 64 + (long long)c->gran_elems * 8 + (long long)c->desc_cap * (long long)sizeof(gsa::PairDesc) +
                   (long long)c->tmoves_cap + (long long)c->tdirs_cap + (long long)c->sbnd_cap * 4 +
-                  (long long)c->tband_cap + (long long)c->tlist_cap * 4;
+                  (long long)c->tband_cap + (long long)c->tlist_cap * 4 + (long long)c->excap +
+                  (long long)c->exdesc_cap + 8 * (long long)(c->xdone_cap + c->stamps_cap + c->clk_cap) +
+                  4 * (long long)c->bidi_cap;
     for (size_t k : c->dcap) b += (long long)k;
     return b;
 }
