@@ -383,6 +383,14 @@ def pass_fields(tm, rank_bytes):
         out["pass2_hbm_frac"] = round(rank_bytes / (p2 * 1e-3) / 1e9 / PEAK_HBM_GBPS, 4)
     if p1 is not None and p2:
         out["pass1_share"] = round(p1 / (p1 + p2), 4)
+    # the runtime's fill kernel over the same output buffer: a box whose pages slow every writer
+    # shows it here, one whose pass 2 alone is slow does not
+    fm, fb = tm.get("out_fill_ms"), tm.get("out_fill_bytes")
+    if fm and fb:
+        out["out_fill_ms"] = round(fm, 4)
+        out["out_fill_GBps"] = round(fb / (fm * 1e-3) / 1e9, 1)
+        if p2:
+            out["pass2_over_out_fill"] = round(fm / p2 * rank_bytes / fb, 4)
     out["nominal_clock_ghz"] = CLOCK_GHZ
     return out
 

@@ -770,13 +770,6 @@ int enqueue_batch(gsa_ctx* ctx, int mode, int npairs, const gsa_pair_dev* pairs,
                 if (ctx->stamps_cap < n)
                 {
                     if (ctx->stamps) (void)hipFree(ctx->stamps);
-    if (ctx->clk) (void)hipFree(ctx->clk);
-    if (ctx->bidi) (void)hipFree(ctx->bidi);
-    for (hipEvent_t ev : ctx->pipe_ev)
-        if (ev) (void)hipEventDestroy(ev);
-    if (ctx->p1stream) (void)hipStreamDestroy(ctx->p1stream);
-    for (hipEvent_t ev : ctx->pev)
-        if (ev) (void)hipEventDestroy(ev);
                     ctx->stamps = nullptr;
                     ctx->stamps_cap = 0;
                     if ((e = hipMalloc(&ctx->stamps, n * sizeof(unsigned long long))) != hipSuccess)
@@ -1202,20 +1195,42 @@ int enqueue_full_twopass(gsa_ctx* ctx, int npairs, const gsa_pair_dev* pairs, co
     // the expansion's descriptors and (batches) its round-robin schedule, staged in a pinned slot and
     // copied in stream order
     std::vector<int> xs;
-    if (npairs > 1 && env_int("GSA_EXPAND_RR", 1))
+    const int rr = env_int("GSA_EXPAND_RR", 1);
+    if (npairs > 1 && rr)
     {
         std::vector<int> ord((size_t)npairs);
         for (int p = 0; p < npairs; ++p) ord[(size_t)p] = p;
         auto ntask = [&](int p) { return ex[(size_t)p].colTiles * ex[(size_t)p].rowChunks; };
         std::stable_sort(ord.begin(), ord.end(), [&](int x, int y) { return ntask(x) > ntask(y); });
         xs.reserve(2 * (size_t)tasks);
+        // rr 2 (probe): pair k of the order starts k / npairs of the way into its tasks
+        std::vector<long long> rot((size_t)npairs, 0);
+        if (rr == 2)
+            for (int k = 0; k < npairs; ++k) rot[(size_t)ord[(size_t)k]] = (long long)ntask(ord[(size_t)k]) * k / npairs;
         for (int j = 0; j < ntask(ord[0]); ++j)
             for (int p : ord)
             {
                 if (ntask(p) <= j) break;
                 xs.push_back(p);
-                xs.push_back(j);
+                xs.push_back((int)((j + rot[(size_t)p]) % ntask(p)));
             }
+        if (rr == 3)
+        {
+            // (probe): the whole schedule shuffled, pairs of ints kept together (fixed seed)
+            uint64_t z = 0x9e3779b97f4a7c15ull;
+            const size_t n = xs.size() / 2;
+            for (size_t i = n; i > 1; --i)
+            {
+                z += 0x9e3779b97f4a7c15ull;
+                uint64_t r = z;
+                r = (r ^ (r >> 30)) * 0xbf58476d1ce4e5b9ull;
+                r = (r ^ (r >> 27)) * 0x94d049bb133111ebull;
+                r ^= r >> 31;
+                const size_t k = (size_t)(r % i);
+                std::swap(xs[2 * (i - 1)], xs[2 * k]);
+                std::swap(xs[2 * (i - 1) + 1], xs[2 * k + 1]);
+            }
+        }
     }
     const size_t descBytes = ((size_t)npairs * sizeof(gsa::ExpandPair) + 15) & ~(size_t)15;
     const size_t exBytes = descBytes + xs.size() * sizeof(int);
@@ -1267,9 +1282,6 @@ int enqueue_full_twopass(gsa_ctx* ctx, int npairs, const gsa_pair_dev* pairs, co
         if (ctx->clk_cap < (size_t)tasks || !ctx->clk)
         {
             if (ctx->clk) (void)hipFree(ctx->clk);
-    for (hipEvent_t ev : ctx->pipe_ev)
-        if (ev) (void)hipEventDestroy(ev);
-    if (ctx->p1stream) (void)hipStreamDestroy(ctx->p1stream);
             ctx->clk = nullptr;
             ctx->clk_cap = 0;
             if ((e = hipMalloc(&ctx->clk, (size_t)std::max<long long>(tasks, 1024) * 8)) != hipSuccess)
@@ -1451,6 +1463,17 @@ void gsa_ctx_destroy(gsa_ctx* ctx)
     if (ctx->exdesc) (void)hipFree(ctx->exdesc);
     if (ctx->xdone) (void)hipFree(ctx->xdone);
     if (ctx->stamps) (void)hipFree(ctx->stamps);
+    if (ctx->clk) (void)hipFree(ctx->clk);
+    if (ctx->bidi) (void)hipFree(ctx->bidi);
+    for (hipEvent_t ev : ctx->pev)
+        if (ev) (void)hipEventDestroy(ev);
+    for (hipEvent_t ev : ctx->pipe_ev)
+        if (ev) (void)hipEventDestroy(ev);
+    if (ctx->p1stream)
+    {
+        (void)hipStreamSynchronize(ctx->p1stream);
+        (void)hipStreamDestroy(ctx->p1stream);
+    }
     for (int k = 0; k < gsa_ctx::kStage; ++k)
     {
         if (ctx->expin[k]) (void)hipHostFree(ctx->expin[k]);

@@ -177,7 +177,19 @@ def gpu_batch_align(device: int = 0, mode: str = "sparse", tileBx: int = 256, re
             cur.append(j)
             cur_sz += sz
         chunks.append(cur)
-        flat = torch.empty(max(sum(sizes[j] for j in c) for c in chunks), dtype=torch.int32, device=dev)
+        shift = int(os.environ.get("GSA_PROBE_FLAT_SHIFT", "0"))  # (probes: the buffer's base offset, ints)
+        flat = torch.empty(max(sum(sizes[j] for j in c) for c in chunks) + shift, dtype=torch.int32, device=dev)[shift:]
+        if timing is not None:
+            timing["out_base"] = int(flat.data_ptr())
+            if mode != "sparse" and os.environ.get("GSA_PROBE_FRESH_FILL"):
+                # (probes: the runtime fill over the buffer before any kernel of ours touched it)
+                for k in range(2):
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record()
+                    flat.fill_(k)
+                    e1.record()
+                    e1.synchronize()
+                    timing[f"fresh_fill{k}_ms"] = e0.elapsed_time(e1)
         # result slices (last cell / last tile's header row and column) of every pair: positions in
         # `flat`, gathered by one index_select per chunk behind its fill, not one copy per pair
         klen = [(g.tileHrowLen + g.tileHcolLen) if g is not None else 1 for g in geoms]
@@ -226,6 +238,19 @@ def gpu_batch_align(device: int = 0, mode: str = "sparse", tileBx: int = 256, re
         secs = (time.perf_counter() - t0) / max(1, repeats)
         if timing is not None and mode != "sparse":
             timing.update(eng.last_full_timing())
+            # the same bytes written by the runtime's fill kernel (after the results were gathered):
+            # separates this kernel from the memory it writes into (pages, placement)
+            best = None
+            for _ in range(2):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                with torch.cuda.stream(stream):
+                    flat.fill_(0)
+                e1.record(stream)
+                e1.synchronize()
+                best = e0.elapsed_time(e1) if best is None else min(best, e0.elapsed_time(e1))
+            timing["out_fill_ms"] = best
+            timing["out_fill_bytes"] = int(flat.numel()) * 4
         costs = []
         for j, g in enumerate(geoms):
             v = keep[j].cpu().numpy()

@@ -94,3 +94,13 @@ def test_full_kernel_label(monkeypatch):
     monkeypatch.setenv("GSA_FULL_KERNEL", "twopass")
     monkeypatch.setenv("GSA_FULL_FUSED", "2")
     assert bench.full_kernel_name(False).startswith("gsa::nw_full_fused_kernel<8,12,true>")
+
+
+def test_pass_fields_out_fill():
+    """full_batch.passes: pass 2's rate beside the runtime fill kernel's over the same output buffer."""
+    tm = {"pass1_ms": 4.0, "pass2_ms": 20.0, "out_fill_ms": 16.0, "out_fill_bytes": 110 * 10**9}
+    f = bench.pass_fields(tm, 100e9)
+    assert f["pass2_write_GBps"] == 5000.0 and f["out_fill_GBps"] == 6875.0
+    assert f["pass2_over_out_fill"] == round(5000.0 / 6875.0, 4)
+    assert f["pass1_share"] == round(4 / 24, 4)
+    assert "out_fill_ms" not in bench.pass_fields({"pass1_ms": 1.0, "pass2_ms": 2.0}, 1e9)
