@@ -318,7 +318,9 @@ def bench_full_batch(world, rank, local, n_pairs):
     pairs = shard.synthetic_batch(n_pairs, 18000, 22000, seed0=1000)
     sub = subst_blosum62()
     tm = {}
-    rep = shard.shard_align(pairs, sub, -11, shard.gpu_batch_align(device=local, mode="full", warmup=1, repeats=3,
+    # 2 untimed launches: the library times its two expansion task orders on this output buffer in
+    # the first two and keeps the faster (gsa_capi.hip enqueue_full_twopass)
+    rep = shard.shard_align(pairs, sub, -11, shard.gpu_batch_align(device=local, mode="full", warmup=2, repeats=3,
                                                                 out_budget_bytes=int(0.9 * 140e9), timing=tm),
                             device=f"cuda:{local}" if world > 1 and not REHEARSE else None)
     gold = load_golden("config4_pairs.json")
@@ -329,7 +331,7 @@ def bench_full_batch(world, rank, local, n_pairs):
     box = box_write_rate(local)
     return {"workload": f"{n_pairs} NW-LG pairs of BASELINE configs[3] (18-22k, seeds 1000+k) as FULL int32 score "
                         f"matrices ({out_bytes / 1e9:.1f} GB), one persistent launch, LPT-sharded over {world} rank(s) "
-                        "(1 untimed + 3 timed launches; seconds per launch)",
+                        "(2 untimed + 3 timed launches; seconds per launch)",
             "value": round(rep.gcups, 2), "unit": "GCUPS", "scaling": "strong", "seconds": round(rep.elapsed_s, 4),
             "kernel": full_kernel_name(False),
             "layout": "pitched: row pitch gsa_full_pitch(adjcols) = 1 mod 32, cell (1,0) on a 128-byte boundary",

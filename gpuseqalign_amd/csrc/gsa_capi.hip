@@ -81,6 +81,15 @@ struct gsa_ctx
     size_t clk_cap = 0, clk_n = 0;
     int timing_state = 0;  // 0 none, 1 two launches (events + stamps), 2 fused (one launch), 3 pipelined
     int timing_groups = 0;
+    // the batch expansion's task order, tuned per output buffer (enqueue_full_twopass): key, the
+    // order each candidate took (ms, < 0: not measured), the order of the last launch and its events
+    const void* xt_key = nullptr;
+    int xt_pairs = 0;
+    long long xt_tasks = 0;
+    float xt_ms[2] = {-1.f, -1.f};
+    int xt_last = -1;
+    bool xt_pending = false;
+    hipEvent_t xt_ev[2] = {nullptr, nullptr};
     // score-only NW from both ends (score_bidi): tap rows of both halves, the reversed sequences, the
     // combine's result, the transposed table
     int* bidi = nullptr;
@@ -1194,8 +1203,46 @@ int enqueue_full_twopass(gsa_ctx* ctx, int npairs, const gsa_pair_dev* pairs, co
     }
     // the expansion's descriptors and (batches) its round-robin schedule, staged in a pinned slot and
     // copied in stream order
+    // Task order of a batch's expansion.  Round-robin over the pairs (one task of every pair in turn)
+    // keeps the tasks in flight spread over all matrices, and its pass 2 runs at one of two speeds on
+    // a given output buffer: the same order on another allocation of the same size, or the same
+    // buffer with every pair's tasks rotated by k/npairs of its range (order 2), takes the other
+    // (64 x 20k: 18.5-20.2 vs 21.2-25.4 ms; which one is fast flips between the two orders;
+    // profiles/r05_outbuf_probe.txt).  So the first two launches on an output buffer run orders 1
+    // and 2 and time their pass 2 (HIP events; the second launch waits for the first's), and later
+    // launches on that buffer take the faster.  GSA_EXPAND_RR fixes the order: 0 pair-major, 1, 2,
+    // 3 shuffled.
+    const int rrEnv = env_int("GSA_EXPAND_RR", -1);
+    int rr = rrEnv >= 0 ? rrEnv : 1;
+    const bool tune = rrEnv < 0 && npairs > 1 && !fused;
+    bool tuneRecord = false;
+    if (tune)
+    {
+        if (ctx->xt_key != (const void*)pairs[0].score || ctx->xt_pairs != npairs || ctx->xt_tasks != tasks)
+        {
+            ctx->xt_key = (const void*)pairs[0].score;
+            ctx->xt_pairs = npairs;
+            ctx->xt_tasks = tasks;
+            ctx->xt_ms[0] = ctx->xt_ms[1] = -1.f;
+            ctx->xt_pending = false;
+        }
+        for (int k = 0; k < 2 && !ctx->xt_ev[k]; ++k)
+            if ((e = hipEventCreate(&ctx->xt_ev[k])) != hipSuccess) return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
+        if (ctx->xt_pending)
+        {
+            float ms = -1.f;
+            if ((e = hipEventSynchronize(ctx->xt_ev[1])) != hipSuccess ||
+                (e = hipEventElapsedTime(&ms, ctx->xt_ev[0], ctx->xt_ev[1])) != hipSuccess)
+                return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
+            ctx->xt_ms[ctx->xt_last] = ms;
+            ctx->xt_pending = false;
+        }
+        const int next = ctx->xt_ms[0] < 0 ? 0 : ctx->xt_ms[1] < 0 ? 1 : (ctx->xt_ms[1] < ctx->xt_ms[0] ? 1 : 0);
+        tuneRecord = ctx->xt_ms[next] < 0;
+        ctx->xt_last = next;
+        rr = next + 1;
+    }
     std::vector<int> xs;
-    const int rr = env_int("GSA_EXPAND_RR", 1);
     if (npairs > 1 && rr)
     {
         std::vector<int> ord((size_t)npairs);
@@ -1304,8 +1351,14 @@ int enqueue_full_twopass(gsa_ctx* ctx, int npairs, const gsa_pair_dev* pairs, co
     if (timed && (e = hipEventRecord(ctx->pev[1], st)) != hipSuccess) return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
     xa.counter = ctx->ctl + 4;
     if (xGrid > 0 && (e = hipMemsetAsync(xa.counter, 0, 4, st)) != hipSuccess) return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
+    if (tuneRecord && (e = hipEventRecord(ctx->xt_ev[0], st)) != hipSuccess) return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
     if ((e = gsa::launch_expand(xa, st, xWaves, xGrid)) != hipSuccess) return fail(ctx, e, GSA_ERROR_KERNEL_FAILURE);
     note_launch(ctx);
+    if (tuneRecord)
+    {
+        if ((e = hipEventRecord(ctx->xt_ev[1], st)) != hipSuccess) return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
+        ctx->xt_pending = true;
+    }
     if (timed)
     {
         if ((e = hipEventRecord(ctx->pev[2], st)) != hipSuccess) return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
@@ -1468,6 +1521,8 @@ void gsa_ctx_destroy(gsa_ctx* ctx)
     for (hipEvent_t ev : ctx->pev)
         if (ev) (void)hipEventDestroy(ev);
     for (hipEvent_t ev : ctx->pipe_ev)
+        if (ev) (void)hipEventDestroy(ev);
+    for (hipEvent_t ev : ctx->xt_ev)
         if (ev) (void)hipEventDestroy(ev);
     if (ctx->p1stream)
     {

@@ -44,7 +44,7 @@ for label, sh, empty in runs:
     if empty:
         torch.cuda.empty_cache()
     tm = {}
-    fn = shard.gpu_batch_align(device=0, mode="full", warmup=1, repeats=1 if pmc else 3,
+    fn = shard.gpu_batch_align(device=0, mode="full", warmup=2, repeats=1 if pmc else 3,
                                out_budget_bytes=int(0.9 * 140e9), timing=tm)
     costs, secs = fn(list(range(64)), pairs, sub, -11)
     print(f"{label:18s} {secs * 1e3:8.3f} ms/launch  {out_bytes / secs / 1e12:5.2f} TB/s  pass1 {tm['pass1_ms']:.3f}  "
