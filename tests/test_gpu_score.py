@@ -261,7 +261,8 @@ def test_score_both_ends_transposed(engine, golden, monkeypatch, k, go, ge):
     sub = rng.integers(-7, 9, size=(n, n)).astype(np.int32)
     assert not np.array_equal(sub, sub.T)
     kk = int(k)
-    for R, C in [(kk * 300 + 1, kk * 400), (kk * 513 + 1, kk * 41), (kk * 77 + 1, kk * 900 + 1), (kk * 2 + 1, kk * 2)]:
+    for R, C in [(kk * 300 + 1, kk * 400), (kk * 513 + 1, kk * 41), (kk * 77 + 1, kk * 900 + 1), (kk * 2 + 1, kk * 2),
+                 (kk * 4, 0), (0, kk * 4), (kk * 4, 1), (1, kk * 4), (kk * 2, kk * 2)]:
         Y, X = random_pair(R, C, 17 * R + C)
         r = engine.score(Y, X, sub, go, ge, False)
         assert (r["score"], r["i_end"], r["j_end"]) == oracle.score_ag(Y, X, sub, go, ge, False), (R, C)
