@@ -1211,7 +1211,7 @@ int enqueue_full_twopass(gsa_ctx* ctx, int npairs, const gsa_pair_dev* pairs, co
     // profiles/r05_outbuf_probe.txt).  So the first two launches on an output buffer run orders 1
     // and 2 and time their pass 2 (HIP events; the second launch waits for the first's), and later
     // launches on that buffer take the faster.  GSA_EXPAND_RR fixes the order: 0 pair-major, 1, 2,
-    // 3 shuffled.
+    // 3 shuffled, 4-6 probe variants.
     const int rrEnv = env_int("GSA_EXPAND_RR", -1);
     int rr = rrEnv >= 0 ? rrEnv : 1;
     const bool tune = rrEnv < 0 && npairs > 1 && !fused;
@@ -1250,16 +1250,20 @@ int enqueue_full_twopass(gsa_ctx* ctx, int npairs, const gsa_pair_dev* pairs, co
         auto ntask = [&](int p) { return ex[(size_t)p].colTiles * ex[(size_t)p].rowChunks; };
         std::stable_sort(ord.begin(), ord.end(), [&](int x, int y) { return ntask(x) > ntask(y); });
         xs.reserve(2 * (size_t)tasks);
-        // rr 2 (probe): pair k of the order starts k / npairs of the way into its tasks
+        // rr 2: pair k of the order starts k / npairs of the way into its tasks (rr 4: k / 2npairs);
+        // rr 5: each pair's tasks from its last; rr 6: every other pair from its last (probes)
         std::vector<long long> rot((size_t)npairs, 0);
-        if (rr == 2)
-            for (int k = 0; k < npairs; ++k) rot[(size_t)ord[(size_t)k]] = (long long)ntask(ord[(size_t)k]) * k / npairs;
+        if (rr == 2 || rr == 4)
+            for (int k = 0; k < npairs; ++k)
+                rot[(size_t)ord[(size_t)k]] = (long long)ntask(ord[(size_t)k]) * k / (rr == 2 ? npairs : 2 * npairs);
         for (int j = 0; j < ntask(ord[0]); ++j)
-            for (int p : ord)
+            for (int k = 0; k < npairs; ++k)
             {
+                const int p = ord[(size_t)k];
                 if (ntask(p) <= j) break;
+                const bool rev = rr == 5 || (rr == 6 && (k & 1));
                 xs.push_back(p);
-                xs.push_back((int)((j + rot[(size_t)p]) % ntask(p)));
+                xs.push_back(rev ? ntask(p) - 1 - j : (int)((j + rot[(size_t)p]) % ntask(p)));
             }
         if (rr == 3)
         {

@@ -177,8 +177,12 @@ def gpu_batch_align(device: int = 0, mode: str = "sparse", tileBx: int = 256, re
             cur.append(j)
             cur_sz += sz
         chunks.append(cur)
-        shift = int(os.environ.get("GSA_PROBE_FLAT_SHIFT", "0"))  # (probes: the buffer's base offset, ints)
-        flat = torch.empty(max(sum(sizes[j] for j in c) for c in chunks) + shift, dtype=torch.int32, device=dev)[shift:]
+        # (probes: the buffer's base offset and spare ints past its end, so that several layouts
+        # can share one allocation)
+        shift = int(os.environ.get("GSA_PROBE_FLAT_SHIFT", "0"))
+        extra = int(os.environ.get("GSA_PROBE_FLAT_EXTRA", "0"))
+        need = max(sum(sizes[j] for j in c) for c in chunks)
+        flat = torch.empty(need + shift + extra, dtype=torch.int32, device=dev)[shift:shift + need]
         if timing is not None:
             timing["out_base"] = int(flat.data_ptr())
             if mode != "sparse" and os.environ.get("GSA_PROBE_FRESH_FILL"):
