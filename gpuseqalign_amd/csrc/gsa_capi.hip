@@ -350,9 +350,34 @@ int score_bidi(gsa_ctx* ctx, const int32_t* seqY, int64_t R, const int32_t* seqX
                hipStream_t st)
 {
     const int64_t TR = (int64_t)(64 * K) * gsa::kSparseNS;
-    const int64_t m = (int64_t)K * (R / (2 * K)), mb = R - m;
-    const int64_t tkTop = (m + TR - 1) / TR, tkBot = (mb + TR - 1) / TR;
     const bool affine = gapo != gape;
+    // The split.  A half whose rows end on a ticket boundary needs no lane tap: its last ticket's
+    // drain writes that row to the granules like any other ticket's, and the combine reads it there.
+    // A lane tap costs its strip 8 global stores per block, and as the half's last strip it sets the
+    // half's end (50k NW-AG 2.94 ms with no tap, 3.19 with two lane taps).  So the top half ends on a
+    // ticket boundary and takes the rows that make both halves end together: skew = p C 64K / (2 hop)
+    // rows past R/2, p the lane tap's share of the C steps (0.117 affine, 0.05 linear: 8 / 4 stores
+    // per block) and hop ~96 steps between strips; the bottom, when R is a multiple of the ticket too,
+    // is free as well and the split even.  Short pairs keep two lane taps (m = K floor(R/2K)).
+    int64_t m = (int64_t)K * (R / (2 * K));
+    bool topFree = false, botFree = false;
+    if (R >= 4 * TR && env_int("GSA_BIDI_GRAN", 1))
+    {
+        const int skewEnv = env_int("GSA_BIDI_SKEW", -1);
+        const double p = affine ? 0.117 : 0.05;
+        const bool both = R % TR == 0;
+        const int64_t skew = both ? 0 : skewEnv >= 0 ? skewEnv : (int64_t)(p * (double)C * 64.0 * K / (2.0 * 96.0));
+        int64_t mt = TR * (int64_t)llround((double)(R / 2 + skew) / (double)TR);
+        mt = std::min(std::max(mt, TR), (R - 2 * K) / TR * TR);
+        if (mt >= TR && R - mt >= 2 * K && (R - mt) % K == 0)
+        {
+            m = mt;
+            topFree = true;
+            botFree = both;
+        }
+    }
+    const int64_t mb = R - m;
+    const int64_t tkTop = (m + TR - 1) / TR, tkBot = (mb + TR - 1) / TR;
     const size_t tapLen = ((size_t)gsa::kTapPad + (size_t)C + 160 + 63) & ~(size_t)63;
     // layout (ints): tap rows H, F of the top, then of the bottom; reversed Y (mb + 1), reversed X
     // (C + 1), the combine's result
@@ -421,8 +446,11 @@ int score_bidi(gsa_ctx* ctx, const int32_t* seqY, int64_t R, const int32_t* seqX
     a.epoch = ++ctx->epoch;
     if (a.epoch == 0) a.epoch = ++ctx->epoch;
     a.q8 = q8;
-    a.tapRow = (int)m;
-    a.tapRowB = (int)mb;
+    a.tapRow = topFree ? 0 : (int)m;
+    a.tapRowB = botFree ? 0 : (int)mb;
+    a.tapGran = (topFree ? 1 : 0) | (botFree ? 2 : 0);
+    if (env_int("GSA_PROBE_NOTAP", 0))  // (timing probe: no tap stores, wrong scores)
+        a.tapRow = a.tapRowB = 0;
     a.tapH = tapH;
     a.tapF = tapF;
     a.tapStride = (int)(2 * tapLen);
@@ -433,7 +461,15 @@ int score_bidi(gsa_ctx* ctx, const int32_t* seqY, int64_t R, const int32_t* seqX
             hipSuccess)
         return fail(ctx, e, GSA_ERROR_KERNEL_FAILURE);
     note_launch(ctx);
-    if ((e = gsa::launch_bidi_combine(tapH, tapF, tapH + 2 * tapLen, tapF + 2 * tapLen, (int)m, (int)mb, (int)C, gapo,
+    // the rows where the halves meet: a lane tap (tap rows, one int per column from kTapPad), or the
+    // half's last-ticket granules (the low word of each 64-bit granule)
+    const int* gTop = (const int*)(ctx->gran + (size_t)(tkTop - 1) * stride);
+    const int* gBot = (const int*)(ctx->gran + (size_t)(tkTop + tkBot - 1) * stride);
+    const int* tH = topFree ? gTop : tapH + gsa::kTapPad;
+    const int* tF = topFree ? gTop + 2 * granAll : tapF + gsa::kTapPad;
+    const int* bH = botFree ? gBot : tapH + 2 * tapLen + gsa::kTapPad;
+    const int* bF = botFree ? gBot + 2 * granAll : tapF + 2 * tapLen + gsa::kTapPad;
+    if ((e = gsa::launch_bidi_combine(tH, tF, topFree ? 2 : 1, bH, bF, botFree ? 2 : 1, (int)m, (int)mb, (int)C, gapo,
                                       gape, affine, res, st)) != hipSuccess)
         return fail(ctx, e, GSA_ERROR_KERNEL_FAILURE);
     (void)hipEventRecord(ctx->ev1, st);

@@ -20,10 +20,12 @@ hipError_t launch_bidi_prep(const PairDesc& d0, const PairDesc& d1, PairDesc* de
 
 // out[0] = max over j = 0 .. C of max(Ht(j) + Hb(C - j), Ft(j) + Fb(C - j) - (go - ge)) (affine), or
 // of Ht(j) + Hb(C - j) (linear), where the tapped rows hold shifted values (Hgo' = H - (i+j) ge +
-// (go - ge), F' = F - (i+j) ge) of row m (top, forward) and of row mb (bottom, reversed) at
-// tap[kTapPad + j]; column 0 is the gap border go + (i-1) ge.  Many workgroups, each folding its
-// columns into out[0] with an atomic max (out[0] starts at -2^31, launch_bidi_prep).
-hipError_t launch_bidi_combine(const int* topH, const int* topF, const int* botH, const int* botF, int m, int mb,
-                               int C, int go, int ge, bool affine, int* out, hipStream_t stream);
+// (go - ge), F' = F - (i+j) ge) of row m (top, forward) and of row mb (bottom, reversed), column j
+// at topH[ts j] (a lane tap: tap + kTapPad, ts = 1; the last ticket's granules: the low word of each
+// 64-bit granule, ts = 2), likewise bottom; column 0 is the gap border go + (i-1) ge.  Many
+// workgroups, each folding its columns into out[0] with an atomic max (out[0] starts at -2^31,
+// launch_bidi_prep).
+hipError_t launch_bidi_combine(const int* topH, const int* topF, int ts, const int* botH, const int* botF, int bs,
+                               int m, int mb, int C, int go, int ge, bool affine, int* out, hipStream_t stream);
 
 }  // namespace gsa

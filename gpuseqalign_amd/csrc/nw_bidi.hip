@@ -35,9 +35,9 @@ __global__ void __launch_bounds__(256) bidi_prep_kernel(PairDesc d0, PairDesc d1
         for (int k = t; k < substsz * substsz; k += stride) substT[k] = subst[(k % substsz) * substsz + k / substsz];
 }
 
-__global__ void __launch_bounds__(256) bidi_combine_kernel(const int* topH, const int* topF, const int* botH,
-                                                           const int* botF, int m, int mb, int C, int go, int ge,
-                                                           int affine, int* out)
+__global__ void __launch_bounds__(256) bidi_combine_kernel(const int* topH, const int* topF, int ts, const int* botH,
+                                                           const int* botF, int bs, int m, int mb, int C, int go,
+                                                           int ge, int affine, int* out)
 {
     __shared__ int red[256];
     const long long d = (long long)go - ge;
@@ -51,15 +51,15 @@ __global__ void __launch_bounds__(256) bidi_combine_kernel(const int* topH, cons
             ht = ft = (long long)go + (long long)(m - 1) * ge;
         else
         {
-            ht = (long long)topH[kTapPad + j] - d + (long long)(m + j) * ge;
-            ft = affine ? (long long)topF[kTapPad + j] + (long long)(m + j) * ge : ht;
+            ht = (long long)topH[(size_t)ts * j] - d + (long long)(m + j) * ge;
+            ft = affine ? (long long)topF[(size_t)ts * j] + (long long)(m + j) * ge : ht;
         }
         if (jb == 0)
             hb = fb = (long long)go + (long long)(mb - 1) * ge;
         else
         {
-            hb = (long long)botH[kTapPad + jb] - d + (long long)(mb + jb) * ge;
-            fb = affine ? (long long)botF[kTapPad + jb] + (long long)(mb + jb) * ge : hb;
+            hb = (long long)botH[(size_t)bs * jb] - d + (long long)(mb + jb) * ge;
+            fb = affine ? (long long)botF[(size_t)bs * jb] + (long long)(mb + jb) * ge : hb;
         }
         long long v = ht + hb;
         if (affine) v = max(v, ft + fb - d);
@@ -90,12 +90,12 @@ hipError_t launch_bidi_prep(const PairDesc& d0, const PairDesc& d1, PairDesc* de
     return hipGetLastError();
 }
 
-hipError_t launch_bidi_combine(const int* topH, const int* topF, const int* botH, const int* botF, int m, int mb,
-                               int C, int go, int ge, bool affine, int* out, hipStream_t stream)
+hipError_t launch_bidi_combine(const int* topH, const int* topF, int ts, const int* botH, const int* botF, int bs,
+                               int m, int mb, int C, int go, int ge, bool affine, int* out, hipStream_t stream)
 {
     const int grid = (C + 1 + 255) / 256 < 256 ? (C + 1 + 255) / 256 : 256;
-    hipLaunchKernelGGL(bidi_combine_kernel, dim3(grid), dim3(256), 0, stream, topH, topF, botH, botF, m, mb, C, go, ge,
-                       affine ? 1 : 0, out);
+    hipLaunchKernelGGL(bidi_combine_kernel, dim3(grid), dim3(256), 0, stream, topH, topF, ts, botH, botF, bs, m, mb, C,
+                       go, ge, affine ? 1 : 0, out);
     return hipGetLastError();
 }
 

@@ -1691,7 +1691,7 @@ __device__ __forceinline__ void ks_drain(const StripArgs& a, const KsLds& L, int
     constexpr bool AG = !is_lin_mode(MODE);
     const int Cp = a.Cp;
     const uint32_t F = L.flags, ringN = L.ring + (uint32_t)NS * (kRing * 4u);
-    if (tk + 1 >= a.nTickets)
+    if (tk + 1 >= a.nTickets && !a.tapGran)
     {
         flag_st(F + kr_cons(NS), kBig);  // nobody reads our last row
         return;
@@ -1793,8 +1793,10 @@ __global__ void __launch_bounds__(64 * kr_waves<kKrowNSDefault>()) nw_kscore_ker
         int h = 0, tk = tkg;
         if (a.bidiTop > 0)
         {
-            h = tkg < 2 * a.bidiTop ? (tkg & 1) : 1;
-            tk = tkg < 2 * a.bidiTop ? (tkg >> 1) : tkg - a.bidiTop;
+            // alternate while both halves have tickets, then the longer half's rest
+            const int nA = a.bidiTop, nB = a.nTicketsTotal - a.bidiTop, n = min(nA, nB);
+            h = tkg < 2 * n ? (tkg & 1) : (nA > nB ? 0 : 1);
+            tk = tkg < 2 * n ? (tkg >> 1) : tkg - n;
         }
         const PairDesc d = kr_desc(a.pairs + h);
         StripArgs pa = a;
@@ -1807,6 +1809,7 @@ __global__ void __launch_bounds__(64 * kr_waves<kKrowNSDefault>()) nw_kscore_ker
         pa.granStride = gran_stride(d.Cp);
         pa.gran = a.gran + d.granOff;
         pa.gran2 = a.gran2 + d.granOff;
+        pa.tapGran = (a.tapGran >> h) & 1;
         if (h)
         {
             pa.tapRow = a.tapRowB;

@@ -122,13 +122,17 @@ struct StripArgs
     // tapRow stores that row's Hgo' (tapH) and, affine, F' (tapF), shifted as the hand-off holds
     // them, at tap[kTapPad + column] for every column the lane computes; tapRow <= 0: none.
     // bidiTop > 0: one launch runs both halves, pairs[0] (bidiTop tickets) and pairs[1] (the rest),
-    // tickets interleaved; half 1 taps row tapRowB into tapH / tapF + tapStride
+    // tickets alternating while both have some, then the longer half's; half 1 taps row tapRowB
+    // into tapH / tapF + tapStride
     int* tapH;
     int* tapF;
     int tapRow;
     int tapRowB;
     int tapStride;
     int bidiTop;
+    // score_bidi: bit h set -> half h's last ticket ends on its tap row, and that ticket's drain
+    // writes its granules like any other ticket's (the combine reads the tap there: no lane tap)
+    int tapGran;
 };
 constexpr int kTapPad = 128;  // tap row buffers: columns -kTapPad .. C + 79
 

@@ -298,3 +298,25 @@ def test_score_both_ends_100k(engine, golden):
         finally:
             del os.environ["GSA_SCORE_BIDI"]
         assert (r1["score"], r1["i_end"], r1["j_end"]) == (r0["score"], r0["i_end"], r0["j_end"])
+
+
+@pytest.mark.parametrize("gran", ["0", "1"])
+@pytest.mark.parametrize("skew", ["-1", "0", "700"])
+def test_score_both_ends_granule_tap(engine, golden, monkeypatch, gran, skew):
+    """The halves' meeting rows read from the last ticket's granules when a half ends on a ticket
+    boundary (GSA_BIDI_GRAN=1, the default past 4 tickets: the top half always, the bottom when R
+    is a multiple of the ticket too), or from lane taps on both sides (GSA_BIDI_GRAN=0); the top
+    half's extra rows (GSA_BIDI_SKEW; -1 = the cost model) move the split.  Both NW modes, both
+    rows-per-lane settings, R a multiple of the ticket (both halves free) and not; the oracle."""
+    import oracle
+    monkeypatch.setenv("GSA_SCORE_BIDI", "2")
+    monkeypatch.setenv("GSA_BIDI_GRAN", gran)
+    monkeypatch.setenv("GSA_BIDI_SKEW", skew)
+    for k in ("2", "4"):
+        monkeypatch.setenv("GSA_SCORE_K", k)
+        for R, C in [(4096, 1500), (5120, 900), (4100, 2600), (6002, 700), (8192, 333)]:
+            Y, X = random_pair(R, C, 29 * R + C)
+            for go, ge in [(-11, -1), (-11, -11), (-4, -2)]:
+                r = engine.score(Y, X, golden.blosum62, go, ge, False)
+                assert (r["score"], r["i_end"], r["j_end"]) == oracle.score_ag(Y, X, golden.blosum62, go, ge, False), \
+                    (k, R, C, go, ge)
