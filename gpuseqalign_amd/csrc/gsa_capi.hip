@@ -449,8 +449,6 @@ int score_bidi(gsa_ctx* ctx, const int32_t* seqY, int64_t R, const int32_t* seqX
     a.tapRow = topFree ? 0 : (int)m;
     a.tapRowB = botFree ? 0 : (int)mb;
     a.tapGran = (topFree ? 1 : 0) | (botFree ? 2 : 0);
-    if (env_int("GSA_PROBE_NOTAP", 0))  // (timing probe: no tap stores, wrong scores)
-        a.tapRow = a.tapRowB = 0;
     a.tapH = tapH;
     a.tapF = tapF;
     a.tapStride = (int)(2 * tapLen);
