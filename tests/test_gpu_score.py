@@ -320,3 +320,20 @@ def test_score_both_ends_granule_tap(engine, golden, monkeypatch, gran, skew):
                 r = engine.score(Y, X, golden.blosum62, go, ge, False)
                 assert (r["score"], r["i_end"], r["j_end"]) == oracle.score_ag(Y, X, golden.blosum62, go, ge, False), \
                     (k, R, C, go, ge)
+
+
+def test_score_both_ends_large_random_shapes(engine, golden, monkeypatch):
+    """Ten random shapes of 4k-30k rows and columns (both parities, both split forms: granule tap or
+    lane taps, transposed when only C suits), random affine / linear gaps: the default path against
+    the one-direction kernel (GSA_SCORE_BIDI=0) on the same inputs."""
+    rng = np.random.default_rng(77)
+    for case in range(10):
+        R, C = (int(v) for v in rng.integers(4000, 30001, 2))
+        ge = -int(rng.integers(1, 4))
+        go = ge - int(rng.integers(0, 12))
+        Y, X = random_pair(R, C, 5000 + case)
+        monkeypatch.setenv("GSA_SCORE_BIDI", "1")
+        r1 = engine.score(Y, X, golden.blosum62, go, ge, False)
+        monkeypatch.setenv("GSA_SCORE_BIDI", "0")
+        r0 = engine.score(Y, X, golden.blosum62, go, ge, False)
+        assert (r1["score"], r1["i_end"], r1["j_end"]) == (r0["score"], r0["i_end"], r0["j_end"]), (case, R, C, go, ge)
