@@ -1260,17 +1260,28 @@ int enqueue_full_twopass(gsa_ctx* ctx, int npairs, const gsa_pair_dev* pairs, co
             ctx->xt_ms[0] = ctx->xt_ms[1] = -1.f;
             ctx->xt_pending = false;
         }
-        for (int k = 0; k < 2 && !ctx->xt_ev[k]; ++k)
-            if ((e = hipEventCreate(&ctx->xt_ev[k])) != hipSuccess) return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
+        // (the tuning is best effort: an event that cannot be created or read ends it on order 1)
+        bool evOk = true;
+        for (int k = 0; k < 2; ++k)
+            if (!ctx->xt_ev[k] && hipEventCreate(&ctx->xt_ev[k]) != hipSuccess)
+            {
+                ctx->xt_ev[k] = nullptr;
+                evOk = false;
+            }
         if (ctx->xt_pending)
         {
             float ms = -1.f;
-            if ((e = hipEventSynchronize(ctx->xt_ev[1])) != hipSuccess ||
-                (e = hipEventElapsedTime(&ms, ctx->xt_ev[0], ctx->xt_ev[1])) != hipSuccess)
-                return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
-            ctx->xt_ms[ctx->xt_last] = ms;
+            if (hipEventSynchronize(ctx->xt_ev[1]) != hipSuccess ||
+                hipEventElapsedTime(&ms, ctx->xt_ev[0], ctx->xt_ev[1]) != hipSuccess || !(ms >= 0.f))
+            {
+                (void)hipGetLastError();
+                evOk = false;
+            }
+            else
+                ctx->xt_ms[ctx->xt_last] = ms;
             ctx->xt_pending = false;
         }
+        if (!evOk) ctx->xt_ms[0] = ctx->xt_ms[1] = 0.f;  // both "measured": order 1 from now on
         const int next = ctx->xt_ms[0] < 0 ? 0 : ctx->xt_ms[1] < 0 ? 1 : (ctx->xt_ms[1] < ctx->xt_ms[0] ? 1 : 0);
         tuneRecord = ctx->xt_ms[next] < 0;
         ctx->xt_last = next;
