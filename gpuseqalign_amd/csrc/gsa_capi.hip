@@ -65,6 +65,14 @@ struct gsa_ctx
     size_t excap = 0;
     void* exdesc = nullptr;
     size_t exdesc_cap = 0;
+    // the split batch (enqueue_full_split): the tail group's pass-1 outputs and descriptors, its
+    // high-priority stream and the events between the groups
+    void* exbuf2 = nullptr;
+    size_t excap2 = 0;
+    void* exdesc2 = nullptr;
+    size_t exdesc_cap2 = 0;
+    hipStream_t splitstream = nullptr;
+    hipEvent_t split_ev[2] = {nullptr, nullptr};
     // fused single-pair fill: one progress word per pass-1 strip (epoch-tagged, cleared once per
     // allocation)
     unsigned long long* xdone = nullptr;
@@ -83,13 +91,26 @@ struct gsa_ctx
     int timing_groups = 0;
     // the batch expansion's task order, tuned per output buffer (enqueue_full_twopass): key, the
     // order each candidate took (ms, < 0: not measured), the order of the last launch and its events
-    const void* xt_key = nullptr;
-    int xt_pairs = 0;
-    long long xt_tasks = 0;
-    float xt_ms[2] = {-1.f, -1.f};
-    int xt_last = -1;
-    bool xt_pending = false;
-    hipEvent_t xt_ev[2] = {nullptr, nullptr};
+    struct XTune
+    {
+        const void* key = nullptr;
+        int pairs = 0;
+        long long tasks = 0;
+        float ms[2] = {-1.f, -1.f};
+        int last = -1;
+        bool pending = false;
+        hipEvent_t ev[2] = {nullptr, nullptr};
+    } xt[2];  // per scratch slot
+    // a batch that can run as two pair groups (enqueue_full_split): whole-job times of the four
+    // candidates (one group or two, expansion order 1 or 2), keyed by the batch (enqueue_full)
+    struct FTune
+    {
+        uint64_t key = 0;
+        float ms[4] = {-1.f, -1.f, -1.f, -1.f};
+        int last = -1;
+        bool pending = false;
+        hipEvent_t ev[2] = {nullptr, nullptr};
+    } ft;
     // score-only NW from both ends (score_bidi): tap rows of both halves, the reversed sequences, the
     // combine's result, the transposed table
     int* bidi = nullptr;
@@ -257,7 +278,8 @@ long long held_bytes(const gsa_ctx* c)
     long long b = 256 + 64 + (long long)c->gran_elems * 8 + (long long)c->desc_cap * (long long)sizeof(gsa::PairDesc) +
                   (long long)c->tmoves_cap + (long long)c->tdirs_cap + (long long)c->sbnd_cap * 4 +
                   (long long)c->tband_cap + (long long)c->tlist_cap * 4 + (long long)c->excap +
-                  (long long)c->exdesc_cap + 8 * (long long)(c->xdone_cap + c->stamps_cap + c->clk_cap) +
+                  (long long)c->exdesc_cap + (long long)c->excap2 + (long long)c->exdesc_cap2 +
+                  8 * (long long)(c->xdone_cap + c->stamps_cap + c->clk_cap) +
                   4 * (long long)c->bidi_cap;
     for (size_t k : c->dcap) b += (long long)k;
     return b;
@@ -1125,9 +1147,24 @@ int enqueue_full_pipelined(gsa_ctx* ctx, int npairs, const gsa_pair_dev* pairs, 
 // width kExpTW, which also keeps rows 64m (XR instance), into the context's scratch; pass 2 =
 // every 64-row x kExpTW tile of every matrix recomputed from its top row and left column at once.
 // lds: row pitches (null: unpadded).
-int enqueue_full_twopass(gsa_ctx* ctx, int npairs, const gsa_pair_dev* pairs, const int32_t* lds, const int32_t* subst,
-                         int32_t substsz, int32_t gapo, hipStream_t st)
+// (enqueue_full_split: slot 1 = the tail group's scratch; afterP1 recorded behind pass 1, beforeP1
+// awaited before it; split: the caller records the timing events and no clock stamps are taken;
+// rr >= 0: that expansion order, untuned; startEv: recorded on st just before pass 1)
+struct TwoPassOpts
 {
+    int slot = 0;
+    hipEvent_t afterP1 = nullptr, beforeP1 = nullptr, timeP1 = nullptr, startEv = nullptr;
+    bool split = false;
+    int rr = -1;
+};
+int enqueue_full_twopass(gsa_ctx* ctx, int npairs, const gsa_pair_dev* pairs, const int32_t* lds, const int32_t* subst,
+                         int32_t substsz, int32_t gapo, hipStream_t st, const TwoPassOpts& opt = TwoPassOpts())
+{
+    void*& exbuf = opt.slot ? ctx->exbuf2 : ctx->exbuf;
+    size_t& excap = opt.slot ? ctx->excap2 : ctx->excap;
+    void*& exdesc = opt.slot ? ctx->exdesc2 : ctx->exdesc;
+    size_t& exdesc_cap = opt.slot ? ctx->exdesc_cap2 : ctx->exdesc_cap;
+    gsa_ctx::XTune& xt = ctx->xt[opt.slot];
     if (npairs < 1 || !pairs || !subst) return GSA_ERROR_INVALID_VALUE;
     if (substsz < 1 || substsz > 32) return GSA_ERROR_INVALID_VALUE;
     // pass-1 geometry as enqueue_batch derives it for the XR instances
@@ -1211,19 +1248,19 @@ int enqueue_full_twopass(gsa_ctx* ctx, int npairs, const gsa_pair_dev* pairs, co
     }
     hipError_t e = hipSetDevice(ctx->device);
     if (e != hipSuccess) return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
-    if (ctx->excap < bytes || !ctx->exbuf)
+    if (excap < bytes || !exbuf)
     {
-        if (ctx->exbuf) (void)hipFree(ctx->exbuf);
-        ctx->exbuf = nullptr;
-        ctx->excap = 0;
-        if ((e = hipMalloc(&ctx->exbuf, std::max<size_t>(bytes, 256))) != hipSuccess)
+        if (exbuf) (void)hipFree(exbuf);
+        exbuf = nullptr;
+        excap = 0;
+        if ((e = hipMalloc(&exbuf, std::max<size_t>(bytes, 256))) != hipSuccess)
         {
             (void)hipGetLastError();  // the caller falls back to the one-pass lane fill
             return kNoScratch;
         }
-        ctx->excap = std::max<size_t>(bytes, 256);
+        excap = std::max<size_t>(bytes, 256);
     }
-    char* base = (char*)ctx->exbuf;
+    char* base = (char*)exbuf;
     std::vector<int*> rows((size_t)npairs);
     for (int p = 0; p < npairs; ++p)
     {
@@ -1246,45 +1283,45 @@ int enqueue_full_twopass(gsa_ctx* ctx, int npairs, const gsa_pair_dev* pairs, co
     // and 2 and time their pass 2 (HIP events; the second launch waits for the first's), and later
     // launches on that buffer take the faster.  GSA_EXPAND_RR fixes the order: 0 pair-major, 1, 2,
     // 3 shuffled, 4-6 probe variants.
-    const int rrEnv = env_int("GSA_EXPAND_RR", -1);
+    const int rrEnv = opt.rr >= 0 ? opt.rr : env_int("GSA_EXPAND_RR", -1);
     int rr = rrEnv >= 0 ? rrEnv : 1;
     const bool tune = rrEnv < 0 && npairs > 1 && !fused;
     bool tuneRecord = false;
     if (tune)
     {
-        if (ctx->xt_key != (const void*)pairs[0].score || ctx->xt_pairs != npairs || ctx->xt_tasks != tasks)
+        if (xt.key != (const void*)pairs[0].score || xt.pairs != npairs || xt.tasks != tasks)
         {
-            ctx->xt_key = (const void*)pairs[0].score;
-            ctx->xt_pairs = npairs;
-            ctx->xt_tasks = tasks;
-            ctx->xt_ms[0] = ctx->xt_ms[1] = -1.f;
-            ctx->xt_pending = false;
+            xt.key = (const void*)pairs[0].score;
+            xt.pairs = npairs;
+            xt.tasks = tasks;
+            xt.ms[0] = xt.ms[1] = -1.f;
+            xt.pending = false;
         }
         // (the tuning is best effort: an event that cannot be created or read ends it on order 1)
         bool evOk = true;
         for (int k = 0; k < 2; ++k)
-            if (!ctx->xt_ev[k] && hipEventCreate(&ctx->xt_ev[k]) != hipSuccess)
+            if (!xt.ev[k] && hipEventCreate(&xt.ev[k]) != hipSuccess)
             {
-                ctx->xt_ev[k] = nullptr;
+                xt.ev[k] = nullptr;
                 evOk = false;
             }
-        if (ctx->xt_pending)
+        if (xt.pending)
         {
             float ms = -1.f;
-            if (hipEventSynchronize(ctx->xt_ev[1]) != hipSuccess ||
-                hipEventElapsedTime(&ms, ctx->xt_ev[0], ctx->xt_ev[1]) != hipSuccess || !(ms >= 0.f))
+            if (hipEventSynchronize(xt.ev[1]) != hipSuccess ||
+                hipEventElapsedTime(&ms, xt.ev[0], xt.ev[1]) != hipSuccess || !(ms >= 0.f))
             {
                 (void)hipGetLastError();
                 evOk = false;
             }
             else
-                ctx->xt_ms[ctx->xt_last] = ms;
-            ctx->xt_pending = false;
+                xt.ms[xt.last] = ms;
+            xt.pending = false;
         }
-        if (!evOk) ctx->xt_ms[0] = ctx->xt_ms[1] = 0.f;  // both "measured": order 1 from now on
-        const int next = ctx->xt_ms[0] < 0 ? 0 : ctx->xt_ms[1] < 0 ? 1 : (ctx->xt_ms[1] < ctx->xt_ms[0] ? 1 : 0);
-        tuneRecord = ctx->xt_ms[next] < 0;
-        ctx->xt_last = next;
+        if (!evOk) xt.ms[0] = xt.ms[1] = 0.f;  // both "measured": order 1 from now on
+        const int next = xt.ms[0] < 0 ? 0 : xt.ms[1] < 0 ? 1 : (xt.ms[1] < xt.ms[0] ? 1 : 0);
+        tuneRecord = xt.ms[next] < 0;
+        xt.last = next;
         rr = next + 1;
     }
     std::vector<int> xs;
@@ -1330,14 +1367,14 @@ int enqueue_full_twopass(gsa_ctx* ctx, int npairs, const gsa_pair_dev* pairs, co
     }
     const size_t descBytes = ((size_t)npairs * sizeof(gsa::ExpandPair) + 15) & ~(size_t)15;
     const size_t exBytes = descBytes + xs.size() * sizeof(int);
-    if (ctx->exdesc_cap < exBytes || !ctx->exdesc)
+    if (exdesc_cap < exBytes || !exdesc)
     {
-        if (ctx->exdesc) (void)hipFree(ctx->exdesc);
-        ctx->exdesc = nullptr;
-        ctx->exdesc_cap = 0;
-        if ((e = hipMalloc(&ctx->exdesc, std::max<size_t>(exBytes, 4096))) != hipSuccess)
+        if (exdesc) (void)hipFree(exdesc);
+        exdesc = nullptr;
+        exdesc_cap = 0;
+        if ((e = hipMalloc(&exdesc, std::max<size_t>(exBytes, 4096))) != hipSuccess)
             return fail(ctx, e, GSA_ERROR_MEMORY_ALLOCATION);
-        ctx->exdesc_cap = std::max<size_t>(exBytes, 4096);
+        exdesc_cap = std::max<size_t>(exBytes, 4096);
     }
     const int slot = ctx->expin_next;
     ctx->expin_next = (slot + 1) % gsa_ctx::kStage;
@@ -1353,7 +1390,7 @@ int enqueue_full_twopass(gsa_ctx* ctx, int npairs, const gsa_pair_dev* pairs, co
     }
     std::memcpy(ctx->expin[slot], ex.data(), (size_t)npairs * sizeof(gsa::ExpandPair));
     if (!xs.empty()) std::memcpy((char*)ctx->expin[slot] + descBytes, xs.data(), xs.size() * sizeof(int));
-    e = hipMemcpyAsync(ctx->exdesc, ctx->expin[slot], exBytes, hipMemcpyHostToDevice, st);
+    e = hipMemcpyAsync(exdesc, ctx->expin[slot], exBytes, hipMemcpyHostToDevice, st);
     if (e == hipSuccess) e = hipEventRecord(ctx->expin_ev[slot], st);
     if (e != hipSuccess) return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
     ctx->expin_used[slot] = true;
@@ -1361,18 +1398,18 @@ int enqueue_full_twopass(gsa_ctx* ctx, int npairs, const gsa_pair_dev* pairs, co
     xa.subst = subst;
     xa.substsz = substsz;
     xa.g = gapo;
-    xa.pairs = (const gsa::ExpandPair*)ctx->exdesc;
+    xa.pairs = (const gsa::ExpandPair*)exdesc;
     xa.nPairs = npairs;
     xa.nTasks = (int)tasks;
-    xa.sched = xs.empty() ? nullptr : (const int*)((char*)ctx->exdesc + descBytes);
+    xa.sched = xs.empty() ? nullptr : (const int*)((char*)exdesc + descBytes);
     xa.knob = env_int("GSA_EXPAND_KNOB", 0);
     xa.mt = xmt;
     // fused batches: GSA_FUSED_P1 workgroups take the pass-1 tickets first (a single pair: all)
     const FusedLaunch fl {&xa, ns, fusedW, npairs == 1 ? (1 << 30) : std::max(1, env_int("GSA_FUSED_P1", 128))};
     // gsa_set_full_timing: events before pass 1, between the passes and after pass 2, and the
     // expansion's clock stamps (one per workgroup)
-    const bool timed = ctx->timing;
-    ctx->timing_state = 0;
+    const bool timed = ctx->timing && !opt.split;
+    if (!opt.split) ctx->timing_state = 0;
     if (timed && !fused && xGrid == 0)
     {
         if (ctx->clk_cap < (size_t)tasks || !ctx->clk)
@@ -1388,6 +1425,9 @@ int enqueue_full_twopass(gsa_ctx* ctx, int npairs, const gsa_pair_dev* pairs, co
         ctx->clk_n = (size_t)tasks;
     }
     if (timed && (e = hipEventRecord(ctx->pev[0], st)) != hipSuccess) return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
+    if (opt.startEv && (e = hipEventRecord(opt.startEv, st)) != hipSuccess) return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
+    if (opt.beforeP1 && (e = hipStreamWaitEvent(st, opt.beforeP1, 0)) != hipSuccess)
+        return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
     int s = enqueue_batch(ctx, gsa::kModeSparse, npairs, p1.data(), subst, substsz, gapo, gsa::kExpHB, st, nullptr, 0,
                           nullptr, rows.data(), fused ? &fl : nullptr);
     if (s != GSA_SUCCESS) return s;
@@ -1398,15 +1438,17 @@ int enqueue_full_twopass(gsa_ctx* ctx, int npairs, const gsa_pair_dev* pairs, co
         return s;
     }
     if (timed && (e = hipEventRecord(ctx->pev[1], st)) != hipSuccess) return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
+    if (opt.afterP1 && (e = hipEventRecord(opt.afterP1, st)) != hipSuccess) return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
+    if (opt.timeP1 && (e = hipEventRecord(opt.timeP1, st)) != hipSuccess) return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
     xa.counter = ctx->ctl + 4;
     if (xGrid > 0 && (e = hipMemsetAsync(xa.counter, 0, 4, st)) != hipSuccess) return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
-    if (tuneRecord && (e = hipEventRecord(ctx->xt_ev[0], st)) != hipSuccess) return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
+    if (tuneRecord && (e = hipEventRecord(xt.ev[0], st)) != hipSuccess) return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
     if ((e = gsa::launch_expand(xa, st, xWaves, xGrid)) != hipSuccess) return fail(ctx, e, GSA_ERROR_KERNEL_FAILURE);
     note_launch(ctx);
     if (tuneRecord)
     {
-        if ((e = hipEventRecord(ctx->xt_ev[1], st)) != hipSuccess) return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
-        ctx->xt_pending = true;
+        if ((e = hipEventRecord(xt.ev[1], st)) != hipSuccess) return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
+        xt.pending = true;
     }
     if (timed)
     {
@@ -1424,13 +1466,224 @@ bool full_twopass(int)
     return !(e && std::strcmp(e, "lane") == 0);
 }
 
-// every full fill: the two-pass fill, or the lane fill (GSA_FULL_KERNEL=lane, or no room for the
-// two-pass scratch); lds: row pitches (null: unpadded)
+// A batch whose pass-1 tickets are k full rounds and a short last one, split in two groups: group A
+// (k rounds of tickets) on the caller's stream, group B (the rest) on a high-priority stream behind
+// A's pass 1.  B's pass 1 then runs on the CUs A's pass 1 leaves, while A's expansion takes the
+// others, instead of the last round's idle CUs waiting for every pair's pass 1.  Whether that pays
+// depends on the box: 64 x 20k pairs, 0.434 -> 0.49-0.52 of HBM peak on four boxes, 0.508 -> 0.475
+// on another (profiles/r05_split_ab.txt), so enqueue_full times both on the batch's first launches.
+struct SplitPlan
+{
+    std::vector<gsa_pair_dev> pa, pb;
+    std::vector<int32_t> la, lb;
+};
+bool split_plan(gsa_ctx* ctx, int npairs, const gsa_pair_dev* pairs, const int32_t* lds, SplitPlan& sp)
+{
+    if (npairs < 2 || env_int("GSA_FULL_FUSED", 1) >= 2 || env_int("GSA_EXPAND_GRID", 0) > 0 ||
+        env_int("GSA_FULL_PIPE", 0) >= 2)
+        return false;
+    long long tileRows = 0;
+    for (int p = 0; p < npairs; ++p)
+    {
+        if (pairs[p].adjrows < 2 || pairs[p].adjcols < 2) return false;
+        tileRows += std::max<long long>(1, ((long long)pairs[p].adjrows - 1 + gsa::kSparseTileBy - 1) / gsa::kSparseTileBy);
+    }
+    if (tileRows <= (long long)std::max(1, ctx->cu_count)) return false;  // 4-strip single round
+    const int ns = env_int("GSA_KROW_NS", 8) == 8 ? 8 : 4;
+    std::vector<long long> t((size_t)npairs);
+    long long T = 0;
+    for (int p = 0; p < npairs; ++p)
+    {
+        gsa_sparse_geom geom;
+        if (gsa_sparse_geometry(pairs[p].adjrows, pairs[p].adjcols, gsa::kExpHB, &geom) != GSA_SUCCESS) return false;
+        t[(size_t)p] = gsa::krow_tickets(geom.tileHdrMatRows, ns, 4);
+        T += t[(size_t)p];
+    }
+    const long long S = std::max(1, ctx->cu_count);  // (8, 4) XR workgroups: one per CU
+    const long long k = T / S, tail = T - k * S;
+    if (k < 1 || tail < 16 || tail > S - 16) return false;
+    // group A: pairs by tickets, largest first, while they fit k rounds; B: the rest
+    std::vector<int> ord((size_t)npairs);
+    for (int p = 0; p < npairs; ++p) ord[(size_t)p] = p;
+    std::stable_sort(ord.begin(), ord.end(), [&](int x, int y) { return t[(size_t)x] > t[(size_t)y]; });
+    long long ta = 0;
+    for (int p : ord)
+    {
+        const bool toA = ta + t[(size_t)p] <= k * S;
+        if (toA) ta += t[(size_t)p];
+        (toA ? sp.pa : sp.pb).push_back(pairs[p]);
+        if (lds) (toA ? sp.la : sp.lb).push_back(lds[p]);
+    }
+    return !sp.pa.empty() && !sp.pb.empty();
+}
+
+// The two groups of a split plan; rr: both groups' expansion order (-1: each tuned on its own
+// scratch slot); startEv: recorded on st before group A's pass 1.  Returns kNoScratch when nothing
+// was enqueued (no room for group A's scratch).
+int enqueue_full_split(gsa_ctx* ctx, const SplitPlan& sp, bool hasLds, const int32_t* subst, int32_t substsz,
+                       int32_t gapo, hipStream_t st, int rr, hipEvent_t startEv)
+{
+    hipError_t e = hipSetDevice(ctx->device);
+    if (e != hipSuccess) return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
+    if (!ctx->splitstream)
+    {
+        int lo = 0, hi = 0;
+        if ((e = hipDeviceGetStreamPriorityRange(&lo, &hi)) != hipSuccess ||
+            (e = hipStreamCreateWithPriority(&ctx->splitstream, hipStreamNonBlocking, hi)) != hipSuccess)
+            return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
+    }
+    for (int q = 0; q < 2; ++q)
+        if (!ctx->split_ev[q] && (e = hipEventCreateWithFlags(&ctx->split_ev[q], hipEventDisableTiming)) != hipSuccess)
+            return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
+    const bool timed = ctx->timing;
+    if (timed && (e = hipEventRecord(ctx->pev[0], st)) != hipSuccess) return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
+    // B's stream waits for everything before this call on the caller's stream too
+    if ((e = hipEventRecord(ctx->split_ev[1], st)) != hipSuccess ||
+        (e = hipStreamWaitEvent(ctx->splitstream, ctx->split_ev[1], 0)) != hipSuccess)
+        return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
+    TwoPassOpts oa, ob;
+    oa.slot = 0;
+    oa.afterP1 = ctx->split_ev[0];
+    oa.timeP1 = timed ? ctx->pev[1] : nullptr;  // pass1_ms: group A's pass 1
+    oa.startEv = startEv;
+    oa.split = true;
+    oa.rr = rr;
+    ob.slot = 1;
+    ob.beforeP1 = ctx->split_ev[0];
+    ob.split = true;
+    ob.rr = rr;
+    int r = enqueue_full_twopass(ctx, (int)sp.pa.size(), sp.pa.data(), hasLds ? sp.la.data() : nullptr, subst, substsz,
+                                 gapo, st, oa);
+    if (r != GSA_SUCCESS) return r;  // (kNoScratch: nothing enqueued yet; the caller's fallback)
+    r = enqueue_full_twopass(ctx, (int)sp.pb.size(), sp.pb.data(), hasLds ? sp.lb.data() : nullptr, subst, substsz,
+                             gapo, ctx->splitstream, ob);
+    if (r == kNoScratch)  // no room for a second scratch: group B on the one-pass lane fill
+    {
+        if ((e = hipStreamWaitEvent(ctx->splitstream, ctx->split_ev[0], 0)) != hipSuccess)
+            return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
+        r = enqueue_batch(ctx, gsa::kModeFull, (int)sp.pb.size(), sp.pb.data(), subst, substsz, gapo, 0,
+                          ctx->splitstream, nullptr, 0, hasLds ? sp.lb.data() : nullptr);
+    }
+    if (r != GSA_SUCCESS) return r;
+    // the caller's stream waits for group B
+    if ((e = hipEventRecord(ctx->split_ev[1], ctx->splitstream)) != hipSuccess ||
+        (e = hipStreamWaitEvent(st, ctx->split_ev[1], 0)) != hipSuccess)
+        return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
+    if (timed)
+    {
+        if ((e = hipEventRecord(ctx->pev[2], st)) != hipSuccess) return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
+        ctx->timing_state = 3;
+        ctx->timing_groups = 2;
+        ctx->clk_n = 0;
+    }
+    return GSA_SUCCESS;
+}
+
+uint64_t batch_key(int npairs, const gsa_pair_dev* pairs, const int32_t* lds)
+{
+    uint64_t h = 0x9e3779b97f4a7c15ull ^ (uint64_t)npairs;
+    auto mix = [&](uint64_t v) {
+        h ^= v + 0x9e3779b97f4a7c15ull + (h << 6) + (h >> 2);
+        h *= 0xbf58476d1ce4e5b9ull;
+        h ^= h >> 31;
+    };
+    for (int p = 0; p < npairs; ++p)
+    {
+        mix((uint64_t)(uintptr_t)pairs[p].score);
+        mix(((uint64_t)(uint32_t)pairs[p].adjrows << 32) | (uint32_t)pairs[p].adjcols);
+        mix(lds ? (uint64_t)(uint32_t)lds[p] : 0);
+    }
+    return h;
+}
+
+// Every full fill: the two-pass fill, or the lane fill (GSA_FULL_KERNEL=lane, or no room for the
+// two-pass scratch); lds: row pitches (null: unpadded).
+// A batch that splits (split_plan) runs, unless GSA_FULL_SPLIT or GSA_EXPAND_RR fix it, four
+// candidates on its first four launches: one group with expansion order 1 and 2, two groups with
+// order 1 and 2, each timed from just before pass 1 to the end on the caller's stream (HIP events;
+// a launch waits on the host for the previous one's end event), and later launches of the same
+// batch (pairs, shapes, output pointers) take the fastest.  Best effort like the order tuning: an
+// event that cannot be created or read ends it on candidate 0.
 int enqueue_full(gsa_ctx* ctx, int npairs, const gsa_pair_dev* pairs, const int32_t* lds, const int32_t* subst,
                  int32_t substsz, int32_t gapo, hipStream_t st)
 {
     if (full_twopass(npairs))
     {
+        const int spEnv = env_int("GSA_FULL_SPLIT", -1), rrEnv = env_int("GSA_EXPAND_RR", -1);
+        SplitPlan sp;
+        const bool can = spEnv != 0 && !(spEnv < 0 && rrEnv >= 0) && split_plan(ctx, npairs, pairs, lds, sp);
+        if (can && spEnv > 0)
+        {
+            const int r = enqueue_full_split(ctx, sp, lds != nullptr, subst, substsz, gapo, st, -1, nullptr);
+            if (r != kNoScratch) return r;
+        }
+        else if (can)
+        {
+            gsa_ctx::FTune& ft = ctx->ft;
+            const uint64_t key = batch_key(npairs, pairs, lds);
+            if (ft.key != key)
+            {
+                ft.key = key;
+                ft.last = -1;
+                for (float& m : ft.ms) m = -1.f;
+                ft.pending = false;
+            }
+            bool evOk = true;
+            for (int k = 0; k < 2; ++k)
+                if (!ft.ev[k] && hipEventCreate(&ft.ev[k]) != hipSuccess)
+                {
+                    (void)hipGetLastError();
+                    ft.ev[k] = nullptr;
+                    evOk = false;
+                }
+            if (ft.pending)
+            {
+                float ms = -1.f;
+                if (hipEventSynchronize(ft.ev[1]) != hipSuccess ||
+                    hipEventElapsedTime(&ms, ft.ev[0], ft.ev[1]) != hipSuccess || !(ms >= 0.f))
+                {
+                    (void)hipGetLastError();
+                    evOk = false;
+                }
+                else
+                    ft.ms[ft.last] = ms;
+                ft.pending = false;
+            }
+            if (!evOk)
+                for (float& m : ft.ms) m = 0.f;  // all "measured": candidate 0 from now on
+            int next = 0;
+            while (next < 4 && ft.ms[next] >= 0.f) ++next;
+            if (next == 4)
+            {
+                next = 0;
+                for (int k = 1; k < 4; ++k)
+                    if (ft.ms[k] < ft.ms[next]) next = k;
+                if (ft.last >= 0 && env_int("GSA_TUNE_LOG", 0))  // (measurement aid: the four times, once)
+                    std::fprintf(stderr, "gsa full-batch tuning: one group %.3f / %.3f ms, two groups %.3f / %.3f ms -> %d\n",
+                                 ft.ms[0], ft.ms[1], ft.ms[2], ft.ms[3], next);
+                ft.last = -1;
+            }
+            const bool rec = ft.ms[next] < 0.f;
+            const int rr = (next & 1) + 1;
+            int r;
+            if (next >= 2)
+                r = enqueue_full_split(ctx, sp, lds != nullptr, subst, substsz, gapo, st, rr, rec ? ft.ev[0] : nullptr);
+            else
+            {
+                TwoPassOpts o;
+                o.rr = rr;
+                o.startEv = rec ? ft.ev[0] : nullptr;
+                r = enqueue_full_twopass(ctx, npairs, pairs, lds, subst, substsz, gapo, st, o);
+            }
+            if (r == GSA_SUCCESS && rec)
+            {
+                hipError_t e = hipEventRecord(ft.ev[1], st);
+                if (e != hipSuccess) return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
+                ft.last = next;
+                ft.pending = true;
+            }
+            if (r != kNoScratch) return r;
+        }
         const int s = enqueue_full_twopass(ctx, npairs, pairs, lds, subst, substsz, gapo, st);
         if (s != kNoScratch) return s;
     }
@@ -1571,8 +1824,20 @@ void gsa_ctx_destroy(gsa_ctx* ctx)
         if (ev) (void)hipEventDestroy(ev);
     for (hipEvent_t ev : ctx->pipe_ev)
         if (ev) (void)hipEventDestroy(ev);
-    for (hipEvent_t ev : ctx->xt_ev)
+    for (auto& t : ctx->xt)
+        for (hipEvent_t ev : t.ev)
+            if (ev) (void)hipEventDestroy(ev);
+    for (hipEvent_t ev : ctx->split_ev)
         if (ev) (void)hipEventDestroy(ev);
+    for (hipEvent_t ev : ctx->ft.ev)
+        if (ev) (void)hipEventDestroy(ev);
+    if (ctx->splitstream)
+    {
+        (void)hipStreamSynchronize(ctx->splitstream);
+        (void)hipStreamDestroy(ctx->splitstream);
+    }
+    if (ctx->exbuf2) (void)hipFree(ctx->exbuf2);
+    if (ctx->exdesc2) (void)hipFree(ctx->exdesc2);
     if (ctx->p1stream)
     {
         (void)hipStreamSynchronize(ctx->p1stream);

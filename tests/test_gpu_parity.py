@@ -493,3 +493,52 @@ def test_expansion_orders_repeated(engine, golden, order, monkeypatch):
             for (Y, X), b, ld, S in zip(pairs, bufs, lds, ref):
                 M = b.cpu().numpy().reshape(len(Y), ld)
                 assert np.array_equal(M[:, :len(X)], S), (buffer_set, launch)
+
+
+@pytest.mark.parametrize("split", ["tuned", "0", "1"])
+def test_full_batch_split(engine, golden, split, monkeypatch):
+    """A full batch whose pass-1 tickets fill one round and part of another, split in two groups
+    (GSA_FULL_SPLIT=1: the first round's pairs on the caller's stream, the rest on a high-priority
+    stream behind their pass 1, each group with its own pass-1 scratch and expansion order), against
+    the same batch in one group (0), and by default (tuned) one group on the first two launches and
+    two on the next two (gsa_capi.hip enqueue_full), then the fastest: every word of every pair
+    equals the oracle on every launch."""
+    import torch
+    monkeypatch.setenv("GSA_FULL_KERNEL", "twopass")
+    monkeypatch.setenv("GSA_FULL_FUSED", "0")
+    if split == "tuned":
+        monkeypatch.delenv("GSA_FULL_SPLIT", raising=False)
+    else:
+        monkeypatch.setenv("GSA_FULL_SPLIT", split)
+    monkeypatch.delenv("GSA_KROW_NS", raising=False)
+    monkeypatch.delenv("GSA_EXPAND_RR", raising=False)
+    sub = golden.blosum62
+    cu = int(engine.cu_count)
+    n = cu + cu // 3  # (8, 4) tickets: 3 per pair of 4100-5100 rows -> 1 round and a part
+    rng = np.random.default_rng(31)
+    shapes = [(int(rng.integers(4100, 5100)), int(rng.integers(200, 700))) for _ in range(n // 3 + 8)]
+    pairs = [random_pair(r, c, 17 * r + c) for r, c in shapes]
+    ref = [oracle.fill_full(Y, X, sub, -11)[0] for Y, X in pairs]
+    dev = torch.device("cuda:0")
+    s = torch.from_numpy(np.ascontiguousarray(sub, dtype=np.int32)).to(dev)
+    ins = [(torch.from_numpy(Y).to(dev), torch.from_numpy(X).to(dev)) for Y, X in pairs]
+    lds = [gsa.full_pitch(len(X)) for _, X in pairs]
+    bufs = [torch.empty((len(Y) * ld,), dtype=torch.int32, device=dev) for (Y, _), ld in zip(pairs, lds)]
+    engine.set_full_timing(True)
+    try:
+        for launch in range(6 if split == "tuned" else 2):
+            for b in bufs:
+                b.fill_(-7)
+            engine.fill_batch_dev([(y.data_ptr(), len(y), x.data_ptr(), len(x), b.data_ptr())
+                                   for (y, x), b in zip(ins, bufs)], s.data_ptr(), 25, -11, mode="full", lds=lds)
+            engine.sync()
+            groups = engine.last_full_timing()["pipelined_groups"]
+            if split == "tuned":
+                assert groups == (0 if launch < 2 else 2) if launch < 4 else groups in (0, 2), launch
+            else:
+                assert groups == (2 if split == "1" else 0)
+            for (Y, X), b, ld, S in zip(pairs, bufs, lds, ref):
+                M = b.cpu().numpy().reshape(len(Y), ld)
+                assert np.array_equal(M[:, :len(X)], S), launch
+    finally:
+        engine.set_full_timing(False)
