@@ -441,12 +441,17 @@ def score_kernel_name(go, ge, local, substsz=25, R=50000, C=50000):
     kb = int(kenv) if kenv in ("2", "4") else 2
     splits = lambda rows: rows % kb == 0 and rows >= 2 * kb and (bidi_env == "2" or rows >= 8 * 64 * kb * 4)
     bidi = krow and not local and bidi_env != "0" and (splits(R) or splits(C))
-    if bidi:
+    # SW: by rows only, three pairs (top forward, bottom reversed, bottom forward from a fresh
+    # border), back to one direction when an alignment through the split decides the result
+    bidi_sw = (krow and local and bidi_env != "0" and os.environ.get("GSA_SCORE_BIDI_SW", "1") != "0"
+               and splits(R))
+    if bidi or bidi_sw:
         k = kb
     q8env = os.environ.get("GSA_KROW_Q8", "1")
     q8 = q8env != "0" and (q8env == "2" or k == 4)
-    return (f"gsa::nw_kscore_kernel<{mode}, {'true' if q8 else 'false'}, {k}> ({mname}"
-            f"{', both ends: two halves in one launch' if bidi else ''})" if krow else
+    tag = (", both ends: two halves in one launch" if bidi else
+           ", both ends: top forward, bottom reversed and bottom fresh in one launch" if bidi_sw else "")
+    return (f"gsa::nw_kscore_kernel<{mode}, {'true' if q8 else 'false'}, {k}> ({mname}{tag})" if krow else
             f"gsa::nw_strip_kernel<4,{mode}> ({mname}, strip kernel)")
 
 

@@ -366,10 +366,18 @@ int sw_idx_bits(int64_t R, int64_t C)
 // best crossing of the rows where they meet.  m = K floor(R/2K), so that row m of the top and row
 // R - m of the reversed bottom are both a lane's last row (the strips' tap); R % K != 0 takes the
 // one-direction path.
+// Local modes (SW) run three pairs: the top half forward, the bottom half reversed, and the bottom
+// half forward from a fresh (zero) border, whose end-cell keys (offset by m rows) share the top's
+// swBest.  The keys then hold the best cell of every alignment that does not cross row m, first in
+// row-major order, and the combine the best score through row m (M_cross).  If M_cross is below
+// that score, or equal to it with the key's cell in the top half (before every crossing end), the
+// key is the answer; otherwise an alignment through row m may end earlier or score more, and the
+// caller runs the one-direction kernel (kBidiFallback).
 constexpr int kScoreTooLargeB = -1001;
+constexpr int kBidiFallback = -1002;
 int score_bidi(gsa_ctx* ctx, const int32_t* seqY, int64_t R, const int32_t* seqX, int64_t C, const int32_t* subst,
                int32_t substsz, int32_t gapo, int32_t gape, int K, bool transposed, gsa_score_result* out,
-               hipStream_t st)
+               hipStream_t st, bool local = false)
 {
     const int64_t TR = (int64_t)(64 * K) * gsa::kSparseNS;
     const bool affine = gapo != gape;
@@ -400,6 +408,7 @@ int score_bidi(gsa_ctx* ctx, const int32_t* seqY, int64_t R, const int32_t* seqX
     }
     const int64_t mb = R - m;
     const int64_t tkTop = (m + TR - 1) / TR, tkBot = (mb + TR - 1) / TR;
+    const int nP = local ? 3 : 2;
     const size_t tapLen = ((size_t)gsa::kTapPad + (size_t)C + 160 + 63) & ~(size_t)63;
     // layout (ints): tap rows H, F of the top, then of the bottom; reversed Y (mb + 1), reversed X
     // (C + 1), the combine's result
@@ -422,12 +431,12 @@ int score_bidi(gsa_ctx* ctx, const int32_t* seqY, int64_t R, const int32_t* seqX
     int* rx = ctx->bidi + oRX;
     int* res = ctx->bidi + oRes;
     int* substT = transposed ? ctx->bidi + oSub : nullptr;
-    int s = ensure_desc(ctx, 2);
+    int s = ensure_desc(ctx, nP);
     if (s != GSA_SUCCESS) return s;
     const size_t stride = (size_t)gsa::gran_stride((int)C);
-    const size_t granAll = (size_t)(tkTop + tkBot) * stride;
+    const size_t granAll = (size_t)(tkTop + (nP - 1) * tkBot) * stride;
     if ((s = ensure_gran(ctx, 2 * granAll, st)) != GSA_SUCCESS) return s;
-    gsa::PairDesc d[2];
+    gsa::PairDesc d[3];
     std::memset(d, 0, sizeof(d));
     d[0].seqY = seqY;
     d[0].seqX = seqX;
@@ -439,8 +448,16 @@ int score_bidi(gsa_ctx* ctx, const int32_t* seqY, int64_t R, const int32_t* seqX
     d[1].R = (int)mb;
     d[1].nTickets = (int)tkBot;
     d[1].granOff = (long long)((size_t)tkTop * stride);
-    for (int h = 0; h < 2; ++h) d[h].C = d[h].Cp = (int)C;
-    const int mode = affine ? gsa::kModeScoreAG : gsa::kModeScoreAGL;
+    // local: the bottom half forward, rows m+1 .. R (seqY + m: its element 0 is row m's letter,
+    // unused), from a fresh border
+    d[2].seqY = seqY + m;
+    d[2].seqX = seqX;
+    d[2].R = (int)mb;
+    d[2].nTickets = (int)tkBot;
+    d[2].granOff = (long long)((size_t)(tkTop + tkBot) * stride);
+    d[2].rowOff = (int)m;
+    for (int h = 0; h < 3; ++h) d[h].C = d[h].Cp = (int)C;
+    const int mode = local ? (affine ? gsa::kModeScoreSW : gsa::kModeScoreSWL) : affine ? gsa::kModeScoreAG : gsa::kModeScoreAGL;
     const int q8env = env_int("GSA_KROW_Q8", 1);
     const int q8 =
         (q8env != 0 && (q8env == 2 || K == 4) && gsa::krow_score_lds_bytes(substsz, true) <= (size_t)ctx->lds_max) ? 1 : 0;
@@ -453,9 +470,11 @@ int score_bidi(gsa_ctx* ctx, const int32_t* seqY, int64_t R, const int32_t* seqX
     a.ge = gape;
     a.ns = gsa::kSparseNS;
     a.pairs = ctx->desc;
-    a.nPairs = 2;
-    a.nTicketsTotal = (int)(tkTop + tkBot);
+    a.nPairs = nP;
+    a.nTicketsTotal = (int)(tkTop + (nP - 1) * tkBot);
     a.bidiTop = (int)tkTop;
+    a.bidiMid = local ? (int)tkBot : 0;
+    a.swBestB = local ? ctx->sctl + 4 : nullptr;  // the reversed half's keys: not read
     a.gran = ctx->gran;
     a.gran2 = ctx->gran + granAll;
     a.ticket = ctx->ctl;
@@ -476,9 +495,8 @@ int score_bidi(gsa_ctx* ctx, const int32_t* seqY, int64_t R, const int32_t* seqX
     a.tapStride = (int)(2 * tapLen);
     (void)hipEventRecord(ctx->ev0, st);
     if ((e = gsa::launch_bidi_prep(d[0], d[1], ctx->desc, seqY, (int)m, (int)R, seqX, (int)C, ry, rx, ctx->ctl, ctx->sctl,
-                                   res, subst, substsz, substT, st)) != hipSuccess ||
-        (e = gsa::launch_krow_score(a, mode, K, std::max(1, std::min((int)(tkTop + tkBot), ctx->cu_count)), st)) !=
-            hipSuccess)
+                                   res, subst, substsz, substT, st, local ? &d[2] : nullptr)) != hipSuccess ||
+        (e = gsa::launch_krow_score(a, mode, K, std::max(1, std::min(a.nTicketsTotal, ctx->cu_count)), st)) != hipSuccess)
         return fail(ctx, e, GSA_ERROR_KERNEL_FAILURE);
     note_launch(ctx);
     // the rows where the halves meet: a lane tap (tap rows, one int per column from kTapPad), or the
@@ -490,7 +508,7 @@ int score_bidi(gsa_ctx* ctx, const int32_t* seqY, int64_t R, const int32_t* seqX
     const int* bH = botFree ? gBot : tapH + 2 * tapLen + gsa::kTapPad;
     const int* bF = botFree ? gBot + 2 * granAll : tapF + 2 * tapLen + gsa::kTapPad;
     if ((e = gsa::launch_bidi_combine(tH, tF, topFree ? 2 : 1, bH, bF, botFree ? 2 : 1, (int)m, (int)mb, (int)C, gapo,
-                                      gape, affine, res, st)) != hipSuccess)
+                                      gape, affine, res, st, local)) != hipSuccess)
         return fail(ctx, e, GSA_ERROR_KERNEL_FAILURE);
     (void)hipEventRecord(ctx->ev1, st);
     unsigned long long rw[4] = {0, 0, 0, 0};
@@ -503,6 +521,25 @@ int score_bidi(gsa_ctx* ctx, const int32_t* seqY, int64_t R, const int32_t* seqX
     const unsigned err = (unsigned)rw[3];
     if (err == 2u) return kScoreTooLargeB;  // a value outside int16: the row scan
     if (err != 0) return GSA_ERROR_KERNEL_FAILURE;
+    if (local)
+    {
+        if (rw[0] & 1u) return kScoreTooLargeB;  // a score >= 2^26: the row scan
+        const int bits = sw_idx_bits(R, C);
+        const unsigned long long mask = (1ull << bits) - 1;
+        const unsigned long long key = rw[1];
+        const unsigned long long idx = key ? mask - (key & mask) : 0;
+        const long long best = key ? (long long)(key >> bits) : 0;
+        const long long ie = (long long)(idx / (unsigned long long)(C + 1));
+        const bool fallback = !((long long)score < best || ((long long)score == best && ie <= m));
+        if (env_int("GSA_BIDI_LOG", 0))  // (tests: which way the pair went)
+            std::fprintf(stderr, "gsa local both ends: m %lld, through m %d, best off it %lld at row %lld -> %s\n",
+                         (long long)m, score, best, ie, fallback ? "one direction" : "answer");
+        if (fallback) return kBidiFallback;
+        out->score = (int32_t)best;
+        out->i_end = ie;
+        out->j_end = (int64_t)(idx % (unsigned long long)(C + 1));
+        return GSA_SUCCESS;
+    }
     out->score = score;
     out->i_end = transposed ? C : R;
     out->j_end = transposed ? R : C;
@@ -541,6 +578,16 @@ int score_ag_strip(gsa_ctx* ctx, const int32_t* seqY, int64_t R, const int32_t* 
         const int sb = tr ? score_bidi(ctx, seqX, C, seqY, R, subst, substsz, gapo, gape, kb, true, out, st)
                           : score_bidi(ctx, seqY, R, seqX, C, subst, substsz, gapo, gape, kb, false, out, st);
         return sb == kScoreTooLargeB ? kScoreTooLarge : sb;
+    }
+    // local: from both ends only by rows (the end cell's row-major tie rule does not survive a
+    // transpose), and back to one direction when an alignment through the split may decide it
+    float bidiMs = 0.f;
+    if (krow && local && bidi != 0 && env_int("GSA_SCORE_BIDI_SW", 1) && splits(R))
+    {
+        const int sb = score_bidi(ctx, seqY, R, seqX, C, subst, substsz, gapo, gape, kb, false, out, st, true);
+        if (sb == kScoreTooLargeB) return kScoreTooLarge;
+        if (sb != kBidiFallback) return sb;
+        bidiMs = out->calc_kernel_ms;
     }
     gsa::StripArgs a;
     std::memset(&a, 0, sizeof(a));
@@ -604,6 +651,7 @@ int score_ag_strip(gsa_ctx* ctx, const int32_t* seqY, int64_t R, const int32_t* 
         return fail(ctx, e, GSA_ERROR_KERNEL_FAILURE);
     const unsigned err = (unsigned)res[3];
     (void)hipEventElapsedTime(&out->calc_kernel_ms, ctx->ev0, ctx->ev1);
+    out->calc_kernel_ms += bidiMs;  // (a local pair back from both ends: both launches)
     // a substitution value outside int16 after the shift: the int32 row scan computes it
     if (err == 2u) return kScoreTooLarge;
     if (err != 0) return GSA_ERROR_KERNEL_FAILURE;

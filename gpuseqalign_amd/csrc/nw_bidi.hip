@@ -14,9 +14,9 @@
 namespace gsa {
 namespace {
 
-__global__ void __launch_bounds__(256) bidi_prep_kernel(PairDesc d0, PairDesc d1, PairDesc* desc, const int* seqY,
-                                                        int m, int R, const int* seqX, int C, int* ry, int* rx,
-                                                        unsigned* ticket, unsigned long long* words, int* out,
+__global__ void __launch_bounds__(256) bidi_prep_kernel(PairDesc d0, PairDesc d1, PairDesc d2, int three, PairDesc* desc,
+                                                        const int* seqY, int m, int R, const int* seqX, int C, int* ry,
+                                                        int* rx, unsigned* ticket, unsigned long long* words, int* out,
                                                         const int* subst, int substsz, int* substT)
 {
     const int t = blockIdx.x * blockDim.x + threadIdx.x, stride = gridDim.x * blockDim.x;
@@ -24,6 +24,7 @@ __global__ void __launch_bounds__(256) bidi_prep_kernel(PairDesc d0, PairDesc d1
     {
         desc[0] = d0;
         desc[1] = d1;
+        if (three) desc[2] = d2;
         ticket[0] = 0;
         for (int k = 0; k < 4; ++k) words[k] = 0;
         out[0] = INT_MIN;
@@ -37,7 +38,7 @@ __global__ void __launch_bounds__(256) bidi_prep_kernel(PairDesc d0, PairDesc d1
 
 __global__ void __launch_bounds__(256) bidi_combine_kernel(const int* topH, const int* topF, int ts, const int* botH,
                                                            const int* botF, int bs, int m, int mb, int C, int go,
-                                                           int ge, int affine, int* out)
+                                                           int ge, int affine, int local, int* out)
 {
     __shared__ int red[256];
     const long long d = (long long)go - ge;
@@ -48,14 +49,28 @@ __global__ void __launch_bounds__(256) bidi_combine_kernel(const int* topH, cons
         // H and F of the forward top at (m, j) and of the reversed bottom at (mb, jb), unshifted
         long long ht, ft, hb, fb;
         if (j == 0)
+        {
             ht = ft = (long long)go + (long long)(m - 1) * ge;
+            if (local)
+            {
+                ht = 0;
+                ft = -(1ll << 40);
+            }
+        }
         else
         {
             ht = (long long)topH[(size_t)ts * j] - d + (long long)(m + j) * ge;
             ft = affine ? (long long)topF[(size_t)ts * j] + (long long)(m + j) * ge : ht;
         }
         if (jb == 0)
+        {
             hb = fb = (long long)go + (long long)(mb - 1) * ge;
+            if (local)
+            {
+                hb = 0;
+                fb = -(1ll << 40);
+            }
+        }
         else
         {
             hb = (long long)botH[(size_t)bs * jb] - d + (long long)(mb + jb) * ge;
@@ -81,21 +96,22 @@ __global__ void __launch_bounds__(256) bidi_combine_kernel(const int* topH, cons
 hipError_t launch_bidi_prep(const PairDesc& d0, const PairDesc& d1, PairDesc* desc, const int* seqY, int m, int R,
                             const int* seqX, int C, int* ry, int* rx, unsigned* ticket,
                             unsigned long long* words, int* out, const int* subst, int substsz, int* substT,
-                            hipStream_t stream)
+                            hipStream_t stream, const PairDesc* d2)
 {
     const int n = (R - m > C ? R - m : C) + 1;
     const int grid = (n + 255) / 256 < 512 ? (n + 255) / 256 : 512;
-    hipLaunchKernelGGL(bidi_prep_kernel, dim3(grid), dim3(256), 0, stream, d0, d1, desc, seqY, m, R, seqX, C, ry, rx,
-                       ticket, words, out, subst, substsz, substT);
+    hipLaunchKernelGGL(bidi_prep_kernel, dim3(grid), dim3(256), 0, stream, d0, d1, d2 ? *d2 : d1, d2 ? 1 : 0, desc, seqY, m,
+                       R, seqX, C, ry, rx, ticket, words, out, subst, substsz, substT);
     return hipGetLastError();
 }
 
 hipError_t launch_bidi_combine(const int* topH, const int* topF, int ts, const int* botH, const int* botF, int bs,
-                               int m, int mb, int C, int go, int ge, bool affine, int* out, hipStream_t stream)
+                               int m, int mb, int C, int go, int ge, bool affine, int* out, hipStream_t stream,
+                               bool local)
 {
     const int grid = (C + 1 + 255) / 256 < 256 ? (C + 1 + 255) / 256 : 256;
     hipLaunchKernelGGL(bidi_combine_kernel, dim3(grid), dim3(256), 0, stream, topH, topF, ts, botH, botF, bs, m, mb, C,
-                       go, ge, affine ? 1 : 0, out);
+                       go, ge, affine ? 1 : 0, local ? 1 : 0, out);
     return hipGetLastError();
 }
 

@@ -1471,7 +1471,8 @@ __device__ __forceinline__ void ks_strip(const StripArgs& a, const KsLds& L, int
             big |= in && best[k] >= (1 << 26);
             if (in && best[k] > 0)
             {
-                const unsigned long long idx = (unsigned long long)(rl + k) * W + (unsigned long long)(tb[k] - lane);
+                const unsigned long long idx =
+                    (unsigned long long)(rl + k + a.rowOff) * W + (unsigned long long)(tb[k] - lane);
                 const unsigned long long kk = ((unsigned long long)best[k] << a.idxBits) | (mask - idx);
                 key = kk > key ? kk : key;
             }
@@ -1788,15 +1789,25 @@ __global__ void __launch_bounds__(64 * kr_waves<kKrowNSDefault>()) nw_kscore_ker
         __syncthreads();
         const int tkg = __builtin_amdgcn_readfirstlane(lds_ld(L.flags + kFTicket));
         if (tkg >= a.nTicketsTotal) break;
-        // one pair (gsa_score), or score_bidi's two halves with their tickets interleaved while both
-        // have some left (each half's tickets are still claimed in order)
+        // one pair (gsa_score), or score_bidi's two (three: local) pairs with their tickets
+        // round-robin while they have some left (each pair's tickets are still claimed in order)
         int h = 0, tk = tkg;
         if (a.bidiTop > 0)
         {
-            // alternate while both halves have tickets, then the longer half's rest
-            const int nA = a.bidiTop, nB = a.nTicketsTotal - a.bidiTop, n = min(nA, nB);
-            h = tkg < 2 * n ? (tkg & 1) : (nA > nB ? 0 : 1);
-            tk = tkg < 2 * n ? (tkg >> 1) : tkg - n;
+            const int n0 = a.bidiTop, n1 = a.bidiMid > 0 ? a.bidiMid : a.nTicketsTotal - n0;
+            const int n2 = a.bidiMid > 0 ? a.nTicketsTotal - n0 - n1 : 0;
+            int g = tkg;
+            for (int r = 0;; ++r)
+            {
+                const int c0 = r < n0, c1 = r < n1, c2 = r < n2;
+                if (g < c0 + c1 + c2)
+                {
+                    h = g == 0 ? (c0 ? 0 : c1 ? 1 : 2) : g == 1 ? (c0 && c1 ? 1 : 2) : 2;
+                    tk = r;
+                    break;
+                }
+                g -= c0 + c1 + c2;
+            }
         }
         const PairDesc d = kr_desc(a.pairs + h);
         StripArgs pa = a;
@@ -1810,12 +1821,16 @@ __global__ void __launch_bounds__(64 * kr_waves<kKrowNSDefault>()) nw_kscore_ker
         pa.gran = a.gran + d.granOff;
         pa.gran2 = a.gran2 + d.granOff;
         pa.tapGran = (a.tapGran >> h) & 1;
-        if (h)
+        pa.rowOff = d.rowOff;
+        if (h == 1)
         {
             pa.tapRow = a.tapRowB;
             pa.tapH = a.tapH + a.tapStride;
             pa.tapF = a.tapF + a.tapStride;
+            if (a.swBestB) pa.swBest = a.swBestB;
         }
+        else if (h == 2)
+            pa.tapRow = 0;
         if (threadIdx.x < 32) lds_st(L.flags + 4u * threadIdx.x, 0);
         // rings: -inf, so columns no writer reaches (past C at the strips' ends) hold nothing larger
         for (int k = threadIdx.x; k < 2 * (NS + 1) * kRing; k += kThreads) lds_st(L.ring + 4u * k, kNegS);
@@ -1832,8 +1847,8 @@ __global__ void __launch_bounds__(64 * kr_waves<kKrowNSDefault>()) nw_kscore_ker
             const int r0 = tk * (64 * K * NS) + 64 * K * w + 1;
             const int rt = pa.tapRow - r0;
             __builtin_amdgcn_s_setprio(3);
-            if (!is_sw_mode(MODE) && pa.tapRow > 0 && rt >= 0 && rt < 64 * K && (rt + 1) % K == 0)
-                ks_strip<MODE, Q8, K, !is_sw_mode(MODE)>(pa, L, tk, w, lane, (rt + 1) / K - 1);
+            if (pa.tapRow > 0 && rt >= 0 && rt < 64 * K && (rt + 1) % K == 0)
+                ks_strip<MODE, Q8, K, true>(pa, L, tk, w, lane, (rt + 1) / K - 1);
             else
                 ks_strip<MODE, Q8, K>(pa, L, tk, w, lane);
             __builtin_amdgcn_s_setprio(0);
@@ -1890,8 +1905,9 @@ size_t krow_score_lds_bytes(int substsz, bool q8) { return (size_t)ks_layout(sub
 
 hipError_t launch_krow_score(const StripArgs& a, int mode, int k, int grid, hipStream_t stream)
 {
-    // one pair, or score_bidi's two halves (bidiTop > 0)
-    if (a.nPairs != (a.bidiTop > 0 ? 2 : 1) || grid <= 0 || (k != 2 && k != 4)) return hipErrorInvalidValue;
+    // one pair, or score_bidi's two halves (bidiTop > 0), three with the fresh bottom (bidiMid > 0)
+    if (a.nPairs != (a.bidiTop > 0 ? (a.bidiMid > 0 ? 3 : 2) : 1) || grid <= 0 || (k != 2 && k != 4))
+        return hipErrorInvalidValue;
     if (mode == kModeScoreAG || mode == kModeScoreSW) return launch_krow_score_affine(a, mode, k, grid, stream);
     if (k == 2)
     {

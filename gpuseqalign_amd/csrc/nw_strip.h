@@ -36,7 +36,8 @@ struct PairDesc
     const int* seqY;
     const int* seqX;
     int R, C, Cp, nTickets;
-    int ticketBase, trows, tcols, pad;
+    int ticketBase, trows, tcols;
+    int rowOff;  // score_bidi, local: the pair's first row - 1 in the whole matrix (the end-cell key)
     int* score;
     long long ld;
     int* hrow;
@@ -133,6 +134,12 @@ struct StripArgs
     // score_bidi: bit h set -> half h's last ticket ends on its tap row, and that ticket's drain
     // writes its granules like any other ticket's (the combine reads the tap there: no lane tap)
     int tapGran;
+    // score_bidi, local: a third pair (bidiMid > 0: pairs[1] has bidiMid tickets, pairs[2] the
+    // rest) runs the bottom half forward from a fresh (zero) border, its end-cell keys offset by
+    // pairs[2].rowOff rows into swBest; the reversed bottom half's keys go to swBestB (unused)
+    int bidiMid;
+    int rowOff;  // per ticket: the pair's rowOff
+    unsigned long long* swBestB;
 };
 constexpr int kTapPad = 128;  // tap row buffers: columns -kTapPad .. C + 79
 

@@ -63,6 +63,7 @@ def test_score_kernel_label(monkeypatch):
     monkeypatch.delenv("GSA_KROW_Q8", raising=False)
     monkeypatch.delenv("GSA_SCORE_K", raising=False)
     monkeypatch.delenv("GSA_SCORE_BIDI", raising=False)
+    monkeypatch.delenv("GSA_SCORE_BIDI_SW", raising=False)
     assert bench.score_kernel_name(-11, -1, False).startswith("gsa::nw_kscore_kernel<3, false, 2>")
     assert bench.score_kernel_name(-11, -11, True).startswith("gsa::nw_kscore_kernel<5, false, 2>")
     # NW at 50k: both ends at 2 rows per lane; one direction for an odd R or a short pair
@@ -71,7 +72,12 @@ def test_score_kernel_label(monkeypatch):
     assert "both ends" in bench.score_kernel_name(-11, -11, False, R=49999)  # transposed
     assert bench.score_kernel_name(-11, -11, False, R=49999, C=49999).startswith("gsa::nw_kscore_kernel<6, true, 4>")
     assert bench.score_kernel_name(-11, -11, False, R=4000, C=4000).startswith("gsa::nw_kscore_kernel<6, true, 4>")
+    # SW: by rows only (three pairs), one direction for an odd R or under GSA_SCORE_BIDI_SW=0
+    assert "bottom fresh" in bench.score_kernel_name(-11, -11, True)
+    assert "both ends" not in bench.score_kernel_name(-11, -11, True, R=49999)
+    monkeypatch.setenv("GSA_SCORE_BIDI_SW", "0")
     assert "both ends" not in bench.score_kernel_name(-11, -11, True)
+    monkeypatch.delenv("GSA_SCORE_BIDI_SW")
     monkeypatch.setenv("GSA_SCORE_BIDI", "0")
     assert bench.score_kernel_name(-11, -11, False).startswith("gsa::nw_kscore_kernel<6, true, 4>")
     monkeypatch.delenv("GSA_SCORE_BIDI")

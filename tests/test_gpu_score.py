@@ -337,3 +337,68 @@ def test_score_both_ends_large_random_shapes(engine, golden, monkeypatch):
         monkeypatch.setenv("GSA_SCORE_BIDI", "0")
         r0 = engine.score(Y, X, golden.blosum62, go, ge, False)
         assert (r1["score"], r1["i_end"], r1["j_end"]) == (r0["score"], r0["i_end"], r0["j_end"]), (case, R, C, go, ge)
+
+
+def _planted(R, C, seed, plants):
+    """A random pair with identical segments planted: plants = [(row, col, length)] (1-based first
+    row / column of the segment in Y / X), so the best local alignments sit where the test wants."""
+    rng = np.random.default_rng(seed)  # (independent streams: random_pair's Y and X overlap when shifted)
+    Y = np.concatenate([[0], rng.integers(0, 20, R)]).astype(np.int32)
+    X = np.concatenate([[0], rng.integers(0, 20, C)]).astype(np.int32)
+    for (r, c, n) in plants:
+        seg = np.random.default_rng(1000 + n).integers(0, 20, n).astype(np.int32)  # equal n: equal segments
+        Y[r:r + n] = seg
+        X[c:c + n] = seg
+    return Y, X
+
+
+@pytest.mark.parametrize("k", ["2", "4"])
+@pytest.mark.parametrize("go,ge", [(-11, -11), (-11, -1), (-5, -2)])
+def test_score_local_both_ends(engine, golden, monkeypatch, capfd, k, go, ge):
+    """SW from both ends (score_bidi, local: top forward, bottom reversed, bottom forward from a
+    fresh border): best alignments planted wholly in the top half, wholly in the bottom, across the
+    split row m (back to one direction), tied in both halves and twice in the bottom (first in
+    row-major), and plain random pairs; every result equals the oracle, and the log names the way
+    each pair went."""
+    import oracle
+    monkeypatch.setenv("GSA_SCORE_BIDI", "2")
+    monkeypatch.setenv("GSA_SCORE_K", k)
+    monkeypatch.setenv("GSA_BIDI_LOG", "1")
+    kk = int(k)
+    R, C = 1600 * kk // 2, 1300
+    m = kk * (R // (2 * kk))
+    cases = [([(100, 200, 60)], "answer"),                       # top half
+             ([(m + 300, 700, 60)], "answer"),                   # bottom half
+             ([(m - 30, 500, 60)], "one direction"),             # across row m
+             # equal segments (tied scores; they also pair across, so either way may be taken)
+             ([(200, 900, 50), (m + 200, 300, 50)], None),
+             ([(m + 100, 1000, 50), (m + 400, 100, 50)], None)]
+    for i, (plants, way) in enumerate(cases):
+        Y, X = _planted(R, C, 40 + i, plants)
+        capfd.readouterr()
+        r = engine.score(Y, X, golden.blosum62, go, ge, True)
+        assert (r["score"], r["i_end"], r["j_end"]) == oracle.score_ag(Y, X, golden.blosum62, go, ge, True), (i, plants)
+        err = capfd.readouterr().err
+        # (at -5/-2 random letters align in the linear regime: long alignments that cross m)
+        assert "gsa local both ends" in err and (way is None or go == -5 or f"-> {way}" in err), (i, plants, err)
+    for R2, C2 in [(2, 1), (4, 5), (130, 700), (1024, 1024), (2052, 257), (4100, 3000)]:
+        R2 -= R2 % kk
+        Y, X = random_pair(R2, C2, 11 * R2 + C2)
+        r = engine.score(Y, X, golden.blosum62, go, ge, True)
+        assert (r["score"], r["i_end"], r["j_end"]) == oracle.score_ag(Y, X, golden.blosum62, go, ge, True), (R2, C2)
+
+
+def test_score_local_both_ends_default_matches_one_direction(engine, golden, monkeypatch):
+    """The default switch on SW (halves of >= 4 tickets, R even): random 6k-20k shapes and a related
+    20k pair (its alignment crosses the split: one direction), against GSA_SCORE_BIDI_SW=0."""
+    rng = np.random.default_rng(91)
+    pairs = [random_pair(int(a) * 2, int(b), 700 + i) for i, (a, b) in enumerate(rng.integers(3000, 10001, (6, 2)))]
+    Yr, Xr = related_pair(20000, 20100)
+    pairs.append((Yr[:len(Yr) - (len(Yr) - 1) % 2], Xr))
+    for Y, X in pairs:
+        for go, ge in [(-11, -11), (-11, -1)]:
+            monkeypatch.delenv("GSA_SCORE_BIDI_SW", raising=False)
+            r1 = engine.score(Y, X, golden.blosum62, go, ge, True)
+            monkeypatch.setenv("GSA_SCORE_BIDI_SW", "0")
+            r0 = engine.score(Y, X, golden.blosum62, go, ge, True)
+            assert (r1["score"], r1["i_end"], r1["j_end"]) == (r0["score"], r0["i_end"], r0["j_end"]), (len(Y), len(X))
