@@ -371,8 +371,11 @@ int sw_idx_bits(int64_t R, int64_t C)
 // swBest.  The keys then hold the best cell of every alignment that does not cross row m, first in
 // row-major order, and the combine the best score through row m (M_cross).  If M_cross is below
 // that score, or equal to it with the key's cell in the top half (before every crossing end), the
-// key is the answer; otherwise an alignment through row m may end earlier or score more, and the
-// caller runs the one-direction kernel (kBidiFallback).
+// key is the answer; otherwise an alignment through row m may end earlier or score more: when the top
+// half ended on a ticket boundary, a second launch continues the pair from its ticket there, its row
+// above the top's last-ticket granules (restamped), and the answer is the better of the top's keys
+// and that run's (GSA_BIDI_SW_CONT=0: not); else the caller runs the one-direction kernel
+// (kBidiFallback).
 constexpr int kScoreTooLargeB = -1001;
 constexpr int kBidiFallback = -1002;
 int score_bidi(gsa_ctx* ctx, const int32_t* seqY, int64_t R, const int32_t* seqX, int64_t C, const int32_t* subst,
@@ -431,11 +434,12 @@ int score_bidi(gsa_ctx* ctx, const int32_t* seqY, int64_t R, const int32_t* seqX
     int* rx = ctx->bidi + oRX;
     int* res = ctx->bidi + oRes;
     int* substT = transposed ? ctx->bidi + oSub : nullptr;
-    int s = ensure_desc(ctx, nP);
+    int s = ensure_desc(ctx, local ? 4 : 2);
     if (s != GSA_SUCCESS) return s;
     const size_t stride = (size_t)gsa::gran_stride((int)C);
     const size_t granAll = (size_t)(tkTop + (nP - 1) * tkBot) * stride;
-    if ((s = ensure_gran(ctx, 2 * granAll, st)) != GSA_SUCCESS) return s;
+    const int64_t tkAll = (R + TR - 1) / TR;  // local, the way back: the whole pair's tickets
+    if ((s = ensure_gran(ctx, 2 * granAll + (local ? 2 * (size_t)tkAll * stride : 0), st)) != GSA_SUCCESS) return s;
     gsa::PairDesc d[3];
     std::memset(d, 0, sizeof(d));
     d[0].seqY = seqY;
@@ -456,6 +460,13 @@ int score_bidi(gsa_ctx* ctx, const int32_t* seqY, int64_t R, const int32_t* seqX
     d[2].nTickets = (int)tkBot;
     d[2].granOff = (long long)((size_t)(tkTop + tkBot) * stride);
     d[2].rowOff = (int)m;
+    // local: keys of the top (StripArgs::swBest, word 1), of the reversed bottom (word 4, unused) and
+    // of the fresh bottom (word 5)
+    if (local)
+    {
+        d[1].swBest = ctx->sctl + 4;
+        d[2].swBest = ctx->sctl + 5;
+    }
     for (int h = 0; h < 3; ++h) d[h].C = d[h].Cp = (int)C;
     const int mode = local ? (affine ? gsa::kModeScoreSW : gsa::kModeScoreSWL) : affine ? gsa::kModeScoreAG : gsa::kModeScoreAGL;
     const int q8env = env_int("GSA_KROW_Q8", 1);
@@ -474,7 +485,6 @@ int score_bidi(gsa_ctx* ctx, const int32_t* seqY, int64_t R, const int32_t* seqX
     a.nTicketsTotal = (int)(tkTop + (nP - 1) * tkBot);
     a.bidiTop = (int)tkTop;
     a.bidiMid = local ? (int)tkBot : 0;
-    a.swBestB = local ? ctx->sctl + 4 : nullptr;  // the reversed half's keys: not read
     a.gran = ctx->gran;
     a.gran2 = ctx->gran + granAll;
     a.ticket = ctx->ctl;
@@ -511,7 +521,7 @@ int score_bidi(gsa_ctx* ctx, const int32_t* seqY, int64_t R, const int32_t* seqX
                                       gape, affine, res, st, local)) != hipSuccess)
         return fail(ctx, e, GSA_ERROR_KERNEL_FAILURE);
     (void)hipEventRecord(ctx->ev1, st);
-    unsigned long long rw[4] = {0, 0, 0, 0};
+    unsigned long long rw[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     int score = 0;
     if ((e = hipMemcpyAsync(rw, ctx->sctl, sizeof(rw), hipMemcpyDeviceToHost, st)) != hipSuccess ||
         (e = hipMemcpyAsync(&score, res, sizeof(int), hipMemcpyDeviceToHost, st)) != hipSuccess ||
@@ -526,17 +536,70 @@ int score_bidi(gsa_ctx* ctx, const int32_t* seqY, int64_t R, const int32_t* seqX
         if (rw[0] & 1u) return kScoreTooLargeB;  // a score >= 2^26: the row scan
         const int bits = sw_idx_bits(R, C);
         const unsigned long long mask = (1ull << bits) - 1;
-        const unsigned long long key = rw[1];
-        const unsigned long long idx = key ? mask - (key & mask) : 0;
-        const long long best = key ? (long long)(key >> bits) : 0;
+        unsigned long long key = std::max(rw[1], rw[5]);  // top, fresh bottom
+        unsigned long long idx = key ? mask - (key & mask) : 0;
+        long long best = key ? (long long)(key >> bits) : 0;
         const long long ie = (long long)(idx / (unsigned long long)(C + 1));
         const bool fallback = !((long long)score < best || ((long long)score == best && ie <= m));
+        const bool cont = fallback && topFree && env_int("GSA_BIDI_SW_CONT", 1) != 0;
         if (env_int("GSA_BIDI_LOG", 0))  // (tests: which way the pair went)
             std::fprintf(stderr, "gsa local both ends: m %lld, through m %d, best off it %lld at row %lld -> %s\n",
-                         (long long)m, score, best, ie, fallback ? "one direction" : "answer");
-        if (fallback) return kBidiFallback;
+                         (long long)m, score, best, ie,
+                         !fallback ? "answer" : cont ? "bottom again from row m" : "one direction");
+        if (fallback && !cont) return kBidiFallback;
+        if (cont)
+        {
+            // the pair from ticket tkTop on, its row above the top's last-ticket granules, in a granule
+            // area of its own (its later tickets must not meet another half's granules)
+            unsigned long long* seedH = ctx->gran + 2 * granAll;
+            unsigned long long* seedF = seedH + (size_t)tkAll * stride;
+            unsigned ep2 = ++ctx->epoch;
+            if (ep2 == 0) ep2 = ++ctx->epoch;
+            const size_t last = (size_t)(tkTop - 1) * stride;
+            gsa::PairDesc dc;
+            std::memset(&dc, 0, sizeof(dc));
+            dc.seqY = seqY;
+            dc.seqX = seqX;
+            dc.R = (int)R;
+            dc.C = dc.Cp = (int)C;
+            dc.nTickets = (int)tkAll;
+            dc.swBest = ctx->sctl + 6;
+            gsa::StripArgs b = a;
+            b.pairs = ctx->desc + 3;
+            b.nPairs = 1;
+            b.bidiTop = b.bidiMid = 0;
+            b.nTicketsTotal = (int)(tkAll - tkTop);
+            b.tkFirst = (int)tkTop;
+            b.gran = seedH;
+            b.gran2 = seedF;
+            b.epoch = ep2;
+            b.tapRow = b.tapRowB = b.tapGran = 0;
+            if ((e = hipMemcpyAsync(ctx->desc + 3, &dc, sizeof(dc), hipMemcpyHostToDevice, st)) != hipSuccess ||
+                (e = hipMemsetAsync(ctx->ctl, 0, 4, st)) != hipSuccess ||
+                (e = hipMemsetAsync(ctx->sctl, 0, 8, st)) != hipSuccess ||
+                (e = hipMemsetAsync(ctx->sctl + 6, 0, 8, st)) != hipSuccess)
+                return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
+            if ((e = gsa::launch_bidi_seed(ctx->gran + last, affine ? ctx->gran + granAll + last : nullptr, seedH + last,
+                                           affine ? seedF + last : nullptr, (long long)stride, ep2, st)) != hipSuccess ||
+                (e = gsa::launch_krow_score(b, mode, K, std::max(1, std::min(b.nTicketsTotal, ctx->cu_count)), st)) !=
+                    hipSuccess)
+                return fail(ctx, e, GSA_ERROR_KERNEL_FAILURE);
+            note_launch(ctx);
+            (void)hipEventRecord(ctx->ev1, st);
+            if ((e = hipMemcpyAsync(rw, ctx->sctl, sizeof(rw), hipMemcpyDeviceToHost, st)) != hipSuccess ||
+                (e = hipStreamSynchronize(st)) != hipSuccess)
+                return fail(ctx, e, GSA_ERROR_KERNEL_FAILURE);
+            (void)hipEventElapsedTime(&out->calc_kernel_ms, ctx->ev0, ctx->ev1);
+            const unsigned err2 = (unsigned)rw[3];
+            if (err2 == 2u) return kScoreTooLargeB;
+            if (err2 != 0) return GSA_ERROR_KERNEL_FAILURE;
+            if (rw[0] & 1u) return kScoreTooLargeB;
+            key = std::max(rw[1], rw[6]);  // the top's keys (word 1 is not touched again), the rest's
+            idx = key ? mask - (key & mask) : 0;
+            best = key ? (long long)(key >> bits) : 0;
+        }
         out->score = (int32_t)best;
-        out->i_end = ie;
+        out->i_end = (int64_t)(idx / (unsigned long long)(C + 1));
         out->j_end = (int64_t)(idx % (unsigned long long)(C + 1));
         return GSA_SUCCESS;
     }

@@ -11,7 +11,7 @@ namespace gsa {
 
 // One launch before the fill: desc[0..1] = d0, d1; ry[0] = rx[0] = 0, ry[i] = seqY[R + 1 - i]
 // (i = 1 .. R - m: rows m+1 .. R reversed), rx[j] = seqX[C + 1 - j]; the launch's ticket word, its
-// 4 result / error words and the combine's output (-2^31) reset; substT non-null: substT[x][y] =
+// 8 result / error words and the combine's output (-2^31) reset; substT non-null: substT[x][y] =
 // subst[y][x] (substsz x substsz; the pair transposed, when R is odd and C even); d2 non-null (local
 // modes): desc[2] = *d2, the bottom half forward from a fresh border.
 hipError_t launch_bidi_prep(const PairDesc& d0, const PairDesc& d1, PairDesc* desc, const int* seqY, int m, int R,
@@ -27,6 +27,12 @@ hipError_t launch_bidi_prep(const PairDesc& d0, const PairDesc& d1, PairDesc* de
 // F = -inf; the sum is then the best local alignment through the lattice point (m, j), which
 // includes those that end or start there).  Many workgroups, each folding its columns into out[0]
 // with an atomic max (out[0] starts at -2^31, launch_bidi_prep).
+// The way back of a local pair (score_bidi): dst[c] = epoch << 32 | low word of src[c], c < n, and
+// likewise dst2 from src2 when non-null (the top half's last-ticket granules, restamped for the
+// continuation launch, which reads them as its first ticket's row above).
+hipError_t launch_bidi_seed(const unsigned long long* src, const unsigned long long* src2, unsigned long long* dst,
+                            unsigned long long* dst2, long long n, unsigned epoch, hipStream_t stream);
+
 hipError_t launch_bidi_combine(const int* topH, const int* topF, int ts, const int* botH, const int* botF, int bs,
                                int m, int mb, int C, int go, int ge, bool affine, int* out, hipStream_t stream,
                                bool local = false);

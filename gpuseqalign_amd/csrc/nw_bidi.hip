@@ -26,7 +26,7 @@ __global__ void __launch_bounds__(256) bidi_prep_kernel(PairDesc d0, PairDesc d1
         desc[1] = d1;
         if (three) desc[2] = d2;
         ticket[0] = 0;
-        for (int k = 0; k < 4; ++k) words[k] = 0;
+        for (int k = 0; k < 8; ++k) words[k] = 0;
         out[0] = INT_MIN;
     }
     const int mb = R - m;
@@ -91,7 +91,28 @@ __global__ void __launch_bounds__(256) bidi_combine_kernel(const int* topH, cons
     if (threadIdx.x == 0) atomicMax(out, red[0]);
 }
 
+__global__ void __launch_bounds__(256) bidi_seed_kernel(const unsigned long long* src, const unsigned long long* src2,
+                                                        unsigned long long* dst, unsigned long long* dst2, long long n,
+                                                        unsigned epoch)
+{
+    const unsigned long long ep = (unsigned long long)epoch << 32;
+    for (long long c = blockIdx.x * (long long)blockDim.x + threadIdx.x; c < n; c += (long long)gridDim.x * blockDim.x)
+    {
+        dst[c] = ep | (src[c] & 0xffffffffull);
+        if (dst2) dst2[c] = ep | (src2[c] & 0xffffffffull);
+    }
+}
+
 }  // namespace
+
+hipError_t launch_bidi_seed(const unsigned long long* src, const unsigned long long* src2, unsigned long long* dst,
+                            unsigned long long* dst2, long long n, unsigned epoch, hipStream_t stream)
+{
+    const long long g = (n + 255) / 256;
+    hipLaunchKernelGGL(bidi_seed_kernel, dim3(g < 256 ? (unsigned)g : 256u), dim3(256), 0, stream, src, src2, dst, dst2, n,
+                       epoch);
+    return hipGetLastError();
+}
 
 hipError_t launch_bidi_prep(const PairDesc& d0, const PairDesc& d1, PairDesc* desc, const int* seqY, int m, int R,
                             const int* seqX, int C, int* ry, int* rx, unsigned* ticket,

@@ -1791,7 +1791,7 @@ __global__ void __launch_bounds__(64 * kr_waves<kKrowNSDefault>()) nw_kscore_ker
         if (tkg >= a.nTicketsTotal) break;
         // one pair (gsa_score), or score_bidi's two (three: local) pairs with their tickets
         // round-robin while they have some left (each pair's tickets are still claimed in order)
-        int h = 0, tk = tkg;
+        int h = 0, tk = tkg + a.tkFirst;
         if (a.bidiTop > 0)
         {
             const int n0 = a.bidiTop, n1 = a.bidiMid > 0 ? a.bidiMid : a.nTicketsTotal - n0;
@@ -1822,12 +1822,12 @@ __global__ void __launch_bounds__(64 * kr_waves<kKrowNSDefault>()) nw_kscore_ker
         pa.gran2 = a.gran2 + d.granOff;
         pa.tapGran = (a.tapGran >> h) & 1;
         pa.rowOff = d.rowOff;
+        if (d.swBest) pa.swBest = d.swBest;
         if (h == 1)
         {
             pa.tapRow = a.tapRowB;
             pa.tapH = a.tapH + a.tapStride;
             pa.tapF = a.tapF + a.tapStride;
-            if (a.swBestB) pa.swBest = a.swBestB;
         }
         else if (h == 2)
             pa.tapRow = 0;

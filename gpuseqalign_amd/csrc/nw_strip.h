@@ -38,6 +38,7 @@ struct PairDesc
     int R, C, Cp, nTickets;
     int ticketBase, trows, tcols;
     int rowOff;  // score_bidi, local: the pair's first row - 1 in the whole matrix (the end-cell key)
+    unsigned long long* swBest;  // score_bidi, local: this pair's end-cell keys (null: StripArgs::swBest)
     int* score;
     long long ld;
     int* hrow;
@@ -136,10 +137,12 @@ struct StripArgs
     int tapGran;
     // score_bidi, local: a third pair (bidiMid > 0: pairs[1] has bidiMid tickets, pairs[2] the
     // rest) runs the bottom half forward from a fresh (zero) border, its end-cell keys offset by
-    // pairs[2].rowOff rows into swBest; the reversed bottom half's keys go to swBestB (unused)
+    // pairs[2].rowOff rows; each pair's keys go to its PairDesc::swBest
     int bidiMid;
     int rowOff;  // per ticket: the pair's rowOff
-    unsigned long long* swBestB;
+    // score_bidi, local, the way back: a one-pair launch that starts at the pair's ticket tkFirst,
+    // its row above in that ticket's predecessor's granules (copied there with this epoch)
+    int tkFirst;
 };
 constexpr int kTapPad = 128;  // tap row buffers: columns -kTapPad .. C + 79
 

@@ -402,3 +402,37 @@ def test_score_local_both_ends_default_matches_one_direction(engine, golden, mon
             monkeypatch.setenv("GSA_SCORE_BIDI_SW", "0")
             r0 = engine.score(Y, X, golden.blosum62, go, ge, True)
             assert (r1["score"], r1["i_end"], r1["j_end"]) == (r0["score"], r0["i_end"], r0["j_end"]), (len(Y), len(X))
+
+
+@pytest.mark.parametrize("k", ["2", "4"])
+@pytest.mark.parametrize("go,ge", [(-11, -11), (-11, -1)])
+def test_score_local_both_ends_continuation(engine, golden, monkeypatch, capfd, k, go, ge):
+    """SW from both ends whose best alignment crosses the split, on a pair long enough for the top half
+    to end on a ticket boundary: the way back continues the pair from that ticket in a second launch
+    (its row above the top's last-ticket granules, restamped) instead of the whole one-direction run;
+    crossing alignments planted at three places around the split row and one in the bottom only,
+    equal to the oracle, and the log shows the way taken (GSA_BIDI_SW_CONT=0: the whole run again,
+    same result)."""
+    import oracle
+    monkeypatch.setenv("GSA_SCORE_K", k)
+    monkeypatch.setenv("GSA_BIDI_LOG", "1")
+    kk = int(k)
+    R, C = 3000 * kk, 1500
+    for i, (dr, way) in enumerate([(-40, "bottom again"), (-5, "bottom again"), (-75, "bottom again"),
+                                   (900, "answer")]):
+        capfd.readouterr()
+        monkeypatch.delenv("GSA_BIDI_SW_CONT", raising=False)
+        Y, X = _planted(R, C, 60 + i, [(0, 0, 0)])
+        r = engine.score(Y, X, golden.blosum62, go, ge, True)
+        assert (r["score"], r["i_end"], r["j_end"]) == oracle.score_ag(Y, X, golden.blosum62, go, ge, True), i
+        m = int(capfd.readouterr().err.split(" m ")[1].split(",")[0])
+        Y, X = _planted(R, C, 60 + i, [(m + dr, 400 + 100 * i, 80)])
+        ref = oracle.score_ag(Y, X, golden.blosum62, go, ge, True)
+        r = engine.score(Y, X, golden.blosum62, go, ge, True)
+        err = capfd.readouterr().err
+        assert (r["score"], r["i_end"], r["j_end"]) == ref, (i, m, err)
+        assert f"-> {way}" in err, (i, m, err)
+        monkeypatch.setenv("GSA_BIDI_SW_CONT", "0")
+        r0 = engine.score(Y, X, golden.blosum62, go, ge, True)
+        assert (r0["score"], r0["i_end"], r0["j_end"]) == ref, (i, m)
+        assert ("-> one direction" if way != "answer" else "-> answer") in capfd.readouterr().err, (i, m)

@@ -29,8 +29,9 @@ for name, (Y, X) in (("related", (yr, x)), ("random", (yrand, xrand))):
     ty, tx = torch.from_numpy(np.ascontiguousarray(Y, dtype=np.int32)).to(dev), torch.from_numpy(np.ascontiguousarray(X, dtype=np.int32)).to(dev)
     for go, ge in ((-11, -11), (-11, -1)):
         line = []
-        for label, env in (("one direction", {"GSA_SCORE_BIDI_SW": "0"}), ("both ends", {})):
-            for k in ("GSA_SCORE_BIDI_SW",):
+        for label, env in (("one direction", {"GSA_SCORE_BIDI_SW": "0"}), ("both ends", {}),
+                           ("both ends, whole rerun", {"GSA_BIDI_SW_CONT": "0"})):
+            for k in ("GSA_SCORE_BIDI_SW", "GSA_BIDI_SW_CONT"):
                 os.environ.pop(k, None)
             os.environ.update(env)
             res = None
