@@ -273,14 +273,17 @@ int gsa_trace_sparse_dev(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, con
  * from it) before its launch; the score kernels report errors in a control word of their own, so
  * the fills' sticky error word is left for the caller's gsa_sync.  Global scores of long pairs run
  * from both ends (the top rows forward, the bottom rows reversed, in one launch; the pair
- * transposed when only adjcols-1 suits the split): same results, context scratch grows by
- * ~4 (adjcols + adjrows) ints. */
+ * transposed when only adjcols-1 suits the split); local ones too, by rows only, with a third
+ * pair (the bottom rows forward from a fresh border) for the end cell and a second launch when
+ * an alignment through the split row decides the result: same results, context scratch grows by
+ * ~4 (adjcols + adjrows) ints and, local, by the granules of one more pass. */
 typedef struct gsa_score_result
 {
     int32_t score;
     int64_t i_end, j_end;  /* local: where the maximum first occurs; global: (adjrows-1, adjcols-1) */
-    float calc_kernel_ms;  /* hipEvent time of the fill: for global scores split in two halves (NW
-                            * from both ends) the prep, fill and combine kernels */
+    float calc_kernel_ms;  /* hipEvent time of the fill: for scores split in two halves (from both
+                            * ends) the prep, fill and combine kernels, and a local
+                            * pair's second launch when it needed one */
 } gsa_score_result;
 int gsa_score_dev(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, const int32_t* seqX, int32_t adjcols,
                   const int32_t* subst, int32_t substsz, int32_t gapo, int32_t gape, int32_t local,
