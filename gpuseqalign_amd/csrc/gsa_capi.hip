@@ -397,7 +397,9 @@ int score_bidi(gsa_ctx* ctx, const int32_t* seqY, int64_t R, const int32_t* seqX
     if (R >= 4 * TR && env_int("GSA_BIDI_GRAN", 1))
     {
         const int skewEnv = env_int("GSA_BIDI_SKEW", -1);
-        const double p = affine ? 0.117 : 0.05;
+        // (local linear: 0.075, the third pair's share of the chip moves the balance; 50k SW-LG
+        // 2.78 -> 2.76 ms, profiles/r05_sw_skew.txt)
+        const double p = affine ? 0.117 : local ? 0.075 : 0.05;
         const bool both = R % TR == 0;
         const int64_t skew = both ? 0 : skewEnv >= 0 ? skewEnv : (int64_t)(p * (double)C * 64.0 * K / (2.0 * 96.0));
         int64_t mt = TR * (int64_t)llround((double)(R / 2 + skew) / (double)TR);
