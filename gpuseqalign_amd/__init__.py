@@ -157,6 +157,12 @@ SIGNATURES = {
                                             _vp, _vp, ctypes.POINTER(CheckResult), _vp]),
     "gsa_check_full_dev": (ctypes.c_int, [_vp, _vp, _i32, _vp, _i32, _vp, _i32, _i32, _vp,
                                           ctypes.POINTER(CheckResult), _vp]),
+    "gsa_check_full_pitched_dev": (ctypes.c_int, [_vp, _vp, _i32, _vp, _i32, _vp, _i32, _i32, _vp, _i32,
+                                                  ctypes.POINTER(CheckResult), _vp]),
+    "gsa_hash_full_dev": (ctypes.c_int, [_vp, _vp, _i32, _i32, _i32, ctypes.POINTER(ctypes.c_uint32), _vp]),
+    "gsa_trace_full_dev": (ctypes.c_int, [_vp, _vp, _i32, _vp, _i32, _vp, _i32, ctypes.c_char_p, _i64,
+                                          ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_uint32), _i32p,
+                                          _vp]),
     "gsa_score_dev": (ctypes.c_int, [_vp, _vp, _i32, _vp, _i32, _vp, _i32, _i32, _i32, _i32,
                                      ctypes.POINTER(ScoreResult), _vp]),
     "gsa_score": (ctypes.c_int, [_vp, _i32p, _i32, _i32p, _i32, _i32p, _i32, _i32, _i32, _i32,
@@ -455,13 +461,44 @@ class Engine:
         return int(h.value), buf.raw[:n.value].decode(), int(cost.value)
 
     def check_full_dev(self, seqY_ptr: int, adjrows: int, seqX_ptr: int, adjcols: int, subst_ptr: int,
-                       substsz: int, gapo: int, score_ptr: int, stream: Optional[int] = None) -> dict:
-        """Every cell of a full matrix against its stored neighbours; synchronous."""
+                       substsz: int, gapo: int, score_ptr: int, stream: Optional[int] = None,
+                       ld: Optional[int] = None) -> dict:
+        """Every cell of a full matrix against its stored neighbours; synchronous.  ld: row pitch
+        (None: unpadded)."""
         r = CheckResult()
-        st = lib().gsa_check_full_dev(self._h, seqY_ptr, adjrows, seqX_ptr, adjcols, subst_ptr, substsz, gapo,
-                                      score_ptr, ctypes.byref(r), stream)
-        self._check(st, "gsa_check_full_dev")
+        if ld is None:
+            st = lib().gsa_check_full_dev(self._h, seqY_ptr, adjrows, seqX_ptr, adjcols, subst_ptr, substsz, gapo,
+                                          score_ptr, ctypes.byref(r), stream)
+        else:
+            st = lib().gsa_check_full_pitched_dev(self._h, seqY_ptr, adjrows, seqX_ptr, adjcols, subst_ptr, substsz,
+                                                  gapo, score_ptr, int(ld), ctypes.byref(r), stream)
+        self._check(st, "gsa_check_full_dev" if ld is None else "gsa_check_full_pitched_dev")
         return r.as_dict()
+
+    def hash_full_dev(self, score_ptr: int, adjrows: int, adjcols: int, ld: Optional[int] = None,
+                      stream: Optional[int] = None) -> int:
+        """NwHash1_Plain of a device-resident full matrix (gsa_hash_full_dev); equals hash_full()
+        of its host copy."""
+        h = ctypes.c_uint32(0)
+        st = lib().gsa_hash_full_dev(self._h, score_ptr, adjrows, adjcols, adjcols if ld is None else int(ld),
+                                     ctypes.byref(h), stream)
+        self._check(st, "gsa_hash_full_dev")
+        return int(h.value)
+
+    def trace_full_dev(self, seqY_ptr: int, adjrows: int, seqX_ptr: int, adjcols: int, score_ptr: int,
+                       ld: Optional[int] = None, stream: Optional[int] = None) -> Tuple[int, str, int]:
+        """NwTrace1_Plain of a device-resident full matrix (gsa_trace_full_dev): (trace_hash, edit
+        string, align_cost), equal to trace_full() of its host copy."""
+        cap = 8 * (adjrows + adjcols) + 64
+        buf = ctypes.create_string_buffer(cap)
+        n = ctypes.c_int64(0)
+        h = ctypes.c_uint32(0)
+        cost = ctypes.c_int32(0)
+        st = lib().gsa_trace_full_dev(self._h, seqY_ptr, adjrows, seqX_ptr, adjcols, score_ptr,
+                                      adjcols if ld is None else int(ld), buf, cap, ctypes.byref(n), ctypes.byref(h),
+                                      ctypes.byref(cost), stream)
+        self._check(st, "gsa_trace_full_dev")
+        return int(h.value), buf.raw[:n.value].decode(), int(cost.value)
 
 
 # ---- host consumers (the reference's L4) ----------------------------------------------

@@ -1291,7 +1291,9 @@ int enqueue_full_twopass(gsa_ctx* ctx, int npairs, const gsa_pair_dev* pairs, co
     const int fusedMode = env_int("GSA_FULL_FUSED", 1);
     bool interior = true;
     for (int p = 0; p < npairs; ++p) interior = interior && pairs[p].adjrows > 1 && pairs[p].adjcols > 1;
-    const bool fused = interior && (npairs == 1 ? fusedMode >= 1 : fusedMode >= 2);
+    // (never inside a split batch: a group of one pair would take the fused branch, which records
+    // neither afterP1 nor timeP1, and group B would then start against an unrecorded event)
+    const bool fused = interior && !opt.split && (npairs == 1 ? fusedMode >= 1 : fusedMode >= 2);
     // GSA_FULL_PIPE = G >= 2: pass 1 pipelined beside the expansion in G pair groups
     // (enqueue_full_pipelined).  Measured slower, so off by default: the 12-wave expansion that leaves
     // room for pass 1 is 14 % slower than the 16-wave one alone, and the co-resident pass 1 costs it
@@ -2331,7 +2333,166 @@ int gsa_check_full_dev(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, const
     a.adjrows = adjrows;
     a.adjcols = adjcols;
     a.score = score;
+    a.ld = adjcols;
     return run_check(ctx, a, false, pick_stream(ctx, stream), out);
+}
+
+int gsa_check_full_pitched_dev(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, const int32_t* seqX,
+                               int32_t adjcols, const int32_t* subst, int32_t substsz, int32_t gapo,
+                               const int32_t* score, int32_t ld, gsa_check_result* out, void* stream)
+{
+    if (!ctx || !seqY || !seqX || !subst || !score || !out) return GSA_ERROR_INVALID_VALUE;
+    int s = check_inputs(adjrows, adjcols, substsz);
+    if (s != GSA_SUCCESS) return s;
+    if (ld < adjcols) return GSA_ERROR_INVALID_VALUE;
+    gsa::CheckArgs a {};
+    a.seqY = seqY;
+    a.seqX = seqX;
+    a.subst = subst;
+    a.substsz = substsz;
+    a.g = gapo;
+    a.adjrows = adjrows;
+    a.adjcols = adjcols;
+    a.score = score;
+    a.ld = ld;
+    return run_check(ctx, a, false, pick_stream(ctx, stream), out);
+}
+
+// NwHash1_Plain (nwtrace1_plain.cpp:133-154) over a matrix that stays in HBM.  djb2-xor is one serial
+// chain over every cell in row-major order, so the host folds it while the DMA brings the next rows:
+// row chunks (~64 MB, unpadded) alternate between two pinned buffers on the context's copy stream.
+int gsa_hash_full_dev(gsa_ctx* ctx, const int32_t* score, int32_t adjrows, int32_t adjcols, int32_t ld,
+                      uint32_t* hash, void* stream)
+{
+    if (!ctx || !score || !hash || adjrows < 1 || adjcols < 1 || ld < adjcols) return GSA_ERROR_INVALID_VALUE;
+    hipError_t e = hipSetDevice(ctx->device);
+    const hipStream_t st = pick_stream(ctx, stream);
+    // (the caller's work on `stream` first: the matrix may still be being filled)
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
+    const int64_t rowsPer = std::max<int64_t>(1, ((int64_t)16 << 20) / adjcols);
+    const int64_t nChunks = (adjrows + rowsPer - 1) / rowsPer;
+    const size_t bufBytes = (size_t)std::min<int64_t>(rowsPer, adjrows) * (size_t)adjcols * 4;
+    void* buf[2] = {nullptr, nullptr};
+    hipEvent_t ev[2] = {nullptr, nullptr};
+    int rc = GSA_SUCCESS;
+    for (int k = 0; k < 2 && e == hipSuccess; ++k)
+    {
+        e = hipHostMalloc(&buf[k], bufBytes, hipHostMallocDefault);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&ev[k], hipEventDisableTiming);
+    }
+    auto issue = [&](int64_t c) {
+        const int64_t r0 = c * rowsPer, n = std::min<int64_t>(rowsPer, adjrows - r0);
+        hipError_t q = hipMemcpy2DAsync(buf[c & 1], (size_t)adjcols * 4, score + r0 * (int64_t)ld, (size_t)ld * 4,
+                                        (size_t)adjcols * 4, (size_t)n, hipMemcpyDeviceToHost, st);
+        return q == hipSuccess ? hipEventRecord(ev[c & 1], st) : q;
+    };
+    uint32_t h = 5381;
+    if (e == hipSuccess) e = issue(0);
+    for (int64_t c = 0; e == hipSuccess && c < nChunks; ++c)
+    {
+        if (c + 1 < nChunks && (e = issue(c + 1)) != hipSuccess) break;
+        if ((e = hipEventSynchronize(ev[c & 1])) != hipSuccess) break;
+        const uint32_t* v = (const uint32_t*)buf[c & 1];
+        const int64_t n = std::min<int64_t>(rowsPer, adjrows - c * rowsPer) * adjcols;
+        for (int64_t k = 0; k < n; ++k) h = ((h << 5) + h) ^ v[k];
+    }
+    if (e != hipSuccess)
+    {
+        (void)hipStreamSynchronize(st);
+        rc = fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
+    }
+    for (int k = 0; k < 2; ++k)
+    {
+        if (buf[k]) (void)hipHostFree(buf[k]);
+        if (ev[k]) (void)hipEventDestroy(ev[k]);
+    }
+    if (rc == GSA_SUCCESS) *hash = h;
+    return rc;
+}
+
+// NwTrace1_Plain (nwtrace1_plain.cpp:6-131) over a matrix that stays in HBM.  The walk reads three
+// stored neighbours per move; it runs on the host over blocks of the matrix copied on demand
+// (kTB rows x kTC columns ending at the walk's position, so a walk up and to the left stays inside
+// a block for up to kTB / kTC moves), and its moves are folded as the device Trace2's are.
+int gsa_trace_full_dev(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, const int32_t* seqX, int32_t adjcols,
+                       const int32_t* score, int32_t ld, char* edit, int64_t cap, int64_t* edit_len,
+                       uint32_t* trace_hash, int32_t* align_cost, void* stream)
+{
+    if (!ctx || !seqY || !seqX || !score || !edit || !edit_len || !trace_hash || adjrows < 1 || adjcols < 1 ||
+        ld < adjcols)
+        return GSA_ERROR_INVALID_VALUE;
+    constexpr int64_t kTB = 1024, kTC = 2048;
+    hipError_t e = hipSetDevice(ctx->device);
+    const hipStream_t st = pick_stream(ctx, stream);
+    std::vector<int32_t> Y((size_t)adjrows), X((size_t)adjcols);
+    if (e == hipSuccess) e = hipMemcpyAsync(Y.data(), seqY, (size_t)adjrows * 4, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(X.data(), seqX, (size_t)adjcols * 4, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
+    int32_t* blk = nullptr;
+    if ((e = hipHostMalloc((void**)&blk, (size_t)(kTB * kTC) * 4, hipHostMallocDefault)) != hipSuccess)
+        return fail(ctx, e, GSA_ERROR_MEMORY_ALLOCATION);
+    int64_t bi0 = -1, bj0 = 0, bh = 0, bw = 0;  // the block held: rows [bi0, bi0 + bh), columns [bj0, bj0 + bw)
+    // make rows i-1..i and columns j-1..j resident (a block ending at (i, j))
+    auto fetch = [&](int64_t i, int64_t j) {
+        const int64_t i0 = std::max<int64_t>(0, i - kTB + 1), j0 = std::max<int64_t>(0, j - kTC + 1);
+        const int64_t h = std::min<int64_t>(kTB, adjrows - i0), w = std::min<int64_t>(kTC, adjcols - j0);
+        hipError_t q = hipMemcpy2DAsync(blk, (size_t)w * 4, score + i0 * (int64_t)ld + j0, (size_t)ld * 4,
+                                        (size_t)w * 4, (size_t)h, hipMemcpyDeviceToHost, st);
+        if (q == hipSuccess) q = hipStreamSynchronize(st);
+        bi0 = i0;
+        bj0 = j0;
+        bh = h;
+        bw = w;
+        return q;
+    };
+    auto held = [&](int64_t i, int64_t j) {
+        const int64_t ilo = i > 0 ? i - 1 : 0, jlo = j > 0 ? j - 1 : 0;
+        return bi0 >= 0 && ilo >= bi0 && i < bi0 + bh && jlo >= bj0 && j < bj0 + bw;
+    };
+    auto at = [&](int64_t i, int64_t j) { return blk[(i - bi0) * bw + (j - bj0)]; };
+    std::vector<unsigned char> moves;
+    moves.reserve((size_t)(adjrows + adjcols));
+    int64_t i = adjrows - 1, j = adjcols - 1;
+    int32_t cost = 0;
+    for (bool first = true; e == hipSuccess; first = false)
+    {
+        if (!held(i, j) && (e = fetch(i, j)) != hipSuccess) break;
+        if (first) cost = at(i, j);
+        // the reference's order: diagonal, then up if strictly greater, then left if strictly greater
+        int64_t best = INT64_MIN;
+        int di = 0, dj = 0;
+        unsigned char m = 0;
+        if (i > 0 && j > 0)
+        {
+            best = at(i - 1, j - 1);
+            di = dj = -1;
+            m = X[(size_t)j] == Y[(size_t)i] ? '=' : 'X';
+        }
+        if (i > 0 && best < at(i - 1, j))
+        {
+            best = at(i - 1, j);
+            di = -1;
+            dj = 0;
+            m = 'I';
+        }
+        if (j > 0 && best < at(i, j - 1))
+        {
+            best = at(i, j - 1);
+            di = 0;
+            dj = -1;
+            m = 'D';
+        }
+        if (di == 0 && dj == 0) break;
+        moves.push_back(m);
+        i += di;
+        j += dj;
+    }
+    (void)hipHostFree(blk);
+    if (e != hipSuccess) return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
+    if (align_cost) *align_cost = cost;
+    return gsa::fold_moves(moves.data(), (int64_t)moves.size(), edit, cap, edit_len, trace_hash);
 }
 
 int gsa_trace_sparse_dev(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, const int32_t* seqX, int32_t adjcols,

@@ -18,6 +18,7 @@ struct CheckArgs
     const int* hrow;
     const int* hcol;
     const int* score;
+    long long ld;  // check_full: row pitch of score in ints (>= adjcols)
     // [0] values compared, [1] mismatches, [2] smallest mismatching index (~0 if none)
     unsigned long long* res;
 };

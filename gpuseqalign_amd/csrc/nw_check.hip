@@ -169,7 +169,9 @@ __global__ void __launch_bounds__(64) check_sparse_kernel(CheckArgs a)
     if (checked) atomicAdd(a.res, checked);
 }
 
-// one thread per cell; blockIdx.y strides over rows
+// one thread per column; blockIdx.y takes a contiguous range of rows, so the row above (`up`) and
+// its left neighbour (`diag`) come from the previous iteration's registers and each cell costs two
+// loads from the same lines (its own value and its left neighbour): ~1x the matrix in HBM reads
 __global__ void __launch_bounds__(256) check_full_kernel(CheckArgs a)
 {
     __shared__ int sub[32 * 32];
@@ -178,13 +180,22 @@ __global__ void __launch_bounds__(256) check_full_kernel(CheckArgs a)
     const long long j = (long long)blockIdx.x * 256 + threadIdx.x;
     if (j >= a.adjcols) return;
     const int g = a.g;
-    const long long ld = a.adjcols;
+    const long long ld = a.ld;
     const gptr<const int> S = G(a.score);
     const int xo = clamp_letter(G(a.seqX)[j], a.substsz);
+    const long long per = (a.adjrows + gridDim.y - 1) / gridDim.y;
+    const long long i0 = (long long)blockIdx.y * per, i1 = min(a.adjrows, i0 + per);
     unsigned long long checked = 0;
-    for (long long i = blockIdx.y; i < a.adjrows; i += gridDim.y)
+    int up = 0, diag = 0;
+    if (i0 > 0 && i0 < i1)
+    {
+        up = S[(i0 - 1) * ld + j];
+        if (j > 0) diag = S[(i0 - 1) * ld + j - 1];
+    }
+    for (long long i = i0; i < i1; ++i)
     {
         const int v = S[i * ld + j];
+        const int left = j > 0 ? S[i * ld + j - 1] : 0;
         int e;
         if (i == 0)
             e = (int)(j * g);
@@ -193,10 +204,12 @@ __global__ void __launch_bounds__(256) check_full_kernel(CheckArgs a)
         else
         {
             const int y = clamp_letter(G(a.seqY)[i], a.substsz);
-            e = max(max(S[(i - 1) * ld + j - 1] + sub[y * a.substsz + xo], S[(i - 1) * ld + j] + g), S[i * ld + j - 1] + g);
+            e = max(max(diag + sub[y * a.substsz + xo], up + g), left + g);
         }
         ++checked;
-        if (v != e) record(a, (unsigned long long)(i * ld + j));
+        if (v != e) record(a, (unsigned long long)(i * a.adjcols + j));
+        up = v;
+        diag = left;
     }
     atomicAdd(a.res, checked);
 }
@@ -214,6 +227,8 @@ hipError_t launch_check_full(const CheckArgs& a, hipStream_t st)
 {
     if (a.substsz > 32) return hipErrorInvalidValue;
     const int gx = (int)((a.adjcols + 255) / 256);
+    if (a.ld < a.adjcols) return hipErrorInvalidValue;
+    // ~64k blocks of 256 columns x a contiguous row range
     const int gy = (int)std::min<long long>(a.adjrows, std::max<long long>(1, 65536 / std::max(gx, 1)));
     hipLaunchKernelGGL(check_full_kernel, dim3(gx, gy), dim3(256), 0, st, a);
     return hipGetLastError();

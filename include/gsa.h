@@ -252,6 +252,25 @@ int gsa_check_sparse_dev(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, con
 int gsa_check_full_dev(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, const int32_t* seqX, int32_t adjcols,
                        const int32_t* subst, int32_t substsz, int32_t gapo, const int32_t* score,
                        gsa_check_result* out, void* stream);
+/* As gsa_check_full_dev for a matrix with row pitch ld (>= adjcols, gsa_fill_full_pitched_dev);
+ * `first` is still i*adjcols+j. */
+int gsa_check_full_pitched_dev(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, const int32_t* seqX,
+                               int32_t adjcols, const int32_t* subst, int32_t substsz, int32_t gapo,
+                               const int32_t* score, int32_t ld, gsa_check_result* out, void* stream);
+
+/* The plain family's consumers over a matrix that stays in HBM (row pitch ld >= adjcols; ld =
+ * adjcols for gsa_fill_full_dev output), so a 100k x 100k matrix (40 GB) is hashed and traced
+ * without a host copy of it.  Results are identical to gsa_hash_full / gsa_trace_full of the
+ * same matrix.  Both wait for `stream` first and are synchronous.
+ * gsa_hash_full_dev: NwHash1_Plain (src/nwtrace1_plain.cpp:133-154); the hash is one serial chain
+ *   over every cell, folded on the host while rows stream through two pinned buffers.
+ * gsa_trace_full_dev: NwTrace1_Plain (src/nwtrace1_plain.cpp:6-131) -- the walk reads blocks of
+ *   the matrix around its position; seqY/seqX are device pointers; align_cost = the last cell. */
+int gsa_hash_full_dev(gsa_ctx* ctx, const int32_t* score, int32_t adjrows, int32_t adjcols, int32_t ld,
+                      uint32_t* hash, void* stream);
+int gsa_trace_full_dev(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, const int32_t* seqX, int32_t adjcols,
+                       const int32_t* score, int32_t ld, char* edit, int64_t cap, int64_t* edit_len,
+                       uint32_t* trace_hash, int32_t* align_cost, void* stream);
 
 /* NwTrace2_Sparse (src/nwtrace2_sparse.cpp:102-257) on the device: the walk and its tile
  * recomputes run on the GPU from device-resident headers; outputs (edit string, trace hash,
