@@ -76,21 +76,20 @@ def lane_ns():
 
 def full_kernel_name(single):
     """Kernels of a full fill (gsa_capi.hip full_twopass): the two-pass fill (pass 1: K-rows XR
-    instance, (4, 4) for one pair and (8, 4) for a batch that overfills the chip; pass 2: the tile
-    expansion), or under GSA_FULL_KERNEL=lane the one-pass lane fill."""
+    instance, (4, 4) for one pair and (8, 4) for a batch that overfills the chip; pass 2: the
+    streamed tile expansion, 7 tile waves + a loader wave per workgroup), fused into one launch for a
+    single pair; or under GSA_FULL_KERNEL=lane the one-pass lane fill."""
     if os.environ.get("GSA_FULL_KERNEL", "") == "lane":
         return lane_kernel_name(single)
     fm = os.environ.get("GSA_FULL_FUSED", "1")
     if single and fm != "0":
         return ("gsa::nw_full_fused_kernel<4,8,true> (both passes in one launch: (4, 4) K-rows pass-1 tickets "
-                "publishing per-strip progress, then 8-wave expansion tasks of 64 x 512 tiles waiting on those words)")
-    if not single and fm == "2":
-        return (f"gsa::nw_full_fused_kernel<8,12,true> (both passes in one launch: GSA_FUSED_P1="
-                f"{os.environ.get('GSA_FUSED_P1', '128')} workgroups take the (8, 4) pass-1 tickets first, the rest "
-                "12-wave expansion tasks of 64 x 512 tiles as their rows come in)")
+                "publishing per-strip progress, then the streamed expansion: a loader wave per workgroup stages "
+                "each 448-row x 512-column task once pass 1 has passed it, 7 tile waves store parallelogram tiles)")
     ns = 4 if single else 8
     name = (f"gsa::nw_krow_kernel<{ns},4,1024,2,true> (pass 1: sparse wavefront keeping every 64th row and the "
-            f"256-column header columns) + gsa::nw_expand_kernel (pass 2: every 64 x 512 tile recomputed)")
+            f"256-column header columns) + gsa::nw_expand_stream_kernel (pass 2: every 64 x 512 tile recomputed, "
+            f"7 tile waves + a loader wave per workgroup)")
     if not single and os.environ.get("GSA_FULL_SPLIT", "") != "0":
         name += ("; a batch whose pass-1 tickets end in a short round may run as two pair groups (tuned on its "
                  "first launches, pipelined_groups in passes): group A (the full rounds) on the caller's stream, "

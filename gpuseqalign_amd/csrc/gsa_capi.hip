@@ -115,10 +115,6 @@ struct gsa_ctx
     // combine's result, the transposed table
     int* bidi = nullptr;
     size_t bidi_cap = 0;  // ints
-    // the pipelined full batch: pass 1 of pair groups 1.. on a stream of its own, one event per group
-    hipStream_t p1stream = nullptr;
-    static constexpr int kMaxGroups = 16;
-    hipEvent_t pipe_ev[kMaxGroups + 1] = {};
     void* expin[kStage] = {nullptr, nullptr, nullptr, nullptr};
     size_t expin_cap[kStage] = {0, 0, 0, 0};
     hipEvent_t expin_ev[kStage] = {nullptr, nullptr, nullptr, nullptr};
@@ -994,268 +990,6 @@ int enqueue_fill(gsa_ctx* ctx, int mode, const int32_t* seqY, int32_t adjrows, c
 // one-pass lane fill, which needs no scratch
 constexpr int kNoScratch = -1000;
 
-// The pipelined full batch: the pairs in G groups (sizes dealt longest first, snake order); group 0's
-// pass 1 runs alone on the whole chip (the XR instance the batch would use), then group g's expansion
-// (persistent 12-wave workgroups, one per CU: 87 KB of LDS, 12 of 16 wave slots) runs on `st` while
-// group g+1's pass 1 runs on the context's p1stream in 4-wave (2, 2) workgroups that fit beside it
-// (74 KB, 4 slots): pass 2 is bound by each CU's store path with its VALU ~15 % busy, so pass 1
-// takes issue slots the expansion leaves idle instead of whole CUs (a CU split or two-stream
-// pipeline of the 16-wave expansion was 15-27 % slower, profiles/r04_probe_q.txt).  Expansion g
-// waits for pass 1 of group g by an event; the kernels never wait on each other inside a launch.
-int enqueue_full_pipelined(gsa_ctx* ctx, int npairs, const gsa_pair_dev* pairs, const int32_t* lds,
-                           const int32_t* subst, int32_t substsz, int32_t gapo, hipStream_t st, int groups)
-{
-    constexpr int kXW = 12;  // expansion waves per workgroup
-    const int G = std::max(2, std::min(groups, std::min(npairs, gsa_ctx::kMaxGroups)));
-    // groups: pairs by cells, dealt in snake order so the groups' cells are even
-    std::vector<int> ord((size_t)npairs);
-    for (int p = 0; p < npairs; ++p) ord[(size_t)p] = p;
-    auto cells = [&](int p) { return (long long)(pairs[p].adjrows - 1) * (long long)(pairs[p].adjcols - 1); };
-    std::stable_sort(ord.begin(), ord.end(), [&](int x, int y) { return cells(x) > cells(y); });
-    std::vector<std::vector<int>> grp((size_t)G);
-    for (int k = 0; k < npairs; ++k)
-    {
-        const int r = k / G, c = k % G;
-        grp[(size_t)((r & 1) ? G - 1 - c : c)].push_back(ord[(size_t)k]);
-    }
-    // per pair: pass-1 geometry (group 0: the batch's XR instance, (8, 4) or (4, 4); others (2, 2)),
-    // scratch offsets, expansion descriptor
-    long long g0Rows = 0;
-    for (int p : grp[0]) g0Rows += std::max(1, (pairs[p].adjrows - 1 + gsa::kSparseTileBy - 1) / gsa::kSparseTileBy);
-    const int ns0 = (grp[0].size() > 1 && g0Rows > (long long)std::max(1, ctx->cu_count)) ? 8 : 4;
-    std::vector<size_t> off((size_t)npairs * 3);
-    std::vector<gsa::ExpandPair> ex((size_t)npairs);
-    std::vector<int> grpOf((size_t)npairs);
-    for (int g = 0; g < G; ++g)
-        for (int p : grp[(size_t)g]) grpOf[(size_t)p] = g;
-    size_t bytes = 0;
-    auto take = [&](size_t b) {
-        const size_t o = bytes;
-        bytes += (b + 255) & ~(size_t)255;
-        return o;
-    };
-    std::vector<long long> granG((size_t)G, 0), tasksG((size_t)G, 0);
-    for (int p = 0; p < npairs; ++p)
-    {
-        const gsa_pair_dev& in = pairs[p];
-        if (in.adjrows < 2 || in.adjcols < 2 || !in.seqY || !in.seqX || !in.score) return GSA_ERROR_INVALID_VALUE;
-        const long long ld = lds ? lds[p] : in.adjcols;
-        if (ld < in.adjcols) return GSA_ERROR_INVALID_VALUE;
-        gsa_sparse_geom geom;
-        int s = gsa_sparse_geometry(in.adjrows, in.adjcols, gsa::kExpHB, &geom);
-        if (s != GSA_SUCCESS) return s;
-        const int g = grpOf[(size_t)p];
-        const int ns = g == 0 ? ns0 : 2, k = g == 0 ? 4 : 2;
-        const int Cp = geom.tileHdrMatCols * gsa::kExpHB;
-        const long long tickets = gsa::krow_tickets(geom.tileHdrMatRows, ns, k);
-        const long long nrows = tickets * ns * k;  // rows 64m written by pass 1, m = 1 .. nrows
-        granG[(size_t)g] += tickets * gsa::gran_stride(Cp);
-        off[3 * p] = take((size_t)geom.hrowElems * 4);
-        off[3 * p + 1] = take((size_t)geom.hcolElems * 4);
-        off[3 * p + 2] = take((size_t)(nrows * gsa::rows64_pitch(Cp)) * 4);
-        gsa::ExpandPair& e = ex[(size_t)p];
-        std::memset(&e, 0, sizeof(e));
-        e.seqY = in.seqY;
-        e.seqX = in.seqX;
-        e.R = in.adjrows - 1;
-        e.C = in.adjcols - 1;
-        e.score = in.score;
-        e.ld = ld;
-        e.rpitch = gsa::rows64_pitch(Cp);
-        e.tcols = geom.tileHdrMatCols;
-        e.colTiles = std::max(1, (e.C + gsa::kExpTW - 1) / gsa::kExpTW);
-        e.lastSplit = e.C - (e.colTiles - 1) * gsa::kExpTW > gsa::kExpHB ? 1 : 0;
-        e.colTiles += e.lastSplit;
-        e.rowChunks = std::max(1, (e.R + kXW * gsa::kExpRows - 1) / (kXW * gsa::kExpRows));
-        e.taskBase = (int)tasksG[(size_t)g];
-        tasksG[(size_t)g] += (long long)e.colTiles * e.rowChunks;
-        if (tasksG[(size_t)g] > (1ll << 30) || tickets > (1ll << 30)) return GSA_ERROR_INVALID_VALUE;
-    }
-    hipError_t e = hipSetDevice(ctx->device);
-    if (e != hipSuccess) return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
-    if (ctx->excap < bytes || !ctx->exbuf)
-    {
-        if (ctx->exbuf) (void)hipFree(ctx->exbuf);
-        ctx->exbuf = nullptr;
-        ctx->excap = 0;
-        if ((e = hipMalloc(&ctx->exbuf, std::max<size_t>(bytes, 256))) != hipSuccess)
-        {
-            (void)hipGetLastError();
-            return kNoScratch;
-        }
-        ctx->excap = std::max<size_t>(bytes, 256);
-    }
-    if (!ctx->p1stream && (e = hipStreamCreateWithFlags(&ctx->p1stream, hipStreamNonBlocking)) != hipSuccess)
-        return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
-    for (int g = 0; g <= G; ++g)
-        if (!ctx->pipe_ev[g] && (e = hipEventCreateWithFlags(&ctx->pipe_ev[g], hipEventDisableTiming)) != hipSuccess)
-            return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
-    // buffers every launch of the pipeline shares, sized once up front (no reallocation while a launch
-    // on the other stream may use them): granules, pass-1 descriptors, expansion descriptors
-    long long granMax = 0, tasksMax = 0;
-    size_t unitsMax = 0;
-    for (int g = 0; g < G; ++g)
-    {
-        granMax = std::max(granMax, granG[(size_t)g]);
-        tasksMax = std::max(tasksMax, tasksG[(size_t)g]);
-        unitsMax = std::max(unitsMax, grp[(size_t)g].size());
-    }
-    int s = ensure_gran(ctx, (size_t)std::max<long long>(granMax, 1), st);
-    if (s != GSA_SUCCESS) return s;
-    // pass-1 descriptors + the round-robin schedule (2 ints per ticket) of the largest group
-    {
-        long long schedMax = 0;
-        for (int g = 0; g < G; ++g)
-        {
-            long long t = 0;
-            for (int p : grp[(size_t)g])
-            {
-                gsa_sparse_geom geom;
-                (void)gsa_sparse_geometry(pairs[p].adjrows, pairs[p].adjcols, gsa::kExpHB, &geom);
-                t += gsa::krow_tickets(geom.tileHdrMatRows, g == 0 ? ns0 : 2, g == 0 ? 4 : 2);
-            }
-            schedMax = std::max(schedMax, t);
-        }
-        const size_t schedUnits = ((size_t)schedMax * 2 * sizeof(int) + sizeof(gsa::PairDesc) - 1) / sizeof(gsa::PairDesc);
-        if ((s = ensure_desc(ctx, unitsMax + schedUnits)) != GSA_SUCCESS) return s;
-    }
-    const size_t descBytesMax = (unitsMax * sizeof(gsa::ExpandPair) + 15) & ~(size_t)15;
-    const size_t exBytesMax = descBytesMax + (size_t)tasksMax * 2 * sizeof(int);
-    if (ctx->exdesc_cap < exBytesMax || !ctx->exdesc)
-    {
-        if (ctx->exdesc) (void)hipFree(ctx->exdesc);
-        ctx->exdesc = nullptr;
-        ctx->exdesc_cap = 0;
-        if ((e = hipMalloc(&ctx->exdesc, std::max<size_t>(exBytesMax, 4096))) != hipSuccess)
-            return fail(ctx, e, GSA_ERROR_MEMORY_ALLOCATION);
-        ctx->exdesc_cap = std::max<size_t>(exBytesMax, 4096);
-    }
-    if (ctx->timing)
-    {
-        const size_t n = (size_t)std::max(1, ctx->cu_count);
-        if (ctx->clk_cap < n || !ctx->clk)
-        {
-            if (ctx->clk) (void)hipFree(ctx->clk);
-            ctx->clk = nullptr;
-            ctx->clk_cap = 0;
-            if ((e = hipMalloc(&ctx->clk, std::max<size_t>(n, 1024) * 8)) != hipSuccess)
-                return fail(ctx, e, GSA_ERROR_MEMORY_ALLOCATION);
-            ctx->clk_cap = std::max<size_t>(n, 1024);
-        }
-    }
-    ctx->timing_state = 0;
-    if (ctx->timing && (e = hipEventRecord(ctx->pev[0], st)) != hipSuccess) return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
-    char* base = (char*)ctx->exbuf;
-    // pass 1 of group g on stream sp (group 0: the caller's stream, alone on the chip)
-    auto pass1 = [&](int g, hipStream_t sp) {
-        const std::vector<int>& gp = grp[(size_t)g];
-        std::vector<gsa_pair_dev> p1(gp.size());
-        std::vector<int*> rows(gp.size());
-        for (size_t i = 0; i < gp.size(); ++i)
-        {
-            const int p = gp[i];
-            p1[i] = pairs[p];
-            p1[i].score = nullptr;
-            p1[i].tileHrowMat = (int32_t*)(base + off[3 * p]);
-            p1[i].tileHcolMat = (int32_t*)(base + off[3 * p + 1]);
-            rows[i] = (int*)(base + off[3 * p + 2]);
-        }
-        return enqueue_batch(ctx, gsa::kModeSparse, (int)gp.size(), p1.data(), subst, substsz, gapo, gsa::kExpHB, sp,
-                             nullptr, 0, nullptr, rows.data(), nullptr, g > 0);
-    };
-    // the expansion of group g on the caller's stream: its descriptors (pair-relative task bases) and
-    // the round-robin task schedule, staged through a pinned slot
-    auto pass2 = [&](int g) {
-        const std::vector<int>& gp = grp[(size_t)g];
-        std::vector<gsa::ExpandPair> xd(gp.size());
-        for (size_t i = 0; i < gp.size(); ++i)
-        {
-            const int p = gp[i];
-            xd[i] = ex[(size_t)p];
-            xd[i].rows64 = (const int*)(base + off[3 * p + 2]);
-            xd[i].hcol = (const int*)(base + off[3 * p + 1]);
-        }
-        std::vector<int> xs;
-        if (gp.size() > 1)
-        {
-            std::vector<int> o(gp.size());
-            for (size_t i = 0; i < gp.size(); ++i) o[i] = (int)i;
-            auto ntask = [&](int i) { return xd[(size_t)i].colTiles * xd[(size_t)i].rowChunks; };
-            std::stable_sort(o.begin(), o.end(), [&](int x, int y) { return ntask(x) > ntask(y); });
-            for (int j = 0; j < ntask(o[0]); ++j)
-                for (int i : o)
-                {
-                    if (ntask(i) <= j) break;
-                    xs.push_back(i);
-                    xs.push_back(j);
-                }
-        }
-        const size_t descBytes = (xd.size() * sizeof(gsa::ExpandPair) + 15) & ~(size_t)15;
-        const size_t exBytes = descBytes + xs.size() * sizeof(int);
-        const int slot = ctx->expin_next;
-        ctx->expin_next = (slot + 1) % gsa_ctx::kStage;
-        hipError_t er = hipSuccess;
-        if (ctx->expin_used[slot] && (er = hipEventSynchronize(ctx->expin_ev[slot])) != hipSuccess)
-            return fail(ctx, er, GSA_ERROR_CUDA_GENERAL);
-        if (ctx->expin_cap[slot] < exBytes)
-        {
-            if (ctx->expin[slot]) (void)hipHostFree(ctx->expin[slot]);
-            ctx->expin[slot] = nullptr;
-            ctx->expin_cap[slot] = 0;
-            if ((er = hipHostMalloc(&ctx->expin[slot], exBytes)) != hipSuccess) return fail(ctx, er, GSA_ERROR_MEMORY_ALLOCATION);
-            ctx->expin_cap[slot] = exBytes;
-        }
-        std::memcpy(ctx->expin[slot], xd.data(), xd.size() * sizeof(gsa::ExpandPair));
-        if (!xs.empty()) std::memcpy((char*)ctx->expin[slot] + descBytes, xs.data(), xs.size() * sizeof(int));
-        er = hipMemcpyAsync(ctx->exdesc, ctx->expin[slot], exBytes, hipMemcpyHostToDevice, st);
-        if (er == hipSuccess) er = hipEventRecord(ctx->expin_ev[slot], st);
-        if (er != hipSuccess) return fail(ctx, er, GSA_ERROR_MEMORY_TRANSFER);
-        ctx->expin_used[slot] = true;
-        gsa::ExpandArgs xa {};
-        xa.subst = subst;
-        xa.substsz = substsz;
-        xa.g = gapo;
-        xa.pairs = (const gsa::ExpandPair*)ctx->exdesc;
-        xa.nPairs = (int)xd.size();
-        xa.nTasks = (int)tasksG[(size_t)g];
-        xa.sched = xs.empty() ? nullptr : (const int*)((char*)ctx->exdesc + descBytes);
-        xa.knob = env_int("GSA_EXPAND_KNOB", 0);
-        xa.mt = 1;
-        xa.counter = ctx->ctl + 4;
-        if (ctx->timing && g == G - 1)
-        {
-            xa.clk = ctx->clk;
-            ctx->clk_n = (size_t)std::min(ctx->cu_count, xa.nTasks);
-        }
-        if ((er = hipMemsetAsync(xa.counter, 0, 4, st)) != hipSuccess) return fail(ctx, er, GSA_ERROR_MEMORY_TRANSFER);
-        if ((er = gsa::launch_expand(xa, st, kXW, ctx->cu_count)) != hipSuccess) return fail(ctx, er, GSA_ERROR_KERNEL_FAILURE);
-        note_launch(ctx);
-        return (int)GSA_SUCCESS;
-    };
-    if ((s = pass1(0, st)) != GSA_SUCCESS) return s;
-    if (ctx->timing && (e = hipEventRecord(ctx->pev[1], st)) != hipSuccess) return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
-    // the side stream starts behind everything on st so far (inputs, granule clear, pass 1 of group 0)
-    if ((e = hipEventRecord(ctx->pipe_ev[0], st)) != hipSuccess || (e = hipStreamWaitEvent(ctx->p1stream, ctx->pipe_ev[0], 0)) != hipSuccess)
-        return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
-    for (int g = 1; g < G; ++g)
-    {
-        if ((s = pass1(g, ctx->p1stream)) != GSA_SUCCESS) return s;
-        if ((e = hipEventRecord(ctx->pipe_ev[g], ctx->p1stream)) != hipSuccess) return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
-    }
-    for (int g = 0; g < G; ++g)
-    {
-        if (g > 0 && (e = hipStreamWaitEvent(st, ctx->pipe_ev[g], 0)) != hipSuccess) return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
-        if ((s = pass2(g)) != GSA_SUCCESS) return s;
-    }
-    if (ctx->timing)
-    {
-        if ((e = hipEventRecord(ctx->pev[2], st)) != hipSuccess) return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
-        ctx->timing_state = 3;
-        ctx->timing_groups = G;
-    }
-    return GSA_SUCCESS;
-}
-
 // Full fills in two passes (nw_expand.h): pass 1 = the K-rows sparse fill of every pair with tile
 // width kExpTW, which also keeps rows 64m (XR instance), into the context's scratch; pass 2 =
 // every 64-row x kExpTW tile of every matrix recomputed from its top row and left column at once.
@@ -1285,33 +1019,19 @@ int enqueue_full_twopass(gsa_ctx* ctx, int npairs, const gsa_pair_dev* pairs, co
     for (int p = 0; p < npairs; ++p)
         tileRows += std::max<long long>(1, ((long long)pairs[p].adjrows - 1 + gsa::kSparseTileBy - 1) / gsa::kSparseTileBy);
     const bool fitsChip = tileRows <= (long long)std::max(1, ctx->cu_count);
-    // both passes in one launch (nw_full_fused_kernel): GSA_FULL_FUSED = 0 never, 1 (default) single
-    // pairs, 2 batches too.  (A matrix without interior cells has no pass-1 tickets: the expansion
-    // alone writes its headers.)
+    // both passes in one launch (nw_full_fused_kernel) for single pairs; GSA_FULL_FUSED=0: two launches.
+    // (A matrix without interior cells has no pass-1 tickets: the expansion alone writes its headers.)
     const int fusedMode = env_int("GSA_FULL_FUSED", 1);
     bool interior = true;
     for (int p = 0; p < npairs; ++p) interior = interior && pairs[p].adjrows > 1 && pairs[p].adjcols > 1;
     // (never inside a split batch: a group of one pair would take the fused branch, which records
     // neither afterP1 nor timeP1, and group B would then start against an unrecorded event)
-    const bool fused = interior && !opt.split && (npairs == 1 ? fusedMode >= 1 : fusedMode >= 2);
-    // GSA_FULL_PIPE = G >= 2: pass 1 pipelined beside the expansion in G pair groups
-    // (enqueue_full_pipelined).  Measured slower, so off by default: the 12-wave expansion that leaves
-    // room for pass 1 is 14 % slower than the 16-wave one alone, and the co-resident pass 1 costs it
-    // more than the 3.9 ms it hides (64 x 20k: 29.5 ms two launches vs 30.1-38 ms at G = 2-8 on one
-    // box, 25.0 vs 30.1 on another; profiles/r05_pipe_ab.txt)
-    const int pipeG = env_int("GSA_FULL_PIPE", 0);
-    if (!fused && interior && npairs > 1 && pipeG >= 2)
-        return enqueue_full_pipelined(ctx, npairs, pairs, lds, subst, substsz, gapo, st, pipeG);
-    // two launches: pass 2 one workgroup of kExpWaves waves per task, or (GSA_EXPAND_GRID > 0)
-    // that many persistent workgroups of GSA_EXPAND_WAVES (8, 12, 16) waves
-    const int xGrid = fused ? 0 : std::max(0, env_int("GSA_EXPAND_GRID", 0));
-    const int xw = env_int("GSA_EXPAND_WAVES", gsa::kExpWaves);
+    const bool fused = interior && !opt.split && npairs == 1 && fusedMode >= 1;
     const int ns = env_int("GSA_KROW_NS", (npairs > 1 && !fitsChip) ? 8 : 4) == 8 ? 8 : 4;  // as enqueue_batch
-    // fused: (4, 4) tickets under 8-wave workgroups, (8, 4) under 12
-    const int fusedW = ns == 4 ? gsa::kExpFusedWaves : gsa::kExpFusedWavesBatch;
-    const int xWaves = fused ? fusedW : (xw == 8 || (xGrid > 0 && xw == 12)) ? xw : gsa::kExpWaves;
-    // tiles per wave per expansion task (GSA_EXPAND_MT, 1..16; default 1)
-    const int xmt = std::min(16, std::max(1, env_int("GSA_EXPAND_MT", 1)));
+    // pass 2 (fused or its own launch): the streamed expansion, kExpStreamWaves - 1 tile waves per
+    // workgroup, tasks of that many 64-row tiles
+    const int xWaves = gsa::kExpStreamWaves - 1;
+    const int xmt = 1;
     std::vector<gsa_pair_dev> p1((size_t)npairs);
     std::vector<gsa::ExpandPair> ex((size_t)npairs);
     std::vector<size_t> off((size_t)npairs * 3);
@@ -1480,6 +1200,34 @@ int enqueue_full_twopass(gsa_ctx* ctx, int npairs, const gsa_pair_dev* pairs, co
             }
         }
     }
+    if (npairs == 1 && ex[0].rowChunks > 1 && env_int("GSA_SINGLE_ORDER", 1))
+    {
+        // The fused single pair's tasks in the order their pass-1 rows arrive.  Task (rc, jT) can
+        // start once strip s1 = the last of its rows' strips has passed column cb + cols + 64; strip s
+        // starts ~s lag steps after strip 0 and sweeps a column per step, so it is ready at about
+        // s1 lag + cb + cols.  Row-chunk-major order (the descriptor order) made the first workgroups
+        // wait for whole rows: at 100k they claimed row chunk 0's tiles to the far end of the
+        // matrix, ready only ~4 ms later (profiles/r06_stamps100k.txt).  lag = columns per 256-row
+        // strip, GSA_FUSED_LAG (default 192: the 100k pair's measured strip-to-strip spacing).
+        const gsa::ExpandPair& d = ex[0];
+        const long long lag = std::max(1, env_int("GSA_FUSED_LAG", 192));
+        const int cm = xWaves * xmt;
+        std::vector<std::pair<long long, int>> key((size_t)d.rowChunks * d.colTiles);
+        for (int rc = 0; rc < d.rowChunks; ++rc)
+            for (int jT = 0; jT < d.colTiles; ++jT)
+            {
+                const long long s1 = std::min<long long>((cm * (rc + 1) - 1) / 4, d.p1Strips - 1);
+                const int tt = rc * d.colTiles + jT;
+                key[(size_t)tt] = {s1 * lag + gsa::ex_cb(d, jT) + gsa::ex_cols(d, jT), tt};
+            }
+        std::stable_sort(key.begin(), key.end());
+        xs.reserve(2 * key.size());
+        for (const auto& k : key)
+        {
+            xs.push_back(0);
+            xs.push_back(k.second);
+        }
+    }
     const size_t descBytes = ((size_t)npairs * sizeof(gsa::ExpandPair) + 15) & ~(size_t)15;
     const size_t exBytes = descBytes + xs.size() * sizeof(int);
     if (exdesc_cap < exBytes || !exdesc)
@@ -1519,25 +1267,30 @@ int enqueue_full_twopass(gsa_ctx* ctx, int npairs, const gsa_pair_dev* pairs, co
     xa.sched = xs.empty() ? nullptr : (const int*)((char*)exdesc + descBytes);
     xa.knob = env_int("GSA_EXPAND_KNOB", 0);
     xa.mt = xmt;
-    // fused batches: GSA_FUSED_P1 workgroups take the pass-1 tickets first (a single pair: all)
-    const FusedLaunch fl {&xa, ns, fusedW, npairs == 1 ? (1 << 30) : std::max(1, env_int("GSA_FUSED_P1", 128))};
+    xa.spin = ctx->spin_ticks;
+    xa.err = ctx->ctl + 1;
+    // (a group of a split batch has a claim counter of its own: the two groups' expansions overlap)
+    xa.counter = ctx->ctl + 8 + opt.slot;
+    // the fused single pair: every workgroup takes pass-1 tickets first
+    const FusedLaunch fl {&xa, ns, gsa::kExpStreamWaves, 1 << 30};
+    const int xGrid = (int)std::max<long long>(1, std::min<long long>(ctx->cu_count, tasks));
     // gsa_set_full_timing: events before pass 1, between the passes and after pass 2, and the
     // expansion's clock stamps (one per workgroup)
     const bool timed = ctx->timing && !opt.split;
     if (!opt.split) ctx->timing_state = 0;
-    if (timed && !fused && xGrid == 0)
+    if (timed && !fused)
     {
-        if (ctx->clk_cap < (size_t)tasks || !ctx->clk)
+        if (ctx->clk_cap < (size_t)xGrid || !ctx->clk)
         {
             if (ctx->clk) (void)hipFree(ctx->clk);
             ctx->clk = nullptr;
             ctx->clk_cap = 0;
-            if ((e = hipMalloc(&ctx->clk, (size_t)std::max<long long>(tasks, 1024) * 8)) != hipSuccess)
+            if ((e = hipMalloc(&ctx->clk, (size_t)std::max(xGrid, 1024) * 8)) != hipSuccess)
                 return fail(ctx, e, GSA_ERROR_MEMORY_ALLOCATION);
-            ctx->clk_cap = (size_t)std::max<long long>(tasks, 1024);
+            ctx->clk_cap = (size_t)std::max(xGrid, 1024);
         }
         xa.clk = ctx->clk;
-        ctx->clk_n = (size_t)tasks;
+        ctx->clk_n = (size_t)xGrid;
     }
     if (timed && (e = hipEventRecord(ctx->pev[0], st)) != hipSuccess) return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
     if (opt.startEv && (e = hipEventRecord(opt.startEv, st)) != hipSuccess) return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
@@ -1555,10 +1308,9 @@ int enqueue_full_twopass(gsa_ctx* ctx, int npairs, const gsa_pair_dev* pairs, co
     if (timed && (e = hipEventRecord(ctx->pev[1], st)) != hipSuccess) return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
     if (opt.afterP1 && (e = hipEventRecord(opt.afterP1, st)) != hipSuccess) return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
     if (opt.timeP1 && (e = hipEventRecord(opt.timeP1, st)) != hipSuccess) return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
-    xa.counter = ctx->ctl + 4;
-    if (xGrid > 0 && (e = hipMemsetAsync(xa.counter, 0, 4, st)) != hipSuccess) return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
+    if ((e = hipMemsetAsync(xa.counter, 0, 4, st)) != hipSuccess) return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
     if (tuneRecord && (e = hipEventRecord(xt.ev[0], st)) != hipSuccess) return fail(ctx, e, GSA_ERROR_CUDA_GENERAL);
-    if ((e = gsa::launch_expand(xa, st, xWaves, xGrid)) != hipSuccess) return fail(ctx, e, GSA_ERROR_KERNEL_FAILURE);
+    if ((e = gsa::launch_expand_stream(xa, st, xGrid)) != hipSuccess) return fail(ctx, e, GSA_ERROR_KERNEL_FAILURE);
     note_launch(ctx);
     if (tuneRecord)
     {
@@ -1937,8 +1689,6 @@ void gsa_ctx_destroy(gsa_ctx* ctx)
     if (ctx->bidi) (void)hipFree(ctx->bidi);
     for (hipEvent_t ev : ctx->pev)
         if (ev) (void)hipEventDestroy(ev);
-    for (hipEvent_t ev : ctx->pipe_ev)
-        if (ev) (void)hipEventDestroy(ev);
     for (auto& t : ctx->xt)
         for (hipEvent_t ev : t.ev)
             if (ev) (void)hipEventDestroy(ev);
@@ -1953,11 +1703,6 @@ void gsa_ctx_destroy(gsa_ctx* ctx)
     }
     if (ctx->exbuf2) (void)hipFree(ctx->exbuf2);
     if (ctx->exdesc2) (void)hipFree(ctx->exdesc2);
-    if (ctx->p1stream)
-    {
-        (void)hipStreamSynchronize(ctx->p1stream);
-        (void)hipStreamDestroy(ctx->p1stream);
-    }
     for (int k = 0; k < gsa_ctx::kStage; ++k)
     {
         if (ctx->expin[k]) (void)hipHostFree(ctx->expin[k]);

@@ -78,9 +78,20 @@ struct ExpandArgs
     // measurement (gsa_set_full_timing): per workgroup, wave 0's s_memtime cycles (low word) and
     // s_memrealtime ticks (100 MHz, high word) from its start to its end; null = off
     unsigned long long* clk;
+    // streamed launches (launch_expand_stream): watchdog ticks (s_memrealtime) and the sticky error
+    // word of the context
+    unsigned long long spin;
+    unsigned* err;
 };
 
 size_t expand_lds_bytes(int substsz, int waves);
+// The streamed expansion (nw_expand_dev.h ex_stream): persistent workgroups of kExpStreamWaves waves,
+// kExpStreamWaves - 1 tile waves (tasks of (kExpStreamWaves - 1) x 64 rows) and one loader wave that
+// claims tasks from a.counter (zeroed before the launch) and stages their inputs in LDS, so the tile
+// waves only compute and store.  grid <= 0: one workgroup per CU.
+constexpr int kExpStreamWaves = 8;
+size_t expand_stream_lds_bytes(int substsz);
+hipError_t launch_expand_stream(const ExpandArgs& a, hipStream_t stream, int grid);
 // one workgroup of `waves` (8, 16) waves per task; or, grid > 0, `grid` persistent workgroups of
 // `waves` (8, 12, 16) waves claiming tasks from a.counter.  rowChunks of every pair must be counted
 // in chunks of waves x kExpRows x mt rows.  Pair arrays in device memory.

@@ -29,9 +29,10 @@ namespace {
 
 using namespace xdev;
 
-// one workgroup per task: 16 waves (one workgroup per CU: 102 KB of LDS) or 8 (two per CU)
+// one workgroup per task: 16 waves or 8, one workgroup per CU either way (115.6 / 94.6 KB of LDS
+// since the parallelogram tiles), so 8 waves may use up to 256 VGPRs
 template <int WAVES>
-__global__ void __launch_bounds__(64 * WAVES, 4) nw_expand_kernel(ExpandArgs a)
+__global__ void __launch_bounds__(64 * WAVES, WAVES == 8 ? 2 : 4) nw_expand_kernel(ExpandArgs a)
 {
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
@@ -150,7 +151,52 @@ hipError_t launch_persist(const ExpandArgs& a, hipStream_t stream, int grid)
     return hipGetLastError();
 }
 
+// the streamed expansion (ex_stream): persistent, one workgroup per CU; wave 0 records the
+// workgroup's effective clock (gsa_set_full_timing)
+__global__ void __launch_bounds__(64 * kExpStreamWaves) nw_expand_stream_kernel(ExpandArgs a)
+{
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    uint64_t c0 = 0, r0 = 0;
+    if (a.clk && w == 0)
+    {
+        c0 = __builtin_amdgcn_s_memtime();
+        r0 = __builtin_amdgcn_s_memrealtime();
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+    }
+    ex_stream<kExpStreamWaves, false>(a, a.counter, ExFused {nullptr, 0u, nullptr}, w, lane);
+    if (a.clk && w == 0)
+    {
+        const uint64_t c1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        if (lane == 0) G(a.clk)[blockIdx.x] = (uint64_t)(uint32_t)(c1 - c0) | ((uint64_t)(uint32_t)(r1 - r0) << 32);
+    }
+}
+
 }  // namespace
+
+size_t expand_stream_lds_bytes(int substsz) { return (size_t)xdev::ex_stream_lds(substsz, kExpStreamWaves - 1); }
+
+hipError_t launch_expand_stream(const ExpandArgs& a, hipStream_t stream, int grid)
+{
+    if (a.nTasks <= 0) return hipSuccess;
+    if (!a.counter || !a.err || a.substsz > 32) return hipErrorInvalidValue;
+    const size_t lds = expand_stream_lds_bytes(a.substsz);
+    auto kern = nw_expand_stream_kernel;
+    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+    if (grid <= 0)
+    {
+        int dev = 0, cus = 0;
+        if ((e = hipGetDevice(&dev)) != hipSuccess) return e;
+        if ((e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess) return e;
+        grid = std::max(1, cus);
+    }
+    grid = std::min(grid, a.nTasks);
+    if ((e = record_foot((const void*)kern, lds, 64 * kExpStreamWaves, grid)) != hipSuccess) return e;
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * kExpStreamWaves), lds, stream, a);
+    return hipGetLastError();
+}
 
 size_t expand_lds_bytes(int substsz, int waves) { return (size_t)xdev::ex_layout(substsz, waves).gfill + 128; }  // the row of g, the claim word
 

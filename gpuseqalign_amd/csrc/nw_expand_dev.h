@@ -12,6 +12,9 @@
 #ifndef GSA_EXPAND_PROBE
 #define GSA_EXPAND_PROBE 0  // diagnostic builds only (tools/r05_xprobe.sh)
 #endif
+#ifndef GSA_EXPAND_STORE
+#define GSA_EXPAND_STORE 0  // matrix stores: 0 plain, 1 nontemporal, 2 write-through (sc1)
+#endif
 
 namespace gsa {
 namespace xdev {
@@ -19,10 +22,16 @@ namespace xdev {
 constexpr int kBlk = 16;           // steps per block
 constexpr int kH = kBlk / 4;       // halo registers (int4) per block
 constexpr int kSubRow = 36;        // dwords per subT row (32 letters + 4)
-constexpr int kQOff = 64;          // Q[y][kQOff + j], j = 1..kExpTW; reads reach j = -63 .. kExpTW + 15
-constexpr int kQS = kQOff + kExpTW + 32;  // Q row stride (dwords), = 0 mod 32: the bank is the column alone
-constexpr int kTopS = kExpTW + 80;        // per-wave top row: topw[t] = H(r0 - 1, cb + t) + g, t < kExpTW + 80
+// A wave computes its tile's columns and kExtra more: its 64 rows are stored as a parallelogram,
+// row r0 + rr from column cb + 64 - rr to cb + cols + 63 - rr (ex_tile), so that every 128-byte line
+// of the pitched layout belongs to one tile and is written whole, by one wave, at once
+constexpr int kExtra = 64;
+constexpr int kQOff = 64;          // Q[y][kQOff + j], j = 1..kExpTW + kExtra; reads reach j = -63 .. 16 NB + 15
+constexpr int kQS = kQOff + kExpTW + kExtra + 96;  // Q row stride (dwords), = 0 mod 32: the bank is the column alone
+constexpr int kTopS = kExpTW + kExtra + 80;        // per-wave top row: topw[t] = H(r0 - 1, cb + t) + g, t < 16 NB
 static_assert(kQS % 32 == 0 && kTopS % 4 == 0 && kExpTW % kExpHB == 0, "LDS strides");
+static_assert(kQOff + 16 * ((kExpTW + kExtra + 79) / 16) + 15 < kQS && 16 * ((kExpTW + kExtra + 79) / 16) <= kTopS,
+              "profile and top-row reads stay in their rows");
 
 extern __shared__ __attribute__((aligned(16))) char xsm[];
 
@@ -37,6 +46,17 @@ __device__ __forceinline__ gptr<T> G(T* p)
 }
 
 __device__ __forceinline__ int lds_ld(uint32_t a) { return *(const int*)(xsm + a); }
+// one 16-byte chunk of the output matrix (GSA_EXPAND_STORE picks the cache policy)
+__device__ __forceinline__ void st_out(gptr<int> p, int4a v)
+{
+#if GSA_EXPAND_STORE == 1
+    __builtin_nontemporal_store(v, (gptr<int4a>)p);
+#elif GSA_EXPAND_STORE == 2
+    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"((int4v)v) : "memory");
+#else
+    *(gptr<int4a>)p = v;
+#endif
+}
 __device__ __forceinline__ void lds_st(uint32_t a, int v) { *(int*)(xsm + a) = v; }
 __device__ __forceinline__ int4v lds_ld4(uint32_t a) { return *(const int4v*)(xsm + a); }
 // lane l <- lane l-1, lane 0 <- 0 (DPP wave_shr:1, bound_ctrl zero)
@@ -47,8 +67,8 @@ struct ExLds
     uint32_t sub, q, top, gfill;
 };
 // LDS of a workgroup of `waves` tile waves: the column profile; subT, which only the profile build
-// reads, overlaid by one top row per wave; a row of g.  (79.9 KB for 8 waves and 25 letters: two
-// workgroups per CU)
+// reads, overlaid by one top row per wave; a row of g.  (94.6 KB for 8 waves and 25 letters, 115.6 KB
+// for 16: one workgroup per CU)
 __host__ __device__ inline ExLds ex_layout(int substsz, int waves)
 {
     ExLds L;
@@ -74,6 +94,9 @@ __device__ __forceinline__ ExpandPair ex_desc(const ExpandPair* p)
     return u.d;
 }
 
+__device__ __forceinline__ void ex_tile_core(const ExpandArgs& a, const ExpandPair& d, uint32_t qbase, uint32_t gfill,
+                                             int lane, int cb, int cols, int r0, int y, int lb, uint32_t topw);
+
 // one 64-row x kExpTW-column tile of the full matrix, one row per lane
 __device__ __forceinline__ void ex_tile(const ExpandArgs& a, const ExpandPair& d, const ExLds& L, int w, int lane,
                                         int cb, int cols, int r0)
@@ -86,7 +109,7 @@ __device__ __forceinline__ void ex_tile(const ExpandArgs& a, const ExpandPair& d
     // left boundary H(r, cb): column 0, or the pass-1 header column of its tile (iT, cb / kExpHB)
     // (element r - iT tBy; rows up to the last tile row's end are computed there, padding included)
     int lb;
-    if (cb == 0)
+    if (cb == 0 || GSA_EXPAND_PROBE == 3)
         lb = r * g;
     else
     {
@@ -94,25 +117,57 @@ __device__ __forceinline__ void ex_tile(const ExpandArgs& a, const ExpandPair& d
         lb = G(d.hcol)[((size_t)iT * (size_t)d.tcols + (size_t)(cb / kExpHB)) * (size_t)(kSparseTileBy + 1) +
                        (size_t)(r - iT * kSparseTileBy)];
     }
-    // top row H(r0 - 1, cb .. cb + kExpTW) + g into LDS: row 0, or pass-1 row 64m (shifted values)
+    // the last column this wave computes validly: kExtra past the tile (the parallelogram's right
+    // part), or the matrix's last
+    const int ce = min(cols + kExtra, d.C - cb);
+    // top row H(r0 - 1, cb .. cb + ce) + g into LDS: row 0, or pass-1 row 64m (shifted values)
     const uint32_t topw = L.top + 4u * (uint32_t)(kTopS * w);
     {
+        // all of the lane's loads in flight at once, then the LDS stores: a load waits behind the
+        // wave's outstanding stores (in-order vmcnt), so a loop of dependent load/store pairs paid
+        // that wait and the loaded-HBM latency once per iteration (9 per tile)
         const int m = (r0 - 1) / kExpRows;
-        for (int j = lane; j <= cols + 3; j += 64)  // (+3: the chunks that straddle the tile's end)
+        constexpr int kIt = (kExpTW + kExtra + 1 + 63) / 64;
+        int v[kIt];
+#pragma unroll
+        for (int i = 0; i < kIt; ++i)
         {
-            const int c = cb + j;
-            const int v = m == 0 ? c * g
-                                 : G(d.rows64)[(size_t)(m - 1) * (size_t)d.rpitch + kRowsPad + c] + (kExpRows * m + c) * g;
-            lds_st(topw + 4u * (uint32_t)j, v + g);
+            const int j = lane + 64 * i, c = cb + j;
+#if GSA_EXPAND_PROBE == 3
+            // diagnostic build: no pass-1 row loads (results wrong)
+            v[i] = c;
+            (void)j;
+#else
+            v[i] = (m == 0 || j > ce) ? 0 : G(d.rows64)[(size_t)(m - 1) * (size_t)d.rpitch + kRowsPad + c];
+#endif
+        }
+#pragma unroll
+        for (int i = 0; i < kIt; ++i)
+        {
+            const int j = lane + 64 * i, c = cb + j;
+            if (j <= ce) lds_st(topw + 4u * (uint32_t)j, (m == 0 ? c * g : v[i] + (kExpRows * m + c) * g) + g);
         }
     }
-    const uint32_t qrow = L.q + 4u * (uint32_t)(y * kQS + kQOff);
-    const uint32_t hbase = (lane == 0) ? topw : L.gfill;  // lanes >= 1 read a row of g (no branch)
-    // lane 63 reaches column cb + cols + 3 at step cols + 66: a chunk that straddles the tile's end is
-    // stored whole by this tile's wave, and skipped by the next tile's, whose ramp stores only the
-    // chunks that start inside it -- no per-element stores except at the matrix's own edges
-    const int ce = min(cols + 3, d.C - cb);                // last column this wave computes validly
+    ex_tile_core(a, d, L.q, L.gfill, lane, cb, cols, r0, y, lb, topw);
+}
+
+// the tile's recurrence and stores, its inputs in place: y = the lane's row letter, lb = its left
+// boundary H(r0 + lane, cb), topw = LDS byte address of its top row (topw[t] = H(r0 - 1, cb + t) + g,
+// t <= ce), qbase / gfill the column profile and the row of g
+__device__ __forceinline__ void ex_tile_core(const ExpandArgs& a, const ExpandPair& d, uint32_t qbase, uint32_t gfill,
+                                             int lane, int cb, int cols, int r0, int y, int lb, uint32_t topw)
+{
+    const int g = a.g;
+    const int ce = min(cols + kExtra, d.C - cb);
+    const uint32_t qrow = qbase + 4u * (uint32_t)(y * kQS + kQOff);
+    const uint32_t hbase = (lane == 0) ? topw : gfill;  // lanes >= 1 read a row of g (no branch)
+    // lane 63 reaches column cb + ce at step ce + 63.  Row r0 + rr is stored over columns
+    // lo(rr) .. hi(rr) (relative to cb): lo = 64 - rr (1 in the first tile column), hi = min(cols + 63
+    // - rr, C - cb): the chunks of blocks 4 .. cols / 16 + 3 of every lane, whole aligned lines, the
+    // next tile's parallelogram starting where this one ends -- per-element stores only at the
+    // matrix's own edges (its first and last columns, rows past R)
     const int NB = (ce + 64 + kBlk - 1) / kBlk;
+    const int hiMax = min(cols + 63, d.C - cb);  // hi(0)
     // transposed output (as nw_lane.hip): store k has lane 16h + n write columns 4h .. 4h+3 of the
     // block's 16 for row r0 + 16k + n
     const gptr<int> xbase = G(d.score) + (ptrdiff_t)(r0 + (lane & 15)) * d.ld + cb + 4 * (lane >> 4) - (lane & 15);
@@ -126,13 +181,25 @@ __device__ __forceinline__ void ex_tile(const ExpandArgs& a, const ExpandPair& d
     int sink = 0;
 #endif
     int tE[kBlk];  // the even block's transposed values, stored with the odd block's
-    bool held = false;
 #pragma unroll
     for (int e = 0; e < kBlk; ++e) tE[e] = 0;
 
-    auto block = [&](int b, int (&qc)[kBlk], int (&qn)[kBlk], auto rampT) {
-        constexpr bool RAMP = decltype(rampT)::value;
+    // the block's stores by phase (compile-time): kRamp = the first 4 blocks (columns <= cb for
+    // some lanes; stored only in the first tile column), kHold / kPair = an even / odd interior
+    // block (the even one's values held and stored with the odd one's, both halves of every
+    // 128-byte line back to back), kEdge = the per-lane path
+    enum { kRamp, kHold, kPair, kEdge };
+    auto block = [&](int b, int (&qc)[kBlk], int (&qn)[kBlk], auto modeT) {
+        constexpr int MODE = decltype(modeT)::value;
+        constexpr bool RAMP = MODE == kRamp;
         int4v hc[kH];
+#if GSA_EXPAND_PROBE == 6
+        // diagnostic build: no LDS reads and no recurrence, the stores alone (results wrong)
+#pragma unroll
+        for (int j = 0; j < kH; ++j) hc[j] = int4v {b, j, 1, 2};
+#pragma unroll
+        for (int u = 0; u < kBlk; ++u) qn[u] = u + b;
+#else
         {
             const uint32_t hb = hbase + (lane == 0 ? 4u * (uint32_t)(kBlk * b) : 0u);
 #pragma unroll
@@ -141,13 +208,14 @@ __device__ __forceinline__ void ex_tile(const ExpandArgs& a, const ExpandPair& d
         // profile of block b+1: columns 16(b+1) - lane .. + 15
 #pragma unroll
         for (int u = 0; u < kBlk; ++u) qn[u] = lds_ld(qrow + 4u * (uint32_t)(kBlk * (b + 1) + u - lane));
+#endif
         int vals[kBlk];
 #pragma unroll
         for (int u = 0; u < kBlk; ++u)
         {
             const int up = shr1z(H) + hc[u >> 2][u & 3];
             const int t1 = U + qc[u];
-#if GSA_EXPAND_PROBE == 1
+#if GSA_EXPAND_PROBE == 1 || GSA_EXPAND_PROBE == 6
             // diagnostic build (tools/r05_xprobe.sh): no recurrence, one add per cell (results wrong)
             int h = t1;
 #else
@@ -179,10 +247,6 @@ __device__ __forceinline__ void ex_tile(const ExpandArgs& a, const ExpandPair& d
                 t[4 * k + dd] = sw[0];
                 t[4 * (k + 1) + dd] = sw[1];
             }
-        // interior blocks (uniform): scalar row bases.  An even interior block's stores wait for the
-        // odd block after it and the two go out back to back, so each 128-byte line of the pitched
-        // layout is written whole at once (unpaired 64-byte halves of ~400k row streams overflow L2)
-        auto interior = [&](int bb) { return kBlk * bb - 63 >= 1 && kBlk * bb + kBlk - 1 <= cols && r0 + 63 <= d.R; };
         auto store4 = [&](int bb, int k, const int (&v)[kBlk]) {
             const gptr<int> ub = G(d.score) + ((ptrdiff_t)(r0 + 16 * k) * d.ld - 16 * k + kBlk * bb + cb);
 #if GSA_EXPAND_PROBE == 2
@@ -190,16 +254,15 @@ __device__ __forceinline__ void ex_tile(const ExpandArgs& a, const ExpandPair& d
             sink ^= v[4 * k] ^ v[4 * k + 1] ^ v[4 * k + 2] ^ v[4 * k + 3];
             (void)ub;
 #else
-            *(gptr<int4a>)(ub + xoff) = int4a {v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]};
+            st_out(ub + xoff, int4a {v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]});
 #endif
         };
-        if (!RAMP && (b & 1) == 0 && b + 1 < NB && interior(b) && interior(b + 1))
+        if constexpr (MODE == kHold)
         {
 #pragma unroll
             for (int e = 0; e < kBlk; ++e) tE[e] = t[e];
-            held = true;
         }
-        else if (held)
+        else if constexpr (MODE == kPair)
         {
 #pragma unroll
             for (int k = 0; k < 4; ++k)
@@ -207,48 +270,52 @@ __device__ __forceinline__ void ex_tile(const ExpandArgs& a, const ExpandPair& d
                 store4(b - 1, k, tE);
                 store4(b, k, t);
             }
-            held = false;
         }
-        else if (interior(b))
-        {
-#pragma unroll
-            for (int k = 0; k < 4; ++k) store4(b, k, t);
-        }
-        else
+        else if ((MODE == kEdge || cb == 0) && kBlk * b - 63 <= hiMax)
 #pragma unroll
             for (int k = 0; k < 4; ++k)
             {
-                // edge block: a chunk (row r0 + rr, tile columns xc .. xc+3) is this wave's if it starts
-                // in the tile; whole (x4) unless it passes the matrix's last column; the first tile also
-                // stores the valid part of the chunk that straddles column 1 (no tile before it)
+                // edge block: the chunk (row r0 + rr, columns xc .. xc+3) is stored where it lies in
+                // lo(rr) .. hi(rr): whole, except where the matrix's first or last column cuts it
                 const int rr = 16 * k + (lane & 15);
                 const int xc = kBlk * b - rr + 4 * (lane >> 4);
+                const int lo = cb == 0 ? 1 : 64 - rr, hi = min(cols + 63 - rr, d.C - cb);
                 if (r0 + rr <= d.R)
                 {
                     const gptr<int> p = xbase + (size_t)k * 16u * (size_t)(d.ld - 1) + kBlk * b;
-                    if (xc >= 1 && xc <= cols && xc + 3 <= ce)
-                        *(gptr<int4a>)p = int4a {t[4 * k], t[4 * k + 1], t[4 * k + 2], t[4 * k + 3]};
-                    else if ((xc >= 1 && xc <= cols) || (cb == 0 && xc + 3 >= 1 && xc <= 0))
+                    if (xc >= lo && xc + 3 <= hi)
+                        st_out(p, int4a {t[4 * k], t[4 * k + 1], t[4 * k + 2], t[4 * k + 3]});
+                    else if (xc + 3 >= lo && xc <= hi)
                     {
 #pragma unroll
                         for (int e = 0; e < 4; ++e)
-                            if (xc + e >= 1 && xc + e <= ce) p[e] = t[4 * k + e];
+                            if (xc + e >= lo && xc + e <= hi) p[e] = t[4 * k + e];
                     }
                 }
             }
     };
-    using T = std::integral_constant<bool, true>;
-    using F = std::integral_constant<bool, false>;
+    using MR = std::integral_constant<int, kRamp>;
+    using MH = std::integral_constant<int, kHold>;
+    using MP = std::integral_constant<int, kPair>;
+    using ME = std::integral_constant<int, kEdge>;
     int b = 0;
     for (; b < 64 / kBlk; b += 2)
     {
-        block(b, qA, qB, T());
-        block(b + 1, qB, qA, T());
+        block(b, qA, qB, MR());
+        block(b + 1, qB, qA, MR());
+    }
+    // interior blocks (uniform): every lane's chunks inside its row's range, every row <= R
+    // (blocks 4 .. (hiMax - 15) / 16); in pairs
+    const int bInt = r0 + 63 <= d.R ? (hiMax - (kBlk - 1)) / kBlk : 3;  // last interior block
+    for (; b + 1 <= bInt; b += 2)
+    {
+        block(b, qA, qB, MH());
+        block(b + 1, qB, qA, MP());
     }
     for (; b < NB; b += 2)
     {
-        block(b, qA, qB, F());
-        if (b + 1 < NB) block(b + 1, qB, qA, F());
+        block(b, qA, qB, ME());
+        if (b + 1 < NB) block(b + 1, qB, qA, ME());
     }
 #if GSA_EXPAND_PROBE == 2
     if (sink == 0x7fffffff) G(d.score)[0] = sink;
@@ -265,24 +332,45 @@ __device__ __forceinline__ void ex_prep(const ExpandArgs& a, const ExpandPair& d
     const ExLds L = ex_layout(a.substsz, WAVES);
     const int jT = tt % d.colTiles, rc = tt / d.colTiles;
     const int cb = ex_cb(d, jT), cols = ex_cols(d, jT);
-    for (int k = threadIdx.x; k < a.substsz * kSubRow; k += 64 * WAVES)
+    // (every global load of the task's prep is issued before the first one is used: a load waits
+    // behind the wave's outstanding stores of the previous task, so dependent load/use loops paid
+    // that wait once per iteration -- 25 per thread in the profile build)
+    constexpr int kQCols = kExpTW + kExtra;
+    constexpr int kSubIt = (32 * kSubRow + 64 * WAVES - 1) / (64 * WAVES);
+    constexpr int kColIt = (kQCols + 64 * WAVES - 1) / (64 * WAVES);
+    int sv[kSubIt], xv[kColIt];
+#pragma unroll
+    for (int i = 0; i < kSubIt; ++i)
     {
+        const int k = (int)threadIdx.x + 64 * WAVES * i;
         const int x = k / kSubRow, yy = k % kSubRow;
-        lds_st(L.sub + 4u * k, yy < a.substsz ? G(a.subst)[yy * a.substsz + x] - a.g : 0);
+        sv[i] = (k < a.substsz * kSubRow && yy < a.substsz) ? G(a.subst)[yy * a.substsz + x] - a.g : 0;
+    }
+#pragma unroll
+    for (int i = 0; i < kColIt; ++i)
+    {
+        const int c = cb + 1 + (int)threadIdx.x + 64 * WAVES * i;
+        int x = ((int)threadIdx.x + 64 * WAVES * i < kQCols && c <= d.C) ? G(d.seqX)[c] : 0;
+        xv[i] = ((unsigned)x < (unsigned)a.substsz) ? x : 0;
+    }
+#pragma unroll
+    for (int i = 0; i < kSubIt; ++i)
+    {
+        const int k = (int)threadIdx.x + 64 * WAVES * i;
+        if (k < a.substsz * kSubRow) lds_st(L.sub + 4u * k, sv[i]);
     }
     if (threadIdx.x < 16) lds_st(L.gfill + 4u * threadIdx.x, a.g);
     __syncthreads();
-    // column profile of the tile column: Q[y][kQOff + j] = s(y, X[cb + j]) - g, j = 1..kExpTW + 4
-    // (the tile and the 3 columns past it, for the chunks that straddle its end; columns past C:
-    // letter 0, never stored)
-    constexpr int kQCols = kExpTW + 4;
-    for (int k = threadIdx.x; k < a.substsz * kQCols; k += 64 * WAVES)
+    // column profile of the tile column: Q[y][kQOff + j] = s(y, X[cb + j]) - g, j = 1..kExpTW + kExtra
+    // (the tile and the columns its parallelogram reaches past it; columns past C: letter 0, never
+    // stored), one column per thread
+#pragma unroll
+    for (int i = 0; i < kColIt; ++i)
     {
-        const int yy = k / kQCols, j = k % kQCols + 1;
-        const int c = cb + j;
-        int x = c <= d.C ? G(d.seqX)[c] : 0;
-        x = ((unsigned)x < (unsigned)a.substsz) ? x : 0;
-        lds_st(L.q + 4u * (uint32_t)(yy * kQS + kQOff + j), lds_ld(L.sub + 4u * (uint32_t)(x * kSubRow + yy)));
+        const int j = (int)threadIdx.x + 64 * WAVES * i + 1;
+        if (j <= kQCols)
+            for (int yy = 0; yy < a.substsz; ++yy)
+                lds_st(L.q + 4u * (uint32_t)(yy * kQS + kQOff + j), lds_ld(L.sub + 4u * (uint32_t)(xv[i] * kSubRow + yy)));
     }
     __syncthreads();
     // the matrix headers H(i, 0) = i g, H(0, j) = j g: column 0 of the chunk's rows (first tile
@@ -323,6 +411,354 @@ __device__ __forceinline__ void ex_task(const ExpandArgs& a, const ExpandPair& d
 
 // a word of the expansion's LDS that ex_prep / ex_tiles never write (expand_lds_bytes counts it)
 __host__ __device__ inline uint32_t ex_word(int substsz, int waves) { return ex_layout(substsz, waves).gfill + 64u; }
+
+
+// ------------------------------------------------------------------------------------
+// The streamed expansion (round 6).  A task's inputs -- its column letters and, for each tile wave,
+// its 64 row letters, left boundary column and top row -- are global loads, and a wave's global load
+// waits for every store that wave issued before it (vmcnt retires in order).  A tile wave that
+// fetched its next task's inputs itself drained its whole store queue first, so each CU's store
+// stream stopped at every task: at 100k x 100k the fused fill's workgroups spent 25-33 % of the
+// expansion between tasks (profiles/r06_fused100k.txt).  Here a workgroup of W waves has W - 1
+// tile waves and one loader wave: the loader claims tasks, (FUSED) waits until pass 1 has written
+// their rows, and stages their inputs in one of two LDS slots; the tile waves build the task's
+// column profile from the slot (LDS only), compute and store -- they never load from global memory
+// and never wait for their stores.  A task is (W - 1) x 64 rows of one tile column.
+// ------------------------------------------------------------------------------------
+constexpr int kSlotHdr = 32;             // dwords: task (-1: no more), pair, tt, then the ExpandPair
+constexpr int kSlotX = kExpTW + kExtra;  // letters of columns cb + 1 .. cb + kExpTW + kExtra
+constexpr int kTileDw = 2 * kExpRows + kTopS;  // per tile wave: y[64], lb[64], top row[kTopS]
+static_assert(sizeof(ExpandPair) % 4 == 0 && 3 + (int)(sizeof(ExpandPair) / 4) <= kSlotHdr, "slot header");
+
+struct ExLdsS
+{
+    uint32_t q, sub, gfill, ctl, slot, slotB;
+};
+// profile Q, subT (kept for the launch), the row of g, control words, two task slots
+__host__ __device__ inline ExLdsS ex_layout_s(int substsz, int nw)
+{
+    ExLdsS L;
+    L.q = 0;
+    L.sub = (uint32_t)substsz * kQS * 4u;
+    L.gfill = L.sub + (((uint32_t)substsz * kSubRow * 4u + 15u) & ~15u);
+    L.ctl = L.gfill + 64u;
+    L.slot = L.ctl + 64u;
+    L.slotB = ((uint32_t)(kSlotHdr + kSlotX + nw * kTileDw) * 4u + 15u) & ~15u;
+    return L;
+}
+__host__ __device__ inline uint32_t ex_stream_lds(int substsz, int nw)
+{
+    const ExLdsS L = ex_layout_s(substsz, nw);
+    return L.slot + 2u * L.slotB;
+}
+
+// LDS words shared by the waves: relaxed workgroup-scope atomics (a single wave's LDS operations
+// execute in order, so a word written after the data it publishes is never seen before it)
+__device__ __forceinline__ int xs_ld(uint32_t a)
+{
+    return __builtin_amdgcn_readfirstlane(
+        __hip_atomic_load((int*)__builtin_assume_aligned(xsm + a, 4), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+}
+__device__ __forceinline__ void xs_st(uint32_t a, int v)
+{
+    asm volatile("" ::: "memory");
+    __hip_atomic_store((int*)__builtin_assume_aligned(xsm + a, 4), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    asm volatile("" ::: "memory");
+}
+__device__ __forceinline__ void xs_add(uint32_t a, int v)
+{
+    asm volatile("" ::: "memory");
+    __hip_atomic_fetch_add((int*)__builtin_assume_aligned(xsm + a, 4), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    asm volatile("" ::: "memory");
+}
+// wait until the LDS word reaches v; false (error word set) after a.spin ticks without it, or when
+// another wave has set the error word (a global load: looked at every 256th idle pass only)
+__device__ __forceinline__ bool xs_wait(const ExpandArgs& a, uint32_t w, int v)
+{
+    if (xs_ld(w) >= v) return true;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    for (unsigned n = 1;; ++n)
+    {
+        __builtin_amdgcn_s_sleep(1);
+        if (xs_ld(w) >= v) return true;
+        if (__builtin_amdgcn_s_memrealtime() - t0 > a.spin ||
+            ((n & 255) == 0 && __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0))
+        {
+            atomicOr(a.err, 1u);
+            return false;
+        }
+    }
+}
+
+__device__ __forceinline__ ExpandPair ex_desc_lds(uint32_t a)
+{
+    constexpr int N = sizeof(ExpandPair) / 4;
+    union
+    {
+        int v[N];
+        ExpandPair d;
+    } u;
+#pragma unroll
+    for (int k = 0; k < N; ++k) u.v[k] = __builtin_amdgcn_readfirstlane(lds_ld(a + 4u * k));
+    return u.d;
+}
+
+// FUSED: the pass-1 strips' progress words (nw_krow.hip kr_strip, PT 3) and this launch's epoch;
+// tstamps: per task [claimed, ready, done] (GSA_STAMPS) or null
+struct ExFused
+{
+    const unsigned long long* xdone;
+    unsigned epoch;
+    unsigned long long* tstamps;
+};
+
+// All W waves of the workgroup (after a barrier: the LDS is reused).  counter: the task claims.
+template <int W, bool FUSED>
+__device__ __forceinline__ void ex_stream(const ExpandArgs& a, unsigned* counter, const ExFused& f, int w, int lane)
+{
+    constexpr int NW = W - 1;
+    const ExLdsS L = ex_layout_s(a.substsz, NW);
+    const uint32_t RDY = L.ctl, DONE = L.ctl + 8u, BAR = L.ctl + 16u;
+    for (int k = threadIdx.x; k < a.substsz * kSubRow; k += 64 * W)
+    {
+        const int x = k / kSubRow, yy = k % kSubRow;
+        lds_st(L.sub + 4u * k, yy < a.substsz ? G(a.subst)[yy * a.substsz + x] - a.g : 0);
+    }
+    if (threadIdx.x < 16)
+    {
+        lds_st(L.gfill + 4u * threadIdx.x, a.g);
+        lds_st(L.ctl + 4u * threadIdx.x, 0);
+    }
+    __syncthreads();
+    if (w == NW)
+    {
+        // ---- the loader wave ----
+        for (int k = 0;; ++k)
+        {
+            const int s = k & 1, gen = (k >> 1) + 1;
+            const uint32_t slot = L.slot + (uint32_t)s * L.slotB;
+            // the slot's previous task is done with it
+            bool ok = k < 2 || xs_wait(a, DONE + 4u * s, NW * (gen - 1));
+            unsigned t = (unsigned)a.nTasks;
+            if (ok && lane == 0)
+                t = __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ? (unsigned)a.nTasks
+                                                                                           : atomicAdd(counter, 1u);
+            const int task = __builtin_amdgcn_readfirstlane((int)t);
+            int lo = 0, tt = -1;
+            ExpandPair d;
+            int jT = 0, rc = 0, cb = 0, cols = 0;
+            if (task < a.nTasks)
+            {
+                if (a.sched)
+                {
+                    lo = __builtin_amdgcn_readfirstlane(G(a.sched)[2 * task]);
+                    tt = __builtin_amdgcn_readfirstlane(G(a.sched)[2 * task + 1]);
+                }
+                else
+                {
+                    int hi = a.nPairs - 1;
+                    while (lo < hi)
+                    {
+                        const int mid = (lo + hi + 1) >> 1;
+                        if (__builtin_amdgcn_readfirstlane(G(a.pairs)[mid].taskBase) <= task)
+                            lo = mid;
+                        else
+                            hi = mid - 1;
+                    }
+                }
+                d = ex_desc(a.pairs + lo);
+                if (tt < 0) tt = task - d.taskBase;
+                jT = tt % d.colTiles;
+                rc = tt / d.colTiles;
+                cb = ex_cb(d, jT);
+                cols = ex_cols(d, jT);
+                if constexpr (FUSED)
+                {
+                    // pass 1 has stored rows 64m, m = NW rc .. NW rc + NW - 1, at the columns the
+                    // tiles read, and the header column cb for their rows: the words of strips
+                    // (NW rc - 1) / 4 .. (NW (rc + 1) - 1) / 4 (256 rows each) reach `need`
+                    unsigned long long* ts = f.tstamps ? f.tstamps + 3 * (size_t)task : nullptr;
+                    if (ts && lane == 0) ts[0] = __builtin_amdgcn_s_memrealtime();
+                    const unsigned need = (unsigned)(min(cb + cols + kExtra, d.C) + 1);
+                    const int s1 = min((NW * (rc + 1) - 1) / 4, d.p1Strips - 1);
+                    const unsigned long long* words = f.xdone + d.p1Strip0;
+                    uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+                    for (int sx = rc > 0 ? (NW * rc - 1) / 4 : 0; sx <= s1 && ok;)
+                    {
+                        const unsigned long long v = __hip_atomic_load(words + sx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        if ((unsigned)(v >> 32) == f.epoch && (unsigned)v >= need)
+                        {
+                            ++sx;
+                            t0 = __builtin_amdgcn_s_memrealtime();
+                            continue;
+                        }
+                        __builtin_amdgcn_s_sleep(2);
+                        if (__builtin_amdgcn_s_memrealtime() - t0 > a.spin ||
+                            __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)
+                        {
+                            if (lane == 0) atomicOr(a.err, 1u);
+                            ok = false;
+                        }
+                    }
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                    if (ts && lane == 0) ts[1] = __builtin_amdgcn_s_memrealtime();
+                }
+            }
+            if (!ok || task >= a.nTasks)
+            {
+                // no more tasks (or an error): the tile waves stop at this slot
+                if (lane == 0) lds_st(slot, -1);
+                xs_st(RDY + 4u * s, gen);
+                return;
+            }
+            // Every input of the task in one round trip: all loads issued (<= 44 per lane, within the
+            // 63 that vmcnt tracks) before the first LDS write.  Under the chip's store stream a load
+            // takes microseconds, and a loader that waited tile by tile fell behind the tile waves.
+            const int ce = min(cols + kExtra, d.C - cb);
+            constexpr int kXIt = (kSlotX + 63) / 64;
+            constexpr int kTIt = (kExpTW + kExtra + 1 + 255) / 256;  // top-row dwordx4 loads per tile
+            int xv[kXIt], yv[NW], lbv[NW];
+            int4v tv[NW][kTIt];
+#pragma unroll
+            for (int i = 0; i < kXIt; ++i)
+            {
+                const int j = lane + 64 * i, c = cb + 1 + j;
+                xv[i] = (j < kSlotX && c <= d.C) ? G(d.seqX)[c] : 0;
+            }
+#pragma unroll
+            for (int i = 0; i < NW; ++i)
+            {
+                const int r0 = rc * NW * kExpRows + kExpRows * i + 1;
+                const int r = r0 + lane;
+                yv[i] = (r <= d.R) ? G(d.seqY)[r] : 0;
+                if (cb == 0 || r0 > d.R)
+                    lbv[i] = r * a.g;
+                else
+                {
+                    // (element r - iT tBy of the pass-1 header column; rows up to the last tile row's
+                    // end are computed there, padding included)
+                    const int iT = (r - 1) / kSparseTileBy;
+                    lbv[i] = G(d.hcol)[((size_t)iT * (size_t)d.tcols + (size_t)(cb / kExpHB)) * (size_t)(kSparseTileBy + 1) +
+                                       (size_t)(r - iT * kSparseTileBy)];
+                }
+                // the top row, pass-1 row 64m (m >= 1), 4 columns per lane per load: cb and the row
+                // buffer's pitch and pad are multiples of 16 ints, and the chunk that passes ce stays
+                // in the row's right pad (columns up to Cp + 63)
+                const int m = (r0 - 1) / kExpRows;
+                const gptr<const int4v> rowp =
+                    (gptr<const int4v>)(G(d.rows64) + (size_t)(m > 0 ? m - 1 : 0) * (size_t)d.rpitch + kRowsPad + cb);
+#pragma unroll
+                for (int q = 0; q < kTIt; ++q)
+                {
+                    const int j = 4 * lane + 256 * q;
+                    tv[i][q] = (m == 0 || r0 > d.R || j > ce) ? int4v {0, 0, 0, 0} : rowp[lane + 64 * q];
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < kXIt; ++i)
+                if (lane + 64 * i < kSlotX)
+                    lds_st(slot + 4u * (uint32_t)(kSlotHdr + lane + 64 * i), ((unsigned)xv[i] < (unsigned)a.substsz) ? xv[i] : 0);
+#pragma unroll
+            for (int i = 0; i < NW; ++i)
+            {
+                const int r0 = rc * NW * kExpRows + kExpRows * i + 1;
+                if (r0 > d.R) break;
+                const uint32_t tb = slot + 4u * (uint32_t)(kSlotHdr + kSlotX + i * kTileDw);
+                lds_st(tb + 4u * (uint32_t)lane, ((unsigned)yv[i] < (unsigned)a.substsz) ? yv[i] : 0);
+                lds_st(tb + 4u * (uint32_t)(kExpRows + lane), lbv[i]);
+                const int m = (r0 - 1) / kExpRows;
+#pragma unroll
+                for (int q = 0; q < kTIt; ++q)
+                {
+                    const int j = 4 * lane + 256 * q;
+                    if (j <= ce)
+                    {
+                        int4v o;
+#pragma unroll
+                        for (int e = 0; e < 4; ++e)
+                        {
+                            const int c = cb + j + e;
+                            o[e] = (m == 0 ? c * a.g : tv[i][q][e] + (kExpRows * m + c) * a.g) + a.g;
+                        }
+                        *(int4v*)(xsm + tb + 4u * (uint32_t)(2 * kExpRows + j)) = o;
+                    }
+                }
+            }
+            {
+                constexpr int N = sizeof(ExpandPair) / 4;
+                const int* dw = (const int*)&d;
+                int dv = 0;
+#pragma unroll
+                for (int q = 0; q < N; ++q)
+                    if (lane == q) dv = dw[q];
+                if (lane < N) lds_st(slot + 4u * (uint32_t)(3 + lane), dv);
+                if (lane == 0)
+                {
+                    lds_st(slot, task);
+                    lds_st(slot + 4u, lo);
+                    lds_st(slot + 8u, tt);
+                }
+            }
+            xs_st(RDY + 4u * s, gen);
+        }
+    }
+    // ---- tile waves ----
+    const int tid = w * 64 + lane;
+    int barGen = 0;
+    auto bar = [&]() {
+        ++barGen;
+        if (lane == 0) xs_add(BAR, 1);
+        return xs_wait(a, BAR, NW * barGen);
+    };
+    for (int k = 0;; ++k)
+    {
+        const int s = k & 1, gen = (k >> 1) + 1;
+        const uint32_t slot = L.slot + (uint32_t)s * L.slotB;
+        if (!xs_wait(a, RDY + 4u * s, gen)) return;
+        const int task = xs_ld(slot);
+        if (task < 0) return;
+        const int tt = xs_ld(slot + 8u);
+        const ExpandPair d = ex_desc_lds(slot + 12u);
+        const int jT = tt % d.colTiles, rc = tt / d.colTiles;
+        const int cb = ex_cb(d, jT), cols = ex_cols(d, jT);
+        // the profile is free once every tile wave is done with the previous task
+        if (!bar()) return;
+        for (int j = tid + 1; j <= kSlotX; j += NW * 64)
+        {
+            // subT row x, 4 letters per read (rows are 36 dwords: 16-byte aligned)
+            const int x = lds_ld(slot + 4u * (uint32_t)(kSlotHdr + j - 1));
+            int4v sv[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+                if (4 * i < a.substsz) sv[i] = lds_ld4(L.sub + 4u * (uint32_t)(x * kSubRow + 4 * i));
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    if (4 * i + e < a.substsz) lds_st(L.q + 4u * (uint32_t)((4 * i + e) * kQS + kQOff + j), sv[i][e]);
+        }
+        if (!bar()) return;
+        // the matrix headers H(i, 0) = i g, H(0, j) = j g the task owns
+        const int kChunk = NW * kExpRows;
+        if (cb == 0)
+            for (int r = rc * kChunk + 1 + tid; r <= min(d.R, rc * kChunk + kChunk); r += NW * 64)
+                G(d.score)[(size_t)r * (size_t)d.ld] = r * a.g;
+        if (rc == 0)
+        {
+            for (int c = cb + 1 + tid; c <= cb + cols; c += NW * 64) G(d.score)[c] = c * a.g;
+            if (cb == 0 && tid == 0) G(d.score)[0] = 0;
+        }
+        const int r0 = rc * kChunk + kExpRows * w + 1;
+        if (r0 <= d.R && cb < d.C && !(a.knob & 1))
+        {
+            const uint32_t tb = slot + 4u * (uint32_t)(kSlotHdr + kSlotX + w * kTileDw);
+            ex_tile_core(a, d, L.q, L.gfill, lane, cb, cols, r0, lds_ld(tb + 4u * (uint32_t)lane),
+                         lds_ld(tb + 4u * (uint32_t)(kExpRows + lane)), tb + 4u * (uint32_t)(2 * kExpRows));
+        }
+        if (FUSED && f.tstamps && w == 0 && lane == 0) f.tstamps[3 * (size_t)task + 2] = __builtin_amdgcn_s_memrealtime();
+        if (lane == 0) xs_add(DONE + 4u * s, 1);
+    }
+}
 
 }  // namespace xdev
 }  // namespace gsa

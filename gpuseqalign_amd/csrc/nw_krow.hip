@@ -41,6 +41,11 @@
 // super-strips (workgroups) the drain wave moves the last row through 8-byte {epoch, H'}
 // granules in HBM (sc1 atomics), polled by the next super-strip's loader wave
 // (MI355X_MICROARCH.md, handoff-1to1).  Every wait is bounded (StripArgs::spin, error word).
+#ifndef GSA_FX_VMCNT
+// fused full fill: a strip publishes every 16 blocks what its stores older than its last GSA_FX_VMCNT
+// vector-memory operations cover (>= 4 per block: blocks <= b - GSA_FX_VMCNT / 4)
+#define GSA_FX_VMCNT 16
+#endif
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -435,8 +440,8 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
                 // vector-memory operations complete covers blocks <= b - 4: row 64m columns
                 // < 16 (b - 7) (block bb stores columns <= 16 (bb - 4) + 15 of its 4 rows) and the
                 // header columns captured by block b - 4 (boundaries <= 16 (b - 7))
-                asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-                fx_publish((unsigned)(kBlk * (b - 7)));
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GSA_FX_VMCNT) : "memory");
+                fx_publish((unsigned)(kBlk * (b - GSA_FX_VMCNT / 4 - 3)));
             }
         if (CAP && cap)
         {
@@ -2050,86 +2055,31 @@ __global__ void __launch_bounds__(64 * W) nw_full_fused_kernel(StripArgs a)
             if (sst && lane == 0) sst[2 * w + 1] = __builtin_amdgcn_s_memrealtime();
         }
     }
-    // pass 2: task tt of a pair is tile column jT of row chunk rc (cm = W xmt tiles of 64 rows).  Its
-    // waves read rows 64m, m = cm rc .. cm rc + cm - 1, at columns < need, and (jT > 0) the header
-    // column of boundary 2 jT for rows 64 cm rc + 1 .. 64 cm (rc + 1): the pair's strips
-    // (cm rc - 1) / 4 .. (cm (rc + 1) - 1) / 4 (256 rows each), words >= need
-    // (the task's profile is built before its wait: it reads no pass-1 output; the claim and ready
-    // words live where the expansion's LDS never writes)
-    const ExpandArgs xa {a.subst, a.substsz, a.g, a.xpair, a.nPairs, a.xTasks, a.xsched, a.xknob, nullptr, a.xmt};
-    const uint32_t xw = xdev::ex_word(a.substsz, W);
-    for (;;)
-    {
-        __syncthreads();
-        if (threadIdx.x == 0) lds_st(xw, err_set(a) ? a.xTasks : (int)atomicAdd(a.xcounter, 1u));
-        __syncthreads();
-        const int task = __builtin_amdgcn_readfirstlane(lds_ld(xw));
-        if (task >= a.xTasks) break;
-        int lo = 0, tt = -1;
-        if (a.xsched)
-        {
-            lo = __builtin_amdgcn_readfirstlane(G(a.xsched)[2 * task]);
-            tt = __builtin_amdgcn_readfirstlane(G(a.xsched)[2 * task + 1]);
-        }
-        else
-        {
-            int hi = a.nPairs - 1;
-            while (lo < hi)
-            {
-                const int mid = (lo + hi + 1) >> 1;
-                if (__builtin_amdgcn_readfirstlane(G(a.xpair)[mid].taskBase) <= task)
-                    lo = mid;
-                else
-                    hi = mid - 1;
-            }
-        }
-        const ExpandPair xd = xdev::ex_desc(a.xpair + lo);
-        if (tt < 0) tt = task - xd.taskBase;
-        xdev::ex_prep<W>(xa, xd, tt);
-        unsigned long long* tstamp = a.stamps ? a.stamps + 2 * (size_t)a.nTicketsTotal * NS + 3 * (size_t)task : nullptr;
-        if (threadIdx.x == 0)
-        {
-            if (tstamp) tstamp[0] = __builtin_amdgcn_s_memrealtime();
-            const int jT = tt % xd.colTiles, rc = tt / xd.colTiles;
-            const int cb = ex_cb(xd, jT);
-            const unsigned need = (unsigned)(min(cb + ex_cols(xd, jT) + 3, xd.C) + 1);  // row-buffer columns < need
-            const int cm = W * a.xmt;  // 64-row tiles per chunk
-            const int s1 = min((cm * (rc + 1) - 1) / 4, xd.p1Strips - 1);
-            const unsigned long long* words = a.xdone + xd.p1Strip0;
-            bool ok = true;
-            uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-            for (int s = rc > 0 ? (cm * rc - 1) / 4 : 0; s <= s1 && ok;)
-            {
-                const unsigned long long v = __hip_atomic_load(words + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if ((unsigned)(v >> 32) == a.epoch && (unsigned)v >= need)
-                {
-                    ++s;
-                    t0 = __builtin_amdgcn_s_memrealtime();
-                    continue;
-                }
-                __builtin_amdgcn_s_sleep(2);  // (s_sleep 32 between polls: same time)
-                if (__builtin_amdgcn_s_memrealtime() - t0 > a.spin || err_set(a))
-                {
-                    atomicOr(a.err, 1u);
-                    ok = false;
-                }
-            }
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            lds_st(xw + 4u, ok ? 0 : 1);
-            if (tstamp) tstamp[1] = __builtin_amdgcn_s_memrealtime();
-        }
-        __syncthreads();
-        if (__builtin_amdgcn_readfirstlane(lds_ld(xw + 4u))) break;
-        xdev::ex_tiles<W>(xa, xd, tt, w, lane);
-        if (tstamp && threadIdx.x == 0) tstamp[2] = __builtin_amdgcn_s_memrealtime();  // (wave 0's tile)
-    }
+    // pass 2: the streamed expansion (nw_expand_dev.h ex_stream): W - 1 tile waves and a loader wave
+    // that claims the tasks in the host's order, waits until the pass-1 strips of a task's rows have
+    // published its columns (their progress words), and stages its inputs in LDS
+    __syncthreads();  // (pass 1's LDS is dead)
+    ExpandArgs xa {};
+    xa.subst = a.subst;
+    xa.substsz = a.substsz;
+    xa.g = a.g;
+    xa.pairs = a.xpair;
+    xa.nPairs = a.nPairs;
+    xa.nTasks = a.xTasks;
+    xa.sched = a.xsched;
+    xa.knob = a.xknob;
+    xa.mt = 1;
+    xa.spin = a.spin;
+    xa.err = a.err;
+    const xdev::ExFused fx {a.xdone, a.epoch, a.stamps ? a.stamps + 2 * (size_t)a.nTicketsTotal * NS : nullptr};
+    xdev::ex_stream<W, true>(xa, a.xcounter, fx, w, lane);
 }
 
 template <int NS, int W, bool Q8>
 hipError_t launch_fused1(const StripArgs& a, int grid, hipStream_t stream, bool foot)
 {
-    const size_t lds = std::max(krow_lds_bytes(NS, 1024, a.substsz, Q8), expand_lds_bytes(a.substsz, W));
+    static_assert(W == kExpStreamWaves, "the streamed expansion's workgroup");
+    const size_t lds = std::max(krow_lds_bytes(NS, 1024, a.substsz, Q8), expand_stream_lds_bytes(a.substsz));
     auto kern = nw_full_fused_kernel<NS, W, Q8>;
     constexpr int kThreads = 64 * W;
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -2165,7 +2115,6 @@ hipError_t launch_full_fused(const StripArgs& a, int ns, int waves, int grid, hi
 {
     if (!a.xpair || !a.xdone || !a.xrole || !a.xcounter) return hipErrorInvalidValue;
     if (ns == 4 && waves == 8) return launch_fused<4, 8>(a, grid, stream);
-    if (ns == 8 && waves == 12) return launch_fused<8, 12>(a, grid, stream);
     return hipErrorInvalidValue;
 }
 #elif defined(GSA_KROW_CO)

@@ -300,25 +300,18 @@ def test_full_fill_kernels(engine, golden, kernel, R, C, monkeypatch):
     assert np.array_equal(r.score, S) and r.align_cost == cost
 
 
-@pytest.mark.parametrize("fused", ["0", "2"])
 @pytest.mark.parametrize("ns", ["4", "8"])
 @pytest.mark.parametrize("name,gapo", [("blosum45", -5), ("blosum80", -30), ("blosum62", 3), ("blosum50", -70)])
-def test_twopass_tables_and_batches(engine, golden, fused, ns, name, gapo, monkeypatch):
+def test_twopass_tables_and_batches(engine, golden, ns, name, gapo, monkeypatch):
     """The two-pass fill of a batch in both pass-1 geometries (4 strips: 1024-row tickets, 8 strips:
-    2048-row tickets, GSA_KROW_NS), in two launches and fused into one (GSA_FULL_FUSED=2; with 3
-    pass-1 workgroups for two of the tables, GSA_FUSED_P1, so most tasks wait on tickets not yet
-    taken; the other two with 3 tiles per wave per expansion task, GSA_EXPAND_MT), other tables and
-    gap costs (a positive gap included; at gap -70 s - 2g leaves int8 and pass 1 runs its int16
-    instance), pitched layout, every word of every pair against the oracle."""
+    2048-row tickets, GSA_KROW_NS) and the streamed expansion (a loader wave staging each task's
+    inputs for 7 tile waves), other tables and gap costs (a positive gap included; at gap -70
+    s - 2g leaves int8 and pass 1 runs its int16 instance), pitched layout, every word of every pair
+    against the oracle, and the words around each matrix untouched."""
     import torch
     monkeypatch.setenv("GSA_FULL_KERNEL", "twopass")
     monkeypatch.setenv("GSA_KROW_NS", ns)
-    monkeypatch.setenv("GSA_FULL_FUSED", fused)
-    if name in ("blosum45", "blosum80"):
-        monkeypatch.setenv("GSA_FUSED_P1", "3")
-    else:
-        monkeypatch.setenv("GSA_EXPAND_MT", "3")  # 3 tiles per wave per expansion task
-        monkeypatch.setenv("GSA_EXPAND_WAVES", "8")  # (two launches: 8-wave expansion workgroups)
+    monkeypatch.setenv("GSA_FULL_FUSED", "0")
     sub = golden.subst_data.matrix(name)
     pairs = [random_pair(r, c, 7 * r + c, alphabet=25) for r, c in ((2100, 900), (1, 5), (700, 2500), (64, 64), (4097, 300))]
     dev = torch.device("cuda:0")
@@ -346,8 +339,6 @@ def test_fused_tables_pitched_repeated(engine, golden, name, gapo, monkeypatch):
     import torch
     monkeypatch.setenv("GSA_FULL_KERNEL", "twopass")
     monkeypatch.setenv("GSA_FULL_FUSED", "1")
-    if gapo == 3:
-        monkeypatch.setenv("GSA_EXPAND_MT", "2")
     sub = golden.subst_data.matrix(name)
     dev = torch.device("cuda:0")
     s = torch.from_numpy(np.ascontiguousarray(sub, dtype=np.int32)).to(dev)
@@ -373,92 +364,34 @@ def test_fused_tables_pitched_repeated(engine, golden, name, gapo, monkeypatch):
                 assert (out[:off] == -7).all() and (out[off + n:] == -7).all()
 
 
-PIPE_PAIRS = ((2100, 900), (700, 2500), (64, 64), (4097, 300), (1500, 1500), (65, 3000), (3000, 65), (257, 513),
-              (1, 400), (1025, 1))
-
-
-@pytest.mark.parametrize("pitched", [True, False])
-@pytest.mark.parametrize("groups", ["2", "3", "4"])
-@pytest.mark.parametrize("name,gapo", [("blosum62", -11), ("blosum80", -30), ("blosum62", 3), ("blosum50", -70)])
-def test_pipelined_full_batch(engine, golden, groups, name, gapo, pitched, monkeypatch):
-    """The pipelined full batch (gsa_capi.hip enqueue_full_pipelined, GSA_FULL_PIPE groups): group 0's
-    pass 1 alone, then each group's expansion (persistent 12-wave workgroups) while the next group's
-    pass 1 runs on the side stream in 4-wave (2, 2) workgroups (nw_krowco.hip); other tables and gaps
-    (-70: the co-resident pass 1's int16 instance behind the declining int8 one; +3: a positive gap),
-    pitched and unpadded, two launches back to back on one stream (a stale row buffer or header
-    column would show), every word of every pair against the oracle.  (Pairs without interior cells
-    take the two-launch path: they are checked here too, as the batch they end up in.)"""
+def test_split_batch_single_pair_group(engine, golden, monkeypatch):
+    """a split batch (GSA_FULL_SPLIT=1) whose group A is one pair, with the fused
+    single-pair fill left at its default: the groups' passes stay ordered by their events (a fused
+    group A recorded none, and group B's pass 1 and expansion then raced it).  Group A: one pair of
+    exactly one round of (8, 4) tickets (cu_count x 2048 rows, 100 columns); group B: two pairs of
+    20 tickets.  Every word of every pair against the oracle, on two launches."""
     import torch
     monkeypatch.setenv("GSA_FULL_KERNEL", "twopass")
-    monkeypatch.setenv("GSA_FULL_FUSED", "0")
-    monkeypatch.setenv("GSA_FULL_PIPE", groups)
-    sub = golden.subst_data.matrix(name)
-    pairs = [random_pair(r, c, 5 * r + c, alphabet=25) for r, c in PIPE_PAIRS[:8]]
-    dev = torch.device("cuda:0")
-    s = torch.from_numpy(np.ascontiguousarray(sub, dtype=np.int32)).to(dev)
-    ins = [(torch.from_numpy(Y).to(dev), torch.from_numpy(X).to(dev)) for Y, X in pairs]
-    lds = [gsa.full_pitch(len(X)) if pitched else len(X) for _, X in pairs]
-    off = 31 if pitched else 0
-    bufs = [torch.full((len(Y) * ld + 64,), -7, dtype=torch.int32, device=dev) for (Y, _), ld in zip(pairs, lds)]
-    engine.set_full_timing(True)
-    try:
-        for rep in range(2):
-            engine.fill_batch_dev([(y.data_ptr(), len(y), x.data_ptr(), len(x), b.data_ptr() + 4 * off)
-                                   for (y, x), b in zip(ins, bufs)], s.data_ptr(), 25, gapo, mode="full",
-                                  lds=lds if pitched else None)
-        t = engine.last_full_timing()
-    finally:
-        engine.set_full_timing(False)
-    engine.sync()
-    assert t["pipelined_groups"] == min(int(groups), len(pairs)) and t["pass1_ms"] > 0 and t["pass2_ms"] > 0
-    for (Y, X), b, ld in zip(pairs, bufs, lds):
-        out = b.cpu().numpy()
-        M = out[off:off + len(Y) * ld].reshape(len(Y), ld)
-        S, _ = oracle.fill_full(Y, X, sub, gapo)
-        assert np.array_equal(M[:, :len(X)], S)
-        assert (out[:off] == -7).all() and (out[off + len(Y) * ld:] == -7).all()
-
-
-def test_pipelined_full_batch_edges(engine, golden, monkeypatch):
-    """A batch with pairs that have no interior cells (1 x n, m x 1) is not pipelined (the two-launch
-    path fills it); every word still equals the oracle."""
-    import torch
-    monkeypatch.setenv("GSA_FULL_KERNEL", "twopass")
-    monkeypatch.setenv("GSA_FULL_PIPE", "4")
-    pairs = [random_pair(r, c, 3 * r + c) for r, c in PIPE_PAIRS]
+    monkeypatch.delenv("GSA_FULL_FUSED", raising=False)
+    monkeypatch.delenv("GSA_KROW_NS", raising=False)
+    monkeypatch.delenv("GSA_EXPAND_RR", raising=False)
+    monkeypatch.setenv("GSA_FULL_SPLIT", "1")
+    cu = int(engine.cu_count)
+    shapes = [(cu * 2048, 100), (40960, 300), (40960, 257)]
+    pairs = [random_pair(r, c, 3 * r + c) for r, c in shapes]
+    ref = [oracle.fill_full(Y, X, golden.blosum62, -11)[0] for Y, X in pairs]
     dev = torch.device("cuda:0")
     s = torch.from_numpy(golden.blosum62).to(dev)
     ins = [(torch.from_numpy(Y).to(dev), torch.from_numpy(X).to(dev)) for Y, X in pairs]
-    bufs = [torch.full((len(Y) * len(X),), -7, dtype=torch.int32, device=dev) for Y, X in pairs]
-    engine.fill_batch_dev([(y.data_ptr(), len(y), x.data_ptr(), len(x), b.data_ptr()) for (y, x), b in zip(ins, bufs)],
-                          s.data_ptr(), 25, -11, mode="full")
-    engine.sync()
-    for (Y, X), b in zip(pairs, bufs):
-        S, _ = oracle.fill_full(Y, X, golden.blosum62, -11)
-        assert np.array_equal(b.cpu().numpy().reshape(len(Y), len(X)), S)
-
-
-def test_pipelined_full_batch_group0_eight_strips(engine, golden, monkeypatch):
-    """Group 0 with more 1024-row tile rows than CUs runs its pass 1 on (8, 4) tickets (2048 rows, the
-    batch geometry), the other groups on the co-resident (2, 2) tickets: tall narrow pairs, 2 groups,
-    every word against the oracle."""
-    import torch
-    monkeypatch.setenv("GSA_FULL_KERNEL", "twopass")
-    monkeypatch.setenv("GSA_FULL_FUSED", "0")
-    monkeypatch.setenv("GSA_FULL_PIPE", "2")
-    pairs = [random_pair(r, c, 11 * k + 1) for k, (r, c) in enumerate([(41000, 260)] * 14 + [(3000, 3000)] * 2)]
-    dev = torch.device("cuda:0")
-    s = torch.from_numpy(golden.blosum62).to(dev)
-    ins = [(torch.from_numpy(Y).to(dev), torch.from_numpy(X).to(dev)) for Y, X in pairs]
-    lds = [gsa.full_pitch(len(X)) for _, X in pairs]
-    bufs = [torch.full((len(Y) * ld + 64,), -7, dtype=torch.int32, device=dev) for (Y, _), ld in zip(pairs, lds)]
-    engine.fill_batch_dev([(y.data_ptr(), len(y), x.data_ptr(), len(x), b.data_ptr() + 4 * 31)
-                           for (y, x), b in zip(ins, bufs)], s.data_ptr(), 25, -11, mode="full", lds=lds)
-    engine.sync()
-    for (Y, X), b, ld in zip(pairs, bufs, lds):
-        M = b.cpu().numpy()[31:31 + len(Y) * ld].reshape(len(Y), ld)
-        S, _ = oracle.fill_full(Y, X, golden.blosum62, -11)
-        assert np.array_equal(M[:, :len(X)], S)
+    bufs = [torch.empty((len(Y) * len(X),), dtype=torch.int32, device=dev) for Y, X in pairs]
+    for launch in range(2):
+        for b in bufs:
+            b.fill_(-7)
+        engine.fill_batch_dev([(y.data_ptr(), len(y), x.data_ptr(), len(x), b.data_ptr())
+                               for (y, x), b in zip(ins, bufs)], s.data_ptr(), 25, -11, mode="full")
+        engine.sync()
+        for (Y, X), b, S in zip(pairs, bufs, ref):
+            assert np.array_equal(b.cpu().numpy().reshape(len(Y), len(X)), S), launch
 
 
 @pytest.mark.parametrize("order", ["tuned", "0", "1", "2", "3"])

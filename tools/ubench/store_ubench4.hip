@@ -1,0 +1,158 @@
+// store_ubench4.hip -- store-only rate of the full-matrix expansion's write pattern on one large
+// matrix (pass 2 of the two-pass full fill, nw_expand_dev.h): tasks of W waves x 64 rows x TW
+// columns claimed from a counter by persistent workgroups; a wave writes its 64 rows x TW columns
+// in pairs of 16-column blocks, each block as 4 dwordx4 instructions of 16 rows x 64 B (the
+// transposed lane-fill shape), the even and odd block of a pair back to back so each 128-B line
+// leaves whole.  Question answered: how fast can this pattern write a 100k x 100k matrix (400 KB
+// row pitch) against a 20k-wide one, by task order, task width and waves per CU.
+// Build: hipcc --offload-arch=gfx950 -O3 store_ubench4.hip -o store_ubench4
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+#include <algorithm>
+#include <vector>
+typedef int int4a __attribute__((ext_vector_type(4), aligned(4)));
+
+// order 0: row-chunk-major (all tile columns of chunk 0, then chunk 1...); 1: tile-column-major;
+// 2: anti-diagonals of (chunk, tile column) weighted as the fused fill's ready time.
+// SHAPE 0: 16 rows x 64 B per instruction (pairs); 1: 8 rows x 128 B; 2: 4 rows x 256 B
+template <int SHAPE, int DELAY = 0, int RAMP = 0>
+__global__ void kern(int* out, long long ld, int R, int C, int TW, int W, const int* sched, unsigned* counter,
+                     int nChunks, int nTiles)
+{
+    __shared__ int task;
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int nTasks = nChunks * nTiles;
+    for (;;)
+    {
+        __syncthreads();
+        if (threadIdx.x == 0) task = (int)atomicAdd(counter, 1u);
+        __syncthreads();
+        const int t = task;
+        if (t >= nTasks) break;
+        const int rc = sched[2 * t], jT = sched[2 * t + 1];
+        const long long r0 = (long long)rc * W * 64 + w * 64 + 1;
+        if (r0 + 63 >= R) continue;
+        const long long cb = (long long)jT * TW;
+        int4a v = {lane, lane + 1, lane + 2, lane + 3};
+        if (RAMP > 0)
+        {
+            // the expansion's ramp: RAMP blocks of compute before the first store (RAMP / 2 pairs)
+            int acc = v[0];
+            for (int q = 0; q < RAMP / 2 * DELAY; ++q) acc = __builtin_amdgcn_update_dpp(0, acc, 0x138, 0xF, 0xF, true) + q;
+            v[1] += acc;
+        }
+        for (int b = 0; b + 1 < TW / 16 && cb + 16 * b + 32 <= C; b += 2)
+        {
+            if (DELAY > 0)
+            {
+                // a dependent VALU chain between store bursts (the expansion's 2 blocks of compute)
+                int acc = v[0];
+#pragma unroll
+                for (int q = 0; q < DELAY; ++q) acc = __builtin_amdgcn_update_dpp(0, acc, 0x138, 0xF, 0xF, true) + q;
+                v[1] += acc;
+            }
+            if (SHAPE == 0)
+            {
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+#pragma unroll
+                    for (int h = 0; h < 2; ++h)
+                    {
+                        const long long rr = r0 + 16 * k + (lane & 15);
+                        const long long c = cb + 16 * (b + h) + 4 * (lane >> 4);
+                        *(int4a*)(out + rr * ld + c) = v;
+                        v += 1;
+                    }
+            }
+            else if (SHAPE == 1)
+            {
+#pragma unroll
+                for (int k = 0; k < 8; ++k)
+                {
+                    const long long rr = r0 + 8 * k + (lane >> 3);
+                    const long long c = cb + 16 * b + 4 * (lane & 7);
+                    *(int4a*)(out + rr * ld + c) = v;
+                    v += 1;
+                }
+            }
+            else if ((b & 3) == 0 && cb + 16 * b + 64 <= C)
+            {
+#pragma unroll
+                for (int k = 0; k < 16; ++k)
+                {
+                    const long long rr = r0 + 4 * k + (lane >> 4);
+                    const long long c = cb + 16 * b + 4 * (lane & 15);
+                    *(int4a*)(out + rr * ld + c) = v;
+                    v += 1;
+                }
+            }
+        }
+        if (RAMP > 0)
+        {
+            int acc = v[0];
+            for (int q = 0; q < RAMP / 2 * DELAY; ++q) acc = __builtin_amdgcn_update_dpp(0, acc, 0x138, 0xF, 0xF, true) + q;
+            if (acc == 0x7fffffff) out[0] = acc;
+        }
+    }
+}
+
+int main(int argc, char** argv)
+{
+    const int R = argc > 1 ? atoi(argv[1]) : 99968;
+    const int C = argc > 2 ? atoi(argv[2]) : 99968;
+    const long long ldAdd = argc > 3 ? atoll(argv[3]) : 32;
+    const long long ld = ((C + 31) / 32) * 32 + ldAdd;  // (a multiple of 32 + ldAdd)
+    int* out = nullptr;
+    const size_t bytes = (size_t)(R + 64) * ld * 4 + 4096;
+    if (hipMalloc(&out, bytes) != hipSuccess) { printf("alloc failed\n"); return 1; }
+    unsigned* counter;
+    hipMalloc(&counter, 4);
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    int dev = 0, cus = 0;
+    hipGetDevice(&dev);
+    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    auto run = [&](auto k, const char* shape, int W, int TW, int order, int wgPerCu) {
+        const int nChunks = (R - 1) / (W * 64), nTiles = C / TW;
+        const size_t lds = wgPerCu == 1 ? 100000 : 0;
+        std::vector<int> hs;
+        std::vector<std::pair<long long, int>> key;
+        for (int rc = 0; rc < nChunks; ++rc)
+            for (int j = 0; j < nTiles; ++j)
+            {
+                const long long kk = order == 0 ? (long long)rc * nTiles + j : order == 1 ? (long long)j * nChunks + rc
+                                                                                       : (long long)rc * 400 + (long long)j * TW;
+                key.push_back({kk, rc * nTiles + j});
+            }
+        std::stable_sort(key.begin(), key.end());
+        for (auto& q : key) { hs.push_back(q.second / nTiles); hs.push_back(q.second % nTiles); }
+        int* sched = nullptr;
+        hipMalloc(&sched, hs.size() * 4);
+        hipMemcpy(sched, hs.data(), hs.size() * 4, hipMemcpyHostToDevice);
+        hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 100000);
+        float best = 1e9;
+        for (int rep = 0; rep < 3; ++rep)
+        {
+            hipMemsetAsync(counter, 0, 4);
+            hipEventRecord(e0);
+            hipLaunchKernelGGL(k, cus * wgPerCu, 64 * W, lds, 0, out, ld, R, C, TW, W, sched, counter, nChunks, nTiles);
+            hipEventRecord(e1);
+            hipEventSynchronize(e1);
+            float ms;
+            hipEventElapsedTime(&ms, e0, e1);
+            best = ms < best ? ms : best;
+        }
+        hipFree(sched);
+        const double wbytes = (double)nChunks * W * 64 * (double)nTiles * TW * 4;
+        printf("R %d C %d ld %lld shape %s W %2d x %d/CU TW %5d order %d: %8.3f ms %8.1f GB/s\n", R, C, ld, shape, W,
+               wgPerCu, TW, order, best, wbytes / best / 1e6);
+    };
+    run(kern<0, 128>, "16x64 d128", 8, 512, 2, 1);
+    run(kern<0, 128, 8>, "16x64 d128 ramp8", 8, 512, 2, 1);
+    run(kern<0, 128, 8>, "16x64 d128 ramp8", 7, 512, 2, 1);
+    run(kern<0, 128, 8>, "16x64 d128 ramp8 tw2048", 8, 2048, 2, 1);
+    run(kern<0, 256, 8>, "16x64 d256 ramp8", 8, 512, 2, 1);
+    return 0;
+}
