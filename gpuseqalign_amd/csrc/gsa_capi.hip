@@ -99,6 +99,7 @@ struct gsa_ctx
         float ms[2] = {-1.f, -1.f};
         int last = -1;
         bool pending = false;
+        bool cold = true;  // the first launch on a key runs untimed (fresh pages, first-touch costs)
         hipEvent_t ev[2] = {nullptr, nullptr};
     } xt[2];  // per scratch slot
     // a batch that can run as two pair groups (enqueue_full_split): whole-job times of the four
@@ -109,6 +110,7 @@ struct gsa_ctx
         float ms[4] = {-1.f, -1.f, -1.f, -1.f};
         int last = -1;
         bool pending = false;
+        bool cold = true;  // the first launch on a key runs untimed (fresh pages, first-touch costs)
         hipEvent_t ev[2] = {nullptr, nullptr};
     } ft;
     // score-only NW from both ends (score_bidi): tap rows of both halves, the reversed sequences, the
@@ -747,8 +749,7 @@ struct FusedLaunch
 // tickets of all pairs (pair-major).  `pairs` holds device pointers.
 int enqueue_batch(gsa_ctx* ctx, int mode, int npairs, const gsa_pair_dev* pairs, const int32_t* subst, int32_t substsz,
                   int32_t gapo, int32_t tileBx, hipStream_t st, unsigned long long* done = nullptr, int ptChunk = 0,
-                  const int32_t* lds = nullptr, int* const* rows64 = nullptr, const FusedLaunch* fused = nullptr,
-                  bool co = false)
+                  const int32_t* lds = nullptr, int* const* rows64 = nullptr, const FusedLaunch* fused = nullptr)
 {
     if (npairs < 1 || !pairs || !subst) return GSA_ERROR_INVALID_VALUE;
     if (substsz < 1 || substsz > 32) return GSA_ERROR_INVALID_VALUE;  // LDS profile holds <= 32 letters
@@ -774,7 +775,6 @@ int enqueue_batch(gsa_ctx* ctx, int mode, int npairs, const gsa_pair_dev* pairs,
     {
         krowK = 4;
         krowNS = fused ? fused->ns : env_int("GSA_KROW_NS", (npairs > 1 && !fitsChip) ? 8 : 4) == 8 ? 8 : 4;
-        if (co) krowK = krowNS = 2;  // the pipelined batch's co-resident instance
     }
     // mlsppt flags one ticket per tile row: only the geometry whose ticket is one tile row
     if (!gsa::krow_ok(krowNS, krowK) || (done && gsa::krow_ticket_rows(krowNS, krowK) != gsa::kSparseTileBy))
@@ -932,7 +932,7 @@ int enqueue_batch(gsa_ctx* ctx, int mode, int npairs, const gsa_pair_dev* pairs,
             a.xsched = fused->xa->sched;
             a.xTasks = fused->xa->nTasks;
             a.xknob = fused->xa->knob;
-            a.xmt = fused->xa->mt;
+            a.xrun = fused->xa->run;
             a.xP = fused->p1;
             a.xrole = ctx->ctl + 4;
             a.xcounter = ctx->ctl + 5;
@@ -963,11 +963,8 @@ int enqueue_batch(gsa_ctx* ctx, int mode, int npairs, const gsa_pair_dev* pairs,
     if (e != hipSuccess) return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
     // one pair: one workgroup per CU (its tickets are a chain); a batch: all resident slots
     int grid = (npairs == 1) ? std::max(1, std::min((int)tickets, ctx->cu_count)) : 0;
-    // (the co-resident pass 1: one workgroup per CU, beside an expansion workgroup)
-    if (co) grid = std::max(1, std::min((int)tickets, ctx->cu_count));
     e = lane     ? gsa::launch_lane_fill(a, a.ns, grid, st)
         : fused  ? gsa::launch_full_fused(a, fused->ns, fused->waves, 0, st)
-        : co     ? gsa::launch_krow_fill_co(a, grid, st)
         : rows64 ? gsa::launch_krow_fill_xr(a, krowNS, grid, st)
         : krow   ? gsa::launch_krow_fill(a, krowNS, krowK, 0, grid, st)
                  : gsa::launch_strip_fill(a, mode, grid, st);
@@ -1131,6 +1128,7 @@ int enqueue_full_twopass(gsa_ctx* ctx, int npairs, const gsa_pair_dev* pairs, co
             xt.tasks = tasks;
             xt.ms[0] = xt.ms[1] = -1.f;
             xt.pending = false;
+            xt.cold = true;
         }
         // (the tuning is best effort: an event that cannot be created or read ends it on order 1)
         bool evOk = true;
@@ -1140,94 +1138,123 @@ int enqueue_full_twopass(gsa_ctx* ctx, int npairs, const gsa_pair_dev* pairs, co
                 xt.ev[k] = nullptr;
                 evOk = false;
             }
-        if (xt.pending)
+        // the previous candidate's time, if its launch has ended: the host never waits for it (a
+        // launch still running keeps the measurement pending and this one runs untimed)
+        bool busy = false;
+        if (xt.pending && evOk)
         {
+            const hipError_t q = hipEventQuery(xt.ev[1]);
             float ms = -1.f;
-            if (hipEventSynchronize(xt.ev[1]) != hipSuccess ||
-                hipEventElapsedTime(&ms, xt.ev[0], xt.ev[1]) != hipSuccess || !(ms >= 0.f))
+            if (q == hipErrorNotReady)
+            {
+                (void)hipGetLastError();
+                busy = true;
+            }
+            else if (q != hipSuccess || hipEventElapsedTime(&ms, xt.ev[0], xt.ev[1]) != hipSuccess || !(ms >= 0.f))
             {
                 (void)hipGetLastError();
                 evOk = false;
             }
             else
                 xt.ms[xt.last] = ms;
+            if (!busy) xt.pending = false;
+        }
+        if (!evOk)
+        {
+            xt.ms[0] = xt.ms[1] = 0.f;  // both "measured": order 1 from now on
             xt.pending = false;
         }
-        if (!evOk) xt.ms[0] = xt.ms[1] = 0.f;  // both "measured": order 1 from now on
         const int next = xt.ms[0] < 0 ? 0 : xt.ms[1] < 0 ? 1 : (xt.ms[1] < xt.ms[0] ? 1 : 0);
-        tuneRecord = xt.ms[next] < 0;
-        xt.last = next;
+        tuneRecord = !busy && !xt.cold && xt.ms[next] < 0;
+        xt.cold = false;
+        if (tuneRecord) xt.last = next;
         rr = next + 1;
     }
+    // The schedule: runs of xRun tasks of one tile column of one pair, consecutive row chunks (a
+    // workgroup claims a run; its tile waves rebuild the column profile only when the tile column
+    // changes: the rebuild and its two barriers stop the workgroup's store stream, ~10 % of the
+    // expansion at 100k one task at a time, profiles/r06_expand_probes.txt), padded with (-1, 0)
+    // entries to whole runs.  Runs in order: a single pair by when their pass-1 rows arrive (the
+    // fused fill; it helps two launches too), a batch round-robin over the pairs (rr 1; rr 2
+    // rotated, 0 pair-major, 3 shuffled).
+    const int xRun = std::min(16, std::max(1, env_int("GSA_EXPAND_RUN", 4)));
     std::vector<int> xs;
-    if (npairs > 1 && rr)
     {
-        std::vector<int> ord((size_t)npairs);
-        for (int p = 0; p < npairs; ++p) ord[(size_t)p] = p;
-        auto ntask = [&](int p) { return ex[(size_t)p].colTiles * ex[(size_t)p].rowChunks; };
-        std::stable_sort(ord.begin(), ord.end(), [&](int x, int y) { return ntask(x) > ntask(y); });
-        xs.reserve(2 * (size_t)tasks);
-        // rr 2: pair k of the order starts k / npairs of the way into its tasks (rr 4: k / 2npairs);
-        // rr 5: each pair's tasks from its last; rr 6: every other pair from its last (probes)
-        std::vector<long long> rot((size_t)npairs, 0);
-        if (rr == 2 || rr == 4)
-            for (int k = 0; k < npairs; ++k)
-                rot[(size_t)ord[(size_t)k]] = (long long)ntask(ord[(size_t)k]) * k / (rr == 2 ? npairs : 2 * npairs);
-        for (int j = 0; j < ntask(ord[0]); ++j)
-            for (int k = 0; k < npairs; ++k)
-            {
-                const int p = ord[(size_t)k];
-                if (ntask(p) <= j) break;
-                const bool rev = rr == 5 || (rr == 6 && (k & 1));
-                xs.push_back(p);
-                xs.push_back(rev ? ntask(p) - 1 - j : (int)((j + rot[(size_t)p]) % ntask(p)));
-            }
-        if (rr == 3)
+        struct Run { int p, g, jT; };
+        auto runs_of = [&](int p) { return ((ex[(size_t)p].rowChunks + xRun - 1) / xRun) * ex[(size_t)p].colTiles; };
+        auto run_at = [&](int p, long long r) { const int ct = ex[(size_t)p].colTiles; return Run {p, (int)(r / ct), (int)(r % ct)}; };
+        std::vector<Run> order;
+        if (npairs == 1)
         {
-            // (probe): the whole schedule shuffled, pairs of ints kept together (fixed seed)
-            uint64_t z = 0x9e3779b97f4a7c15ull;
-            const size_t n = xs.size() / 2;
-            for (size_t i = n; i > 1; --i)
+            // Task (rc, jT) can start once strip s1 = the last of its rows' strips has passed column
+            // cb + cols + 64; strip s starts ~s lag steps after strip 0 and sweeps a column per
+            // step, so it is ready at about s1 lag + cb + cols.  Row-chunk-major order made the first
+            // workgroups wait for whole rows: at 100k they claimed row chunk 0's tiles to the far end
+            // of the matrix, ready only ~4 ms later (profiles/r06_fused100k.txt).  lag = columns per
+            // 256-row strip, GSA_FUSED_LAG (default 192: the 100k pair's strip-to-strip spacing).
+            const gsa::ExpandPair& d = ex[0];
+            const long long lag = std::max(1, env_int("GSA_FUSED_LAG", 192));
+            const int cm = xWaves * xmt;
+            std::vector<std::pair<long long, long long>> key;
+            for (long long r = 0; r < runs_of(0); ++r)
             {
-                z += 0x9e3779b97f4a7c15ull;
-                uint64_t r = z;
-                r = (r ^ (r >> 30)) * 0xbf58476d1ce4e5b9ull;
-                r = (r ^ (r >> 27)) * 0x94d049bb133111ebull;
-                r ^= r >> 31;
-                const size_t k = (size_t)(r % i);
-                std::swap(xs[2 * (i - 1)], xs[2 * k]);
-                std::swap(xs[2 * (i - 1) + 1], xs[2 * k + 1]);
+                const Run u = run_at(0, r);
+                const long long s1 = std::min<long long>((cm * (u.g * xRun + 1) - 1) / 4, d.p1Strips - 1);
+                key.push_back({s1 * lag + gsa::ex_cb(d, u.jT) + gsa::ex_cols(d, u.jT), r});
+            }
+            std::stable_sort(key.begin(), key.end());
+            for (const auto& k : key) order.push_back(run_at(0, k.second));
+        }
+        else if (rr == 0)
+        {
+            for (int p = 0; p < npairs; ++p)
+                for (long long r = 0; r < runs_of(p); ++r) order.push_back(run_at(p, r));
+        }
+        else
+        {
+            std::vector<int> ord((size_t)npairs);
+            for (int p = 0; p < npairs; ++p) ord[(size_t)p] = p;
+            std::stable_sort(ord.begin(), ord.end(), [&](int x, int y) { return runs_of(x) > runs_of(y); });
+            // rr 2: pair k of the order starts k / npairs of the way into its runs
+            std::vector<long long> rot((size_t)npairs, 0);
+            if (rr == 2)
+                for (int k = 0; k < npairs; ++k)
+                    rot[(size_t)ord[(size_t)k]] = runs_of(ord[(size_t)k]) * k / npairs;
+            for (long long j = 0; j < runs_of(ord[0]); ++j)
+                for (int k = 0; k < npairs; ++k)
+                {
+                    const int p = ord[(size_t)k];
+                    if (runs_of(p) <= j) break;
+                    order.push_back(run_at(p, (j + rot[(size_t)p]) % runs_of(p)));
+                }
+            if (rr == 3)
+            {
+                // the whole schedule shuffled (fixed seed)
+                uint64_t z = 0x9e3779b97f4a7c15ull;
+                for (size_t i = order.size(); i > 1; --i)
+                {
+                    z += 0x9e3779b97f4a7c15ull;
+                    uint64_t q = z;
+                    q = (q ^ (q >> 30)) * 0xbf58476d1ce4e5b9ull;
+                    q = (q ^ (q >> 27)) * 0x94d049bb133111ebull;
+                    q ^= q >> 31;
+                    std::swap(order[i - 1], order[(size_t)(q % i)]);
+                }
+            }
+        }
+        xs.reserve(2 * order.size() * (size_t)xRun);
+        for (const Run& u : order)
+        {
+            const gsa::ExpandPair& d = ex[(size_t)u.p];
+            for (int i = 0; i < xRun; ++i)
+            {
+                const int rc = u.g * xRun + i;
+                xs.push_back(rc < d.rowChunks ? u.p : -1);
+                xs.push_back(rc < d.rowChunks ? rc * d.colTiles + u.jT : 0);
             }
         }
     }
-    if (npairs == 1 && ex[0].rowChunks > 1 && env_int("GSA_SINGLE_ORDER", 1))
-    {
-        // The fused single pair's tasks in the order their pass-1 rows arrive.  Task (rc, jT) can
-        // start once strip s1 = the last of its rows' strips has passed column cb + cols + 64; strip s
-        // starts ~s lag steps after strip 0 and sweeps a column per step, so it is ready at about
-        // s1 lag + cb + cols.  Row-chunk-major order (the descriptor order) made the first workgroups
-        // wait for whole rows: at 100k they claimed row chunk 0's tiles to the far end of the
-        // matrix, ready only ~4 ms later (profiles/r06_stamps100k.txt).  lag = columns per 256-row
-        // strip, GSA_FUSED_LAG (default 192: the 100k pair's measured strip-to-strip spacing).
-        const gsa::ExpandPair& d = ex[0];
-        const long long lag = std::max(1, env_int("GSA_FUSED_LAG", 192));
-        const int cm = xWaves * xmt;
-        std::vector<std::pair<long long, int>> key((size_t)d.rowChunks * d.colTiles);
-        for (int rc = 0; rc < d.rowChunks; ++rc)
-            for (int jT = 0; jT < d.colTiles; ++jT)
-            {
-                const long long s1 = std::min<long long>((cm * (rc + 1) - 1) / 4, d.p1Strips - 1);
-                const int tt = rc * d.colTiles + jT;
-                key[(size_t)tt] = {s1 * lag + gsa::ex_cb(d, jT) + gsa::ex_cols(d, jT), tt};
-            }
-        std::stable_sort(key.begin(), key.end());
-        xs.reserve(2 * key.size());
-        for (const auto& k : key)
-        {
-            xs.push_back(0);
-            xs.push_back(k.second);
-        }
-    }
+    const long long nEntries = (long long)(xs.size() / 2);
     const size_t descBytes = ((size_t)npairs * sizeof(gsa::ExpandPair) + 15) & ~(size_t)15;
     const size_t exBytes = descBytes + xs.size() * sizeof(int);
     if (exdesc_cap < exBytes || !exdesc)
@@ -1263,17 +1290,17 @@ int enqueue_full_twopass(gsa_ctx* ctx, int npairs, const gsa_pair_dev* pairs, co
     xa.g = gapo;
     xa.pairs = (const gsa::ExpandPair*)exdesc;
     xa.nPairs = npairs;
-    xa.nTasks = (int)tasks;
-    xa.sched = xs.empty() ? nullptr : (const int*)((char*)exdesc + descBytes);
+    xa.nTasks = (int)nEntries;
+    xa.run = xRun;
+    xa.sched = (const int*)((char*)exdesc + descBytes);
     xa.knob = env_int("GSA_EXPAND_KNOB", 0);
-    xa.mt = xmt;
     xa.spin = ctx->spin_ticks;
     xa.err = ctx->ctl + 1;
     // (a group of a split batch has a claim counter of its own: the two groups' expansions overlap)
     xa.counter = ctx->ctl + 8 + opt.slot;
     // the fused single pair: every workgroup takes pass-1 tickets first
     const FusedLaunch fl {&xa, ns, gsa::kExpStreamWaves, 1 << 30};
-    const int xGrid = (int)std::max<long long>(1, std::min<long long>(ctx->cu_count, tasks));
+    const int xGrid = (int)std::max<long long>(1, std::min<long long>(ctx->cu_count, (nEntries + xRun - 1) / xRun));
     // gsa_set_full_timing: events before pass 1, between the passes and after pass 2, and the
     // expansion's clock stamps (one per workgroup)
     const bool timed = ctx->timing && !opt.split;
@@ -1494,6 +1521,7 @@ int enqueue_full(gsa_ctx* ctx, int npairs, const gsa_pair_dev* pairs, const int3
                 ft.last = -1;
                 for (float& m : ft.ms) m = -1.f;
                 ft.pending = false;
+                ft.cold = true;
             }
             bool evOk = true;
             for (int k = 0; k < 2; ++k)
@@ -1503,24 +1531,37 @@ int enqueue_full(gsa_ctx* ctx, int npairs, const gsa_pair_dev* pairs, const int3
                     ft.ev[k] = nullptr;
                     evOk = false;
                 }
-            if (ft.pending)
+            // the previous candidate's time if its launch has ended (never a host wait: a launch
+            // still running keeps it pending, and this one runs untimed)
+            bool busy = false;
+            if (ft.pending && evOk)
             {
+                const hipError_t q = hipEventQuery(ft.ev[1]);
                 float ms = -1.f;
-                if (hipEventSynchronize(ft.ev[1]) != hipSuccess ||
-                    hipEventElapsedTime(&ms, ft.ev[0], ft.ev[1]) != hipSuccess || !(ms >= 0.f))
+                if (q == hipErrorNotReady)
+                {
+                    (void)hipGetLastError();
+                    busy = true;
+                }
+                else if (q != hipSuccess || hipEventElapsedTime(&ms, ft.ev[0], ft.ev[1]) != hipSuccess || !(ms >= 0.f))
                 {
                     (void)hipGetLastError();
                     evOk = false;
                 }
                 else
                     ft.ms[ft.last] = ms;
-                ft.pending = false;
+                if (!busy) ft.pending = false;
             }
             if (!evOk)
+            {
                 for (float& m : ft.ms) m = 0.f;  // all "measured": candidate 0 from now on
+                ft.pending = false;
+            }
             int next = 0;
             while (next < 4 && ft.ms[next] >= 0.f) ++next;
-            if (next == 4)
+            if (busy || ft.cold)
+                next = 0;  // (untimed: the first launch on fresh buffers, or a measurement pending)
+            else if (next == 4)
             {
                 next = 0;
                 for (int k = 1; k < 4; ++k)
@@ -1530,7 +1571,8 @@ int enqueue_full(gsa_ctx* ctx, int npairs, const gsa_pair_dev* pairs, const int3
                                  ft.ms[0], ft.ms[1], ft.ms[2], ft.ms[3], next);
                 ft.last = -1;
             }
-            const bool rec = ft.ms[next] < 0.f;
+            const bool rec = !busy && !ft.cold && ft.ms[next] < 0.f;
+            ft.cold = false;
             const int rr = (next & 1) + 1;
             int r;
             if (next >= 2)

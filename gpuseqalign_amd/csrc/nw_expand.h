@@ -14,10 +14,7 @@ constexpr int kExpHB = 256;       // pass-1 tile width (tBx): its header columns
 constexpr int kExpTW = 512;       // pass-2 tile width, a multiple of kExpHB (the header columns between
                                   // are recomputed: fewer ramp blocks per tile, 8 of 36)
 constexpr int kExpRows = 64;      // rows of a wave's tile (one per lane)
-constexpr int kExpWaves = 16;     // waves per workgroup: a 1024-row chunk of one tile column
 constexpr int kRowsPad = 64;      // left pad (columns) of the pass-1 row buffer
-constexpr int kExpFusedWaves = 8; // waves per workgroup of the fused single-pair fill (512-row chunks)
-constexpr int kExpFusedWavesBatch = 12;  // ... of the fused batch fill (768-row chunks; (8, 4) pass 1)
 constexpr unsigned kXDone = 0x3fffffffu;  // a pass-1 strip's progress word: the strip has finished
 
 // Pass-1 row buffer of a pair: row 64m (m = 1 .. 4 x strips of pass 1) as shifted values
@@ -37,7 +34,7 @@ struct ExpandPair
     const int* hcol;    // pass-1 tile header columns, tile-major, 1 + kSparseTileBy per tile, unshifted
     int tcols;          // pass-1 tile columns (tBx = kExpHB)
     int colTiles;       // ceil(C / kExpTW)
-    int rowChunks;      // ceil(R / (waves * kExpRows * mt)), waves = kExpWaves (kExpFusedWaves when fused)
+    int rowChunks;      // ceil(R / ((kExpStreamWaves - 1) kExpRows)): tasks of the tile waves' rows
     int taskBase;       // first workgroup task of this pair (colTiles * rowChunks tasks)
     int p1Strip0;       // fused fill: the pair's first pass-1 strip word (ticketBase x ns)
     int p1Strips;       // ... and its strip count (tickets x ns)
@@ -67,34 +64,26 @@ struct ExpandArgs
     const ExpandPair* pairs;
     int nPairs;
     int nTasks;
-    // round-robin over the pairs (task k of every pair, then task k+1): {pair, task within the pair}
-    // per workgroup, or null (pair-major by taskBase).  Workgroups in flight then write all the
-    // matrices of a batch at once, not one matrix's rows
+    // the schedule: {pair, task within the pair} per entry, in runs of `run` entries of one tile
+    // column (a claim takes a run; an entry of pair -1 is padding); nTasks = its entries
     const int* sched;
+    int run;
     int knob;  // probes only (GSA_EXPAND_KNOB): 1 = no tile computed or stored (results wrong)
-    // persistent launches: workgroups claim tasks from *counter (zeroed before the launch)
-    unsigned* counter;
-    int mt;  // tiles per wave per task: a task is waves x 64 x mt rows of one tile column
+    unsigned* counter;  // the run claims (zeroed before the launch)
     // measurement (gsa_set_full_timing): per workgroup, wave 0's s_memtime cycles (low word) and
     // s_memrealtime ticks (100 MHz, high word) from its start to its end; null = off
     unsigned long long* clk;
-    // streamed launches (launch_expand_stream): watchdog ticks (s_memrealtime) and the sticky error
-    // word of the context
+    // watchdog ticks (s_memrealtime) and the sticky error word of the context
     unsigned long long spin;
     unsigned* err;
 };
 
-size_t expand_lds_bytes(int substsz, int waves);
 // The streamed expansion (nw_expand_dev.h ex_stream): persistent workgroups of kExpStreamWaves waves,
 // kExpStreamWaves - 1 tile waves (tasks of (kExpStreamWaves - 1) x 64 rows) and one loader wave that
-// claims tasks from a.counter (zeroed before the launch) and stages their inputs in LDS, so the tile
-// waves only compute and store.  grid <= 0: one workgroup per CU.
+// claims runs of tasks from a.counter and stages their inputs in LDS, so the tile waves only compute
+// and store.  grid <= 0: one workgroup per CU.  Pair arrays and the schedule in device memory.
 constexpr int kExpStreamWaves = 8;
 size_t expand_stream_lds_bytes(int substsz);
 hipError_t launch_expand_stream(const ExpandArgs& a, hipStream_t stream, int grid);
-// one workgroup of `waves` (8, 16) waves per task; or, grid > 0, `grid` persistent workgroups of
-// `waves` (8, 12, 16) waves claiming tasks from a.counter.  rowChunks of every pair must be counted
-// in chunks of waves x kExpRows x mt rows.  Pair arrays in device memory.
-hipError_t launch_expand(const ExpandArgs& a, hipStream_t stream, int waves = kExpWaves, int grid = 0);
 
 }  // namespace gsa

@@ -14,9 +14,12 @@
 // A wave owns one tile, one row per lane, with the step of nw_lane.hip (unshifted values, 4 VALU
 // per cell): lane l owns row r0 + l and at step t works on column cb + t - l; columns <= cb are the
 // tile's left boundary (pass-1 header column), lane 0's row above is the tile's top row (pass-1
-// row buffer).  A workgroup = 8 waves = a 512-row chunk of one tile column, sharing one column
-// profile Q[y][j] = s(y, X[cb + j]) - g in LDS.  Output: the lane fill's transposed stores (16 rows
-// x 64 bytes per store instruction), 64-byte aligned in the pitched layout (gsa_full_pitch).
+// row buffer).  The tile is stored as a parallelogram (row r0 + rr over columns cb + 64 - rr ..
+// cb + cols + 63 - rr), so every 128-byte line of the pitched layout (gsa_full_pitch) belongs to
+// one tile and leaves whole: the transposed stores of nw_lane.hip, 16 rows x 64 bytes per
+// instruction, the two halves of each line back to back.  A workgroup = 7 tile waves (a 448-row
+// task of one tile column, sharing the column profile Q[y][j] = s(y, X[cb + j]) - g in LDS) and a
+// loader wave that stages each task's inputs (nw_expand_dev.h ex_stream).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -28,128 +31,6 @@ namespace gsa {
 namespace {
 
 using namespace xdev;
-
-// one workgroup per task: 16 waves or 8, one workgroup per CU either way (115.6 / 94.6 KB of LDS
-// since the parallelogram tiles), so 8 waves may use up to 256 VGPRs
-template <int WAVES>
-__global__ void __launch_bounds__(64 * WAVES, WAVES == 8 ? 2 : 4) nw_expand_kernel(ExpandArgs a)
-{
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    const int task = blockIdx.x;
-    // effective clock (gsa_set_full_timing): s_memtime counts shader cycles, s_memrealtime 100 MHz
-    // ticks; both scalar reads, waited for here, before any LDS traffic of the task
-    uint64_t c0 = 0, r0 = 0;
-    if (a.clk && w == 0)
-    {
-        c0 = __builtin_amdgcn_s_memtime();
-        r0 = __builtin_amdgcn_s_memrealtime();
-        __builtin_amdgcn_s_waitcnt(0xC07F);
-    }
-    int lo = 0, tt = -1;
-    if (a.sched)
-    {
-        lo = __builtin_amdgcn_readfirstlane(G(a.sched)[2 * task]);
-        tt = __builtin_amdgcn_readfirstlane(G(a.sched)[2 * task + 1]);
-    }
-    else
-    {
-        int hi = a.nPairs - 1;
-        while (lo < hi)
-        {
-            const int mid = (lo + hi + 1) >> 1;
-            if (__builtin_amdgcn_readfirstlane(G(a.pairs)[mid].taskBase) <= task)
-                lo = mid;
-            else
-                hi = mid - 1;
-        }
-    }
-    const ExpandPair d = ex_desc(a.pairs + lo);
-    if (tt < 0) tt = task - d.taskBase;
-    ex_task<WAVES>(a, d, tt, w, lane);
-    if (a.clk && w == 0)
-    {
-        const uint64_t c1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
-        __builtin_amdgcn_s_waitcnt(0xC07F);
-        if (lane == 0) G(a.clk)[task] = (uint64_t)(uint32_t)(c1 - c0) | ((uint64_t)(uint32_t)(r1 - r0) << 32);
-    }
-}
-
-template <int WAVES>
-hipError_t launch_pertask(const ExpandArgs& a, hipStream_t stream)
-{
-    const size_t lds = expand_lds_bytes(a.substsz, WAVES);
-    auto kern = nw_expand_kernel<WAVES>;
-    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return e;
-    if ((e = record_foot((const void*)kern, lds, 64 * WAVES, a.nTasks)) != hipSuccess) return e;
-    hipLaunchKernelGGL(kern, dim3(a.nTasks), dim3(64 * WAVES), lds, stream, a);
-    return hipGetLastError();
-}
-
-// persistent: `gridDim.x` workgroups claim tasks in schedule order until none is left
-template <int WAVES>
-__global__ void __launch_bounds__(64 * WAVES, 4) nw_expand_persist_kernel(ExpandArgs a)
-{
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    const uint32_t word = ex_word(a.substsz, WAVES);
-    uint64_t c0 = 0, r0 = 0;  // effective clock over the workgroup's life (gsa_set_full_timing)
-    if (a.clk && w == 0)
-    {
-        c0 = __builtin_amdgcn_s_memtime();
-        r0 = __builtin_amdgcn_s_memrealtime();
-        __builtin_amdgcn_s_waitcnt(0xC07F);
-    }
-    for (;;)
-    {
-        __syncthreads();
-        if (threadIdx.x == 0) lds_st(word, (int)atomicAdd(a.counter, 1u));
-        __syncthreads();
-        const int task = __builtin_amdgcn_readfirstlane(lds_ld(word));
-        if (task >= a.nTasks) break;
-        int lo = 0, tt = -1;
-        if (a.sched)
-        {
-            lo = __builtin_amdgcn_readfirstlane(G(a.sched)[2 * task]);
-            tt = __builtin_amdgcn_readfirstlane(G(a.sched)[2 * task + 1]);
-        }
-        else
-        {
-            int hi = a.nPairs - 1;
-            while (lo < hi)
-            {
-                const int mid = (lo + hi + 1) >> 1;
-                if (__builtin_amdgcn_readfirstlane(G(a.pairs)[mid].taskBase) <= task)
-                    lo = mid;
-                else
-                    hi = mid - 1;
-            }
-        }
-        const ExpandPair d = ex_desc(a.pairs + lo);
-        if (tt < 0) tt = task - d.taskBase;
-        ex_task<WAVES>(a, d, tt, w, lane);
-    }
-    if (a.clk && w == 0)
-    {
-        const uint64_t c1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
-        __builtin_amdgcn_s_waitcnt(0xC07F);
-        if (lane == 0) G(a.clk)[blockIdx.x] = (uint64_t)(uint32_t)(c1 - c0) | ((uint64_t)(uint32_t)(r1 - r0) << 32);
-    }
-}
-
-template <int WAVES>
-hipError_t launch_persist(const ExpandArgs& a, hipStream_t stream, int grid)
-{
-    const size_t lds = expand_lds_bytes(a.substsz, WAVES);
-    auto kern = nw_expand_persist_kernel<WAVES>;
-    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return e;
-    grid = std::min(grid, a.nTasks);
-    if ((e = record_foot((const void*)kern, lds, 64 * WAVES, grid)) != hipSuccess) return e;
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * WAVES), lds, stream, a);
-    return hipGetLastError();
-}
 
 // the streamed expansion (ex_stream): persistent, one workgroup per CU; wave 0 records the
 // workgroup's effective clock (gsa_set_full_timing)
@@ -196,21 +77,6 @@ hipError_t launch_expand_stream(const ExpandArgs& a, hipStream_t stream, int gri
     if ((e = record_foot((const void*)kern, lds, 64 * kExpStreamWaves, grid)) != hipSuccess) return e;
     hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * kExpStreamWaves), lds, stream, a);
     return hipGetLastError();
-}
-
-size_t expand_lds_bytes(int substsz, int waves) { return (size_t)xdev::ex_layout(substsz, waves).gfill + 128; }  // the row of g, the claim word
-
-hipError_t launch_expand(const ExpandArgs& a, hipStream_t stream, int waves, int grid)
-{
-    if (a.nTasks <= 0) return hipSuccess;
-    if (grid > 0)
-    {
-        if (!a.counter) return hipErrorInvalidValue;
-        return waves == 8 ? launch_persist<8>(a, stream, grid)
-               : waves == 12 ? launch_persist<12>(a, stream, grid)
-                             : launch_persist<16>(a, stream, grid);
-    }
-    return waves == 8 ? launch_pertask<8>(a, stream) : waves == 16 ? launch_pertask<16>(a, stream) : hipErrorInvalidValue;
 }
 
 }  // namespace gsa

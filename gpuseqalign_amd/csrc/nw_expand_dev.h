@@ -12,6 +12,13 @@
 #ifndef GSA_EXPAND_PROBE
 #define GSA_EXPAND_PROBE 0  // diagnostic builds only (tools/r05_xprobe.sh)
 #endif
+#if GSA_EXPAND_PROBE == 8 || GSA_EXPAND_PROBE == 9
+// (8: probe 7 and a loader that loads nothing from HBM; 9: probe 7 without the per-task profile
+// build and its two barriers)
+#define GSA_EXPAND_PROBE_STORES_ONLY 1
+#else
+#define GSA_EXPAND_PROBE_STORES_ONLY (GSA_EXPAND_PROBE == 7)
+#endif
 #ifndef GSA_EXPAND_STORE
 #define GSA_EXPAND_STORE 0  // matrix stores: 0 plain, 1 nontemporal, 2 write-through (sc1)
 #endif
@@ -62,24 +69,6 @@ __device__ __forceinline__ int4v lds_ld4(uint32_t a) { return *(const int4v*)(xs
 // lane l <- lane l-1, lane 0 <- 0 (DPP wave_shr:1, bound_ctrl zero)
 __device__ __forceinline__ int shr1z(int v) { return __builtin_amdgcn_update_dpp(0, v, 0x138, 0xF, 0xF, true); }
 
-struct ExLds
-{
-    uint32_t sub, q, top, gfill;
-};
-// LDS of a workgroup of `waves` tile waves: the column profile; subT, which only the profile build
-// reads, overlaid by one top row per wave; a row of g.  (94.6 KB for 8 waves and 25 letters, 115.6 KB
-// for 16: one workgroup per CU)
-__host__ __device__ inline ExLds ex_layout(int substsz, int waves)
-{
-    ExLds L;
-    L.q = 0;
-    L.sub = (uint32_t)substsz * kQS * 4u;
-    L.top = L.sub;
-    const uint32_t subB = (uint32_t)substsz * kSubRow * 4u, topB = (uint32_t)waves * kTopS * 4u;
-    L.gfill = L.top + (subB > topB ? subB : topB);
-    return L;
-}
-
 __device__ __forceinline__ ExpandPair ex_desc(const ExpandPair* p)
 {
     constexpr int N = sizeof(ExpandPair) / 4;
@@ -92,63 +81,6 @@ __device__ __forceinline__ ExpandPair ex_desc(const ExpandPair* p)
 #pragma unroll
     for (int k = 0; k < N; ++k) u.v[k] = __builtin_amdgcn_readfirstlane(G(wds)[k]);
     return u.d;
-}
-
-__device__ __forceinline__ void ex_tile_core(const ExpandArgs& a, const ExpandPair& d, uint32_t qbase, uint32_t gfill,
-                                             int lane, int cb, int cols, int r0, int y, int lb, uint32_t topw);
-
-// one 64-row x kExpTW-column tile of the full matrix, one row per lane
-__device__ __forceinline__ void ex_tile(const ExpandArgs& a, const ExpandPair& d, const ExLds& L, int w, int lane,
-                                        int cb, int cols, int r0)
-{
-    const int g = a.g;
-    // left boundary column cb of the tile, columns cb+1 .. cb+cols (ex_cb, ex_cols)
-    const int r = r0 + lane;
-    int y = (r <= d.R) ? G(d.seqY)[r] : 0;
-    y = ((unsigned)y < (unsigned)a.substsz) ? y : 0;
-    // left boundary H(r, cb): column 0, or the pass-1 header column of its tile (iT, cb / kExpHB)
-    // (element r - iT tBy; rows up to the last tile row's end are computed there, padding included)
-    int lb;
-    if (cb == 0 || GSA_EXPAND_PROBE == 3)
-        lb = r * g;
-    else
-    {
-        const int iT = (r - 1) / kSparseTileBy;
-        lb = G(d.hcol)[((size_t)iT * (size_t)d.tcols + (size_t)(cb / kExpHB)) * (size_t)(kSparseTileBy + 1) +
-                       (size_t)(r - iT * kSparseTileBy)];
-    }
-    // the last column this wave computes validly: kExtra past the tile (the parallelogram's right
-    // part), or the matrix's last
-    const int ce = min(cols + kExtra, d.C - cb);
-    // top row H(r0 - 1, cb .. cb + ce) + g into LDS: row 0, or pass-1 row 64m (shifted values)
-    const uint32_t topw = L.top + 4u * (uint32_t)(kTopS * w);
-    {
-        // all of the lane's loads in flight at once, then the LDS stores: a load waits behind the
-        // wave's outstanding stores (in-order vmcnt), so a loop of dependent load/store pairs paid
-        // that wait and the loaded-HBM latency once per iteration (9 per tile)
-        const int m = (r0 - 1) / kExpRows;
-        constexpr int kIt = (kExpTW + kExtra + 1 + 63) / 64;
-        int v[kIt];
-#pragma unroll
-        for (int i = 0; i < kIt; ++i)
-        {
-            const int j = lane + 64 * i, c = cb + j;
-#if GSA_EXPAND_PROBE == 3
-            // diagnostic build: no pass-1 row loads (results wrong)
-            v[i] = c;
-            (void)j;
-#else
-            v[i] = (m == 0 || j > ce) ? 0 : G(d.rows64)[(size_t)(m - 1) * (size_t)d.rpitch + kRowsPad + c];
-#endif
-        }
-#pragma unroll
-        for (int i = 0; i < kIt; ++i)
-        {
-            const int j = lane + 64 * i, c = cb + j;
-            if (j <= ce) lds_st(topw + 4u * (uint32_t)j, (m == 0 ? c * g : v[i] + (kExpRows * m + c) * g) + g);
-        }
-    }
-    ex_tile_core(a, d, L.q, L.gfill, lane, cb, cols, r0, y, lb, topw);
 }
 
 // the tile's recurrence and stores, its inputs in place: y = the lane's row letter, lb = its left
@@ -193,8 +125,9 @@ __device__ __forceinline__ void ex_tile_core(const ExpandArgs& a, const ExpandPa
         constexpr int MODE = decltype(modeT)::value;
         constexpr bool RAMP = MODE == kRamp;
         int4v hc[kH];
-#if GSA_EXPAND_PROBE == 6
-        // diagnostic build: no LDS reads and no recurrence, the stores alone (results wrong)
+#if GSA_EXPAND_PROBE == 6 || GSA_EXPAND_PROBE_STORES_ONLY
+        // diagnostic build: no LDS reads and no recurrence, the stores alone (7: no transposes either;
+        // results wrong)
 #pragma unroll
         for (int j = 0; j < kH; ++j) hc[j] = int4v {b, j, 1, 2};
 #pragma unroll
@@ -215,7 +148,7 @@ __device__ __forceinline__ void ex_tile_core(const ExpandArgs& a, const ExpandPa
         {
             const int up = shr1z(H) + hc[u >> 2][u & 3];
             const int t1 = U + qc[u];
-#if GSA_EXPAND_PROBE == 1 || GSA_EXPAND_PROBE == 6
+#if GSA_EXPAND_PROBE == 1 || GSA_EXPAND_PROBE == 6 || GSA_EXPAND_PROBE_STORES_ONLY
             // diagnostic build (tools/r05_xprobe.sh): no recurrence, one add per cell (results wrong)
             int h = t1;
 #else
@@ -229,6 +162,7 @@ __device__ __forceinline__ void ex_tile_core(const ExpandArgs& a, const ExpandPa
         int t[kBlk];
 #pragma unroll
         for (int e = 0; e < kBlk; ++e) t[e] = vals[e];
+#if !GSA_EXPAND_PROBE_STORES_ONLY
 #pragma unroll
         for (int k = 0; k < 2; ++k)
 #pragma unroll
@@ -247,6 +181,7 @@ __device__ __forceinline__ void ex_tile_core(const ExpandArgs& a, const ExpandPa
                 t[4 * k + dd] = sw[0];
                 t[4 * (k + 1) + dd] = sw[1];
             }
+#endif
         auto store4 = [&](int bb, int k, const int (&v)[kBlk]) {
             const gptr<int> ub = G(d.score) + ((ptrdiff_t)(r0 + 16 * k) * d.ld - 16 * k + kBlk * bb + cb);
 #if GSA_EXPAND_PROBE == 2
@@ -323,96 +258,6 @@ __device__ __forceinline__ void ex_tile_core(const ExpandArgs& a, const ExpandPa
 }
 
 
-// one task: the tile column jT of the `WAVES * kExpRows * a.mt`-row chunk rc of pair d (all threads
-// of the workgroup).  ex_prep: subT and the column profile into LDS, the matrix headers the task
-// owns -- none of it reads pass-1 output; ex_tiles: a.mt tiles per wave
-template <int WAVES>
-__device__ __forceinline__ void ex_prep(const ExpandArgs& a, const ExpandPair& d, int tt)
-{
-    const ExLds L = ex_layout(a.substsz, WAVES);
-    const int jT = tt % d.colTiles, rc = tt / d.colTiles;
-    const int cb = ex_cb(d, jT), cols = ex_cols(d, jT);
-    // (every global load of the task's prep is issued before the first one is used: a load waits
-    // behind the wave's outstanding stores of the previous task, so dependent load/use loops paid
-    // that wait once per iteration -- 25 per thread in the profile build)
-    constexpr int kQCols = kExpTW + kExtra;
-    constexpr int kSubIt = (32 * kSubRow + 64 * WAVES - 1) / (64 * WAVES);
-    constexpr int kColIt = (kQCols + 64 * WAVES - 1) / (64 * WAVES);
-    int sv[kSubIt], xv[kColIt];
-#pragma unroll
-    for (int i = 0; i < kSubIt; ++i)
-    {
-        const int k = (int)threadIdx.x + 64 * WAVES * i;
-        const int x = k / kSubRow, yy = k % kSubRow;
-        sv[i] = (k < a.substsz * kSubRow && yy < a.substsz) ? G(a.subst)[yy * a.substsz + x] - a.g : 0;
-    }
-#pragma unroll
-    for (int i = 0; i < kColIt; ++i)
-    {
-        const int c = cb + 1 + (int)threadIdx.x + 64 * WAVES * i;
-        int x = ((int)threadIdx.x + 64 * WAVES * i < kQCols && c <= d.C) ? G(d.seqX)[c] : 0;
-        xv[i] = ((unsigned)x < (unsigned)a.substsz) ? x : 0;
-    }
-#pragma unroll
-    for (int i = 0; i < kSubIt; ++i)
-    {
-        const int k = (int)threadIdx.x + 64 * WAVES * i;
-        if (k < a.substsz * kSubRow) lds_st(L.sub + 4u * k, sv[i]);
-    }
-    if (threadIdx.x < 16) lds_st(L.gfill + 4u * threadIdx.x, a.g);
-    __syncthreads();
-    // column profile of the tile column: Q[y][kQOff + j] = s(y, X[cb + j]) - g, j = 1..kExpTW + kExtra
-    // (the tile and the columns its parallelogram reaches past it; columns past C: letter 0, never
-    // stored), one column per thread
-#pragma unroll
-    for (int i = 0; i < kColIt; ++i)
-    {
-        const int j = (int)threadIdx.x + 64 * WAVES * i + 1;
-        if (j <= kQCols)
-            for (int yy = 0; yy < a.substsz; ++yy)
-                lds_st(L.q + 4u * (uint32_t)(yy * kQS + kQOff + j), lds_ld(L.sub + 4u * (uint32_t)(xv[i] * kSubRow + yy)));
-    }
-    __syncthreads();
-    // the matrix headers H(i, 0) = i g, H(0, j) = j g: column 0 of the chunk's rows (first tile
-    // column), row 0 of the tile's columns (first row chunk)
-    const int kChunk = WAVES * kExpRows * a.mt;
-    if (cb == 0)
-        for (int r = rc * kChunk + 1 + (int)threadIdx.x; r <= min(d.R, rc * kChunk + kChunk); r += 64 * WAVES)
-            G(d.score)[(size_t)r * (size_t)d.ld] = r * a.g;
-    if (rc == 0)
-    {
-        for (int c = cb + 1 + (int)threadIdx.x; c <= cb + cols; c += 64 * WAVES) G(d.score)[c] = c * a.g;
-        if (cb == 0 && threadIdx.x == 0) G(d.score)[0] = 0;
-    }
-}
-
-// the tiles of task tt: wave w's are rows 64 (w + WAVES i) of the chunk, i < mt (no barrier between
-// them: each wave has its own top-row buffer).  After ex_prep and a barrier.
-template <int WAVES>
-__device__ __forceinline__ void ex_tiles(const ExpandArgs& a, const ExpandPair& d, int tt, int w, int lane)
-{
-    const ExLds L = ex_layout(a.substsz, WAVES);
-    const int jT = tt % d.colTiles, rc = tt / d.colTiles;
-    const int cb = ex_cb(d, jT), cols = ex_cols(d, jT);
-    const int kChunk = WAVES * kExpRows * a.mt;
-    for (int i = 0; i < a.mt; ++i)
-    {
-        const int r0 = rc * kChunk + kExpRows * (w + WAVES * i) + 1;
-        if (r0 <= d.R && cb < d.C && !(a.knob & 1)) ex_tile(a, d, L, w, lane, cb, cols, r0);
-    }
-}
-
-template <int WAVES>
-__device__ __forceinline__ void ex_task(const ExpandArgs& a, const ExpandPair& d, int tt, int w, int lane)
-{
-    ex_prep<WAVES>(a, d, tt);
-    ex_tiles<WAVES>(a, d, tt, w, lane);
-}
-
-// a word of the expansion's LDS that ex_prep / ex_tiles never write (expand_lds_bytes counts it)
-__host__ __device__ inline uint32_t ex_word(int substsz, int waves) { return ex_layout(substsz, waves).gfill + 64u; }
-
-
 // ------------------------------------------------------------------------------------
 // The streamed expansion (round 6).  A task's inputs -- its column letters and, for each tile wave,
 // its 64 row letters, left boundary column and top row -- are global loads, and a wave's global load
@@ -446,10 +291,21 @@ __host__ __device__ inline ExLdsS ex_layout_s(int substsz, int nw)
     L.slotB = ((uint32_t)(kSlotHdr + kSlotX + nw * kTileDw) * 4u + 15u) & ~15u;
     return L;
 }
+// task slots: as many as the CU's 160 KB of LDS holds, up to kMaxSlots -- the loader runs that many
+// tasks ahead of the tile waves, and its loads wait behind the CU's own store stream (the vector
+// memory path is shared), so one task of lead starved the tile waves at 100k
+constexpr int kMaxSlots = 4;
+constexpr uint32_t kLdsBudget = 160u * 1024u;
+__host__ __device__ inline int ex_nslot(int substsz, int nw)
+{
+    const ExLdsS L = ex_layout_s(substsz, nw);
+    const int n = L.slot + 2u * L.slotB > kLdsBudget ? 2 : (int)((kLdsBudget - L.slot) / L.slotB);
+    return n < 2 ? 2 : n > kMaxSlots ? kMaxSlots : n;
+}
 __host__ __device__ inline uint32_t ex_stream_lds(int substsz, int nw)
 {
     const ExLdsS L = ex_layout_s(substsz, nw);
-    return L.slot + 2u * L.slotB;
+    return L.slot + (uint32_t)ex_nslot(substsz, nw) * L.slotB;
 }
 
 // LDS words shared by the waves: relaxed workgroup-scope atomics (a single wave's LDS operations
@@ -518,7 +374,8 @@ __device__ __forceinline__ void ex_stream(const ExpandArgs& a, unsigned* counter
 {
     constexpr int NW = W - 1;
     const ExLdsS L = ex_layout_s(a.substsz, NW);
-    const uint32_t RDY = L.ctl, DONE = L.ctl + 8u, BAR = L.ctl + 16u;
+    const int NS = ex_nslot(a.substsz, NW);
+    const uint32_t RDY = L.ctl, DONE = L.ctl + 4u * kMaxSlots, BAR = L.ctl + 8u * kMaxSlots;
     for (int k = threadIdx.x; k < a.substsz * kSubRow; k += 64 * W)
     {
         const int x = k / kSubRow, yy = k % kSubRow;
@@ -533,41 +390,37 @@ __device__ __forceinline__ void ex_stream(const ExpandArgs& a, unsigned* counter
     if (w == NW)
     {
         // ---- the loader wave ----
+        // claims runs of a.run schedule entries (one tile column: the tile waves keep its profile)
+        int runBase = 0, runLeft = 0;
         for (int k = 0;; ++k)
         {
-            const int s = k & 1, gen = (k >> 1) + 1;
+            const int s = k % NS, gen = k / NS + 1;
             const uint32_t slot = L.slot + (uint32_t)s * L.slotB;
             // the slot's previous task is done with it
-            bool ok = k < 2 || xs_wait(a, DONE + 4u * s, NW * (gen - 1));
-            unsigned t = (unsigned)a.nTasks;
-            if (ok && lane == 0)
-                t = __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ? (unsigned)a.nTasks
-                                                                                           : atomicAdd(counter, 1u);
-            const int task = __builtin_amdgcn_readfirstlane((int)t);
-            int lo = 0, tt = -1;
+            bool ok = k < NS || xs_wait(a, DONE + 4u * s, NW * (gen - 1));
+            int task = a.nTasks, lo = -1, tt = 0;
+            while (ok && lo < 0)
+            {
+                if (runLeft == 0)
+                {
+                    unsigned t = (unsigned)a.nTasks;
+                    if (lane == 0 && __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
+                        t = atomicAdd(counter, 1u) * (unsigned)a.run;
+                    runBase = __builtin_amdgcn_readfirstlane((int)min(t, (unsigned)a.nTasks));
+                    runLeft = runBase < a.nTasks ? min(a.run, a.nTasks - runBase) : 0;
+                    if (runLeft == 0) break;  // no more runs
+                }
+                task = runBase++;
+                --runLeft;
+                lo = __builtin_amdgcn_readfirstlane(G(a.sched)[2 * task]);
+                tt = __builtin_amdgcn_readfirstlane(G(a.sched)[2 * task + 1]);
+            }
+            if (lo < 0) task = a.nTasks;
             ExpandPair d;
             int jT = 0, rc = 0, cb = 0, cols = 0;
             if (task < a.nTasks)
             {
-                if (a.sched)
-                {
-                    lo = __builtin_amdgcn_readfirstlane(G(a.sched)[2 * task]);
-                    tt = __builtin_amdgcn_readfirstlane(G(a.sched)[2 * task + 1]);
-                }
-                else
-                {
-                    int hi = a.nPairs - 1;
-                    while (lo < hi)
-                    {
-                        const int mid = (lo + hi + 1) >> 1;
-                        if (__builtin_amdgcn_readfirstlane(G(a.pairs)[mid].taskBase) <= task)
-                            lo = mid;
-                        else
-                            hi = mid - 1;
-                    }
-                }
                 d = ex_desc(a.pairs + lo);
-                if (tt < 0) tt = task - d.taskBase;
                 jT = tt % d.colTiles;
                 rc = tt / d.colTiles;
                 cb = ex_cb(d, jT);
@@ -623,15 +476,15 @@ __device__ __forceinline__ void ex_stream(const ExpandArgs& a, unsigned* counter
             for (int i = 0; i < kXIt; ++i)
             {
                 const int j = lane + 64 * i, c = cb + 1 + j;
-                xv[i] = (j < kSlotX && c <= d.C) ? G(d.seqX)[c] : 0;
+                xv[i] = (GSA_EXPAND_PROBE != 8 && j < kSlotX && c <= d.C) ? G(d.seqX)[c] : 0;
             }
 #pragma unroll
             for (int i = 0; i < NW; ++i)
             {
                 const int r0 = rc * NW * kExpRows + kExpRows * i + 1;
                 const int r = r0 + lane;
-                yv[i] = (r <= d.R) ? G(d.seqY)[r] : 0;
-                if (cb == 0 || r0 > d.R)
+                yv[i] = (GSA_EXPAND_PROBE != 8 && r <= d.R) ? G(d.seqY)[r] : 0;
+                if (cb == 0 || r0 > d.R || GSA_EXPAND_PROBE == 8)
                     lbv[i] = r * a.g;
                 else
                 {
@@ -651,7 +504,7 @@ __device__ __forceinline__ void ex_stream(const ExpandArgs& a, unsigned* counter
                 for (int q = 0; q < kTIt; ++q)
                 {
                     const int j = 4 * lane + 256 * q;
-                    tv[i][q] = (m == 0 || r0 > d.R || j > ce) ? int4v {0, 0, 0, 0} : rowp[lane + 64 * q];
+                    tv[i][q] = (GSA_EXPAND_PROBE == 8 || m == 0 || r0 > d.R || j > ce) ? int4v {0, 0, 0, 0} : rowp[lane + 64 * q];
                 }
             }
 #pragma unroll
@@ -705,6 +558,7 @@ __device__ __forceinline__ void ex_stream(const ExpandArgs& a, unsigned* counter
     // ---- tile waves ----
     const int tid = w * 64 + lane;
     int barGen = 0;
+    int qPair = -1, qCol = -1;  // the pair and tile column the profile in LDS belongs to
     auto bar = [&]() {
         ++barGen;
         if (lane == 0) xs_add(BAR, 1);
@@ -712,16 +566,23 @@ __device__ __forceinline__ void ex_stream(const ExpandArgs& a, unsigned* counter
     };
     for (int k = 0;; ++k)
     {
-        const int s = k & 1, gen = (k >> 1) + 1;
+        const int s = k % NS, gen = k / NS + 1;
         const uint32_t slot = L.slot + (uint32_t)s * L.slotB;
         if (!xs_wait(a, RDY + 4u * s, gen)) return;
         const int task = xs_ld(slot);
         if (task < 0) return;
-        const int tt = xs_ld(slot + 8u);
+        const int pr = xs_ld(slot + 4u), tt = xs_ld(slot + 8u);
         const ExpandPair d = ex_desc_lds(slot + 12u);
         const int jT = tt % d.colTiles, rc = tt / d.colTiles;
         const int cb = ex_cb(d, jT), cols = ex_cols(d, jT);
+        // the profile of the previous task's tile column serves this one too: no rebuild
+        const bool same = pr == qPair && jT == qCol;
+        qPair = pr;
+        qCol = jT;
         // the profile is free once every tile wave is done with the previous task
+#if GSA_EXPAND_PROBE != 9
+        if (!same)
+        {
         if (!bar()) return;
         for (int j = tid + 1; j <= kSlotX; j += NW * 64)
         {
@@ -738,6 +599,8 @@ __device__ __forceinline__ void ex_stream(const ExpandArgs& a, unsigned* counter
                     if (4 * i + e < a.substsz) lds_st(L.q + 4u * (uint32_t)((4 * i + e) * kQS + kQOff + j), sv[i][e]);
         }
         if (!bar()) return;
+        }
+#endif
         // the matrix headers H(i, 0) = i g, H(0, j) = j g the task owns
         const int kChunk = NW * kExpRows;
         if (cb == 0)

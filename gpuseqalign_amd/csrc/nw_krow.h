@@ -34,11 +34,6 @@ hipError_t launch_krow_fill(const StripArgs& a, int ns, int k, int lw, int grid,
 // Pass 1 of the two-pass full fill (nw_expand.h): the sparse fill (K = 4, ns = 4 or 8, a.tBx =
 // kExpHB) that also stores rows 64m into each pair's rows64 / rpitch (PairDesc).
 hipError_t launch_krow_fill_xr(const StripArgs& a, int ns, int grid, hipStream_t stream);
-// Pass 1 of the pipelined full batch (nw_krowco.hip): the XR fill on (2, 2) tickets (krow_tickets(
-// trows, 2, 2); rows 64m as launch_krow_fill_xr) in 4-wave workgroups that fit beside a 12-wave
-// expansion workgroup (gsa_capi.hip enqueue_full_twopass).  grid <= 0: every resident slot.
-size_t krow_co_lds_bytes(int substsz, bool q8);
-hipError_t launch_krow_fill_co(const StripArgs& a, int grid, hipStream_t stream);
 // Both passes of the two-pass full fill in one launch: the first a.xP workgroups take pass-1
 // tickets (the XR fill on (ns, 4) tickets) until none is left, then, like the rest, expansion
 // tasks of `waves` x 64 rows (a.xpair, a.xsched, a.xTasks), each task waiting for the progress

@@ -41,6 +41,9 @@
 // super-strips (workgroups) the drain wave moves the last row through 8-byte {epoch, H'}
 // granules in HBM (sc1 atomics), polled by the next super-strip's loader wave
 // (MI355X_MICROARCH.md, handoff-1to1).  Every wait is bounded (StripArgs::spin, error word).
+#ifndef GSA_PROBE_P1
+#define GSA_PROBE_P1 0  // diagnostic builds only (tools/r06_xprobe_build.sh)
+#endif
 #ifndef GSA_FX_VMCNT
 // fused full fill: a strip publishes every 16 blocks what its stores older than its last GSA_FX_VMCNT
 // vector-memory operations cover (>= 4 per block: blocks <= b - GSA_FX_VMCNT / 4)
@@ -336,7 +339,11 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
                    "v"(int4v {lt[12], lt[13], lt[14], lt[15]})                                           \
                  : "memory")
             if constexpr (PT == 3)
+            {
+#if GSA_PROBE_P1 != 2  // (diagnostic build 2: no row-buffer stores, results wrong)
                 GSA_XR_STORES(" sc1");
+#endif
+            }
             else
                 GSA_XR_STORES("");
 #undef GSA_XR_STORES
@@ -534,6 +541,80 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
 }
 
 // ------------------------------------------------------------------------------------
+// feeder wave (the loader's feed job in a wave of its own, kr_split): the row above strip 0 from
+// the previous super-strip's granules, kFeedWin 64-column windows per poll round, all of a round's
+// loads in flight together.  A granule read is a memory round trip (sc1 stores, agent-scope
+// loads), and one 64-column poll per round trip fed strip 0 at 64 columns per round trip: under
+// the full fill's store stream a round trip grew to ~3.5 us, below the ~24 columns/us a strip
+// sweeps, and every ticket ran at the feed's pace (100k x 100k fused: inter-ticket lag 6 -> 14-20
+// us, first strip's sweep 4.2 -> 4.7-6.4 ms; profiles/r06_fused100k.txt).
+// ------------------------------------------------------------------------------------
+constexpr int kFeedWin = 4;
+template <int NS, int K, int LW>
+__device__ __forceinline__ void kr_feed(const StripArgs& a, const KrLds& L, int tk, int lane)
+{
+    const int Cp = a.Cp;
+    const uint32_t F = L.flags, ring0 = L.ring;
+    const gptr<const unsigned long long> gprev = G((const unsigned long long*)a.gran) + (size_t)(tk > 0 ? tk - 1 : 0) * a.granStride;
+    int hnext = 0;  // next column of the row above to feed into ring 0
+    int c0 = 0;     // ring 0's consumer word, re-read only when it blocks
+    uint64_t last = __builtin_amdgcn_s_memrealtime();
+    unsigned idle = 0;  // idle passes (error-word polls)
+    while (hnext <= Cp)
+    {
+        // whole windows whose ring elements (c + 64) strip 0 has released (< c0 + kRing)
+        if (hnext + 64 * kFeedWin + 64 > c0 + kRing) c0 = flag_ld(F + kr_cons(0));
+        const int room = min(kFeedWin, (c0 + kRing - 64 - hnext) / 64);
+        bool moved = false;
+        if (room > 0)
+        {
+            unsigned long long q[kFeedWin];
+#pragma unroll
+            for (int j = 0; j < kFeedWin; ++j)
+            {
+                const int c = hnext + 64 * j + lane;
+                q[j] = (tk > 0 && j < room && c <= Cp) ? __hip_atomic_load(gprev + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                                       : 0ull;
+            }
+            // the published prefix, in column order (columns past Cp: nothing to feed)
+            int n = 0;
+            bool stop = false;
+#pragma unroll
+            for (int j = 0; j < kFeedWin; ++j)
+            {
+                if (stop || j >= room) break;
+                const int c = hnext + 64 * j + lane;
+                const bool good = c > Cp || tk == 0 || (uint32_t)(q[j] >> 32) == a.epoch;
+                const uint64_t badm = __ballot(!good);
+                const int nj = badm ? __builtin_ctzll(badm) : 64;
+                if (c <= Cp && lane < nj) lds_st(ring0 + 4u * (uint32_t)((c + 64) & (kRing - 1)), tk > 0 ? (int)(uint32_t)q[j] : 0);
+                n += nj;
+                stop = nj < 64;
+            }
+            if (n > 0)
+            {
+                hnext += n;
+                flag_st(F, hnext > Cp ? kBig : hnext + 64);
+                moved = true;
+            }
+        }
+        const uint64_t now = __builtin_amdgcn_s_memrealtime();
+        if (moved)
+            last = now;
+        else
+        {
+            // the error word is a global load; another wave's error is looked at every 64th idle pass
+            if (now - last > a.spin || ((++idle & 63) == 0 && err_set(a)))
+            {
+                atomicOr(a.err, 1u);
+                return;
+            }
+            if (tk == 0) __builtin_amdgcn_s_sleep(1);
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------
 // loader wave: the column profile and the row above strip 0 (granules of the previous
 // super-strip, or row 0)
 // ------------------------------------------------------------------------------------
@@ -541,14 +622,24 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
 template <int NS, int K, int LW, int ROLE, bool Q8>
 __device__ __forceinline__ void kr_loader(const StripArgs& a, const KrLds& L, int tk, int lane)
 {
+    if constexpr (ROLE == 1)
+    {
+        kr_feed<NS, K, LW>(a, L, tk, lane);
+        return;
+    }
     const int Cp = a.Cp, C = a.C;
     constexpr int kLW = LW, kQRS = kr_qrs(LW, Q8), kQW = Q8 ? kLW / 4 : kLW / 2;
     const uint32_t F = L.flags;
     const uint32_t ring0 = L.ring;
     const gptr<const unsigned long long> gprev = G((const unsigned long long*)a.gran) + (size_t)(tk > 0 ? tk - 1 : 0) * a.granStride;
     auto letter = [&](int c) {
+#if GSA_PROBE_P1 == 1
+        // diagnostic build: no letter loads (results wrong)
+        return (c & 7) + 1 < a.substsz ? (c & 7) + 1 : 0;
+#else
         int x = (c >= 1 && c <= C) ? G(a.seqX)[c] : 0;  // padded columns: letter 0
         return ((unsigned)x < (unsigned)a.substsz) ? x : 0;
+#endif
     };
     int qn = 0;     // the profile holds columns < qn
     int hnext = 0;  // next column of the row above to feed into ring 0
@@ -934,10 +1025,8 @@ __device__ __forceinline__ PairDesc kr_desc(const PairDesc* p)
 
 // waves per workgroup: NS strips, the loader (split into a feeder and a profiler wave when the SIMDs
 // have room: NS <= 4), the drain
-// (PT = 4, the pipelined full batch's pass 1, keeps one loader wave: its 4-wave workgroup fits the
-// wave slots an expansion workgroup leaves on the CU)
 template <int NS, int PT = 0>
-constexpr bool kr_split() { return NS <= 4 && PT != 4; }
+constexpr bool kr_split() { return NS <= 4; }
 template <int NS, int PT = 0>
 constexpr int kr_waves() { return NS + 2 + (kr_split<NS, PT>() ? 1 : 0); }
 
@@ -947,7 +1036,7 @@ constexpr int kr_waves() { return NS + 2 + (kr_split<NS, PT>() ? 1 : 0); }
 // profiles in one kernel (a uniform branch, or the int16 path out of line) cost the int8 path its
 // code generation: 5.49 / 5.75 ms against 5.30 for the int8 instance alone.
 template <int NS, int K, int LW, int PT, bool Q8>
-__global__ void __launch_bounds__((64 * kr_waves<NS, PT>()), (PT == 4 ? 4 : 1)) nw_krow_kernel(StripArgs a)
+__global__ void __launch_bounds__((64 * kr_waves<NS, PT>()), 1) nw_krow_kernel(StripArgs a)
 {
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
@@ -2068,7 +2157,7 @@ __global__ void __launch_bounds__(64 * W) nw_full_fused_kernel(StripArgs a)
     xa.nTasks = a.xTasks;
     xa.sched = a.xsched;
     xa.knob = a.xknob;
-    xa.mt = 1;
+    xa.run = a.xrun;
     xa.spin = a.spin;
     xa.err = a.err;
     const xdev::ExFused fx {a.xdone, a.epoch, a.stamps ? a.stamps + 2 * (size_t)a.nTicketsTotal * NS : nullptr};
@@ -2116,17 +2205,6 @@ hipError_t launch_full_fused(const StripArgs& a, int ns, int waves, int grid, hi
     if (!a.xpair || !a.xdone || !a.xrole || !a.xcounter) return hipErrorInvalidValue;
     if (ns == 4 && waves == 8) return launch_fused<4, 8>(a, grid, stream);
     return hipErrorInvalidValue;
-}
-#elif defined(GSA_KROW_CO)
-// nw_krowco.hip: pass 1 of the pipelined full batch (gsa_capi.hip enqueue_full_twopass): the XR
-// fill on (2, 2) tickets (256 rows; a 512-column profile ring) in 4-wave workgroups of at most 128
-// VGPRs and 74 KB of LDS, which fit beside a 12-wave expansion workgroup of the previous pair group
-// on every CU (16 wave slots, 160 KB of LDS)
-size_t krow_co_lds_bytes(int substsz, bool q8) { return (size_t)kr_layout(2, 512, substsz, q8).flags + 256; }
-
-hipError_t launch_krow_fill_co(const StripArgs& a, int grid, hipStream_t stream)
-{
-    return launch_kr<2, 2, 512, 4>(a, grid, stream);
 }
 #elif defined(GSA_KROW_BATCH8)
 // nw_krow8.hip: the 8-strip batch instance in a translation unit of its own, so it can be built

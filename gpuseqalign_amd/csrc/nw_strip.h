@@ -111,7 +111,7 @@ struct StripArgs
     const int* xsched;
     int xTasks;
     int xP;
-    int xmt;  // expansion tiles per wave per task
+    int xrun;  // expansion tasks per claim (a run of one tile column: gsa_capi.hip enqueue_full_twopass)
     int xknob;
     unsigned* xrole;
     unsigned* xcounter;

@@ -227,16 +227,32 @@ def gpu_batch_align(device: int = 0, mode: str = "sparse", tileBx: int = 256, re
         t0 = time.perf_counter()
         for it in range(max(0, warmup) + max(1, repeats)):
             if it == max(0, warmup):
-                # untimed warmup passes (first launch: code object load, buffer allocation) done
+                # untimed warmup passes (first launch: code object load, buffer allocation, the
+                # library's candidate timing for a full batch) done
                 eng.sync(stream.cuda_stream)
                 torch.cuda.synchronize(dev)
                 t0 = time.perf_counter()
+            e0 = e1 = None
+            if it == 0 and timing is not None:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                w0 = time.perf_counter()
             for (d, dl), (gidx, gout) in zip(descs, gathers):
                 eng.fill_batch_dev([e[:5] for e in d], ts.data_ptr(), substsz, gapo, mode=mode, tileBx=tileBx,
                                    stream=stream.cuda_stream, lds=dl)
                 # result slices, in stream order behind the fill (before the next chunk reuses flat)
                 with torch.cuda.stream(stream):
                     torch.index_select(flat, 0, gidx, out=gout)
+            if e0 is not None:
+                # the batch's first launch as a one-off caller sees it: fresh buffers, no tuning yet
+                e1.record(stream)
+                eng.sync(stream.cuda_stream)
+                timing["first_launch_ms"] = e0.elapsed_time(e1)
+                timing["first_launch_wall_ms"] = (time.perf_counter() - w0) * 1e3
+            elif it < max(0, warmup):
+                # (the library times its candidates on a batch's first launches when their events
+                # have completed: warmup launches one at a time, so the timed ones run the choice)
+                eng.sync(stream.cuda_stream)
         eng.sync(stream.cuda_stream)
         torch.cuda.synchronize(dev)
         secs = (time.perf_counter() - t0) / max(1, repeats)

@@ -150,7 +150,10 @@ typedef struct gsa_pair_dev
 /* `pairs` is a host array of `npairs` entries; results are identical to one fill per pair.
  * The reference runs pairs one at a time through its benchmark loop (src/benchmark.cpp:
  * 393-520); a batch replaces that loop for throughput runs (BASELINE configs[3]).
- * Launches on one context must be ordered (same stream, or synchronised). */
+ * Launches on one context must be ordered (same stream, or synchronised).  Asynchronous: a full
+ * batch times its candidate schedules on its first launches with HIP events that are read only
+ * once complete (never a host wait); the host blocks only when more than 4 launches' descriptors
+ * are in flight on the context. */
 int gsa_fill_full_batch_dev(gsa_ctx* ctx, int32_t npairs, const gsa_pair_dev* pairs, const int32_t* subst,
                             int32_t substsz, int32_t gapo, void* stream);
 /* As gsa_fill_full_batch_dev, pair p's matrix with row pitch lds[p] (>= its adjcols; see

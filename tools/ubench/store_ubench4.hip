@@ -97,6 +97,59 @@ __global__ void kern(int* out, long long ld, int R, int C, int TW, int W, const 
     }
 }
 
+
+// The streamed expansion's task structure (nw_expand_dev.h ex_stream): W waves of which W - 1 store
+// (one idle, the loader's slot), per task two workgroup barriers around a PREP-cycle delay (the
+// profile build), then per wave 4 ramp blocks (compute only), 32 stored blocks in pairs, 4 tail
+// blocks; BLK = dependent-VALU cycles per block (the recurrence).
+template <int PREP, int BLK>
+__global__ void kernX(int* out, long long ld, int R, int C, int TW, int W, const int* sched, unsigned* counter,
+                      int nChunks, int nTiles)
+{
+    __shared__ int task;
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int NW = W - 1;
+    const int nTasks = nChunks * nTiles;
+    int acc = lane;
+    auto delay = [&](int n) {
+        for (int q = 0; q < n; ++q) acc = __builtin_amdgcn_update_dpp(0, acc, 0x138, 0xF, 0xF, true) + q;
+    };
+    for (;;)
+    {
+        __syncthreads();
+        if (threadIdx.x == 0) task = (int)atomicAdd(counter, 1u);
+        __syncthreads();
+        const int t = task;
+        if (t >= nTasks) break;
+        delay(PREP);
+        __syncthreads();
+        if (w == NW) continue;
+        const int rc = sched[2 * t], jT = sched[2 * t + 1];
+        const long long r0 = (long long)rc * NW * 64 + w * 64 + 1;
+        if (r0 + 63 >= R) continue;
+        const long long cb = (long long)jT * TW;
+        int4a v = {lane, lane + 1, lane + 2, lane + 3};
+        delay(4 * BLK);
+        for (int b = 0; b + 1 < TW / 16 && cb + 16 * b + 32 <= C; b += 2)
+        {
+            delay(2 * BLK);
+            v[1] += acc;
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+#pragma unroll
+                for (int h = 0; h < 2; ++h)
+                {
+                    const long long rr = r0 + 16 * k + (lane & 15);
+                    const long long c = cb + 16 * (b + h) + 4 * (lane >> 4);
+                    *(int4a*)(out + rr * ld + c) = v;
+                    v += 1;
+                }
+        }
+        delay(4 * BLK);
+    }
+    if (acc == 0x7fffffff) out[0] = acc;
+}
+
 int main(int argc, char** argv)
 {
     const int R = argc > 1 ? atoi(argv[1]) : 99968;
@@ -114,8 +167,8 @@ int main(int argc, char** argv)
     int dev = 0, cus = 0;
     hipGetDevice(&dev);
     hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    auto run = [&](auto k, const char* shape, int W, int TW, int order, int wgPerCu) {
-        const int nChunks = (R - 1) / (W * 64), nTiles = C / TW;
+    auto run = [&](auto k, const char* shape, int W, int TW, int order, int wgPerCu, int rowsW = 0) {
+        const int nChunks = (R - 1) / ((rowsW ? rowsW : W) * 64), nTiles = C / TW;
         const size_t lds = wgPerCu == 1 ? 100000 : 0;
         std::vector<int> hs;
         std::vector<std::pair<long long, int>> key;
@@ -145,14 +198,15 @@ int main(int argc, char** argv)
             best = ms < best ? ms : best;
         }
         hipFree(sched);
-        const double wbytes = (double)nChunks * W * 64 * (double)nTiles * TW * 4;
+        const double wbytes = (double)nChunks * (rowsW ? rowsW : W) * 64 * (double)nTiles * TW * 4;
         printf("R %d C %d ld %lld shape %s W %2d x %d/CU TW %5d order %d: %8.3f ms %8.1f GB/s\n", R, C, ld, shape, W,
                wgPerCu, TW, order, best, wbytes / best / 1e6);
     };
     run(kern<0, 128>, "16x64 d128", 8, 512, 2, 1);
-    run(kern<0, 128, 8>, "16x64 d128 ramp8", 8, 512, 2, 1);
-    run(kern<0, 128, 8>, "16x64 d128 ramp8", 7, 512, 2, 1);
-    run(kern<0, 128, 8>, "16x64 d128 ramp8 tw2048", 8, 2048, 2, 1);
-    run(kern<0, 256, 8>, "16x64 d256 ramp8", 8, 512, 2, 1);
+    run(kernX<0, 0>, "X prep0 blk0", 8, 512, 2, 1, 7);
+    run(kernX<300, 0>, "X prep300 blk0", 8, 512, 2, 1, 7);
+    run(kernX<300, 40>, "X prep300 blk40", 8, 512, 2, 1, 7);
+    run(kernX<300, 80>, "X prep300 blk80", 8, 512, 2, 1, 7);
+    run(kernX<0, 80>, "X prep0 blk80", 8, 512, 2, 1, 7);
     return 0;
 }
