@@ -351,6 +351,45 @@ def bench_full_batch(world, rank, local, n_pairs):
             "pairs": n_pairs, "pairs_matching_golden": match}
 
 
+def bench_full100k(dev, eng, tS, sh, stream, steps, warmup, world):
+    """The north star's own pair as a FULL matrix: the config-3 100k x 100k NW-LG related pair (9.99e9
+    cells, 40 GB int32) in HBM, pitched layout (gsa_fill_full_pitched_dev: row pitch gsa_full_pitch,
+    cell (1, 0) on a 128-byte boundary), the fused two-pass fill in one launch.  Bound: HBM writes,
+    4 B per cell.  align_cost (the last cell) against the oracle golden; the device hash / trace /
+    recurrence check of the same matrix are tests/test_gpu_full100k.py's."""
+    import torch
+    import gpuseqalign_amd as gsa
+    Y, X = config3_pair()
+    R1, C1 = len(Y), len(X)
+    ld, off = gsa.full_pitch(C1), gsa.full_base_offset()
+    try:
+        buf = torch.empty((R1 - 1) * ld + C1 + off + 64, dtype=torch.int32, device=dev)
+    except RuntimeError as ex:  # (no room: the field says so)
+        return {"error": str(ex)[:120]}
+    tY, tX = torch.from_numpy(Y).to(dev), torch.from_numpy(X).to(dev)
+    base = buf.data_ptr() + 4 * off
+
+    def step():
+        eng.fill_full_dev(tY.data_ptr(), R1, tX.data_ptr(), C1, tS.data_ptr(), 25, -11, base, sh, ld=ld)
+
+    el, km = timed_steps(step, stream, dev, steps, warmup, world, eng)
+    cost = int(buf[off + (R1 - 1) * ld + C1 - 1].item())
+    gold = load_golden("config3_100k.json")
+    b = 4.0 * R1 * C1
+    del buf
+    torch.cuda.empty_cache()
+    return {"workload": "BASELINE configs[2] pair (100k x 100k NW-LG, related) as a FULL int32 score matrix "
+                        f"({b / 1e9:.1f} GB) in HBM, pitched rows (ld {ld}), one fused launch per step",
+            "value": round(world * (R1 - 1) * (C1 - 1) * steps / el / 1e9, 1), "unit": "GCUPS",
+            "ms_per_step": round(el * 1e3 / steps, 4), "kernel_ms": round(km, 4), "steps": steps,
+            "kernel": full_kernel_name(True),
+            "hbm_write_GBps": round(b / (km * 1e-3) / 1e9, 1),
+            "hbm_frac": round(b / (km * 1e-3) / 1e9 / PEAK_HBM_GBPS, 4),
+            "bound": "hbm (4 B written per cell; MI355X 8 TB/s spec)",
+            "align_cost": cost,
+            "golden_align_cost": None if gold is None else gold["pairs"]["related"]["align_cost"]}
+
+
 def box_write_rate(local, gib=16, reps=5):
     """What this box's HBM takes in plain writes: torch fill_ of a 16 GiB int32 buffer (the runtime's
     fill kernel, 16-byte stores, every CU), best of 5.  The full batch's rate over this one separates
@@ -567,6 +606,7 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--config4-pairs", type=int, default=512, help="0 = skip the configs[3] batch field")
     ap.add_argument("--no-10k", action="store_true", help="skip the configs[1] full-matrix field")
+    ap.add_argument("--no-100k-full", action="store_true", help="skip the 100k x 100k full-matrix field")
     ap.add_argument("--no-rank-share", action="store_true", help="skip the config4_rank_share field")
     ap.add_argument("--full-batch-pairs", type=int, default=64, help="0 = skip the full-matrix batch field")
     ap.add_argument("--no-config5", action="store_true", help="skip the configs[4] score-only field")
@@ -670,6 +710,10 @@ def main():
                                      critical_path(C2, -(-R2 // 256), 9, km2, 256))}
         del score
         torch.cuda.empty_cache()
+    # ---- the headline pair as a full matrix (40 GB) ----------------------------------------
+    full100k = None
+    if not a.no_100k_full:
+        full100k = bench_full100k(dev, eng, tS, sh, stream, max(3, a.steps // 4), 2, world)
     cfg5 = None
     if not a.no_config5:
         cfg5 = bench_config5(dev, eng, max(3, a.steps // 4), 2, 0 if a.no_cpu_baseline else a.config5_cpu_sample,
@@ -711,7 +755,7 @@ def main():
                          "critical_path": critical_path(C, -(-R // 256), 9, kern_ms, 256)},
             "align_costs": costs[:8], "golden_align_cost": gold_cost,
             "golden_match": None if gold_cost is None else all(c == gold_cost for c in costs),
-            "fill_10k_full": full10k, "config4": cfg4, "config4_rank_share": share, "full_batch": fullb, "config5": cfg5,
+            "fill_10k_full": full10k, "fill_100k_full": full100k, "config4": cfg4, "config4_rank_share": share, "full_batch": fullb, "config5": cfg5,
         }
         if not a.no_cpu_baseline and world == 1:  # the CPU leg runs on rank 0 at N = 1 only
             out["cpu_baseline"] = cpu_baseline(Y, X, sub, budget_s=a.cpu_budget)

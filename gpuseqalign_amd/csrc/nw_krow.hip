@@ -98,6 +98,15 @@ __host__ __device__ constexpr uint32_t kr_cons(int i) { return 8u * (uint32_t)(i
 constexpr uint32_t kFXo = 4, kFTicket = 132;
 // mlsppt: strip w's header columns of tile columns < word are in memory (kBig: all), at kFCap + 4w
 constexpr uint32_t kFCap = 160;
+// the fused fill (PT 3): its strips stage their row-64m segments in LDS (kXD blocks deep per strip,
+// after the progress words) for a storer wave, so no strip issues a row-buffer store.  Words at
+// kr_xwords: [0, NS) blocks staged, [NS, 2NS) blocks stored (slots free), [2NS, 3NS) header columns
+// of boundaries < the word in memory (kXDone: all); the data at kr_xdata: 64 bytes per (strip,
+// slot, row 64j).
+constexpr int kXD = 32;
+__host__ __device__ constexpr uint32_t kr_xwords(uint32_t flags) { return flags + 256u; }
+__host__ __device__ constexpr uint32_t kr_xdata(uint32_t flags) { return flags + 256u + 64u; }
+[[maybe_unused]] __host__ __device__ constexpr uint32_t kr_xstage_bytes(int ns) { return 64u + (uint32_t)ns * kXD * 256u; }
 
 extern __shared__ __attribute__((aligned(16))) char krsm[];
 
@@ -289,6 +298,9 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
     // XR: byte address of block 0's segment of this lane's row 64m (lanes 16j - 1 only)
     // (lanes (64/K) j - 1, j = 1 .. K, hold the strip's rows 64 j - 1 as their last row)
     constexpr int kXL = 64 / K;  // lanes per 64 rows
+    // fused (PT 3): this strip's staging words and lane 16j - 1's 64-byte slice of each slot
+    const uint32_t xsWords = kr_xwords(L.flags);
+    const uint32_t xsData = kr_xdata(L.flags) + (uint32_t)(w * kXD * 256) + 64u * (uint32_t)((lane + 1) / kXL - 1);
     uint64_t xrBase = 0;
     if constexpr (PT >= 2)
     {
@@ -340,9 +352,22 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
                  : "memory")
             if constexpr (PT == 3)
             {
-#if GSA_PROBE_P1 != 2  // (diagnostic build 2: no row-buffer stores, results wrong)
-                GSA_XR_STORES(" sc1");
-#endif
+                // the fused fill: into the storer wave's LDS slot (kr_xstore), same lanes
+                const uint32_t sa = xsData + 64u * (uint32_t)(4 * (bb % kXD));
+                asm volatile("s_mov_b64 %0, exec\n"
+                             "s_mov_b64 exec, %1\n"
+                             "ds_write_b128 %2, %3\n"
+                             "ds_write_b128 %2, %4 offset:16\n"
+                             "ds_write_b128 %2, %5 offset:32\n"
+                             "ds_write_b128 %2, %6 offset:48\n"
+                             "s_mov_b64 exec, %0"
+                             : "=&s"(sv)
+                             : "s"(K == 4 ? 0x8000800080008000ull : 0x8000000080000000ull), "v"(sa),
+                               "v"(int4v {lt[0], lt[1], lt[2], lt[3]}), "v"(int4v {lt[4], lt[5], lt[6], lt[7]}),
+                               "v"(int4v {lt[8], lt[9], lt[10], lt[11]}), "v"(int4v {lt[12], lt[13], lt[14], lt[15]})
+                             : "memory");
+                flag_st(xsWords + 4u * (uint32_t)w, bb + 1);
+                (void)addr;
             }
             else
                 GSA_XR_STORES("");
@@ -362,18 +387,10 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
     // mlsppt: tile columns [0, ptPend) captured, to be published once their stores are acknowledged
     // (at the next capture block, or at the strip's end); header stores are then system-scope
     constexpr bool pt = PT == 1;
-    // fused: this strip's progress word, epoch << 32 | X: row 64m columns < X and the header columns
-    // of boundaries <= X stored and acknowledged (kXDone: all), published every 16 blocks.  (A
-    // publisher wave forwarding LDS words instead costs the strip on its SIMD more than the store:
-    // 10k 0.668 -> 0.683 ms.)
+    // fused: the strip's row-64m segments go to the storer wave through LDS (kr_xstore), and every 16
+    // blocks its header-column progress: boundaries < the word stored and acknowledged (kXDone: all)
     constexpr bool fx = PT == 3;
     int ptPend = 0;
-    unsigned long long* const xword = fx ? a.xdone + (size_t)tk * NS + w : nullptr;
-    auto fx_publish = [&](unsigned n) {
-        if constexpr (PT == 3)
-            if (lane == 0)
-                __hip_atomic_store(xword, ((unsigned long long)a.epoch << 32) | n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    };
 
     // One body for blocks with and without a header-column capture (cap, uniform): separate
     // bodies get different register assignments and ~100 v_mov per block to reconcile them.
@@ -443,12 +460,22 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
         if constexpr (fx && !RAMP)
             if ((b & 15) == 15)
             {
-                // every block issues >= 4 stores (its row-buffer segments), so all but the last 16
-                // vector-memory operations complete covers blocks <= b - 4: row 64m columns
-                // < 16 (b - 7) (block bb stores columns <= 16 (bb - 4) + 15 of its 4 rows) and the
-                // header columns captured by block b - 4 (boundaries <= 16 (b - 7))
-                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GSA_FX_VMCNT) : "memory");
-                fx_publish((unsigned)(kBlk * (b - GSA_FX_VMCNT / 4 - 3)));
+                // the strip's only global stores are its header columns, 4K per boundary (4 capture
+                // blocks x K rows): all but the last 8K vector-memory operations complete covers
+                // every boundary but the last two captured (boundaries <= 16 b - 2 tBx)
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(8 * K) : "memory");
+                flag_st(xsWords + 4u * (uint32_t)(2 * NS + w), max(0, kBlk * (b + 1) - 2 * tBx - 64));
+                // room in the staging ring for the next 16 blocks (the storer keeps up: rarely waits)
+                const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+                for (unsigned it = 1; flag_ld(xsWords + 4u * (uint32_t)(NS + w)) + kXD < b + 1 + 16; ++it)
+                {
+                    __builtin_amdgcn_s_sleep(1);
+                    if (__builtin_amdgcn_s_memrealtime() - t0 > a.spin || ((it & 31) == 0 && err_set(a)))
+                    {
+                        atomicOr(a.err, 1u);
+                        return false;
+                    }
+                }
             }
         if (CAP && cap)
         {
@@ -536,7 +563,8 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
     if (fx)
     {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        fx_publish(kXDone);
+        flag_st(xsWords + 4u * (uint32_t)w, NB);  // (every block staged)
+        flag_st(xsWords + 4u * (uint32_t)(2 * NS + w), (int)kXDone);
     }
 }
 
@@ -1005,6 +1033,105 @@ __device__ __forceinline__ void kr_drain(const StripArgs& a, const KrLds& L, int
                 }
                 __builtin_amdgcn_s_sleep(1);
             }
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// storer wave (the fused fill, PT 3; the workgroup's eighth wave): the strips' row-64m segments
+// from their LDS staging slots to the row buffer, 4 blocks of a strip per store instruction (64
+// lanes x 16 bytes: block, row, 16-byte chunk), write-through; then, behind vmcnt(0), the strip's
+// progress word for the expansion -- epoch << 32 | X, row 64m columns < X and header columns of
+// boundaries < X in memory.  The strips issued these stores themselves before (4 four-lane store
+// instructions per block): under the expansion's store stream their write-through stores filled
+// each strip's 63 outstanding vector-memory slots and stalled it (100k x 100k: pass 1 6.2 -> 8.4 ms,
+// profiles/r06_fused100k.txt).
+// ------------------------------------------------------------------------------------
+template <int NS, int K>
+__device__ __forceinline__ void kr_xstore(const StripArgs& a, const KrLds& L, int tk, int lane)
+{
+    static_assert(K == 4, "4 rows 64m per strip: a store instruction = 4 blocks x 4 rows x 4 chunks");
+    const int NB = (a.Cp + 65 + kBlk - 1) / kBlk;  // blocks of a strip (kr_strip's NB)
+    const uint32_t W = kr_xwords(L.flags), D = kr_xdata(L.flags);
+    constexpr int kXL = 64 / K;
+    const int kk = lane >> 4, jj = (lane >> 2) & 3, c = lane & 3;  // block of the group, row 64(jj+1), chunk
+    unsigned long long* const xword = a.xdone + (size_t)tk * NS;
+    // this lane's int offset in the row buffer, less 16 bb, per strip
+    long long rowOff[NS];
+#pragma unroll
+    for (int w = 0; w < NS; ++w)
+    {
+        const long long m = (long long)(K * NS) * tk + K * w + jj + 1;  // row 64m of the matrix
+        rowOff[w] = (m - 1) * a.rpitch + kRowsPad - kXL * (jj + 1) + kBlk * kk + 4 * c;
+    }
+    int sb[NS], pub[NS];
+#pragma unroll
+    for (int w = 0; w < NS; ++w) sb[w] = pub[w] = 0;
+    int since = 0;  // blocks stored since the last publication
+    uint64_t last = __builtin_amdgcn_s_memrealtime();
+    for (unsigned idle = 1;; ++idle)
+    {
+        bool moved = false, fin = true;
+#pragma unroll
+        for (int w = 0; w < NS; ++w)
+        {
+            const int p = flag_ld(W + 4u * (uint32_t)w);  // blocks staged
+            // whole groups of 4 blocks, and the strip's last ones
+            while (sb[w] < p && (sb[w] + 4 <= p || p >= NB))
+            {
+                const int bb = sb[w] + kk;
+                if (bb < p)
+                {
+                    const int4v v =
+                        lds_ld4(D + 256u * (uint32_t)(w * kXD + bb % kXD) + 64u * (uint32_t)jj + 16u * (uint32_t)c);
+                    const uint64_t addr =
+                        (uint64_t)(uintptr_t)a.rows64 + 4ull * (uint64_t)(rowOff[w] + (long long)kBlk * sb[w]);
+                    // write-through (sc1): read by other workgroups of the launch
+                    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(addr), "v"(v) : "memory");
+                }
+                const int n = min(4, p - sb[w]);
+                sb[w] += n;
+                since += n;
+                flag_st(W + 4u * (uint32_t)(NS + w), sb[w]);  // slots of blocks < sb[w] free (the reads precede)
+                moved = true;
+            }
+            fin = fin && sb[w] >= NB;
+        }
+        // publish every 16 blocks per strip (vmcnt(0) waits for this wave's stores only), and at the end
+        if (since >= 16 * NS || fin)
+        {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            since = 0;
+            bool all = true;
+#pragma unroll
+            for (int w = 0; w < NS; ++w)
+            {
+                const int hdr = flag_ld(W + 4u * (uint32_t)(2 * NS + w));
+                const int x = (sb[w] >= NB && hdr == (int)kXDone) ? (int)kXDone : min(kBlk * sb[w] - 64, hdr);
+                if (x > pub[w])
+                {
+                    if (lane == 0)
+                        __hip_atomic_store(xword + w, ((unsigned long long)a.epoch << 32) | (unsigned)x, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+                    pub[w] = x;
+                    moved = true;
+                }
+                all = all && pub[w] == (int)kXDone;
+            }
+            if (all) return;
+        }
+        const uint64_t now = __builtin_amdgcn_s_memrealtime();
+        if (moved)
+            last = now;
+        else
+        {
+            // idle while the strips wait for their input: the strips' own watchdog is a.spin per wait
+            if (now - last > 4 * a.spin || ((idle & 63) == 0 && err_set(a)))
+            {
+                atomicOr(a.err, 1u);
+                return;
+            }
+            __builtin_amdgcn_s_sleep(1);
         }
     }
 }
@@ -2128,8 +2255,11 @@ __global__ void __launch_bounds__(64 * W) nw_full_fused_kernel(StripArgs a)
         unsigned long long* const sst = a.stamps ? a.stamps + 2 * ((size_t)d.ticketBase + tk) * NS : nullptr;
         if (threadIdx.x < 32) lds_st(L.flags + 4u * threadIdx.x, 0);
         if (threadIdx.x >= kFCap / 4 && threadIdx.x < kFCap / 4 + 8) lds_st(L.flags + 4u * threadIdx.x, 0);
+        if (threadIdx.x >= 64 && threadIdx.x < 64 + 3 * NS) lds_st(kr_xwords(L.flags) + 4u * (threadIdx.x - 64), 0);
         __syncthreads();
-        if (w == NS + 1)
+        if (w == NS + 3)
+            kr_xstore<NS, K>(pa, L, tk, lane);
+        else if (w == NS + 1)
             kr_drain<NS, K, LW, 3>(pa, L, tk, lane);
         else if (w == NS)
             kr_loader<NS, K, LW, kr_split<NS>() ? 1 : 0, Q8>(pa, L, tk, lane);
@@ -2168,7 +2298,8 @@ template <int NS, int W, bool Q8>
 hipError_t launch_fused1(const StripArgs& a, int grid, hipStream_t stream, bool foot)
 {
     static_assert(W == kExpStreamWaves, "the streamed expansion's workgroup");
-    const size_t lds = std::max(krow_lds_bytes(NS, 1024, a.substsz, Q8), expand_stream_lds_bytes(a.substsz));
+    static_assert(kr_waves<NS>() < W, "a storer wave beside the pass-1 roles");
+    const size_t lds = std::max(krow_lds_bytes(NS, 1024, a.substsz, Q8) + kr_xstage_bytes(NS), expand_stream_lds_bytes(a.substsz));
     auto kern = nw_full_fused_kernel<NS, W, Q8>;
     constexpr int kThreads = 64 * W;
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
