@@ -1300,7 +1300,8 @@ int enqueue_full_twopass(gsa_ctx* ctx, int npairs, const gsa_pair_dev* pairs, co
     xa.counter = ctx->ctl + 8 + opt.slot;
     // the fused single pair: every workgroup takes pass-1 tickets first
     const FusedLaunch fl {&xa, ns, gsa::kExpStreamWaves, 1 << 30};
-    const int xGrid = (int)std::max<long long>(1, std::min<long long>(ctx->cu_count, (nEntries + xRun - 1) / xRun));
+    int xGrid = (int)std::max<long long>(1, std::min<long long>(ctx->cu_count, (nEntries + xRun - 1) / xRun));
+    if (env_int("GSA_EXPAND_GRID", 0) > 0) xGrid = std::min(xGrid, env_int("GSA_EXPAND_GRID", 0));
     // gsa_set_full_timing: events before pass 1, between the passes and after pass 2, and the
     // expansion's clock stamps (one per workgroup)
     const bool timed = ctx->timing && !opt.split;

@@ -103,7 +103,6 @@ __device__ __forceinline__ void ex_tile_core(const ExpandArgs& a, const ExpandPa
     // transposed output (as nw_lane.hip): store k has lane 16h + n write columns 4h .. 4h+3 of the
     // block's 16 for row r0 + 16k + n
     const gptr<int> xbase = G(d.score) + (ptrdiff_t)(r0 + (lane & 15)) * d.ld + cb + 4 * (lane >> 4) - (lane & 15);
-    const uint32_t xoff = (uint32_t)(lane & 15) * (uint32_t)(d.ld - 1) + 4u * (uint32_t)(lane >> 4);
 
     int qA[kBlk], qB[kBlk];
 #pragma unroll
@@ -162,51 +161,128 @@ __device__ __forceinline__ void ex_tile_core(const ExpandArgs& a, const ExpandPa
         int t[kBlk];
 #pragma unroll
         for (int e = 0; e < kBlk; ++e) t[e] = vals[e];
-#if !GSA_EXPAND_PROBE_STORES_ONLY
+        // the per-block transposed shape (ramp and edge blocks): store k has lane 16h + n write
+        // columns 4h .. 4h+3 of the block's 16 for row r0 + 16k + n -- lane bits 5, 4 swapped with
+        // the chunk index
+        auto xpose16 = [&]() {
 #pragma unroll
-        for (int k = 0; k < 2; ++k)
+            for (int k = 0; k < 2; ++k)
 #pragma unroll
-            for (int dd = 0; dd < 4; ++dd)
-            {
-                const auto sw = __builtin_amdgcn_permlane32_swap(t[4 * k + dd], t[4 * (k + 2) + dd], false, false);
-                t[4 * k + dd] = sw[0];
-                t[4 * (k + 2) + dd] = sw[1];
-            }
+                for (int dd = 0; dd < 4; ++dd)
+                {
+                    const auto sw = __builtin_amdgcn_permlane32_swap(t[4 * k + dd], t[4 * (k + 2) + dd], false, false);
+                    t[4 * k + dd] = sw[0];
+                    t[4 * (k + 2) + dd] = sw[1];
+                }
 #pragma unroll
-        for (int k = 0; k < 4; k += 2)
+            for (int k = 0; k < 4; k += 2)
 #pragma unroll
-            for (int dd = 0; dd < 4; ++dd)
-            {
-                const auto sw = __builtin_amdgcn_permlane16_swap(t[4 * k + dd], t[4 * (k + 1) + dd], false, false);
-                t[4 * k + dd] = sw[0];
-                t[4 * (k + 1) + dd] = sw[1];
-            }
-#endif
-        auto store4 = [&](int bb, int k, const int (&v)[kBlk]) {
-            const gptr<int> ub = G(d.score) + ((ptrdiff_t)(r0 + 16 * k) * d.ld - 16 * k + kBlk * bb + cb);
-#if GSA_EXPAND_PROBE == 2
-            // diagnostic build: interior stores only into one line per wave (results wrong)
-            sink ^= v[4 * k] ^ v[4 * k + 1] ^ v[4 * k + 2] ^ v[4 * k + 3];
-            (void)ub;
-#else
-            st_out(ub + xoff, int4a {v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]});
-#endif
+                for (int dd = 0; dd < 4; ++dd)
+                {
+                    const auto sw = __builtin_amdgcn_permlane16_swap(t[4 * k + dd], t[4 * (k + 1) + dd], false, false);
+                    t[4 * k + dd] = sw[0];
+                    t[4 * (k + 1) + dd] = sw[1];
+                }
         };
         if constexpr (MODE == kHold)
         {
+            // the even block's values, untransposed: stored with the odd block's
 #pragma unroll
             for (int e = 0; e < kBlk; ++e) tE[e] = t[e];
         }
         else if constexpr (MODE == kPair)
         {
+            // whole 128-byte lines per instruction, each lane quad 64 contiguous bytes: store k
+            // (0..7) writes rows rr = 32 (k >> 2) + 4m + (k & 3), m = 0..7, lane 4m + q (+ 32 for the
+            // line's second half) columns 4c .. 4c+3 of the pair's 32, chunk c = q + 4 (lane >> 5).  A
+            // CU writes 96 GB/s in this shape against 33 in the transposed 16-row x 64-B one (a quad
+            // covering 4 rows: tools/ubench/store_ubench4.hip, profiles/r06_store_shape.txt).  Chunk c
+            // of the lane's own row: c < 4 the even block's (tE), c >= 4 the odd one's; lane bit 5
+            // swaps with chunk bit 2 (permlane32 swaps), lane bits 1 and 0 with chunk bits 1 and 0
+            // (quad permutes)
+            int A[8][4];
 #pragma unroll
-            for (int k = 0; k < 4; ++k)
+            for (int c = 0; c < 4; ++c)
+#pragma unroll
+                for (int dd = 0; dd < 4; ++dd)
+                {
+                    A[c][dd] = tE[4 * c + dd];
+                    A[c + 4][dd] = t[4 * c + dd];
+                }
+#if !GSA_EXPAND_PROBE_STORES_ONLY
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+#pragma unroll
+                for (int dd = 0; dd < 4; ++dd)
+                {
+                    const auto sw = __builtin_amdgcn_permlane32_swap(A[c][dd], A[c + 4][dd], false, false);
+                    A[c][dd] = sw[0];
+                    A[c + 4][dd] = sw[1];
+                }
+            // lane bit m (1, then 0) with chunk bit m, per pair of chunks (x: bit m clear, y: set): a
+            // lane with lane bit m clear keeps its x and takes its quad partner's x as y, the others
+            // keep y and take the partner's y as x -- one v_cndmask_b32 per output, its first operand
+            // read across the quad (DPP).  (s_nop 1: the DPP operand may have been written by the
+            // instruction before the block.)
+            const uint64_t lo1 = 0x3333333333333333ull, lo0 = 0x5555555555555555ull;
+            auto qswap = [&](auto mT) {
+                constexpr int m = decltype(mT)::value;
+                const uint64_t mlo = m ? lo1 : lo0, mhi = ~mlo;
+#pragma unroll
+                for (int c = 0; c < 8; ++c)
+                    if (((c >> m) & 1) == 0)
+                    {
+                        int* x = A[c];
+                        int* y = A[c | (1 << m)];
+                        int nx0, nx1, nx2, nx3, ny0, ny1, ny2, ny3;
+#define GSA_QSWAP(QP)                                                                                              \
+    asm volatile("s_nop 1\n"                                                                                       \
+                 "s_mov_b64 vcc, %16\n"                                                                            \
+                 "v_cndmask_b32_dpp %0, %12, %8, vcc " QP " row_mask:0xf bank_mask:0xf\n"                          \
+                 "v_cndmask_b32_dpp %1, %13, %9, vcc " QP " row_mask:0xf bank_mask:0xf\n"                          \
+                 "v_cndmask_b32_dpp %2, %14, %10, vcc " QP " row_mask:0xf bank_mask:0xf\n"                         \
+                 "v_cndmask_b32_dpp %3, %15, %11, vcc " QP " row_mask:0xf bank_mask:0xf\n"                         \
+                 "s_mov_b64 vcc, %17\n"                                                                            \
+                 "v_cndmask_b32_dpp %4, %8, %12, vcc " QP " row_mask:0xf bank_mask:0xf\n"                          \
+                 "v_cndmask_b32_dpp %5, %9, %13, vcc " QP " row_mask:0xf bank_mask:0xf\n"                          \
+                 "v_cndmask_b32_dpp %6, %10, %14, vcc " QP " row_mask:0xf bank_mask:0xf\n"                         \
+                 "v_cndmask_b32_dpp %7, %11, %15, vcc " QP " row_mask:0xf bank_mask:0xf"                            \
+                 : "=&v"(nx0), "=&v"(nx1), "=&v"(nx2), "=&v"(nx3), "=&v"(ny0), "=&v"(ny1), "=&v"(ny2), "=&v"(ny3)    \
+                 : "v"(x[0]), "v"(x[1]), "v"(x[2]), "v"(x[3]), "v"(y[0]), "v"(y[1]), "v"(y[2]), "v"(y[3]), "s"(mlo), \
+                   "s"(mhi)                                                                                        \
+                 : "vcc")
+                        if constexpr (m == 1)
+                            GSA_QSWAP("quad_perm:[2,3,0,1]");
+                        else
+                            GSA_QSWAP("quad_perm:[1,0,3,2]");
+#undef GSA_QSWAP
+                        x[0] = nx0, x[1] = nx1, x[2] = nx2, x[3] = nx3;
+                        y[0] = ny0, y[1] = ny1, y[2] = ny2, y[3] = ny3;
+                    }
+            };
+            qswap(std::integral_constant<int, 1>());
+            qswap(std::integral_constant<int, 0>());
+#endif
+            const uint32_t xoffQ = (uint32_t)(4 * ((lane >> 2) & 7)) * (uint32_t)(d.ld - 1) +
+                                   4u * (uint32_t)((lane & 3) | ((lane >> 5) << 2));
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
             {
-                store4(b - 1, k, tE);
-                store4(b, k, t);
+                const int rk = 32 * (k >> 2) + (k & 3);
+                const gptr<int> ub = G(d.score) + ((ptrdiff_t)(r0 + rk) * d.ld - rk + kBlk * (b - 1) + cb);
+#if GSA_EXPAND_PROBE == 2
+                sink ^= A[k][0] ^ A[k][1] ^ A[k][2] ^ A[k][3];
+                (void)ub;
+#else
+                st_out(ub + xoffQ, int4a {A[k][0], A[k][1], A[k][2], A[k][3]});
+#endif
             }
         }
         else if ((MODE == kEdge || cb == 0) && kBlk * b - 63 <= hiMax)
+        {
+#if !GSA_EXPAND_PROBE_STORES_ONLY
+            xpose16();
+#endif
 #pragma unroll
             for (int k = 0; k < 4; ++k)
             {
@@ -228,6 +304,7 @@ __device__ __forceinline__ void ex_tile_core(const ExpandArgs& a, const ExpandPa
                     }
                 }
             }
+        }
     };
     using MR = std::integral_constant<int, kRamp>;
     using MH = std::integral_constant<int, kHold>;
@@ -390,8 +467,20 @@ __device__ __forceinline__ void ex_stream(const ExpandArgs& a, unsigned* counter
     if (w == NW)
     {
         // ---- the loader wave ----
-        // claims runs of a.run schedule entries (one tile column: the tile waves keep its profile)
-        int runBase = 0, runLeft = 0;
+        // claims runs of a.run schedule entries (one tile column: the tile waves keep its profile).
+        // Its global accesses are round trips that queue behind the CU's own store stream --
+        // microseconds each under the full fill, and a loader that made six per task (claim,
+        // schedule entry, pair descriptor, one readiness word after the other, inputs) supplied a
+        // task every ~37 us, the expansion's whole rate per CU.  So a run's claim is made one run
+        // ahead and its schedule entries come in one load, the pair's descriptor is kept while the
+        // pair stays, and a task's readiness words are read together: per task one readiness read
+        // and one input load.
+        int runBase = 0, runLeft = 0, runPos = 0;
+        int sv = 0;  // the run's schedule entries: lanes 2i, 2i + 1 = {pair, task} of entry i
+        int curLo = -1;
+        ExpandPair d {};
+        unsigned nextV = 0;  // (lane 0) the next run's claim, in flight
+        if (lane == 0) nextV = atomicAdd(counter, 1u);
         for (int k = 0;; ++k)
         {
             const int s = k % NS, gen = k / NS + 1;
@@ -403,24 +492,29 @@ __device__ __forceinline__ void ex_stream(const ExpandArgs& a, unsigned* counter
             {
                 if (runLeft == 0)
                 {
-                    unsigned t = (unsigned)a.nTasks;
-                    if (lane == 0 && __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
-                        t = atomicAdd(counter, 1u) * (unsigned)a.run;
-                    runBase = __builtin_amdgcn_readfirstlane((int)min(t, (unsigned)a.nTasks));
+                    const unsigned t = (unsigned)__builtin_amdgcn_readfirstlane((int)nextV) * (unsigned)a.run;
+                    runBase = (int)min(t, (unsigned)a.nTasks);
                     runLeft = runBase < a.nTasks ? min(a.run, a.nTasks - runBase) : 0;
                     if (runLeft == 0) break;  // no more runs
+                    sv = lane < 2 * runLeft ? G(a.sched)[2 * runBase + lane] : -1;
+                    if (lane == 0) nextV = atomicAdd(counter, 1u);
+                    runPos = 0;
                 }
-                task = runBase++;
+                task = runBase + runPos;
+                lo = __builtin_amdgcn_readlane(sv, 2 * runPos);
+                tt = __builtin_amdgcn_readlane(sv, 2 * runPos + 1);
+                ++runPos;
                 --runLeft;
-                lo = __builtin_amdgcn_readfirstlane(G(a.sched)[2 * task]);
-                tt = __builtin_amdgcn_readfirstlane(G(a.sched)[2 * task + 1]);
             }
             if (lo < 0) task = a.nTasks;
-            ExpandPair d;
             int jT = 0, rc = 0, cb = 0, cols = 0;
             if (task < a.nTasks)
             {
-                d = ex_desc(a.pairs + lo);
+                if (lo != curLo)
+                {
+                    d = ex_desc(a.pairs + lo);
+                    curLo = lo;
+                }
                 jT = tt % d.colTiles;
                 rc = tt / d.colTiles;
                 cb = ex_cb(d, jT);
@@ -429,28 +523,31 @@ __device__ __forceinline__ void ex_stream(const ExpandArgs& a, unsigned* counter
                 {
                     // pass 1 has stored rows 64m, m = NW rc .. NW rc + NW - 1, at the columns the
                     // tiles read, and the header column cb for their rows: the words of strips
-                    // (NW rc - 1) / 4 .. (NW (rc + 1) - 1) / 4 (256 rows each) reach `need`
+                    // (NW rc - 1) / 4 .. (NW (rc + 1) - 1) / 4 (256 rows each) reach `need`; lane i
+                    // reads strip s0 + i's
                     unsigned long long* ts = f.tstamps ? f.tstamps + 3 * (size_t)task : nullptr;
                     if (ts && lane == 0) ts[0] = __builtin_amdgcn_s_memrealtime();
                     const unsigned need = (unsigned)(min(cb + cols + kExtra, d.C) + 1);
-                    const int s1 = min((NW * (rc + 1) - 1) / 4, d.p1Strips - 1);
-                    const unsigned long long* words = f.xdone + d.p1Strip0;
-                    uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-                    for (int sx = rc > 0 ? (NW * rc - 1) / 4 : 0; sx <= s1 && ok;)
+                    const int s0 = rc > 0 ? (NW * rc - 1) / 4 : 0;
+                    const int nWords = min((NW * (rc + 1) - 1) / 4, d.p1Strips - 1) - s0 + 1;
+                    const unsigned long long* words = f.xdone + d.p1Strip0 + s0;
+                    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+                    for (unsigned it = 1;; ++it)
                     {
-                        const unsigned long long v = __hip_atomic_load(words + sx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        if ((unsigned)(v >> 32) == f.epoch && (unsigned)v >= need)
+                        bool rdy = true;
+                        if (lane < nWords)
                         {
-                            ++sx;
-                            t0 = __builtin_amdgcn_s_memrealtime();
-                            continue;
+                            const unsigned long long v = __hip_atomic_load(words + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            rdy = (unsigned)(v >> 32) == f.epoch && (unsigned)v >= need;
                         }
+                        if (__builtin_amdgcn_ballot_w64(!rdy) == 0) break;
                         __builtin_amdgcn_s_sleep(2);
                         if (__builtin_amdgcn_s_memrealtime() - t0 > a.spin ||
-                            __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)
+                            ((it & 15) == 0 && __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0))
                         {
                             if (lane == 0) atomicOr(a.err, 1u);
                             ok = false;
+                            break;
                         }
                     }
                     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");

@@ -1,13 +1,17 @@
 set -e
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-L=gpurun_out/r06_s17.log
+L=gpurun_out/r06_px2.log
 : > $L
-timeout -k 10 120 python -u tools/r06_stamps100k.py _st >> $L 2>&1
-grep -v amdgpu.ids $L | grep "^{" | python3 -c "
+for lib in "" xp1 xp6 xp7; do
+  so=""; [ -n "$lib" ] && so=gpuseqalign_amd/libgsa_$lib.so
+  for g in 64 256; do
+    GSA_LIB=$so GSA_FULL_FUSED=0 GSA_EXPAND_GRID=$g timeout -k 10 120 python -u tools/r06_full100k.py --pitched --timing --reps 2 --tag "$lib g$g" >> $L 2>&1
+  done
+done
+grep "^{" $L | python3 -c "
 import sys, json
 for l in sys.stdin:
     j = json.loads(l)
-    print('fused', j['ms'], j['cost_ok'], 'strip end first/last', j['strip_end_us']['first'], j['strip_end_us']['last'], j['tasks_done_per_500us'])"
-timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_full100k.py tests/test_gpu_parity.py > gpurun_out/r06_t17.log 2>&1 || { tail -30 gpurun_out/r06_t17.log; exit 1; }
-tail -3 gpurun_out/r06_t17.log
+    t = j.get('timing') or {}
+    print(j['tag'], j['ms_mean'], j['align_cost'], 'p1', t.get('pass1_ms'), 'p2', t.get('pass2_ms'), 'p2 GB/s', round(j['bytes']/ (t.get('pass2_ms', 1e9)*1e-3)/1e9, 1), 'clk', t.get('pass2_clock_ghz', t.get('clock')))"

@@ -16,7 +16,7 @@ typedef int int4a __attribute__((ext_vector_type(4), aligned(4)));
 // order 0: row-chunk-major (all tile columns of chunk 0, then chunk 1...); 1: tile-column-major;
 // 2: anti-diagonals of (chunk, tile column) weighted as the fused fill's ready time.
 // SHAPE 0: 16 rows x 64 B per instruction (pairs); 1: 8 rows x 128 B; 2: 4 rows x 256 B
-template <int SHAPE, int DELAY = 0, int RAMP = 0>
+template <int SHAPE, int DELAY = 0, int RAMP = 0, int NT = 0>
 __global__ void kern(int* out, long long ld, int R, int C, int TW, int W, const int* sched, unsigned* counter,
                      int nChunks, int nTiles)
 {
@@ -61,7 +61,10 @@ __global__ void kern(int* out, long long ld, int R, int C, int TW, int W, const 
                     {
                         const long long rr = r0 + 16 * k + (lane & 15);
                         const long long c = cb + 16 * (b + h) + 4 * (lane >> 4);
-                        *(int4a*)(out + rr * ld + c) = v;
+                        if (NT)
+                            __builtin_nontemporal_store(v, (int4a*)(out + rr * ld + c));
+                        else
+                            *(int4a*)(out + rr * ld + c) = v;
                         v += 1;
                     }
             }
@@ -72,6 +75,25 @@ __global__ void kern(int* out, long long ld, int R, int C, int TW, int W, const 
                 {
                     const long long rr = r0 + 8 * k + (lane >> 3);
                     const long long c = cb + 16 * b + 4 * (lane & 7);
+                    *(int4a*)(out + rr * ld + c) = v;
+                    v += 1;
+                }
+            }
+            else if (SHAPE >= 3)
+            {
+                // 8 rows x 128 B per instruction, lane -> (row, chunk) by SHAPE: 3 row = L & 7, chunk =
+                // L >> 3; 4 row bits at lane bits {0, 4, 5}, chunk {1, 2, 3}; 5 row {2, 3, 5}, chunk
+                // {0, 1, 4}; 6 row {2, 3, 4}, chunk {0, 1, 5}
+                int row, ch;
+                if (SHAPE == 3) { row = lane & 7; ch = lane >> 3; }
+                else if (SHAPE == 4) { row = (lane & 1) | ((lane >> 4) << 1); ch = (lane >> 1) & 7; }
+                else if (SHAPE == 5) { row = ((lane >> 2) & 3) | ((lane >> 5) << 2); ch = (lane & 3) | (((lane >> 4) & 1) << 2); }
+                else { row = (lane >> 2) & 7; ch = (lane & 3) | ((lane >> 5) << 2); }
+#pragma unroll
+                for (int k = 0; k < 8; ++k)
+                {
+                    const long long rr = r0 + 8 * k + row;
+                    const long long c = cb + 16 * b + 4 * ch;
                     *(int4a*)(out + rr * ld + c) = v;
                     v += 1;
                 }
@@ -167,7 +189,7 @@ int main(int argc, char** argv)
     int dev = 0, cus = 0;
     hipGetDevice(&dev);
     hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    auto run = [&](auto k, const char* shape, int W, int TW, int order, int wgPerCu, int rowsW = 0) {
+    auto run = [&](auto k, const char* shape, int W, int TW, int order, int wgPerCu, int rowsW = 0, int grid = 0) {
         const int nChunks = (R - 1) / ((rowsW ? rowsW : W) * 64), nTiles = C / TW;
         const size_t lds = wgPerCu == 1 ? 100000 : 0;
         std::vector<int> hs;
@@ -190,7 +212,7 @@ int main(int argc, char** argv)
         {
             hipMemsetAsync(counter, 0, 4);
             hipEventRecord(e0);
-            hipLaunchKernelGGL(k, cus * wgPerCu, 64 * W, lds, 0, out, ld, R, C, TW, W, sched, counter, nChunks, nTiles);
+            hipLaunchKernelGGL(k, grid ? grid : cus * wgPerCu, 64 * W, lds, 0, out, ld, R, C, TW, W, sched, counter, nChunks, nTiles);
             hipEventRecord(e1);
             hipEventSynchronize(e1);
             float ms;
@@ -199,14 +221,16 @@ int main(int argc, char** argv)
         }
         hipFree(sched);
         const double wbytes = (double)nChunks * (rowsW ? rowsW : W) * 64 * (double)nTiles * TW * 4;
-        printf("R %d C %d ld %lld shape %s W %2d x %d/CU TW %5d order %d: %8.3f ms %8.1f GB/s\n", R, C, ld, shape, W,
-               wgPerCu, TW, order, best, wbytes / best / 1e6);
+        const int g = grid ? grid : cus * wgPerCu;
+        printf("R %d C %d ld %lld shape %s W %2d x %d/CU TW %5d order %d grid %d: %8.3f ms %8.1f GB/s %6.2f GB/s/WG\n", R, C,
+               ld, shape, W, wgPerCu, TW, order, g, best, wbytes / best / 1e6, wbytes / best / 1e6 / g);
     };
-    run(kern<0, 128>, "16x64 d128", 8, 512, 2, 1);
-    run(kernX<0, 0>, "X prep0 blk0", 8, 512, 2, 1, 7);
-    run(kernX<300, 0>, "X prep300 blk0", 8, 512, 2, 1, 7);
-    run(kernX<300, 40>, "X prep300 blk40", 8, 512, 2, 1, 7);
-    run(kernX<300, 80>, "X prep300 blk80", 8, 512, 2, 1, 7);
-    run(kernX<0, 80>, "X prep0 blk80", 8, 512, 2, 1, 7);
+    // per-CU store rate by the lane layout of an 8-row x 128-B instruction (64 CUs)
+    run(kern<1, 0>, "8x128 row-major", 8, 512, 2, 1, 0, 64);
+    run(kern<3, 0>, "8x128 chunk-major", 8, 512, 2, 1, 0, 64);
+    run(kern<4, 0>, "8x128 ch{1,2,3}", 8, 512, 2, 1, 0, 64);
+    run(kern<5, 0>, "8x128 ch{0,1,4}", 8, 512, 2, 1, 0, 64);
+    run(kern<6, 0>, "8x128 ch{0,1,5}", 8, 512, 2, 1, 0, 64);
+    run(kern<0, 0>, "16x64 pure", 8, 512, 2, 1, 0, 64);
     return 0;
 }
