@@ -940,7 +940,7 @@ int enqueue_batch(gsa_ctx* ctx, int mode, int npairs, const gsa_pair_dev* pairs,
             ctx->stamps_n = 0;
             if (env_int("GSA_STAMPS", 0))
             {
-                const size_t n = 2 * words + 3 * (size_t)a.xTasks;
+                const size_t n = 4 * words + 3 * (size_t)a.xTasks;
                 if (ctx->stamps_cap < n)
                 {
                     if (ctx->stamps) (void)hipFree(ctx->stamps);
@@ -958,6 +958,26 @@ int enqueue_batch(gsa_ctx* ctx, int mode, int npairs, const gsa_pair_dev* pairs,
             }
         }
         a.xdone = ctx->xdone;
+    }
+    if (!fused && krow && !lane && env_int("GSA_STAMPS", 0))
+    {
+        // the K-rows fill's ledger (nw_krow_kernel): 6 words per strip
+        const size_t n = 6 * (size_t)tickets * (size_t)krowNS;
+        ctx->stamps_n = 0;
+        if (ctx->stamps_cap < n)
+        {
+            if (ctx->stamps) (void)hipFree(ctx->stamps);
+            ctx->stamps = nullptr;
+            ctx->stamps_cap = 0;
+            if ((e = hipMalloc(&ctx->stamps, n * sizeof(unsigned long long))) != hipSuccess)
+                return fail(ctx, e, GSA_ERROR_MEMORY_ALLOCATION);
+            ctx->stamps_cap = n;
+        }
+        if ((e = hipMemsetAsync(ctx->stamps, 0, n * sizeof(unsigned long long), st)) != hipSuccess)
+            return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
+        a.stamps = ctx->stamps;
+        ctx->stamps_n = n;
+        ctx->stamps_stream = st;
     }
     e = hipMemsetAsync(ctx->ctl, 0, 4, st);  // the ticket; the error word stays sticky
     if (e != hipSuccess) return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);

@@ -90,15 +90,20 @@ __device__ __forceinline__ void ex_tile_core(const ExpandArgs& a, const ExpandPa
                                              int lane, int cb, int cols, int r0, int y, int lb, uint32_t topw)
 {
     const int g = a.g;
-    const int ce = min(cols + kExtra, d.C - cb);
     const uint32_t qrow = qbase + 4u * (uint32_t)(y * kQS + kQOff);
     const uint32_t hbase = (lane == 0) ? topw : gfill;  // lanes >= 1 read a row of g (no branch)
-    // lane 63 reaches column cb + ce at step ce + 63.  Row r0 + rr is stored over columns
+    // Row r0 + rr is stored over columns
     // lo(rr) .. hi(rr) (relative to cb): lo = 64 - rr (1 in the first tile column), hi = min(cols + 63
     // - rr, C - cb): the chunks of blocks 4 .. cols / 16 + 3 of every lane, whole aligned lines, the
     // next tile's parallelogram starting where this one ends -- per-element stores only at the
     // matrix's own edges (its first and last columns, rows past R)
-    const int NB = (ce + 64 + kBlk - 1) / kBlk;
+    // the last stored element is lane 63's column cols at step cols + 63: later steps (columns past
+    // every row's hi) are not computed
+#ifdef GSA_EXPAND_FULLNB
+    const int NB = (min(cols + kExtra, d.C - cb) + 64 + kBlk - 1) / kBlk;  // (A/B: the round-5 extent)
+#else
+    const int NB = (cols + 63) / kBlk + 1;
+#endif
     const int hiMax = min(cols + 63, d.C - cb);  // hi(0)
     // transposed output (as nw_lane.hip): store k has lane 16h + n write columns 4h .. 4h+3 of the
     // block's 16 for row r0 + 16k + n

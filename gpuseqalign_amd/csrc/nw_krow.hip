@@ -225,12 +225,25 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
     };
     // the error word is a global load, which waits for this wave's outstanding header stores
     // (vmcnt retires in order): polled once per 32 LDS polls
+    // ledger (GSA_STAMPS=1, plain fills): shader-clock cycles spent waiting here, and the waits
+    constexpr bool kLedger = PT != 3;
+    uint64_t spinCyc = 0;
+    unsigned spinN = 0;
     auto spin = [&](int b) {
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        const uint64_t c0 = (kLedger && a.stamps) ? __builtin_amdgcn_s_memtime() : 0;
         for (int it = 1;; ++it)
         {
             const int pin = flag_ld(f_in), pco = flag_ld(c_out), pxo = (w == 0) ? flag_ld(f_xo) : 0;
-            if (ok(pin, pco, pxo, b)) return true;
+            if (ok(pin, pco, pxo, b))
+            {
+                if (kLedger && a.stamps)
+                {
+                    spinCyc += __builtin_amdgcn_s_memtime() - c0;
+                    ++spinN;
+                }
+                return true;
+            }
             __builtin_amdgcn_s_sleep(1);
             if (__builtin_amdgcn_s_memrealtime() - t0 > a.spin || ((it & 31) == 0 && err_set(a)))
             {
@@ -554,6 +567,11 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
         if (!block(b, qA, qB, F(), advance(b))) return;
         if (b + 1 >= NB) break;
         if (!block(b + 1, qB, qA, F(), advance(b + 1))) return;
+    }
+    if (kLedger && a.stamps && lane == 0)
+    {
+        a.stamps[6 * w + 4] = spinCyc;
+        a.stamps[6 * w + 5] = spinN;
     }
     if (pt)
     {
@@ -1250,9 +1268,23 @@ __global__ void __launch_bounds__((64 * kr_waves<NS, PT>()), 1) nw_krow_kernel(S
             kr_loader<NS, K, LW, 2, Q8>(pa, L, tk, lane);
         else
         {
+            // ledger (GSA_STAMPS=1): per strip [realtime start, end, shader clock start, end, cycles
+            // waiting for input, waits]
+            unsigned long long* const lg = a.stamps ? a.stamps + 6 * ((size_t)tkg * NS + w) : nullptr;
+            pa.stamps = lg ? a.stamps + 6 * (size_t)tkg * NS : nullptr;
+            if (lg && lane == 0)
+            {
+                lg[0] = __builtin_amdgcn_s_memrealtime();
+                lg[2] = __builtin_amdgcn_s_memtime();
+            }
             __builtin_amdgcn_s_setprio(3);
             kr_strip<NS, K, LW, PT, Q8>(pa, L, tk, w, lane);
             __builtin_amdgcn_s_setprio(0);
+            if (lg && lane == 0)
+            {
+                lg[1] = __builtin_amdgcn_s_memrealtime();
+                lg[3] = __builtin_amdgcn_s_memtime();
+            }
         }
     }
 }
@@ -2252,7 +2284,7 @@ __global__ void __launch_bounds__(64 * W) nw_full_fused_kernel(StripArgs a)
         pa.xdone = a.xdone + (size_t)d.ticketBase * NS;  // the pair's strip words
         // (stamps: the ticket's start, and each strip's end -- the strips of a pair sweep the same
         // columns at the same pace, so their ends are spaced by the wavefront's lag)
-        unsigned long long* const sst = a.stamps ? a.stamps + 2 * ((size_t)d.ticketBase + tk) * NS : nullptr;
+        unsigned long long* const sst = a.stamps ? a.stamps + 4 * ((size_t)d.ticketBase + tk) * NS : nullptr;
         if (threadIdx.x < 32) lds_st(L.flags + 4u * threadIdx.x, 0);
         if (threadIdx.x >= kFCap / 4 && threadIdx.x < kFCap / 4 + 8) lds_st(L.flags + 4u * threadIdx.x, 0);
         if (threadIdx.x >= 64 && threadIdx.x < 64 + 3 * NS) lds_st(kr_xwords(L.flags) + 4u * (threadIdx.x - 64), 0);
@@ -2267,11 +2299,19 @@ __global__ void __launch_bounds__(64 * W) nw_full_fused_kernel(StripArgs a)
             kr_loader<NS, K, LW, 2, Q8>(pa, L, tk, lane);
         else if (w < NS)
         {
-            if (sst && lane == 0) sst[2 * w] = __builtin_amdgcn_s_memrealtime();
+            if (sst && lane == 0)
+            {
+                sst[4 * w] = __builtin_amdgcn_s_memrealtime();
+                sst[4 * w + 2] = __builtin_amdgcn_s_memtime();
+            }
             __builtin_amdgcn_s_setprio(3);
             kr_strip<NS, K, LW, 3, Q8>(pa, L, tk, w, lane);
             __builtin_amdgcn_s_setprio(0);
-            if (sst && lane == 0) sst[2 * w + 1] = __builtin_amdgcn_s_memrealtime();
+            if (sst && lane == 0)
+            {
+                sst[4 * w + 1] = __builtin_amdgcn_s_memrealtime();
+                sst[4 * w + 3] = __builtin_amdgcn_s_memtime();
+            }
         }
     }
     // pass 2: the streamed expansion (nw_expand_dev.h ex_stream): W - 1 tile waves and a loader wave
@@ -2290,7 +2330,7 @@ __global__ void __launch_bounds__(64 * W) nw_full_fused_kernel(StripArgs a)
     xa.run = a.xrun;
     xa.spin = a.spin;
     xa.err = a.err;
-    const xdev::ExFused fx {a.xdone, a.epoch, a.stamps ? a.stamps + 2 * (size_t)a.nTicketsTotal * NS : nullptr};
+    const xdev::ExFused fx {a.xdone, a.epoch, a.stamps ? a.stamps + 4 * (size_t)a.nTicketsTotal * NS : nullptr};
     xdev::ex_stream<W, true>(xa, a.xcounter, fx, w, lane);
 }
 

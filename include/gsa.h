@@ -182,8 +182,11 @@ int gsa_align_sparse_pt(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, cons
                         int32_t* tileHcolMat_out, gsa_sparse_geom* geom, int32_t* align_cost, gsa_laps* laps);
 
 /* Measurement aid, not part of the reference's interface: with GSA_STAMPS=1 in the environment a
- * fused full fill records s_memrealtime stamps (100 MHz): [start, end] per pass-1
- * strip, then [claimed, ready, done] per expansion task.  Copies the last such launch's *n stamps
+ * fused full fill records stamps: [start, end] (s_memrealtime, 100 MHz) and [start,
+ * end] (s_memtime, shader clock) per pass-1 strip, then [claimed, ready, done] (s_memrealtime) per
+ * expansion task; a K-rows sparse fill or a full fill's separate pass 1 records its strip ledger:
+ * [realtime start, end, shader clock start, end, cycles waiting for input, waits] per strip.  Copies
+ * the last such launch's *n stamps
  * into out (cap >= *n, else errorInvalidValue; out may be null to query *n); synchronizes the stream
  * that launch ran on. */
 int gsa_debug_stamps(gsa_ctx* ctx, uint64_t* out, int64_t cap, int64_t* n);

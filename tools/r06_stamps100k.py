@@ -42,8 +42,8 @@ def main():
     nstrips = tickets * ns
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     np.savez_compressed(os.path.join(ROOT, "gpurun_out", f"r06_stamps100k{tag}.npz"), st=st, nstrips=nstrips)
-    strips = st[:2 * nstrips].reshape(nstrips, 2)
-    tasks = st[2 * nstrips:].reshape(-1, 3)
+    strips = st[:4 * nstrips].reshape(nstrips, 4)
+    tasks = st[4 * nstrips:].reshape(-1, 3)
     t0 = min(strips[:, 0].min(), tasks[tasks[:, 0] > 0, 0].min())
     us = lambda v: (v - t0) / 100.0
     end = us(strips[:, 1])
@@ -57,6 +57,9 @@ def main():
            "strip_end_us": {"first": round(float(end.min()), 1), "median": round(float(np.median(end)), 1),
                             "last": round(float(end.max()), 1)},
            "strip_start_us_last": round(float(us(strips[:, 0]).max()), 1),
+           "strip_clock_ghz": {"first": round(float((strips[0, 3] - strips[0, 2]) / ((strips[0, 1] - strips[0, 0]) * 10.0)), 3),
+                               "median": round(float(np.median((strips[:, 3] - strips[:, 2]) /
+                                                               ((strips[:, 1] - strips[:, 0]) * 10.0))), 3)},
            "task_wait_us": {"median": round(float(np.median(wait)), 2), "p90": round(float(np.percentile(wait, 90)), 2),
                             "sum_ms": round(float(wait.sum()) / 1e3, 2)},
            "task_dur_us": {"median": round(float(np.median(dur)), 2), "p10": round(float(np.percentile(dur, 10)), 2),
