@@ -386,8 +386,18 @@ def bench_full100k(dev, eng, tS, sh, stream, steps, warmup, world):
             "hbm_write_GBps": round(b / (km * 1e-3) / 1e9, 1),
             "hbm_frac": round(b / (km * 1e-3) / 1e9 / PEAK_HBM_GBPS, 4),
             "bound": "hbm (4 B written per cell; MI355X 8 TB/s spec)",
+            "pmc_write_over_algorithmic": pmc_full100k_ratio(),
+            "rocprof": "profiles/r06_full100k_kernel_stats.csv (nw_full_fused_kernel<4, 8, true>, this fill alone)",
             "align_cost": cost,
             "golden_align_cost": None if gold is None else gold["pairs"]["related"]["align_cost"]}
+
+
+def pmc_full100k_ratio():
+    """WRITE_SIZE of the fused 100k x 100k fill over its matrix bytes (profiles/r06_pmc.json)."""
+    try:
+        return json.load(open(os.path.join(ROOT, "profiles", "r06_pmc.json")))["pmc"]["f"]["write_over_algorithmic"]
+    except Exception:
+        return None
 
 
 def box_write_rate(local, gib=16, reps=5):
@@ -447,10 +457,10 @@ def pass_fields(tm, rank_bytes):
 
 
 def pmc_write_ratio(n_pairs, kernel):
-    """HBM bytes written (PMC WRITE_SIZE of both passes, profiles/r04_pmc_full_batch.json, collected
-    by tools/r04_pmc_full.sh on the same batch) over the matrix bytes, or None for another
+    """HBM bytes written (PMC WRITE_SIZE of both passes, profiles/r06_pmc_full_batch.json, collected
+    by tools/r06_prof.sh on the same batch) over the matrix bytes, or None for another
     shape/kernel: the physical write rate is hbm_write_GBps times this."""
-    p = os.path.join(ROOT, "profiles", "r04_pmc_full_batch.json")
+    p = os.path.join(ROOT, "profiles", "r06_pmc_full_batch.json")
     try:
         j = json.load(open(p))
         if n_pairs == 64 and j.get("kernel", "").split(" ")[0] == kernel.split(" ")[0]:
