@@ -361,7 +361,8 @@ class Engine:
         """The stamps of the last launch made under GSA_STAMPS=1 (gsa_debug_stamps), uint64: a fused
         full fill's [realtime start, end, shader clock start, end] per pass-1 strip, then [claimed,
         ready, done] per expansion task; a K-rows fill's strip ledger [realtime start, end, clock
-        start, end, cycles waiting, waits] per strip; empty if none were recorded."""
+        start, end, cycles waiting, waits, 4 block spans (diagnostic builds)] per strip; empty if
+        none were recorded."""
         import numpy as np
         n = ctypes.c_int64(0)
         self._check(lib().gsa_debug_stamps(self._h, None, 0, ctypes.byref(n)), "gsa_debug_stamps")

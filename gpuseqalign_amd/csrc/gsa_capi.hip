@@ -961,8 +961,8 @@ int enqueue_batch(gsa_ctx* ctx, int mode, int npairs, const gsa_pair_dev* pairs,
     }
     if (!fused && krow && !lane && env_int("GSA_STAMPS", 0))
     {
-        // the K-rows fill's ledger (nw_krow_kernel): 6 words per strip
-        const size_t n = 6 * (size_t)tickets * (size_t)krowNS;
+        // the K-rows fill's ledger (nw_krow_kernel): 10 words per strip
+        const size_t n = 10 * (size_t)tickets * (size_t)krowNS;
         ctx->stamps_n = 0;
         if (ctx->stamps_cap < n)
         {

@@ -104,6 +104,10 @@ constexpr uint32_t kFCap = 160;
 // of boundaries < the word in memory (kXDone: all); the data at kr_xdata: 64 bytes per (strip,
 // slot, row 64j).
 constexpr int kXD = 32;
+constexpr int kLedgerWords = 10;  // GSA_STAMPS words per strip of a K-rows fill (gsa_debug_stamps)
+#ifndef GSA_KR_BLOCK_LEDGER
+#define GSA_KR_BLOCK_LEDGER 0
+#endif
 __host__ __device__ constexpr uint32_t kr_xwords(uint32_t flags) { return flags + 256u; }
 __host__ __device__ constexpr uint32_t kr_xdata(uint32_t flags) { return flags + 256u + 64u; }
 [[maybe_unused]] __host__ __device__ constexpr uint32_t kr_xstage_bytes(int ns) { return 64u + (uint32_t)ns * kXD * 256u; }
@@ -229,6 +233,21 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
     constexpr bool kLedger = PT != 3;
     uint64_t spinCyc = 0;
     unsigned spinN = 0;
+#if GSA_KR_BLOCK_LEDGER
+    // diagnostic build (tools/r06_ledger.py): s_memtime at each block's start, after its input wait
+    // and halo read, after its 16 steps and at its end; per strip the sums of the three spans and of
+    // the gaps between blocks (the s_memtime results are awaited where they are subtracted, which
+    // adds lgkmcnt waits: the spans are upper bounds)
+    uint64_t ldg[4] = {0, 0, 0, 0}, ldgEnd = 0;
+    // (sched_barrier: no instruction moves across a stamp)
+    auto ldgT = []() {
+        __builtin_amdgcn_sched_barrier(0);
+        const uint64_t t = __builtin_amdgcn_s_memtime();
+        __builtin_amdgcn_sched_barrier(0);
+        return t;
+    };
+#define GSA_LDG_T() ldgT()
+#endif
     auto spin = [&](int b) {
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
         const uint64_t c0 = (kLedger && a.stamps) ? __builtin_amdgcn_s_memtime() : 0;
@@ -410,6 +429,10 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
     auto block = [&](int b, int (&qc)[K][kQD], int (&qn)[K][kQD], auto rampT, bool cap) {
         constexpr bool RAMP = decltype(rampT)::value;
         constexpr bool CAP = !RAMP;  // ramp blocks hold no boundary (tBx >= 64)
+#if GSA_KR_BLOCK_LEDGER
+        const uint64_t lt0 = GSA_LDG_T();
+        if (ldgEnd) ldg[3] += lt0 - ldgEnd;
+#endif
         {
             const int pin = __builtin_amdgcn_readfirstlane(rpin), pco = __builtin_amdgcn_readfirstlane(rpco);
             const int pxo = (w == 0) ? __builtin_amdgcn_readfirstlane(rpxo) : 0;
@@ -421,6 +444,9 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
             if (!ok(pin, pco, pxo, b) && !spin(b)) return false;
         }
         halo_load(b);
+#if GSA_KR_BLOCK_LEDGER
+        const uint64_t lt1 = GSA_LDG_T();
+#endif
         const uint32_t pn = q_off(b + 1);
         int va[CAP ? K : 1][CAP ? kBlk : 1];
 #pragma unroll
@@ -469,6 +495,9 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
         // the block's hand-off at its end (the next strip sees it a block earlier than when it is
         // written behind the next block's halo reads: measured 1 % faster at 100k, slightly slower
         // per block)
+#if GSA_KR_BLOCK_LEDGER
+        const uint64_t lt2 = GSA_LDG_T();
+#endif
         handoff(b);
         if constexpr (fx && !RAMP)
             if ((b & 15) == 15)
@@ -545,6 +574,12 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
                 if (pt && (jb % a.ptChunk == 0 || jb == tcols)) ptPend = jb;
             }
         }
+#if GSA_KR_BLOCK_LEDGER
+        ldgEnd = GSA_LDG_T();
+        ldg[0] += lt1 - lt0;
+        ldg[1] += lt2 - lt1;
+        ldg[2] += ldgEnd - lt2;
+#endif
         return true;
     };
 
@@ -570,8 +605,11 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
     }
     if (kLedger && a.stamps && lane == 0)
     {
-        a.stamps[6 * w + 4] = spinCyc;
-        a.stamps[6 * w + 5] = spinN;
+        a.stamps[kLedgerWords * w + 4] = spinCyc;
+        a.stamps[kLedgerWords * w + 5] = spinN;
+#if GSA_KR_BLOCK_LEDGER
+        for (int q = 0; q < 4; ++q) a.stamps[kLedgerWords * w + 6 + q] = ldg[q];
+#endif
     }
     if (pt)
     {
@@ -1269,9 +1307,9 @@ __global__ void __launch_bounds__((64 * kr_waves<NS, PT>()), 1) nw_krow_kernel(S
         else
         {
             // ledger (GSA_STAMPS=1): per strip [realtime start, end, shader clock start, end, cycles
-            // waiting for input, waits]
-            unsigned long long* const lg = a.stamps ? a.stamps + 6 * ((size_t)tkg * NS + w) : nullptr;
-            pa.stamps = lg ? a.stamps + 6 * (size_t)tkg * NS : nullptr;
+            // waiting for input, waits, and in a GSA_KR_BLOCK_LEDGER build the block spans]
+            unsigned long long* const lg = a.stamps ? a.stamps + kLedgerWords * ((size_t)tkg * NS + w) : nullptr;
+            pa.stamps = lg ? a.stamps + kLedgerWords * (size_t)tkg * NS : nullptr;
             if (lg && lane == 0)
             {
                 lg[0] = __builtin_amdgcn_s_memrealtime();

@@ -185,7 +185,8 @@ int gsa_align_sparse_pt(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, cons
  * fused full fill records stamps: [start, end] (s_memrealtime, 100 MHz) and [start,
  * end] (s_memtime, shader clock) per pass-1 strip, then [claimed, ready, done] (s_memrealtime) per
  * expansion task; a K-rows sparse fill or a full fill's separate pass 1 records its strip ledger:
- * [realtime start, end, shader clock start, end, cycles waiting for input, waits] per strip.  Copies
+ * [realtime start, end, shader clock start, end, cycles waiting for input, waits, four block spans of
+ * a diagnostic build] per strip (10 words).  Copies
  * the last such launch's *n stamps
  * into out (cap >= *n, else errorInvalidValue; out may be null to query *n); synchronizes the stream
  * that launch ran on. */

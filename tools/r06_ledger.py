@@ -49,7 +49,7 @@ def main():
         e1.record()
         eng.sync()
         ms.append(e0.elapsed_time(e1))
-    st = eng.debug_stamps().astype(np.int64).reshape(-1, 6)
+    st = eng.debug_stamps().astype(np.int64).reshape(-1, 10)
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     np.save(os.path.join(ROOT, "gpurun_out", f"r06_ledger_{R}x{C}{'_xr' if xr else ''}.npy"), st)
     st = st[st[:, 1] > 0]
@@ -74,6 +74,14 @@ def main():
                       "waits": int(np.median(st[:, 5]))},
            "strip_start_lag_us": round(float(np.median(np.diff(np.sort(start)))), 3),
            "strip_end_lag_us": round(float(np.median(np.diff(np.sort(end)))), 3)}
+    if st[:, 6:].any():
+        # GSA_KR_BLOCK_LEDGER build: per-step cycles of the block's spans (input wait + halo read,
+        # 16 steps, hand-off and captures, between blocks), first strip and median
+        spans = st[:, 6:10].astype(np.float64) / (16 * nblk)
+        names = ["wait_and_halo", "steps", "handoff_capture", "between_blocks"]
+        out["block_ledger_cycles_per_step"] = {
+            "first_strip": {k: round(float(v), 2) for k, v in zip(names, spans[0])},
+            "median": {k: round(float(v), 2) for k, v in zip(names, np.median(spans, axis=0))}}
     # the critical path: the last strip's end = the first strip's sweep + the lags
     out["ledger_ms"] = {"first_sweep": round(float(span_us[0]) / 1e3, 4),
                         "lag_total": round(float(end.max() - end[np.argmin(start)]) / 1e3, 4)}
