@@ -120,6 +120,7 @@ SIGNATURES = {
     "gsa_version": (ctypes.c_char_p, []),
     "gsa_debug_stamps": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64)]),
     "gsa_set_lap_callback": (ctypes.c_int, [_vp, _vp, _vp]),
+    "gsa_set_knob": (ctypes.c_int, [_vp, ctypes.c_char_p, ctypes.c_char_p]),
     "gsa_set_full_timing": (ctypes.c_int, [_vp, _i32]),
     "gsa_last_full_timing": (ctypes.c_int, [_vp, ctypes.POINTER(FullTiming)]),
     "gsa_sparse_tile_by": (_i32, []),
@@ -386,6 +387,13 @@ class Engine:
         return {"pass1_ms": f(t.pass1_ms), "pass2_ms": f(t.pass2_ms), "clock_ghz_median": f(t.clock_ghz_median),
                 "clock_ghz_mean": f(t.clock_ghz_mean), "clock_workgroups": int(t.workgroups), "fused": bool(t.fused),
                 "pipelined_groups": int(t.groups)}
+
+    def set_knob(self, name: str, value: Optional[str]):
+        """Set a measurement / test switch (GSA_FULL_KERNEL, GSA_KROW_NS, ...) for this context
+        (gsa_set_knob); None unsets it.  A context takes the knobs from the environment once, when
+        it is created."""
+        self._check(lib().gsa_set_knob(self._h, name.encode(), None if value is None else str(value).encode()),
+                    "gsa_set_knob")
 
     def set_lap_callback(self, fn: Optional[Callable[[str], None]]):
         """fn(lap_name) at every phase boundary of the host-buffer entry points (align_full,

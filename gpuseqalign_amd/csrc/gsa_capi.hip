@@ -13,7 +13,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <new>
+#include <string>
 #include <thread>
 #include <vector>
 
@@ -160,6 +162,8 @@ struct gsa_ctx
     // phase-boundary callback of the host-buffer entry points (gsa_set_lap_callback)
     gsa_lap_fn lap_fn = nullptr;
     void* lap_user = nullptr;
+    // the knobs (kKnobNames): the environment when the context was created, then gsa_set_knob
+    std::map<std::string, std::string> knobs;
 };
 
 namespace {
@@ -236,30 +240,55 @@ int check_inputs(int32_t adjrows, int32_t adjcols, int32_t substsz)
     return GSA_SUCCESS;
 }
 
+// Knobs: measurement and test switches, named as environment variables.  A context reads them
+// once, from the environment, when it is created (gsa_ctx_create); gsa_set_knob changes them per
+// context.  Launches never read the environment.
+constexpr const char* kKnobNames[] = {
+    "GSA_SPARSE_KERNEL", "GSA_KROW_K",      "GSA_KROW_NS",      "GSA_KROW_Q8",       "GSA_LANE_NS",
+    "GSA_LANE_FEED",     "GSA_LANE_PAIR",   "GSA_FULL_KERNEL",  "GSA_FULL_FUSED",    "GSA_FULL_SPLIT",
+    "GSA_EXPAND_RR",     "GSA_BATCH_ORDER", "GSA_SCORE_SCAN",   "GSA_SCORE_KERNEL",  "GSA_SCORE_K",
+    "GSA_SCORE_BIDI",    "GSA_SCORE_BIDI_SW", "GSA_BIDI_GRAN",  "GSA_BIDI_SKEW",     "GSA_BIDI_SW_CONT",
+    "GSA_BIDI_LOG",      "GSA_TRACE_BAND",  "GSA_TRACE_BAND_BUDGET", "GSA_STAMPS"};
+
+bool knob_known(const char* name)
+{
+    for (const char* k : kKnobNames)
+        if (std::strcmp(k, name) == 0) return true;
+    return false;
+}
+
+// the knob's value in this context, or null (unset)
+const char* knob(const gsa_ctx* ctx, const char* name)
+{
+    auto it = ctx->knobs.find(name);
+    return it == ctx->knobs.end() ? nullptr : it->second.c_str();
+}
+
+int env_int(const gsa_ctx* ctx, const char* name, int dflt)
+{
+    const char* e = knob(ctx, name);
+    return e ? std::atoi(e) : dflt;
+}
+
 // Sparse fills run on the K-rows-per-lane kernel (nw_krow.hip, K = 4): 5.9 vs 8.0 ms for the
 // 100k pair and 5.7 vs 4.3 TCUPS for 512 pairs of 20k against the strip kernel (nw_strip.hip).
 // mlsppt runs on the K-rows kernel too, in its (NS 4, K 4) geometry (one tile row per ticket,
 // enqueue_batch).  GSA_SPARSE_KERNEL=strip forces the strip kernel (read per launch, tested);
 // GSA_KROW_K (2, 4) and GSA_KROW_NS (2, 4, 8) pick the K-rows geometry.
 enum SparseKern { kSpStrip, kSpKrow };
-SparseKern sparse_kernel()
+SparseKern sparse_kernel(const gsa_ctx* ctx)
 {
-    const char* e = std::getenv("GSA_SPARSE_KERNEL");
+    const char* e = knob(ctx, "GSA_SPARSE_KERNEL");
     return (e && std::strcmp(e, "strip") == 0) ? kSpStrip : kSpKrow;
 }
 
-int env_int(const char* name, int dflt)
-{
-    const char* e = std::getenv(name);
-    return e ? std::atoi(e) : dflt;
-}
 
 
 // Full fills run on the one-row-per-lane kernel (nw_lane.hip); GSA_LANE_NS = lane strips per
 // workgroup (1..4, 6, 8; read per launch, tested; 4 is the default and the fastest measured).
-int lane_ns()
+int lane_ns(const gsa_ctx* ctx)
 {
-    const char* e = std::getenv("GSA_LANE_NS");
+    const char* e = knob(ctx, "GSA_LANE_NS");
     const int v = e ? std::atoi(e) : gsa::kLaneNSDefault;
     return ((v >= 1 && v <= 4) || v == 6 || v == 8) ? v : gsa::kLaneNSDefault;
 }
@@ -334,18 +363,18 @@ int run_check(gsa_ctx* ctx, gsa::CheckArgs& a, bool sparse, hipStream_t st, gsa_
 // Score-only kernels: global alignments run on the strip kernel in its affine mode (shifted
 // Gotoh, nw_strip.hip kModeScoreAG); local ones on the row scan (nw_scan.hip).  GSA_SCORE_SCAN=1
 // sends global ones to the row scan as well (tests compare the two).
-bool score_scan_forced()
+bool score_scan_forced(const gsa_ctx* ctx)
 {
-    const char* e = std::getenv("GSA_SCORE_SCAN");
+    const char* e = knob(ctx, "GSA_SCORE_SCAN");
     return e && std::atoi(e) == 1;
 }
 
 constexpr int kScoreTooLarge = 1000;  // internal: score_ag_strip -> row scan
 
 // score-only fills on the K-rows layout (default) or, with GSA_SCORE_KERNEL=strip, the strip kernel
-bool score_kernel_krow()
+bool score_kernel_krow(const gsa_ctx* ctx)
 {
-    const char* e = std::getenv("GSA_SCORE_KERNEL");
+    const char* e = knob(ctx, "GSA_SCORE_KERNEL");
     return !(e && std::strcmp(e, "strip") == 0);
 }
 
@@ -392,9 +421,9 @@ int score_bidi(gsa_ctx* ctx, const int32_t* seqY, int64_t R, const int32_t* seqX
     // is free as well and the split even.  Short pairs keep two lane taps (m = K floor(R/2K)).
     int64_t m = (int64_t)K * (R / (2 * K));
     bool topFree = false, botFree = false;
-    if (R >= 4 * TR && env_int("GSA_BIDI_GRAN", 1))
+    if (R >= 4 * TR && env_int(ctx, "GSA_BIDI_GRAN", 1))
     {
-        const int skewEnv = env_int("GSA_BIDI_SKEW", -1);
+        const int skewEnv = env_int(ctx, "GSA_BIDI_SKEW", -1);
         // (local linear: 0.075, the third pair's share of the chip moves the balance; 50k SW-LG
         // 2.78 -> 2.76 ms, profiles/r05_sw_skew.txt)
         const double p = affine ? 0.117 : local ? 0.075 : 0.05;
@@ -469,7 +498,7 @@ int score_bidi(gsa_ctx* ctx, const int32_t* seqY, int64_t R, const int32_t* seqX
     }
     for (int h = 0; h < 3; ++h) d[h].C = d[h].Cp = (int)C;
     const int mode = local ? (affine ? gsa::kModeScoreSW : gsa::kModeScoreSWL) : affine ? gsa::kModeScoreAG : gsa::kModeScoreAGL;
-    const int q8env = env_int("GSA_KROW_Q8", 1);
+    const int q8env = env_int(ctx, "GSA_KROW_Q8", 1);
     const int q8 =
         (q8env != 0 && (q8env == 2 || K == 4) && gsa::krow_score_lds_bytes(substsz, true) <= (size_t)ctx->lds_max) ? 1 : 0;
     gsa::StripArgs a;
@@ -541,8 +570,8 @@ int score_bidi(gsa_ctx* ctx, const int32_t* seqY, int64_t R, const int32_t* seqX
         long long best = key ? (long long)(key >> bits) : 0;
         const long long ie = (long long)(idx / (unsigned long long)(C + 1));
         const bool fallback = !((long long)score < best || ((long long)score == best && ie <= m));
-        const bool cont = fallback && topFree && env_int("GSA_BIDI_SW_CONT", 1) != 0;
-        if (env_int("GSA_BIDI_LOG", 0))  // (tests: which way the pair went)
+        const bool cont = fallback && topFree && env_int(ctx, "GSA_BIDI_SW_CONT", 1) != 0;
+        if (env_int(ctx, "GSA_BIDI_LOG", 0))  // (tests: which way the pair went)
             std::fprintf(stderr, "gsa local both ends: m %lld, through m %d, best off it %lld at row %lld -> %s\n",
                          (long long)m, score, best, ie,
                          !fallback ? "answer" : cont ? "bottom again from row m" : "one direction");
@@ -617,12 +646,12 @@ int score_ag_strip(gsa_ctx* ctx, const int32_t* seqY, int64_t R, const int32_t* 
     // twice the strips shorten it), 4 for NW-LG; same box, 5k-100k pairs: NW-AG -5..-7 %, SW-AG
     // -9..-11 %, SW-LG -2..-5 % with 2, NW-LG +12..18 % (profiles/r04_score_k.txt).  GSA_SCORE_K
     // = 2 / 4 forces one
-    const int kenv = env_int("GSA_SCORE_K", 0);
+    const int kenv = env_int(ctx, "GSA_SCORE_K", 0);
     const int scoreK = kenv == 2 || kenv == 4 ? kenv : (!local && gapo == gape) ? 4 : 2;
     // the K-rows score kernel unless GSA_SCORE_KERNEL=strip, or its LDS (a profile of substsz rows)
     // does not fit, or SW with ge > 0 (its per-row key offsets assume z grows along j); the strip
     // kernel's score modes otherwise, on its own 1024-row tickets
-    const bool krow = score_kernel_krow() && (!local || gape <= 0) && gsa::krow_score_lds_bytes(substsz) <= ctx->lds_max;
+    const bool krow = score_kernel_krow(ctx) && (!local || gape <= 0) && gsa::krow_score_lds_bytes(substsz) <= ctx->lds_max;
     const int64_t TR = krow ? (int64_t)(64 * scoreK) * gsa::kSparseNS : (int64_t)gsa::kWaveRows * gsa::kSparseNS;
     const int64_t tickets = (R + TR - 1) / TR;
     if (tickets > (1ll << 30) || C > (1ll << 30)) return GSA_ERROR_INVALID_VALUE;
@@ -631,7 +660,7 @@ int score_ag_strip(gsa_ctx* ctx, const int32_t* seqY, int64_t R, const int32_t* 
     // 2.11 ms, profiles/r05_bidi_ab.txt).  GSA_SCORE_BIDI: 0 never, 2 at any size (tests)
     // A pair whose R is not a multiple of K but whose C is runs transposed (X down the rows, Y along
     // them, the table transposed: the same global score, and gaps cost the same either way).
-    const int bidi = env_int("GSA_SCORE_BIDI", 1);
+    const int bidi = env_int(ctx, "GSA_SCORE_BIDI", 1);
     const int kb = kenv == 2 || kenv == 4 ? kenv : 2;
     const int64_t TRb = (int64_t)(64 * kb) * gsa::kSparseNS;
     auto splits = [&](int64_t rows) { return rows % kb == 0 && rows >= 2 * kb && (bidi == 2 || rows >= 8 * TRb); };
@@ -645,7 +674,7 @@ int score_ag_strip(gsa_ctx* ctx, const int32_t* seqY, int64_t R, const int32_t* 
     // local: from both ends only by rows (the end cell's row-major tie rule does not survive a
     // transpose), and back to one direction when an alignment through the split may decide it
     float bidiMs = 0.f;
-    if (krow && local && bidi != 0 && env_int("GSA_SCORE_BIDI_SW", 1) && splits(R))
+    if (krow && local && bidi != 0 && env_int(ctx, "GSA_SCORE_BIDI_SW", 1) && splits(R))
     {
         const int sb = score_bidi(ctx, seqY, R, seqX, C, subst, substsz, gapo, gape, kb, false, out, st, true);
         if (sb == kScoreTooLargeB) return kScoreTooLarge;
@@ -701,7 +730,7 @@ int score_ag_strip(gsa_ctx* ctx, const int32_t* seqY, int64_t R, const int32_t* 
     // int16 instance behind it runs) for the 4-rows-per-lane geometry (NW-LG): 50k 2.52 -> 2.46 ms;
     // at 2 rows per lane the int16 profile is faster (SW-LG 3.71 -> 3.42 ms, NW-AG 4.16 -> 3.87;
     // profiles/r04_score_k.txt).  GSA_KROW_Q8=0 / 2: int16 / int8 always
-    const int q8env = env_int("GSA_KROW_Q8", 1);
+    const int q8env = env_int(ctx, "GSA_KROW_Q8", 1);
     a.q8 = (q8env != 0 && (q8env == 2 || scoreK == 4) && gsa::krow_score_lds_bytes(substsz, true) <= (size_t)ctx->lds_max) ? 1 : 0;
     a.q8flag = ctx->ctl + 2;
     if ((e = krow ? gsa::launch_krow_score(a, mode, scoreK, grid, st) : gsa::launch_strip_fill(a, mode, grid, st)) != hipSuccess)
@@ -760,7 +789,7 @@ int enqueue_batch(gsa_ctx* ctx, int mode, int npairs, const gsa_pair_dev* pairs,
     a.g = gapo;
     const bool lane = mode == gsa::kModeFull;
     // mlsppt publishes column chunks from the K-rows kernel only
-    const bool krow = mode == gsa::kModeSparse && (sparse_kernel() == kSpKrow || done || rows64);
+    const bool krow = mode == gsa::kModeSparse && (sparse_kernel(ctx) == kSpKrow || done || rows64);
     // single pairs: 4 strips per workgroup (each on its own SIMD: the pair's critical path);
     // batches: 8 (two strips per SIMD share the issue slots a single strip leaves idle, 512 x 20k
     // 5.7 -> 7.3 TCUPS; a single 100k pair 5.9 -> 8.4 ms), unless the batch's 4-strip tickets
@@ -770,11 +799,11 @@ int enqueue_batch(gsa_ctx* ctx, int mode, int npairs, const gsa_pair_dev* pairs,
         tileRows += std::max<long long>(1, ((long long)pairs[p].adjrows - 1 + gsa::kSparseTileBy - 1) / gsa::kSparseTileBy);
     const bool fitsChip = tileRows <= (long long)std::max(1, ctx->cu_count);
     const int nsDefault = (npairs > 1 && !fitsChip) ? gsa::kKrowNSBatchDefault : gsa::kKrowNSDefault;
-    int krowK = env_int("GSA_KROW_K", gsa::kKrowKDefault), krowNS = env_int("GSA_KROW_NS", nsDefault);
+    int krowK = env_int(ctx, "GSA_KROW_K", gsa::kKrowKDefault), krowNS = env_int(ctx, "GSA_KROW_NS", nsDefault);
     if (rows64)  // pass 1 of the two-pass full fill: the XR instances, K = 4 on 4 or 8 strips
     {
         krowK = 4;
-        krowNS = fused ? fused->ns : env_int("GSA_KROW_NS", (npairs > 1 && !fitsChip) ? 8 : 4) == 8 ? 8 : 4;
+        krowNS = fused ? fused->ns : env_int(ctx, "GSA_KROW_NS", (npairs > 1 && !fitsChip) ? 8 : 4) == 8 ? 8 : 4;
     }
     // mlsppt flags one ticket per tile row: only the geometry whose ticket is one tile row
     if (!gsa::krow_ok(krowNS, krowK) || (done && gsa::krow_ticket_rows(krowNS, krowK) != gsa::kSparseTileBy))
@@ -782,10 +811,10 @@ int enqueue_batch(gsa_ctx* ctx, int mode, int npairs, const gsa_pair_dev* pairs,
         krowK = gsa::kKrowKDefault;
         krowNS = gsa::kKrowNSDefault;
     }
-    a.ns = lane ? lane_ns() : krow ? krowNS : gsa::kSparseNS;
+    a.ns = lane ? lane_ns(ctx) : krow ? krowNS : gsa::kSparseNS;
     // the K-rows fill's int8 column profile (its instance declines a table outside int8 and the int16
     // one runs instead) wherever its LDS fits; GSA_KROW_Q8=0 keeps the int16 profile
-    if (krow && env_int("GSA_KROW_Q8", 1) != 0)
+    if (krow && env_int(ctx, "GSA_KROW_Q8", 1) != 0)
         a.q8 = gsa::krow_lds_bytes(krowNS, krowNS == 2 ? 512 : 1024, substsz, true) <= (size_t)ctx->lds_max ? 1 : 0;
     a.q8flag = ctx->ctl + 2;
     const int fullRows = gsa::kLaneRows * a.ns;  // rows per ticket of a full fill
@@ -850,7 +879,7 @@ int enqueue_batch(gsa_ctx* ctx, int mode, int npairs, const gsa_pair_dev* pairs,
     // resident workgroups run the first tickets of every pair side by side instead of one pair's
     // chain of dependent tickets; ticket j of a pair stays behind its ticket j-1
     std::vector<int> sched;
-    const char* order = std::getenv("GSA_BATCH_ORDER");  // "pair": pair-major (comparisons)
+    const char* order = knob(ctx, "GSA_BATCH_ORDER");  // "pair": pair-major (comparisons)
     if (npairs > 1 && !(order && std::strcmp(order, "pair") == 0))
     {
         std::vector<int> ord((size_t)npairs);
@@ -931,14 +960,13 @@ int enqueue_batch(gsa_ctx* ctx, int mode, int npairs, const gsa_pair_dev* pairs,
             a.xpair = fused->xa->pairs;
             a.xsched = fused->xa->sched;
             a.xTasks = fused->xa->nTasks;
-            a.xknob = fused->xa->knob;
             a.xrun = fused->xa->run;
             a.xP = fused->p1;
             a.xrole = ctx->ctl + 4;
             a.xcounter = ctx->ctl + 5;
             if ((e = hipMemsetAsync(a.xrole, 0, 8, st)) != hipSuccess) return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
             ctx->stamps_n = 0;
-            if (env_int("GSA_STAMPS", 0))
+            if (env_int(ctx, "GSA_STAMPS", 0))
             {
                 const size_t n = 4 * words + 3 * (size_t)a.xTasks;
                 if (ctx->stamps_cap < n)
@@ -959,7 +987,7 @@ int enqueue_batch(gsa_ctx* ctx, int mode, int npairs, const gsa_pair_dev* pairs,
         }
         a.xdone = ctx->xdone;
     }
-    if (!fused && krow && !lane && env_int("GSA_STAMPS", 0))
+    if (!fused && krow && !lane && env_int(ctx, "GSA_STAMPS", 0))
     {
         // the K-rows fill's ledger (nw_krow_kernel): 10 words per strip
         const size_t n = 10 * (size_t)tickets * (size_t)krowNS;
@@ -983,6 +1011,8 @@ int enqueue_batch(gsa_ctx* ctx, int mode, int npairs, const gsa_pair_dev* pairs,
     if (e != hipSuccess) return fail(ctx, e, GSA_ERROR_MEMORY_TRANSFER);
     // one pair: one workgroup per CU (its tickets are a chain); a batch: all resident slots
     int grid = (npairs == 1) ? std::max(1, std::min((int)tickets, ctx->cu_count)) : 0;
+    a.laneFeed = knob(ctx, "GSA_LANE_FEED") ? env_int(ctx, "GSA_LANE_FEED", 0) : -1;
+    a.lanePair = knob(ctx, "GSA_LANE_PAIR") ? env_int(ctx, "GSA_LANE_PAIR", 0) : -1;
     e = lane     ? gsa::launch_lane_fill(a, a.ns, grid, st)
         : fused  ? gsa::launch_full_fused(a, fused->ns, fused->waves, 0, st)
         : rows64 ? gsa::launch_krow_fill_xr(a, krowNS, grid, st)
@@ -1038,13 +1068,13 @@ int enqueue_full_twopass(gsa_ctx* ctx, int npairs, const gsa_pair_dev* pairs, co
     const bool fitsChip = tileRows <= (long long)std::max(1, ctx->cu_count);
     // both passes in one launch (nw_full_fused_kernel) for single pairs; GSA_FULL_FUSED=0: two launches.
     // (A matrix without interior cells has no pass-1 tickets: the expansion alone writes its headers.)
-    const int fusedMode = env_int("GSA_FULL_FUSED", 1);
+    const int fusedMode = env_int(ctx, "GSA_FULL_FUSED", 1);
     bool interior = true;
     for (int p = 0; p < npairs; ++p) interior = interior && pairs[p].adjrows > 1 && pairs[p].adjcols > 1;
     // (never inside a split batch: a group of one pair would take the fused branch, which records
     // neither afterP1 nor timeP1, and group B would then start against an unrecorded event)
     const bool fused = interior && !opt.split && npairs == 1 && fusedMode >= 1;
-    const int ns = env_int("GSA_KROW_NS", (npairs > 1 && !fitsChip) ? 8 : 4) == 8 ? 8 : 4;  // as enqueue_batch
+    const int ns = env_int(ctx, "GSA_KROW_NS", (npairs > 1 && !fitsChip) ? 8 : 4) == 8 ? 8 : 4;  // as enqueue_batch
     // pass 2 (fused or its own launch): the streamed expansion, kExpStreamWaves - 1 tile waves per
     // workgroup, tasks of that many 64-row tiles
     const int xWaves = gsa::kExpStreamWaves - 1;
@@ -1135,7 +1165,7 @@ int enqueue_full_twopass(gsa_ctx* ctx, int npairs, const gsa_pair_dev* pairs, co
     // and 2 and time their pass 2 (HIP events; the second launch waits for the first's), and later
     // launches on that buffer take the faster.  GSA_EXPAND_RR fixes the order: 0 pair-major, 1, 2,
     // 3 shuffled, 4-6 probe variants.
-    const int rrEnv = opt.rr >= 0 ? opt.rr : env_int("GSA_EXPAND_RR", -1);
+    const int rrEnv = opt.rr >= 0 ? opt.rr : env_int(ctx, "GSA_EXPAND_RR", -1);
     int rr = rrEnv >= 0 ? rrEnv : 1;
     const bool tune = rrEnv < 0 && npairs > 1 && !fused;
     bool tuneRecord = false;
@@ -1197,7 +1227,7 @@ int enqueue_full_twopass(gsa_ctx* ctx, int npairs, const gsa_pair_dev* pairs, co
     // entries to whole runs.  Runs in order: a single pair by when their pass-1 rows arrive (the
     // fused fill; it helps two launches too), a batch round-robin over the pairs (rr 1; rr 2
     // rotated, 0 pair-major, 3 shuffled).
-    const int xRun = std::min(16, std::max(1, env_int("GSA_EXPAND_RUN", 4)));
+    constexpr int xRun = 4;  // (runs of 8 and 16 measured equal at 100k, r06)
     std::vector<int> xs;
     {
         struct Run { int p, g, jT; };
@@ -1213,7 +1243,7 @@ int enqueue_full_twopass(gsa_ctx* ctx, int npairs, const gsa_pair_dev* pairs, co
             // of the matrix, ready only ~4 ms later (profiles/r06_fused100k.txt).  lag = columns per
             // 256-row strip, GSA_FUSED_LAG (default 192: the 100k pair's strip-to-strip spacing).
             const gsa::ExpandPair& d = ex[0];
-            const long long lag = std::max(1, env_int("GSA_FUSED_LAG", 192));
+            constexpr long long lag = 192;
             const int cm = xWaves * xmt;
             std::vector<std::pair<long long, long long>> key;
             for (long long r = 0; r < runs_of(0); ++r)
@@ -1313,15 +1343,13 @@ int enqueue_full_twopass(gsa_ctx* ctx, int npairs, const gsa_pair_dev* pairs, co
     xa.nTasks = (int)nEntries;
     xa.run = xRun;
     xa.sched = (const int*)((char*)exdesc + descBytes);
-    xa.knob = env_int("GSA_EXPAND_KNOB", 0);
     xa.spin = ctx->spin_ticks;
     xa.err = ctx->ctl + 1;
     // (a group of a split batch has a claim counter of its own: the two groups' expansions overlap)
     xa.counter = ctx->ctl + 8 + opt.slot;
     // the fused single pair: every workgroup takes pass-1 tickets first
     const FusedLaunch fl {&xa, ns, gsa::kExpStreamWaves, 1 << 30};
-    int xGrid = (int)std::max<long long>(1, std::min<long long>(ctx->cu_count, (nEntries + xRun - 1) / xRun));
-    if (env_int("GSA_EXPAND_GRID", 0) > 0) xGrid = std::min(xGrid, env_int("GSA_EXPAND_GRID", 0));
+    const int xGrid = (int)std::max<long long>(1, std::min<long long>(ctx->cu_count, (nEntries + xRun - 1) / xRun));
     // gsa_set_full_timing: events before pass 1, between the passes and after pass 2, and the
     // expansion's clock stamps (one per workgroup)
     const bool timed = ctx->timing && !opt.split;
@@ -1375,9 +1403,9 @@ int enqueue_full_twopass(gsa_ctx* ctx, int npairs, const gsa_pair_dev* pairs, co
 
 // full fills: the two-pass fill (same box: 10k 100 -> 141 GCUPS, 64 x 20k batch 1084 -> 1093-1102
 // GCUPS, profiles/r04_twopass.txt); GSA_FULL_KERNEL=lane: the one-pass lane fill (nw_lane.hip)
-bool full_twopass(int)
+bool full_twopass(const gsa_ctx* ctx)
 {
-    const char* e = std::getenv("GSA_FULL_KERNEL");
+    const char* e = knob(ctx, "GSA_FULL_KERNEL");
     return !(e && std::strcmp(e, "lane") == 0);
 }
 
@@ -1394,9 +1422,7 @@ struct SplitPlan
 };
 bool split_plan(gsa_ctx* ctx, int npairs, const gsa_pair_dev* pairs, const int32_t* lds, SplitPlan& sp)
 {
-    if (npairs < 2 || env_int("GSA_FULL_FUSED", 1) >= 2 || env_int("GSA_EXPAND_GRID", 0) > 0 ||
-        env_int("GSA_FULL_PIPE", 0) >= 2)
-        return false;
+    if (npairs < 2 || env_int(ctx, "GSA_FULL_FUSED", 1) >= 2) return false;
     long long tileRows = 0;
     for (int p = 0; p < npairs; ++p)
     {
@@ -1404,7 +1430,7 @@ bool split_plan(gsa_ctx* ctx, int npairs, const gsa_pair_dev* pairs, const int32
         tileRows += std::max<long long>(1, ((long long)pairs[p].adjrows - 1 + gsa::kSparseTileBy - 1) / gsa::kSparseTileBy);
     }
     if (tileRows <= (long long)std::max(1, ctx->cu_count)) return false;  // 4-strip single round
-    const int ns = env_int("GSA_KROW_NS", 8) == 8 ? 8 : 4;
+    const int ns = env_int(ctx, "GSA_KROW_NS", 8) == 8 ? 8 : 4;
     std::vector<long long> t((size_t)npairs);
     long long T = 0;
     for (int p = 0; p < npairs; ++p)
@@ -1522,9 +1548,9 @@ uint64_t batch_key(int npairs, const gsa_pair_dev* pairs, const int32_t* lds)
 int enqueue_full(gsa_ctx* ctx, int npairs, const gsa_pair_dev* pairs, const int32_t* lds, const int32_t* subst,
                  int32_t substsz, int32_t gapo, hipStream_t st)
 {
-    if (full_twopass(npairs))
+    if (full_twopass(ctx))
     {
-        const int spEnv = env_int("GSA_FULL_SPLIT", -1), rrEnv = env_int("GSA_EXPAND_RR", -1);
+        const int spEnv = env_int(ctx, "GSA_FULL_SPLIT", -1), rrEnv = env_int(ctx, "GSA_EXPAND_RR", -1);
         SplitPlan sp;
         const bool can = spEnv != 0 && !(spEnv < 0 && rrEnv >= 0) && split_plan(ctx, npairs, pairs, lds, sp);
         if (can && spEnv > 0)
@@ -1587,9 +1613,6 @@ int enqueue_full(gsa_ctx* ctx, int npairs, const gsa_pair_dev* pairs, const int3
                 next = 0;
                 for (int k = 1; k < 4; ++k)
                     if (ft.ms[k] < ft.ms[next]) next = k;
-                if (ft.last >= 0 && env_int("GSA_TUNE_LOG", 0))  // (measurement aid: the four times, once)
-                    std::fprintf(stderr, "gsa full-batch tuning: one group %.3f / %.3f ms, two groups %.3f / %.3f ms -> %d\n",
-                                 ft.ms[0], ft.ms[1], ft.ms[2], ft.ms[3], next);
                 ft.last = -1;
             }
             const bool rec = !busy && !ft.cold && ft.ms[next] < 0.f;
@@ -1701,6 +1724,8 @@ int gsa_ctx_create(int device, gsa_ctx** out)
     gsa_ctx* ctx = new (std::nothrow) gsa_ctx();
     if (!ctx) return GSA_ERROR_MEMORY_ALLOCATION;
     ctx->device = device;
+    for (const char* k : kKnobNames)
+        if (const char* v = std::getenv(k)) ctx->knobs[k] = v;
     hipError_t e = hipSetDevice(device);
     if (e == hipSuccess) e = hipDeviceGetAttribute(&ctx->cu_count, hipDeviceAttributeMultiprocessorCount, device);
     if (e == hipSuccess)
@@ -1926,6 +1951,16 @@ int gsa_set_lap_callback(gsa_ctx* ctx, gsa_lap_fn fn, void* user)
     if (!ctx) return GSA_ERROR_INVALID_VALUE;
     ctx->lap_fn = fn;
     ctx->lap_user = fn ? user : nullptr;
+    return GSA_SUCCESS;
+}
+
+int gsa_set_knob(gsa_ctx* ctx, const char* name, const char* value)
+{
+    if (!ctx || !name || !knob_known(name)) return GSA_ERROR_INVALID_VALUE;
+    if (value)
+        ctx->knobs[name] = value;
+    else
+        ctx->knobs.erase(name);
     return GSA_SUCCESS;
 }
 
@@ -2378,14 +2413,14 @@ int gsa_trace_sparse_dev(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, con
     // (GSA_TRACE_BAND_BUDGET, bytes, lowers the cap), and if its buffers cannot be had the walk
     // runs alone and recomputes every tile it enters.
     {
-        const int band = env_int("GSA_TRACE_BAND", 1024);
+        const int band = env_int(ctx, "GSA_TRACE_BAND", 1024);
         const int trows = g.tileHdrMatRows, tcols = g.tileHdrMatCols;
         const size_t words = gsa::trace_dir_words(g.tileBy, g.tileBx);
         size_t budget = (size_t)512 << 20;
         {
             size_t freeB = 0, totalB = 0;
             if (hipMemGetInfo(&freeB, &totalB) == hipSuccess) budget = std::min(budget, freeB / 2);
-            const char* eb = std::getenv("GSA_TRACE_BAND_BUDGET");
+            const char* eb = knob(ctx, "GSA_TRACE_BAND_BUDGET");
             if (eb) budget = std::min(budget, (size_t)std::strtoull(eb, nullptr, 10));
         }
         const size_t maxSlots = budget / (words * 4);
@@ -2511,7 +2546,7 @@ int score_dev_impl(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, const int
     // values (i+j)*ge apart within int32 with margin; otherwise the row scan
     // (and scores below 2^26 by construction, so that no shifted key can wrap before the kernel flags it)
     const bool stripOk = (!local || (gapo < 0 && bits + 27 <= 63 && smax * std::min(R, C) < (1ll << 26))) && span < (1ll << 28);
-    if (!score_scan_forced() && stripOk)
+    if (!score_scan_forced(ctx) && stripOk)
     {
         s = score_ag_strip(ctx, seqY, R, seqX, C, subst, substsz, gapo, gape, local, out, st);
         if (s != kScoreTooLarge) return s;
@@ -2731,8 +2766,6 @@ int gsa_align_sparse_pt(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, cons
         }
     } joinAtExit {prefault};
     int copied = 0;  // chunks copied back
-    const bool ptdbg = std::getenv("GSA_PT_DEBUG") != nullptr;  // diagnostics: when chunks become ready
-    auto t0dbg = Clock::now();
     // Two pinned slots: the strided DMA of one batch of chunks (ptstream) runs while the copy
     // threads scatter the previous batch into the tile-major host matrices.
     const size_t chunkBytes = trows * (size_t)cw * (rowW + rowH);
@@ -2753,12 +2786,6 @@ int gsa_align_sparse_pt(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, cons
             if (n > 0) (void)hipStreamSynchronize(c->ptstream);
         }
     } drainAtExit {ctx, nInflight};
-    auto dbg = [&](const char* what, int c0, int c1) {
-        if (ptdbg)
-            std::fprintf(stderr, "mlsppt %.3f ms: %s %d..%d (fill %s)\n",
-                         std::chrono::duration<float, std::milli>(Clock::now() - t0dbg).count(), what, c0, c1,
-                         hipStreamQuery(ctx->stream) == hipSuccess ? "done" : "running");
-    };
     auto batch_geom = [&](const Batch& bt, size_t& j0, size_t& wr, size_t& wc, char*& hh, char*& hc) {
         j0 = (size_t)bt.c0 * cw;
         const size_t j1 = std::min((size_t)tcols, (size_t)bt.c1 * cw);
@@ -2786,7 +2813,6 @@ int gsa_align_sparse_pt(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, cons
         inflight[nInflight++] = bt;
         issued = bt.c1;
         nextSlot ^= 1;
-        dbg("dma issued", bt.c0, bt.c1);
         return hipSuccess;
     };
     // scatter the oldest batch once its DMA is done (wait: block until it is)
@@ -2814,7 +2840,6 @@ int gsa_align_sparse_pt(gsa_ctx* ctx, const int32_t* seqY, int32_t adjrows, cons
         copied = bt.c1;
         inflight[0] = inflight[1];
         --nInflight;
-        dbg("scattered", bt.c0, bt.c1);
         return hipSuccess;
     };
     // one pipeline step: issue a DMA for ready chunks if a slot is free, scatter a finished batch

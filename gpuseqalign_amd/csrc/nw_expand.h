@@ -68,7 +68,6 @@ struct ExpandArgs
     // column (a claim takes a run; an entry of pair -1 is padding); nTasks = its entries
     const int* sched;
     int run;
-    int knob;  // probes only (GSA_EXPAND_KNOB): 1 = no tile computed or stored (results wrong)
     unsigned* counter;  // the run claims (zeroed before the launch)
     // measurement (gsa_set_full_timing): per workgroup, wave 0's s_memtime cycles (low word) and
     // s_memrealtime ticks (100 MHz, high word) from its start to its end; null = off

@@ -714,7 +714,7 @@ __device__ __forceinline__ void ex_stream(const ExpandArgs& a, unsigned* counter
             if (cb == 0 && tid == 0) G(d.score)[0] = 0;
         }
         const int r0 = rc * kChunk + kExpRows * w + 1;
-        if (r0 <= d.R && cb < d.C && !(a.knob & 1))
+        if (r0 <= d.R && cb < d.C)
         {
             const uint32_t tb = slot + 4u * (uint32_t)(kSlotHdr + kSlotX + w * kTileDw);
             ex_tile_core(a, d, L.q, L.gfill, lane, cb, cols, r0, lds_ld(tb + 4u * (uint32_t)lane),

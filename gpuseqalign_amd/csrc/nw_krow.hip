@@ -2364,7 +2364,6 @@ __global__ void __launch_bounds__(64 * W) nw_full_fused_kernel(StripArgs a)
     xa.nPairs = a.nPairs;
     xa.nTasks = a.xTasks;
     xa.sched = a.xsched;
-    xa.knob = a.xknob;
     xa.run = a.xrun;
     xa.spin = a.spin;
     xa.err = a.err;

@@ -604,14 +604,12 @@ hipError_t launch_lane_fill(const StripArgs& a, int ns, int grid, hipStream_t st
     if (ns == 1) return launch_lane<1>(a, grid, stream);
     if (ns == 3) return launch_lane<3>(a, grid, stream);
     // a single pair: the feed in a wave of its own (a 7th wave would cost a batch its second
-    // workgroup per CU); GSA_LANE_FEED=0/1 overrides
-    const char* fe = getenv("GSA_LANE_FEED");
-    const bool fd = fe && *fe ? atoi(fe) != 0 : a.nPairs == 1;
+    // workgroup per CU); a.laneFeed (knob GSA_LANE_FEED) overrides
+    const bool fd = a.laneFeed >= 0 ? a.laneFeed != 0 : a.nPairs == 1;
     // paired output stores (lane_strip) for batches: 64 x 20k pitched 977-988 -> 1097 GCUPS; a single
     // pair's strips run on their critical path, where the held block costs (10k 100 -> 93 GCUPS,
-    // profiles/r04_full_pitch_pair.txt); GSA_LANE_PAIR=0/1 overrides
-    const char* pe = getenv("GSA_LANE_PAIR");
-    const bool pair = pe && *pe ? atoi(pe) != 0 : !fd;
+    // profiles/r04_full_pitch_pair.txt); a.lanePair (knob GSA_LANE_PAIR) overrides
+    const bool pair = a.lanePair >= 0 ? a.lanePair != 0 : !fd;
     if (ns == 4)
         return fd ? (pair ? launch_lane<4, true, true>(a, grid, stream) : launch_lane<4, true, false>(a, grid, stream))
                   : (pair ? launch_lane<4, false, true>(a, grid, stream) : launch_lane<4, false, false>(a, grid, stream));

@@ -112,7 +112,7 @@ struct StripArgs
     int xTasks;
     int xP;
     int xrun;  // expansion tasks per claim (a run of one tile column: gsa_capi.hip enqueue_full_twopass)
-    int xknob;
+    int laneFeed, lanePair;  // nw_lane.hip: the feeder wave / paired stores, 0 or 1 (< 0: its own choice)
     unsigned* xrole;
     unsigned* xcounter;
     unsigned long long* xdone;

@@ -84,6 +84,11 @@ int gsa_last_hip_error(const gsa_ctx* ctx);
 int gsa_device_cu_count(const gsa_ctx* ctx);
 const char* gsa_version(void);
 int gsa_set_lap_callback(gsa_ctx* ctx, gsa_lap_fn fn, void* user);
+/* Not part of the reference's interface: the measurement / test switches, named as environment
+ * variables (GSA_FULL_KERNEL, GSA_KROW_NS, ...; DESIGN.md lists them).  A context takes them from
+ * the environment once, in gsa_ctx_create; this sets one for this context (value NULL: unset, the
+ * built-in choice).  errorInvalidValue for a name the library does not know. */
+int gsa_set_knob(gsa_ctx* ctx, const char* name, const char* value);
 
 /* Tile height (tileBy) of the sparse representation this build produces: 1024, the rows of one
  * K-rows workgroup ticket (4 strip waves x 64 lanes x 4 rows per lane). */

@@ -28,3 +28,25 @@ def engine():
     e = gsa.Engine(0)
     yield e
     e.close()
+
+
+@pytest.fixture
+def knobs(engine, monkeypatch):
+    """Set library knobs for one test: on the session engine (gsa_set_knob -- a context reads the
+    environment only when it is created) and in the environment, for the engines the test creates
+    itself (shard.gpu_batch_align and the like).  Both are undone after the test."""
+    names = []
+
+    def set_knob(name, value):
+        if value is None:  # unset: the library's own choice
+            monkeypatch.delenv(name, raising=False)
+            engine.set_knob(name, None)
+            return
+        value = str(value)
+        monkeypatch.setenv(name, value)
+        engine.set_knob(name, value)
+        names.append(name)
+
+    yield set_knob
+    for n in names:
+        engine.set_knob(n, None)

@@ -93,14 +93,14 @@ def test_config4_512_pairs_match_golden(golden, tBx):
 
 @pytest.mark.timeout(600)
 @pytest.mark.parametrize("ns", ["batch-default", "4"])
-def test_config4_headers_at_size(engine, golden, monkeypatch, ns):
+def test_config4_headers_at_size(engine, golden, monkeypatch, ns, knobs):
     """configs[3] at full size, header by header: one persistent launch over all 512 pairs (the
     batch default is 8 strips per workgroup, two tile rows per ticket), then every pair's
     tile headers through the device checker, and 16 pairs' headers against the oracle."""
     import torch
     from gpuseqalign_amd import shard
     if ns != "batch-default":
-        monkeypatch.setenv("GSA_KROW_NS", ns)
+        knobs("GSA_KROW_NS", ns)
     gold = _load("config4_pairs.json")
     hd = gold["headers"]
     tBx = hd["tileBx"]

@@ -50,7 +50,7 @@ def test_lap_callback_order_and_totals(golden, what):
         assert len(names) == len(want)  # removed: no further calls
 
 
-def test_trace_band_budget_fallback(engine, golden, monkeypatch):
+def test_trace_band_budget_fallback(engine, golden, monkeypatch, knobs):
     """The band precompute is a speed-up only: with no memory budget for it (as when its buffers
     cannot be allocated) the device walk runs alone and still equals the host Trace2."""
     import torch
@@ -65,7 +65,7 @@ def test_trace_band_budget_fallback(engine, golden, monkeypatch):
     engine.sync()
     host = gsa.trace_sparse(gsa.SparseResult(hr.cpu().numpy(), hc.cpu().numpy(), geom, 0, {}), Y, X, sub, -11)
     for budget in ("0", "70000"):  # none, and one 1024 x 256 tile's codes (64 KB)
-        monkeypatch.setenv("GSA_TRACE_BAND_BUDGET", budget)
+        knobs("GSA_TRACE_BAND_BUDGET", budget)
         assert engine.trace_sparse_dev(*args, geom, hr.data_ptr(), hc.data_ptr()) == host
 
 

@@ -41,16 +41,16 @@ def test_overlap_equals_oracle(engine, golden, R, C, tBx):
 
 
 @pytest.mark.parametrize("kern,ns,k", [("krow", 2, 2), ("krow", 8, 4), ("strip", 4, 4)])
-def test_overlap_other_geometries(engine, golden, monkeypatch, kern, ns, k):
+def test_overlap_other_geometries(engine, golden, monkeypatch, kern, ns, k, knobs):
     """mlsppt publishes one word per tile row from the K-rows kernel: a geometry whose ticket is
     not one tile row (GSA_KROW_NS / GSA_KROW_K), or GSA_SPARSE_KERNEL=strip, falls back to the
     single-pair default geometry; every word equals the plain path's."""
     import oracle
     Y, X = random_pair(3100, 2200, 41)
     a = engine.align_sparse(Y, X, golden.blosum62, -11, tileBx=128)
-    monkeypatch.setenv("GSA_SPARSE_KERNEL", kern)
-    monkeypatch.setenv("GSA_KROW_NS", str(ns))
-    monkeypatch.setenv("GSA_KROW_K", str(k))
+    knobs("GSA_SPARSE_KERNEL", kern)
+    knobs("GSA_KROW_NS", str(ns))
+    knobs("GSA_KROW_K", str(k))
     b = engine.align_sparse(Y, X, golden.blosum62, -11, tileBx=128, overlap=True)
     assert np.array_equal(a.hrow, b.hrow) and np.array_equal(a.hcol, b.hcol)
     assert a.align_cost == b.align_cost == oracle.fill_full(Y, X, golden.blosum62, -11)[1]

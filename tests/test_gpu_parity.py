@@ -102,10 +102,10 @@ def test_other_substitution_and_gaps(engine, golden, name, gapo):
 
 @pytest.mark.parametrize("ns", [4, 8])
 @pytest.mark.parametrize("name,gapo", [("blosum45", -4), ("blosum50", 3), ("blosum90", -30)])
-def test_other_substitution_and_gaps_multi_ticket(engine, golden, monkeypatch, ns, name, gapo):
+def test_other_substitution_and_gaps_multi_ticket(engine, golden, monkeypatch, ns, name, gapo, knobs):
     """Same over several K-rows tickets (2.5 tile rows): the feed, drain and (ns = 8) mid header
     row carry values of other tables and gap costs, positive included."""
-    monkeypatch.setenv("GSA_KROW_NS", str(ns))
+    knobs("GSA_KROW_NS", str(ns))
     sub = golden.subst_data.matrix(name)
     Y, X = random_pair(2500, 2100, 41, alphabet=25)
     rs = engine.align_sparse(Y, X, sub, gapo, tileBx=128)
@@ -166,12 +166,12 @@ def test_mlsp_40k_related(engine, golden):
 @pytest.mark.parametrize("ns", ["1", "2", "3", "4", "6", "8"])
 @pytest.mark.parametrize("R,C", [(1, 1), (1, 700), (63, 64), (64, 65), (127, 300), (128, 128), (129, 1029),
                                  (300, 1), (385, 1500), (1100, 2222), (2049, 777)])
-def test_full_kernel_shapes(engine, golden, ns, R, C, monkeypatch):
+def test_full_kernel_shapes(engine, golden, ns, R, C, monkeypatch, knobs):
     """The full-fill kernel (nw_lane.hip, one row per lane) with 1..4, 6, 8 strips per workgroup
     (GSA_LANE_NS, read per launch): every super-strip boundary, ragged last strips, rows beyond
     R, every word."""
-    monkeypatch.setenv("GSA_FULL_KERNEL", "lane")
-    monkeypatch.setenv("GSA_LANE_NS", ns)
+    knobs("GSA_FULL_KERNEL", "lane")
+    knobs("GSA_LANE_NS", ns)
     Y, X = random_pair(R, C, 3 * R + C)
     r = engine.align_full(Y, X, golden.blosum62, -11)
     S, cost = oracle.fill_full(Y, X, golden.blosum62, -11)
@@ -179,11 +179,11 @@ def test_full_kernel_shapes(engine, golden, ns, R, C, monkeypatch):
 
 
 @pytest.mark.parametrize("ns", ["1", "2", "3", "4", "8"])
-def test_lane_kernel_wide_pair(engine, golden, ns, monkeypatch):
+def test_lane_kernel_wide_pair(engine, golden, ns, monkeypatch, knobs):
     """Columns past the profile ring (512 columns, 1024 from NS = 5) and its guard copies,
     several super-strips."""
-    monkeypatch.setenv("GSA_FULL_KERNEL", "lane")
-    monkeypatch.setenv("GSA_LANE_NS", ns)
+    knobs("GSA_FULL_KERNEL", "lane")
+    knobs("GSA_LANE_NS", ns)
     Y, X = related_pair(5000, 17)
     r = engine.align_full(Y, X, golden.blosum62, -11)
     S, cost = oracle.fill_full(Y, X, golden.blosum62, -11)
@@ -257,16 +257,16 @@ def test_full_pitch_contract(engine):
 
 @pytest.mark.parametrize("pair", ["0", "1"])
 @pytest.mark.parametrize("ns", ["2", "4", "8"])
-def test_full_batch_pitched(engine, golden, ns, pair, monkeypatch):
+def test_full_batch_pitched(engine, golden, ns, pair, monkeypatch, knobs):
     """The one-pass lane fill's batch path (GSA_FULL_KERNEL=lane; batches default to the two-pass
     fill, covered by test_twopass_tables_and_batches) into pitched matrices
     (gsa_fill_full_batch_pitched_dev) and unpadded ones (shard.gpu_batch_align), with and without
     paired stores (GSA_LANE_PAIR; NS != 4 always pairs): every cell of every pair against the oracle."""
     import torch
     from gpuseqalign_amd import shard
-    monkeypatch.setenv("GSA_FULL_KERNEL", "lane")
-    monkeypatch.setenv("GSA_LANE_NS", ns)
-    monkeypatch.setenv("GSA_LANE_PAIR", pair)
+    knobs("GSA_FULL_KERNEL", "lane")
+    knobs("GSA_LANE_NS", ns)
+    knobs("GSA_LANE_PAIR", pair)
     pairs = [random_pair(r, c, 11 * r + c) for r, c in ((700, 900), (1, 5), (1500, 333), (257, 2049), (64, 64))]
     dev = torch.device("cuda:0")
     s = torch.from_numpy(golden.blosum62).to(dev)
@@ -287,13 +287,13 @@ def test_full_batch_pitched(engine, golden, ns, pair, monkeypatch):
 @pytest.mark.parametrize("kernel", ["lane", "twopass", "fused"])
 @pytest.mark.parametrize("R,C", [(1, 1), (1, 300), (300, 1), (63, 64), (64, 64), (65, 257), (255, 256), (256, 512),
                                  (511, 513), (513, 1024), (1023, 700), (1025, 1029), (2049, 300), (3100, 2222)])
-def test_full_fill_kernels(engine, golden, kernel, R, C, monkeypatch):
+def test_full_fill_kernels(engine, golden, kernel, R, C, monkeypatch, knobs):
     """The full-fill kernels (GSA_FULL_KERNEL, GSA_FULL_FUSED): the one-pass lane fill, the two-pass
     fill in two launches (K-rows pass 1 keeping every 64th row and the 256-column tile header columns,
     then every 64 x 512 tile recomputed by nw_expand.hip) and in one (the fused single-pair kernel):
     every word, around the 64-row, 256-column and 1024-row tile edges."""
-    monkeypatch.setenv("GSA_FULL_KERNEL", "lane" if kernel == "lane" else "twopass")
-    monkeypatch.setenv("GSA_FULL_FUSED", "1" if kernel == "fused" else "0")
+    knobs("GSA_FULL_KERNEL", "lane" if kernel == "lane" else "twopass")
+    knobs("GSA_FULL_FUSED", "1" if kernel == "fused" else "0")
     Y, X = random_pair(R, C, 13 * R + C)
     r = engine.align_full(Y, X, golden.blosum62, -11)
     S, cost = oracle.fill_full(Y, X, golden.blosum62, -11)
@@ -302,16 +302,16 @@ def test_full_fill_kernels(engine, golden, kernel, R, C, monkeypatch):
 
 @pytest.mark.parametrize("ns", ["4", "8"])
 @pytest.mark.parametrize("name,gapo", [("blosum45", -5), ("blosum80", -30), ("blosum62", 3), ("blosum50", -70)])
-def test_twopass_tables_and_batches(engine, golden, ns, name, gapo, monkeypatch):
+def test_twopass_tables_and_batches(engine, golden, ns, name, gapo, monkeypatch, knobs):
     """The two-pass fill of a batch in both pass-1 geometries (4 strips: 1024-row tickets, 8 strips:
     2048-row tickets, GSA_KROW_NS) and the streamed expansion (a loader wave staging each task's
     inputs for 7 tile waves), other tables and gap costs (a positive gap included; at gap -70
     s - 2g leaves int8 and pass 1 runs its int16 instance), pitched layout, every word of every pair
     against the oracle, and the words around each matrix untouched."""
     import torch
-    monkeypatch.setenv("GSA_FULL_KERNEL", "twopass")
-    monkeypatch.setenv("GSA_KROW_NS", ns)
-    monkeypatch.setenv("GSA_FULL_FUSED", "0")
+    knobs("GSA_FULL_KERNEL", "twopass")
+    knobs("GSA_KROW_NS", ns)
+    knobs("GSA_FULL_FUSED", "0")
     sub = golden.subst_data.matrix(name)
     pairs = [random_pair(r, c, 7 * r + c, alphabet=25) for r, c in ((2100, 900), (1, 5), (700, 2500), (64, 64), (4097, 300))]
     dev = torch.device("cuda:0")
@@ -331,14 +331,14 @@ def test_twopass_tables_and_batches(engine, golden, ns, name, gapo, monkeypatch)
 
 
 @pytest.mark.parametrize("name,gapo", [("blosum45", -5), ("blosum62", 3), ("blosum50", -70)])
-def test_fused_tables_pitched_repeated(engine, golden, name, gapo, monkeypatch):
+def test_fused_tables_pitched_repeated(engine, golden, name, gapo, monkeypatch, knobs):
     """The fused single-pair fill (pass-1 tickets and expansion tasks in one launch, hand-off through
     per-strip progress words): other tables and gaps (-70: the int16 instance behind the declining
     int8 one), pitched and unpadded, launched back to back on one stream (a task that ran ahead of
     its strips' words would read the previous launch's rows): every word every time."""
     import torch
-    monkeypatch.setenv("GSA_FULL_KERNEL", "twopass")
-    monkeypatch.setenv("GSA_FULL_FUSED", "1")
+    knobs("GSA_FULL_KERNEL", "twopass")
+    knobs("GSA_FULL_FUSED", "1")
     sub = golden.subst_data.matrix(name)
     dev = torch.device("cuda:0")
     s = torch.from_numpy(np.ascontiguousarray(sub, dtype=np.int32)).to(dev)
@@ -364,18 +364,18 @@ def test_fused_tables_pitched_repeated(engine, golden, name, gapo, monkeypatch):
                 assert (out[:off] == -7).all() and (out[off + n:] == -7).all()
 
 
-def test_split_batch_single_pair_group(engine, golden, monkeypatch):
+def test_split_batch_single_pair_group(engine, golden, monkeypatch, knobs):
     """a split batch (GSA_FULL_SPLIT=1) whose group A is one pair, with the fused
     single-pair fill left at its default: the groups' passes stay ordered by their events (a fused
     group A recorded none, and group B's pass 1 and expansion then raced it).  Group A: one pair of
     exactly one round of (8, 4) tickets (cu_count x 2048 rows, 100 columns); group B: two pairs of
     20 tickets.  Every word of every pair against the oracle, on two launches."""
     import torch
-    monkeypatch.setenv("GSA_FULL_KERNEL", "twopass")
-    monkeypatch.delenv("GSA_FULL_FUSED", raising=False)
-    monkeypatch.delenv("GSA_KROW_NS", raising=False)
-    monkeypatch.delenv("GSA_EXPAND_RR", raising=False)
-    monkeypatch.setenv("GSA_FULL_SPLIT", "1")
+    knobs("GSA_FULL_KERNEL", "twopass")
+    knobs("GSA_FULL_FUSED", None)
+    knobs("GSA_KROW_NS", None)
+    knobs("GSA_EXPAND_RR", None)
+    knobs("GSA_FULL_SPLIT", "1")
     cu = int(engine.cu_count)
     shapes = [(cu * 2048, 100), (40960, 300), (40960, 257)]
     pairs = [random_pair(r, c, 3 * r + c) for r, c in shapes]
@@ -395,19 +395,19 @@ def test_split_batch_single_pair_group(engine, golden, monkeypatch):
 
 
 @pytest.mark.parametrize("order", ["tuned", "0", "1", "2", "3"])
-def test_expansion_orders_repeated(engine, golden, order, monkeypatch):
+def test_expansion_orders_repeated(engine, golden, order, monkeypatch, knobs):
     """A batch's expansion task orders (gsa_capi.hip enqueue_full_twopass): by default the first two
     launches on an output buffer run orders 1 and 2 (timed) and later ones the faster; fixed orders
     under GSA_EXPAND_RR (0 pair-major, 1 round-robin, 2 rotated round-robin, 3 shuffled).  Four
     launches back to back on the same buffers (the matrices cleared in between), every word against
     the oracle each time; then a new buffer set restarts the tuning."""
     import torch
-    monkeypatch.setenv("GSA_FULL_KERNEL", "twopass")
-    monkeypatch.setenv("GSA_FULL_FUSED", "0")
+    knobs("GSA_FULL_KERNEL", "twopass")
+    knobs("GSA_FULL_FUSED", "0")
     if order == "tuned":
-        monkeypatch.delenv("GSA_EXPAND_RR", raising=False)
+        knobs("GSA_EXPAND_RR", None)
     else:
-        monkeypatch.setenv("GSA_EXPAND_RR", order)
+        knobs("GSA_EXPAND_RR", order)
     sub = golden.blosum62
     pairs = [random_pair(r, c, 3 * r + c + 1) for r, c in ((1500, 900), (300, 2500), (2100, 700), (65, 64), (900, 1300))]
     ref = [oracle.fill_full(Y, X, sub, -11)[0] for Y, X in pairs]
@@ -429,7 +429,7 @@ def test_expansion_orders_repeated(engine, golden, order, monkeypatch):
 
 
 @pytest.mark.parametrize("split", ["tuned", "0", "1"])
-def test_full_batch_split(engine, golden, split, monkeypatch):
+def test_full_batch_split(engine, golden, split, monkeypatch, knobs):
     """A full batch whose pass-1 tickets fill one round and part of another, split in two groups
     (GSA_FULL_SPLIT=1: the first round's pairs on the caller's stream, the rest on a high-priority
     stream behind their pass 1, each group with its own pass-1 scratch and expansion order), against
@@ -437,14 +437,14 @@ def test_full_batch_split(engine, golden, split, monkeypatch):
     one group on the next two launches and two on the two after (gsa_capi.hip enqueue_full), then
     the fastest: every word of every pair equals the oracle on every launch."""
     import torch
-    monkeypatch.setenv("GSA_FULL_KERNEL", "twopass")
-    monkeypatch.setenv("GSA_FULL_FUSED", "0")
+    knobs("GSA_FULL_KERNEL", "twopass")
+    knobs("GSA_FULL_FUSED", "0")
     if split == "tuned":
-        monkeypatch.delenv("GSA_FULL_SPLIT", raising=False)
+        knobs("GSA_FULL_SPLIT", None)
     else:
-        monkeypatch.setenv("GSA_FULL_SPLIT", split)
-    monkeypatch.delenv("GSA_KROW_NS", raising=False)
-    monkeypatch.delenv("GSA_EXPAND_RR", raising=False)
+        knobs("GSA_FULL_SPLIT", split)
+    knobs("GSA_KROW_NS", None)
+    knobs("GSA_EXPAND_RR", None)
     sub = golden.blosum62
     cu = int(engine.cu_count)
     n = cu + cu // 3  # (8, 4) tickets: 3 per pair of 4100-5100 rows -> 1 round and a part

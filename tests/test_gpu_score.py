@@ -68,11 +68,11 @@ def test_config5_50k(engine, golden, go, ge, local):
 
 @pytest.mark.parametrize("R,C", [(1, 300), (700, 130), (2049, 1500)])
 @pytest.mark.parametrize("go,ge,local", MODES)
-def test_row_scan_path(engine, golden, R, C, go, ge, local, monkeypatch):
+def test_row_scan_path(engine, golden, R, C, go, ge, local, monkeypatch, knobs):
     """Scores normally run on the strip kernel (affine / local modes); GSA_SCORE_SCAN=1 keeps the
     row-scan kernel reachable: both equal the oracle."""
     import oracle
-    monkeypatch.setenv("GSA_SCORE_SCAN", "1")
+    knobs("GSA_SCORE_SCAN", "1")
     Y, X = random_pair(R, C, 5 * R + C)
     r = engine.score(Y, X, golden.blosum62, go, ge, local)
     assert (r["score"], r["i_end"], r["j_end"]) == oracle.score_ag(Y, X, golden.blosum62, go, ge, local)
@@ -133,11 +133,11 @@ def test_local_fallbacks_to_row_scan(engine, golden):
 
 @pytest.mark.parametrize("R,C", [(300, 1), (65, 63), (700, 130), (1500, 1000)])
 @pytest.mark.parametrize("go,ge,local", MODES)
-def test_strip_kernel_path(engine, golden, R, C, go, ge, local, monkeypatch):
+def test_strip_kernel_path(engine, golden, R, C, go, ge, local, monkeypatch, knobs):
     """GSA_SCORE_KERNEL=strip: the strip kernel's score modes (nw_strip.hip), kept reachable beside
     the K-rows score kernel (nw_kscore.hip) that runs by default."""
     import oracle
-    monkeypatch.setenv("GSA_SCORE_KERNEL", "strip")
+    knobs("GSA_SCORE_KERNEL", "strip")
     Y, X = random_pair(R, C, 7 * R + C)
     r = engine.score(Y, X, golden.blosum62, go, ge, local)
     assert (r["score"], r["i_end"], r["j_end"]) == oracle.score_ag(Y, X, golden.blosum62, go, ge, local)
@@ -146,12 +146,12 @@ def test_strip_kernel_path(engine, golden, R, C, go, ge, local, monkeypatch):
 @pytest.mark.parametrize("k", ["2", "4"])
 @pytest.mark.parametrize("R", [2048, 2049, 2050, 2051, 2052, 3071])
 @pytest.mark.parametrize("go,ge,local", MODES)
-def test_result_row_positions(engine, golden, monkeypatch, k, R, go, ge, local):
+def test_result_row_positions(engine, golden, monkeypatch, k, R, go, ge, local, knobs):
     """The K-rows score kernel reads the NW result cell (R, C) from the lane and row that hold it
     (row kR = (R - r0) mod K of lane (R - r0) / K of a later ticket's strip): every kR, a strip's
     first and last rows, at K = 2 and 4 rows per lane (GSA_SCORE_K)."""
     import oracle
-    monkeypatch.setenv("GSA_SCORE_K", k)
+    knobs("GSA_SCORE_K", k)
     Y, X = random_pair(R, 257, R + 11)
     r = engine.score(Y, X, golden.blosum62, go, ge, local)
     assert (r["score"], r["i_end"], r["j_end"]) == oracle.score_ag(Y, X, golden.blosum62, go, ge, local)
@@ -173,7 +173,7 @@ def test_alphabet_sizes(engine, golden, substsz, go, ge, local):
 @pytest.mark.parametrize("k", ["2", "4"])
 @pytest.mark.parametrize("q8", ["0", "1", "2"])
 @pytest.mark.parametrize("go,ge,local", MODES + [(-120, -120, False), (-120, -120, True), (-70, -60, False)])
-def test_profile_widths_and_stale_columns(engine, golden, monkeypatch, q8, k, go, ge, local):
+def test_profile_widths_and_stale_columns(engine, golden, monkeypatch, q8, k, go, ge, local, knobs):
     """The K-rows score kernel's int16 and int8 column profiles (GSA_KROW_Q8 = 0 / 2; 1 = int8 for
     linear modes only), the int8 instance's decline for s - go - ge outside int8 (gap -120, -70/-60:
     the int16 instance runs), and columns right of C: a long pair first leaves real letters in the
@@ -182,8 +182,8 @@ def test_profile_widths_and_stale_columns(engine, golden, monkeypatch, q8, k, go
     once gave SW-AG 64 x 65 the score 197).  Both strip heights: 2 and 4 rows per lane (GSA_SCORE_K;
     by default 4 for NW-LG, 2 otherwise), so the result cell falls at every row of a lane."""
     import oracle
-    monkeypatch.setenv("GSA_KROW_Q8", q8)
-    monkeypatch.setenv("GSA_SCORE_K", k)
+    knobs("GSA_KROW_Q8", q8)
+    knobs("GSA_SCORE_K", k)
     for R, C in [(3, 3000), (64, 65), (200, 3000), (65, 100), (1, 200), (64, 65)]:
         Y, X = random_pair(R, C, 11 * R + C)
         r = engine.score(Y, X, golden.blosum62, go, ge, local)
@@ -193,15 +193,15 @@ def test_profile_widths_and_stale_columns(engine, golden, monkeypatch, q8, k, go
 @pytest.mark.parametrize("k", ["2", "4"])
 @pytest.mark.parametrize("q8", ["0", "1"])
 @pytest.mark.parametrize("go,ge,local", MODES)
-def test_score_both_ends(engine, golden, monkeypatch, k, q8, go, ge, local):
+def test_score_both_ends(engine, golden, monkeypatch, k, q8, go, ge, local, knobs):
     """NW from both ends (gsa_capi.hip score_bidi, nw_bidi.hip), forced at every size
     (GSA_SCORE_BIDI=2; by default pairs whose halves keep >= 4 tickets): the top half's tap row m,
     the reversed bottom half's row R - m and the combine.  Odd R (R % K != 0) and local modes keep the
     one-direction kernel; both equal the oracle."""
     import oracle
-    monkeypatch.setenv("GSA_SCORE_BIDI", "2")
-    monkeypatch.setenv("GSA_SCORE_K", k)
-    monkeypatch.setenv("GSA_KROW_Q8", q8)
+    knobs("GSA_SCORE_BIDI", "2")
+    knobs("GSA_SCORE_K", k)
+    knobs("GSA_KROW_Q8", q8)
     for R, C in [(2, 1), (4, 5), (8, 300), (130, 1), (130, 700), (512, 64), (514, 1000), (1024, 1024), (1027, 900),
                  (2052, 257), (4100, 3000)]:
         Y, X = random_pair(R, C, 13 * R + C)
@@ -212,13 +212,13 @@ def test_score_both_ends(engine, golden, monkeypatch, k, q8, go, ge, local):
 @pytest.mark.parametrize("k", ["2", "4"])
 @pytest.mark.parametrize("go,ge", [(-11, -11), (-11, -1), (-5, -2), (-3, -1)])
 @pytest.mark.parametrize("ins", [1, 7, 40, 300])
-def test_score_both_ends_gap_across_split(engine, golden, monkeypatch, k, go, ge, ins):
+def test_score_both_ends_gap_across_split(engine, golden, monkeypatch, k, go, ge, ins, knobs):
     """A vertical gap that crosses the split row m = K floor(R / 2K): Y is X with ins letters
     inserted around the middle, so the best path's gap spans rows m and m + 1 and pays its open once
     (the combine's F + F^r - (go - ge) term); also a horizontal gap at the split (X longer)."""
     import oracle
-    monkeypatch.setenv("GSA_SCORE_BIDI", "2")
-    monkeypatch.setenv("GSA_SCORE_K", k)
+    knobs("GSA_SCORE_BIDI", "2")
+    knobs("GSA_SCORE_K", k)
     rng = np.random.default_rng(ins * 31 + int(k))
     base = rng.integers(0, 20, 1200).astype(np.int32)
     extra = rng.integers(0, 20, ins).astype(np.int32)
@@ -232,16 +232,16 @@ def test_score_both_ends_gap_across_split(engine, golden, monkeypatch, k, go, ge
             assert (r["score"], r["i_end"], r["j_end"]) == oracle.score_ag(A, B, golden.blosum62, go, ge, False), cut
 
 
-def test_score_both_ends_default_matches_one_direction(engine, golden, monkeypatch):
+def test_score_both_ends_default_matches_one_direction(engine, golden, monkeypatch, knobs):
     """The default switch (GSA_SCORE_BIDI=1: halves of >= 4 tickets) on a 20k related pair, NW-LG
     and NW-AG, against the one-direction kernel (GSA_SCORE_BIDI=0) and the oracle's tiled restatement."""
     import oracle
     Y, X = related_pair(20000, 20100)
     Y = Y[:len(Y) - (len(Y) - 1) % 4]  # R % K == 0: the split's rows are lanes' last rows
     for go, ge in [(-11, -11), (-11, -1)]:
-        monkeypatch.setenv("GSA_SCORE_BIDI", "1")
+        knobs("GSA_SCORE_BIDI", "1")
         r1 = engine.score(Y, X, golden.blosum62, go, ge, False)
-        monkeypatch.setenv("GSA_SCORE_BIDI", "0")
+        knobs("GSA_SCORE_BIDI", "0")
         r0 = engine.score(Y, X, golden.blosum62, go, ge, False)
         ref = oracle.score_ag(Y, X, golden.blosum62, go, ge, False, mt=True, blocksz=256, nthreads=8)
         assert (r1["score"], r1["i_end"], r1["j_end"]) == (r0["score"], r0["i_end"], r0["j_end"]) == ref
@@ -249,13 +249,13 @@ def test_score_both_ends_default_matches_one_direction(engine, golden, monkeypat
 
 @pytest.mark.parametrize("k", ["2", "4"])
 @pytest.mark.parametrize("go,ge", [(-11, -11), (-11, -1), (-4, -3)])
-def test_score_both_ends_transposed(engine, golden, monkeypatch, k, go, ge):
+def test_score_both_ends_transposed(engine, golden, monkeypatch, k, go, ge, knobs):
     """R not a multiple of K but C one: the pair runs transposed from both ends (X down the rows, the
     table transposed), on an asymmetric table so a missed transpose shows; R and C both off the
     multiple keep one direction.  All equal the oracle, end cell (R, C)."""
     import oracle
-    monkeypatch.setenv("GSA_SCORE_BIDI", "2")
-    monkeypatch.setenv("GSA_SCORE_K", k)
+    knobs("GSA_SCORE_BIDI", "2")
+    knobs("GSA_SCORE_K", k)
     n = int(round(np.sqrt(golden.blosum62.size)))
     rng = np.random.default_rng(int(k) * 7 + go)
     sub = rng.integers(-7, 9, size=(n, n)).astype(np.int32)
@@ -268,11 +268,11 @@ def test_score_both_ends_transposed(engine, golden, monkeypatch, k, go, ge):
         assert (r["score"], r["i_end"], r["j_end"]) == oracle.score_ag(Y, X, sub, go, ge, False), (R, C)
 
 
-def test_score_both_ends_random_shapes(engine, golden, monkeypatch):
+def test_score_both_ends_random_shapes(engine, golden, monkeypatch, knobs):
     """40 random NW shapes (R, C in 1..3000, either parity), random gap pairs and tables, forced from
     both ends where the shape allows (GSA_SCORE_BIDI=2): equal to the oracle."""
     import oracle
-    monkeypatch.setenv("GSA_SCORE_BIDI", "2")
+    knobs("GSA_SCORE_BIDI", "2")
     n = int(round(np.sqrt(golden.blosum62.size)))
     rng = np.random.default_rng(2024)
     for case in range(40):
@@ -302,18 +302,18 @@ def test_score_both_ends_100k(engine, golden):
 
 @pytest.mark.parametrize("gran", ["0", "1"])
 @pytest.mark.parametrize("skew", ["-1", "0", "700"])
-def test_score_both_ends_granule_tap(engine, golden, monkeypatch, gran, skew):
+def test_score_both_ends_granule_tap(engine, golden, monkeypatch, gran, skew, knobs):
     """The halves' meeting rows read from the last ticket's granules when a half ends on a ticket
     boundary (GSA_BIDI_GRAN=1, the default past 4 tickets: the top half always, the bottom when R
     is a multiple of the ticket too), or from lane taps on both sides (GSA_BIDI_GRAN=0); the top
     half's extra rows (GSA_BIDI_SKEW; -1 = the cost model) move the split.  Both NW modes, both
     rows-per-lane settings, R a multiple of the ticket (both halves free) and not; the oracle."""
     import oracle
-    monkeypatch.setenv("GSA_SCORE_BIDI", "2")
-    monkeypatch.setenv("GSA_BIDI_GRAN", gran)
-    monkeypatch.setenv("GSA_BIDI_SKEW", skew)
+    knobs("GSA_SCORE_BIDI", "2")
+    knobs("GSA_BIDI_GRAN", gran)
+    knobs("GSA_BIDI_SKEW", skew)
     for k in ("2", "4"):
-        monkeypatch.setenv("GSA_SCORE_K", k)
+        knobs("GSA_SCORE_K", k)
         for R, C in [(4096, 1500), (5120, 900), (4100, 2600), (6002, 700), (8192, 333)]:
             Y, X = random_pair(R, C, 29 * R + C)
             for go, ge in [(-11, -1), (-11, -11), (-4, -2)]:
@@ -322,7 +322,7 @@ def test_score_both_ends_granule_tap(engine, golden, monkeypatch, gran, skew):
                     (k, R, C, go, ge)
 
 
-def test_score_both_ends_large_random_shapes(engine, golden, monkeypatch):
+def test_score_both_ends_large_random_shapes(engine, golden, monkeypatch, knobs):
     """Ten random shapes of 4k-30k rows and columns (both parities, both split forms: granule tap or
     lane taps, transposed when only C suits), random affine / linear gaps: the default path against
     the one-direction kernel (GSA_SCORE_BIDI=0) on the same inputs."""
@@ -332,9 +332,9 @@ def test_score_both_ends_large_random_shapes(engine, golden, monkeypatch):
         ge = -int(rng.integers(1, 4))
         go = ge - int(rng.integers(0, 12))
         Y, X = random_pair(R, C, 5000 + case)
-        monkeypatch.setenv("GSA_SCORE_BIDI", "1")
+        knobs("GSA_SCORE_BIDI", "1")
         r1 = engine.score(Y, X, golden.blosum62, go, ge, False)
-        monkeypatch.setenv("GSA_SCORE_BIDI", "0")
+        knobs("GSA_SCORE_BIDI", "0")
         r0 = engine.score(Y, X, golden.blosum62, go, ge, False)
         assert (r1["score"], r1["i_end"], r1["j_end"]) == (r0["score"], r0["i_end"], r0["j_end"]), (case, R, C, go, ge)
 
@@ -354,16 +354,16 @@ def _planted(R, C, seed, plants):
 
 @pytest.mark.parametrize("k", ["2", "4"])
 @pytest.mark.parametrize("go,ge", [(-11, -11), (-11, -1), (-5, -2)])
-def test_score_local_both_ends(engine, golden, monkeypatch, capfd, k, go, ge):
+def test_score_local_both_ends(engine, golden, monkeypatch, capfd, k, go, ge, knobs):
     """SW from both ends (score_bidi, local: top forward, bottom reversed, bottom forward from a
     fresh border): best alignments planted wholly in the top half, wholly in the bottom, across the
     split row m (back to one direction), tied in both halves and twice in the bottom (first in
     row-major), and plain random pairs; every result equals the oracle, and the log names the way
     each pair went."""
     import oracle
-    monkeypatch.setenv("GSA_SCORE_BIDI", "2")
-    monkeypatch.setenv("GSA_SCORE_K", k)
-    monkeypatch.setenv("GSA_BIDI_LOG", "1")
+    knobs("GSA_SCORE_BIDI", "2")
+    knobs("GSA_SCORE_K", k)
+    knobs("GSA_BIDI_LOG", "1")
     kk = int(k)
     R, C = 1600 * kk // 2, 1300
     m = kk * (R // (2 * kk))
@@ -388,7 +388,7 @@ def test_score_local_both_ends(engine, golden, monkeypatch, capfd, k, go, ge):
         assert (r["score"], r["i_end"], r["j_end"]) == oracle.score_ag(Y, X, golden.blosum62, go, ge, True), (R2, C2)
 
 
-def test_score_local_both_ends_default_matches_one_direction(engine, golden, monkeypatch):
+def test_score_local_both_ends_default_matches_one_direction(engine, golden, monkeypatch, knobs):
     """The default switch on SW (halves of >= 4 tickets, R even): random 6k-20k shapes and a related
     20k pair (its alignment crosses the split: one direction), against GSA_SCORE_BIDI_SW=0."""
     rng = np.random.default_rng(91)
@@ -397,16 +397,16 @@ def test_score_local_both_ends_default_matches_one_direction(engine, golden, mon
     pairs.append((Yr[:len(Yr) - (len(Yr) - 1) % 2], Xr))
     for Y, X in pairs:
         for go, ge in [(-11, -11), (-11, -1)]:
-            monkeypatch.delenv("GSA_SCORE_BIDI_SW", raising=False)
+            knobs("GSA_SCORE_BIDI_SW", None)
             r1 = engine.score(Y, X, golden.blosum62, go, ge, True)
-            monkeypatch.setenv("GSA_SCORE_BIDI_SW", "0")
+            knobs("GSA_SCORE_BIDI_SW", "0")
             r0 = engine.score(Y, X, golden.blosum62, go, ge, True)
             assert (r1["score"], r1["i_end"], r1["j_end"]) == (r0["score"], r0["i_end"], r0["j_end"]), (len(Y), len(X))
 
 
 @pytest.mark.parametrize("k", ["2", "4"])
 @pytest.mark.parametrize("go,ge", [(-11, -11), (-11, -1)])
-def test_score_local_both_ends_continuation(engine, golden, monkeypatch, capfd, k, go, ge):
+def test_score_local_both_ends_continuation(engine, golden, monkeypatch, capfd, k, go, ge, knobs):
     """SW from both ends whose best alignment crosses the split, on a pair long enough for the top half
     to end on a ticket boundary: the way back continues the pair from that ticket in a second launch
     (its row above the top's last-ticket granules, restamped) instead of the whole one-direction run;
@@ -414,14 +414,14 @@ def test_score_local_both_ends_continuation(engine, golden, monkeypatch, capfd, 
     equal to the oracle, and the log shows the way taken (GSA_BIDI_SW_CONT=0: the whole run again,
     same result)."""
     import oracle
-    monkeypatch.setenv("GSA_SCORE_K", k)
-    monkeypatch.setenv("GSA_BIDI_LOG", "1")
+    knobs("GSA_SCORE_K", k)
+    knobs("GSA_BIDI_LOG", "1")
     kk = int(k)
     R, C = 3000 * kk, 1500
     for i, (dr, way) in enumerate([(-40, "bottom again"), (-5, "bottom again"), (-75, "bottom again"),
                                    (900, "answer")]):
         capfd.readouterr()
-        monkeypatch.delenv("GSA_BIDI_SW_CONT", raising=False)
+        engine.set_knob("GSA_BIDI_SW_CONT", None)
         Y, X = _planted(R, C, 60 + i, [(0, 0, 0)])
         r = engine.score(Y, X, golden.blosum62, go, ge, True)
         assert (r["score"], r["i_end"], r["j_end"]) == oracle.score_ag(Y, X, golden.blosum62, go, ge, True), i
@@ -432,7 +432,7 @@ def test_score_local_both_ends_continuation(engine, golden, monkeypatch, capfd, 
         err = capfd.readouterr().err
         assert (r["score"], r["i_end"], r["j_end"]) == ref, (i, m, err)
         assert f"-> {way}" in err, (i, m, err)
-        monkeypatch.setenv("GSA_BIDI_SW_CONT", "0")
+        knobs("GSA_BIDI_SW_CONT", "0")
         r0 = engine.score(Y, X, golden.blosum62, go, ge, True)
         assert (r0["score"], r0["i_end"], r0["j_end"]) == ref, (i, m)
         assert ("-> one direction" if way != "answer" else "-> answer") in capfd.readouterr().err, (i, m)

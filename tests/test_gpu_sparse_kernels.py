@@ -62,14 +62,14 @@ def test_sparse_profile_range_is_checked(engine, golden):
 
 @pytest.mark.parametrize("R,C", [(63, 2000), (1500, 1300), (3000, 2100)])
 @pytest.mark.parametrize("gapo,q8", [(-11, "0"), (-80, "1"), (-59, "1"), (-58, "1"), (-11, "1")])
-def test_krow_profile_width(engine, golden, R, C, gapo, q8, monkeypatch):
+def test_krow_profile_width(engine, golden, R, C, gapo, q8, monkeypatch, knobs):
     """The K-rows fill keeps s - 2g in an int8 column profile when the table allows it and falls
     back to the int16 instance otherwise (blosum62 has -4 <= s <= 11: gapo -58 fits, s + 116 <= 127;
     -59 and -80 do not, and their int8 launches decline; a fitting fill after a declined one checks
     that the per-launch word is not stale); GSA_KROW_Q8=0 forces int16.  Headers word for word
     against the oracle."""
     import oracle
-    monkeypatch.delenv("GSA_SPARSE_KERNEL", raising=False)
+    knobs("GSA_SPARSE_KERNEL", None)
     monkeypatch.setenv("GSA_KROW_Q8", q8)
     Y, X = random_pair(R, C, R + 3 * C)
     res = engine.align_sparse(Y, X, golden.blosum62, gapo, tileBx=256)

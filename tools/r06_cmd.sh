@@ -1,7 +1,5 @@
 set -e
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-L=gpurun_out/r06_s22.log
-: > $L
-timeout -k 10 120 python -u tools/r06_stamps100k.py _s22 >> $L 2>&1
-grep "^{" $L
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/r06_gpu_all.log 2>&1 || { tail -40 gpurun_out/r06_gpu_all.log; exit 1; }
+tail -3 gpurun_out/r06_gpu_all.log
