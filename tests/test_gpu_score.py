@@ -196,8 +196,9 @@ def test_profile_widths_and_stale_columns(engine, golden, monkeypatch, q8, k, go
 def test_score_both_ends(engine, golden, monkeypatch, k, q8, go, ge, local, knobs):
     """NW from both ends (gsa_capi.hip score_bidi, nw_bidi.hip), forced at every size
     (GSA_SCORE_BIDI=2; by default pairs whose halves keep >= 4 tickets): the top half's tap row m,
-    the reversed bottom half's row R - m and the combine.  Odd R (R % K != 0) and local modes keep the
-    one-direction kernel; both equal the oracle."""
+    the reversed bottom half's row R - m and the combine.  Local modes with R % K == 0 take the
+    three-pair SW from both ends (GSA_SCORE_BIDI_SW defaults to on); R % K != 0 keeps the
+    one-direction kernel in every mode.  All equal the oracle."""
     import oracle
     knobs("GSA_SCORE_BIDI", "2")
     knobs("GSA_SCORE_K", k)
