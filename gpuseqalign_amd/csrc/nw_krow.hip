@@ -383,24 +383,7 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
                    "v"(int4v {lt[12], lt[13], lt[14], lt[15]})                                           \
                  : "memory")
             if constexpr (PT == 3)
-            {
-                // the fused fill: into the storer wave's LDS slot (kr_xstore), same lanes
-                const uint32_t sa = xsData + 64u * (uint32_t)(4 * (bb % kXD));
-                asm volatile("s_mov_b64 %0, exec\n"
-                             "s_mov_b64 exec, %1\n"
-                             "ds_write_b128 %2, %3\n"
-                             "ds_write_b128 %2, %4 offset:16\n"
-                             "ds_write_b128 %2, %5 offset:32\n"
-                             "ds_write_b128 %2, %6 offset:48\n"
-                             "s_mov_b64 exec, %0"
-                             : "=&s"(sv)
-                             : "s"(K == 4 ? 0x8000800080008000ull : 0x8000000080000000ull), "v"(sa),
-                               "v"(int4v {lt[0], lt[1], lt[2], lt[3]}), "v"(int4v {lt[4], lt[5], lt[6], lt[7]}),
-                               "v"(int4v {lt[8], lt[9], lt[10], lt[11]}), "v"(int4v {lt[12], lt[13], lt[14], lt[15]})
-                             : "memory");
-                flag_st(xsWords + 4u * (uint32_t)w, bb + 1);
-                (void)addr;
-            }
+                (void)addr;  // the fused fill: staged at the next block's start (halo_stage)
             else
                 GSA_XR_STORES("");
 #undef GSA_XR_STORES
@@ -408,6 +391,43 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
         // {prog[w+1], cons[w]}: block bb's 16 elements handed off; ring_in elements < 16bb+80
         // (block bb's halo, read at its start) no longer needed
         flag_st2(f_out, bb + 1 == NB ? kBig : kBlk * bb + kBlk, kBlk * bb + 64 + kBlk);
+    };
+    // the fused fill (PT 3): block b's halo read together with block b-1's row-64m segments into the
+    // storer wave's LDS slot (kr_xstore) and the staged count; only the halo reads are awaited.  The
+    // staging writes at the hand-off, in the LDS queue ahead of the next block's halo read, held every
+    // block's start behind them: 100k x 100k pass 1 without the expansion 109 -> 98 cycles per step
+    // without them (profiles/r06_fused100k.txt)
+    auto halo_stage = [&](int b) {
+        if constexpr (PT == 3)
+        {
+            const uint32_t hb = ring_in + 4u * (uint32_t)((kBlk * b + 64) & (kRing - 1));
+            const uint32_t sa = xsData + 64u * (uint32_t)(4 * ((b - 1) % kXD));
+            uint64_t sv;
+            asm volatile(
+                "s_mov_b64 %4, exec\n"
+                "s_mov_b64 exec, 1\n"
+                "ds_read_b128 %0, %5\n"
+                "ds_read_b128 %1, %5 offset:16\n"
+                "ds_read_b128 %2, %5 offset:32\n"
+                "ds_read_b128 %3, %5 offset:48\n"
+                "s_mov_b64 exec, %6\n"
+                "ds_write_b128 %7, %8\n"
+                "ds_write_b128 %7, %9 offset:16\n"
+                "ds_write_b128 %7, %10 offset:32\n"
+                "ds_write_b128 %7, %11 offset:48\n"
+                "s_mov_b64 exec, 1\n"
+                "ds_write_b32 %12, %13\n"
+                "s_mov_b64 exec, %4\n"
+                "s_waitcnt lgkmcnt(5)"
+                : "+v"(hc[0]), "+v"(hc[1]), "+v"(hc[2]), "+v"(hc[3]), "=&s"(sv)
+                : "v"(hb), "s"(K == 4 ? 0x8000800080008000ull : 0x8000000080000000ull), "v"(sa),
+                  "v"(int4v {lt[0], lt[1], lt[2], lt[3]}), "v"(int4v {lt[4], lt[5], lt[6], lt[7]}),
+                  "v"(int4v {lt[8], lt[9], lt[10], lt[11]}), "v"(int4v {lt[12], lt[13], lt[14], lt[15]}),
+                  "v"(xsWords + 4u * (uint32_t)w), "v"(b)
+                : "memory");
+        }
+        else
+            halo_load(b);
     };
     int rpin = 0, rpco = 0, rpxo = 0;  // progress words read in mid-block, checked at the next block
     int rsink = 0;                     // the read's 4th dword (unused)
@@ -443,7 +463,10 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
             asm volatile("" ::"v"(rpin), "v"(rpco), "v"(rpxo), "v"(rsink));
             if (!ok(pin, pco, pxo, b) && !spin(b)) return false;
         }
-        halo_load(b);
+        if (PT == 3 && b > 0)
+            halo_stage(b);
+        else
+            halo_load(b);
 #if GSA_KR_BLOCK_LEDGER
         const uint64_t lt1 = GSA_LDG_T();
 #endif
@@ -618,6 +641,23 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
     }
     if (fx)
     {
+        // block NB-1's segments (halo_stage stages each block at the next one's start)
+        {
+            const uint32_t sa = xsData + 64u * (uint32_t)(4 * ((NB - 1) % kXD));
+            uint64_t sv;
+            asm volatile("s_mov_b64 %0, exec\n"
+                         "s_mov_b64 exec, %1\n"
+                         "ds_write_b128 %2, %3\n"
+                         "ds_write_b128 %2, %4 offset:16\n"
+                         "ds_write_b128 %2, %5 offset:32\n"
+                         "ds_write_b128 %2, %6 offset:48\n"
+                         "s_mov_b64 exec, %0"
+                         : "=&s"(sv)
+                         : "s"(K == 4 ? 0x8000800080008000ull : 0x8000000080000000ull), "v"(sa),
+                           "v"(int4v {lt[0], lt[1], lt[2], lt[3]}), "v"(int4v {lt[4], lt[5], lt[6], lt[7]}),
+                           "v"(int4v {lt[8], lt[9], lt[10], lt[11]}), "v"(int4v {lt[12], lt[13], lt[14], lt[15]})
+                         : "memory");
+        }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         flag_st(xsWords + 4u * (uint32_t)w, NB);  // (every block staged)
         flag_st(xsWords + 4u * (uint32_t)(2 * NS + w), (int)kXDone);
@@ -2368,7 +2408,9 @@ __global__ void __launch_bounds__(64 * W) nw_full_fused_kernel(StripArgs a)
     xa.spin = a.spin;
     xa.err = a.err;
     const xdev::ExFused fx {a.xdone, a.epoch, a.stamps ? a.stamps + 4 * (size_t)a.nTicketsTotal * NS : nullptr};
+#ifndef GSA_FUSED_NO_EXPAND  // (diagnostic builds: pass 1 alone inside the fused kernel, results wrong)
     xdev::ex_stream<W, true>(xa, a.xcounter, fx, w, lane);
+#endif
 }
 
 template <int NS, int W, bool Q8>
