@@ -1227,7 +1227,13 @@ int enqueue_full_twopass(gsa_ctx* ctx, int npairs, const gsa_pair_dev* pairs, co
     // entries to whole runs.  Runs in order: a single pair by when their pass-1 rows arrive (the
     // fused fill; it helps two launches too), a batch round-robin over the pairs (rr 1; rr 2
     // rotated, 0 pair-major, 3 shuffled).
-    constexpr int xRun = 4;  // (runs of 8 and 16 measured equal at 100k, r06)
+    // runs of 4 (8 and 16 measured equal at 100k, r06), shorter when the runs would not cover the
+    // CUs twice: a 10k pair's 483 tasks were 121 runs of 4, one per workgroup, four tasks in a row
+    // on half the CUs, and its last run alone set the fill's tail (48 us after the last strip)
+    long long allTasks = 0;
+    for (int p = 0; p < npairs; ++p) allTasks += (long long)ex[(size_t)p].rowChunks * ex[(size_t)p].colTiles;
+    const long long cus = std::max(1, ctx->cu_count);
+    const int xRun = allTasks >= 8 * cus ? 4 : allTasks >= 4 * cus ? 2 : 1;
     std::vector<int> xs;
     {
         struct Run { int p, g, jT; };

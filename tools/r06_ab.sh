@@ -1,5 +1,5 @@
 # A/B of variant libraries on one box: fused 100k full fill (pitched), alternating, 3 rounds
-# usage: LIBS="name1 name2" bash tools/r06_ab.sh   ("" = the default libgsa.so)
+# usage: LIBS="name1 name2" [PAIR=10k REPS=20] bash tools/r06_ab.sh   (default = libgsa.so)
 set -e
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -8,7 +8,7 @@ L=gpurun_out/r06_ab.log
 for round in 1 2 3; do
   for lib in default $LIBS; do
     so=""; [ "$lib" != default ] && so=gpuseqalign_amd/libgsa_$lib.so
-    GSA_LIB=$so timeout -k 10 120 python -u tools/r06_full100k.py --pitched --reps 4 --tag "$lib" >> $L 2>&1
+    GSA_LIB=$so timeout -k 10 120 python -u tools/r06_full100k.py --pitched --reps ${REPS:-4} --pair ${PAIR:-100k} --tag "$lib" >> $L 2>&1
   done
 done
 grep "^{" $L | python3 -c "

@@ -22,12 +22,13 @@ def main():
     ap.add_argument("--trace", action="store_true")
     ap.add_argument("--timing", action="store_true")
     ap.add_argument("--tag", default="")
+    ap.add_argument("--pair", default="100k", choices=["100k", "10k"], help="10k: BASELINE configs[1]")
     a = ap.parse_args()
     import numpy as np
     import torch
     import bench
     import gpuseqalign_amd as gsa
-    Y, X = bench.config3_pair()
+    Y, X = bench.config2_pair() if a.pair == "10k" else bench.config3_pair()
     sub = bench.subst_blosum62()
     R, C = len(Y) - 1, len(X) - 1
     dev = torch.device("cuda", 0)
@@ -70,7 +71,7 @@ def main():
     corner = buf[off + R * ld + C: off + R * ld + C + 1].cpu().numpy()
     out["align_cost"] = int(corner[0])
     g = bench.load_golden("config3_100k.json")
-    out["golden_cost"] = g["pairs"]["related"]["align_cost"]
+    out["golden_cost"] = -4922 if a.pair == "10k" else g["pairs"]["related"]["align_cost"]
     if a.check and not a.pitched:
         t1 = time.time()
         r = eng.check_full_dev(tY.data_ptr(), R + 1, tX.data_ptr(), C + 1, tS.data_ptr(), 25, -11, base)
