@@ -246,6 +246,7 @@ int check_inputs(int32_t adjrows, int32_t adjcols, int32_t substsz)
 constexpr const char* kKnobNames[] = {
     "GSA_SPARSE_KERNEL", "GSA_KROW_K",      "GSA_KROW_NS",      "GSA_KROW_Q8",       "GSA_LANE_NS",
     "GSA_LANE_FEED",     "GSA_LANE_PAIR",   "GSA_FULL_KERNEL",  "GSA_FULL_FUSED",    "GSA_FULL_SPLIT",
+    "GSA_FUSED_STAGED",
     "GSA_EXPAND_RR",     "GSA_BATCH_ORDER", "GSA_SCORE_SCAN",   "GSA_SCORE_KERNEL",  "GSA_SCORE_K",
     "GSA_SCORE_BIDI",    "GSA_SCORE_BIDI_SW", "GSA_BIDI_GRAN",  "GSA_BIDI_SKEW",     "GSA_BIDI_SW_CONT",
     "GSA_BIDI_LOG",      "GSA_TRACE_BAND",  "GSA_TRACE_BAND_BUDGET", "GSA_STAMPS"};
@@ -772,6 +773,7 @@ struct FusedLaunch
 {
     const gsa::ExpandArgs* xa;
     int ns, waves, p1;
+    bool staged;  // nw_full_fused_kernel's row-64m hand-off through a storer wave (PTF 3), else direct
 };
 
 // One batched launch: headers of every pair, then the persistent strip kernel over the
@@ -1014,7 +1016,7 @@ int enqueue_batch(gsa_ctx* ctx, int mode, int npairs, const gsa_pair_dev* pairs,
     a.laneFeed = knob(ctx, "GSA_LANE_FEED") ? env_int(ctx, "GSA_LANE_FEED", 0) : -1;
     a.lanePair = knob(ctx, "GSA_LANE_PAIR") ? env_int(ctx, "GSA_LANE_PAIR", 0) : -1;
     e = lane     ? gsa::launch_lane_fill(a, a.ns, grid, st)
-        : fused  ? gsa::launch_full_fused(a, fused->ns, fused->waves, 0, st)
+        : fused  ? gsa::launch_full_fused(a, fused->ns, fused->waves, fused->staged, 0, st)
         : rows64 ? gsa::launch_krow_fill_xr(a, krowNS, grid, st)
         : krow   ? gsa::launch_krow_fill(a, krowNS, krowK, 0, grid, st)
                  : gsa::launch_strip_fill(a, mode, grid, st);
@@ -1353,8 +1355,14 @@ int enqueue_full_twopass(gsa_ctx* ctx, int npairs, const gsa_pair_dev* pairs, co
     xa.err = ctx->ctl + 1;
     // (a group of a split batch has a claim counter of its own: the two groups' expansions overlap)
     xa.counter = ctx->ctl + 8 + opt.slot;
-    // the fused single pair: every workgroup takes pass-1 tickets first
-    const FusedLaunch fl {&xa, ns, gsa::kExpStreamWaves, 1 << 30};
+    // the fused single pair: every workgroup takes pass-1 tickets first.  A large pair's expansion
+    // fills HBM, and its strips hand row 64m to a storer wave (their own write-through stores stalled
+    // them); a small one's keeps HBM idle enough for the strips to store it directly, without the
+    // staging's ~5 % per step (nw_krow.hip nw_full_fused_kernel): 10k direct, 100k staged
+    const int stagedKnob = env_int(ctx, "GSA_FUSED_STAGED", -1);  // (tests: both instances at every size)
+    const bool staged = stagedKnob >= 0 ? stagedKnob != 0
+                                        : (long long)(pairs[0].adjrows - 1) * (long long)(pairs[0].adjcols - 1) > (1ll << 30);
+    const FusedLaunch fl {&xa, ns, gsa::kExpStreamWaves, 1 << 30, staged};
     const int xGrid = (int)std::max<long long>(1, std::min<long long>(ctx->cu_count, (nEntries + xRun - 1) / xRun));
     // gsa_set_full_timing: events before pass 1, between the passes and after pass 2, and the
     // expansion's clock stamps (one per workgroup)

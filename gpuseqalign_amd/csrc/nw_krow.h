@@ -39,7 +39,8 @@ hipError_t launch_krow_fill_xr(const StripArgs& a, int ns, int grid, hipStream_t
 // tasks of `waves` x 64 rows (a.xpair, a.xsched, a.xTasks), each task waiting for the progress
 // words a.xdone of the strips whose rows and header column it reads.  (ns, waves): (4, 8) or
 // (8, 12).  grid <= 0: every resident slot.
-hipError_t launch_full_fused(const StripArgs& a, int ns, int waves, int grid, hipStream_t stream);
+// staged: the strips hand row 64m to a storer wave (large pairs); else they store it themselves
+hipError_t launch_full_fused(const StripArgs& a, int ns, int waves, bool staged, int grid, hipStream_t stream);
 
 // Score-only NW / SW (modes kModeScoreAG/AGL/SW/SWL of nw_strip.h, same StripArgs contract as
 // launch_strip_fill for one pair: go, ge, gran + gran2, agResult, swBest, idxBits) on the K-rows

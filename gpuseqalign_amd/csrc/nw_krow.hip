@@ -230,7 +230,7 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
     // the error word is a global load, which waits for this wave's outstanding header stores
     // (vmcnt retires in order): polled once per 32 LDS polls
     // ledger (GSA_STAMPS=1, plain fills): shader-clock cycles spent waiting here, and the waits
-    constexpr bool kLedger = PT != 3;
+    constexpr bool kLedger = PT < 3;
     uint64_t spinCyc = 0;
     unsigned spinN = 0;
 #if GSA_KR_BLOCK_LEDGER
@@ -384,6 +384,8 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
                  : "memory")
             if constexpr (PT == 3)
                 (void)addr;  // the fused fill: staged at the next block's start (halo_stage)
+            else if constexpr (PT == 4)
+                GSA_XR_STORES(" sc1");  // the fused fill, direct: write-through, read by other workgroups
             else
                 GSA_XR_STORES("");
 #undef GSA_XR_STORES
@@ -441,7 +443,7 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
     constexpr bool pt = PT == 1;
     // fused: the strip's row-64m segments go to the storer wave through LDS (kr_xstore), and every 16
     // blocks its header-column progress: boundaries < the word stored and acknowledged (kXDone: all)
-    constexpr bool fx = PT == 3;
+    constexpr bool fx = PT >= 3;
     int ptPend = 0;
 
     // One body for blocks with and without a header-column capture (cap, uniform): separate
@@ -522,7 +524,20 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
         const uint64_t lt2 = GSA_LDG_T();
 #endif
         handoff(b);
-        if constexpr (fx && !RAMP)
+        if constexpr (PT == 4 && !RAMP)
+            if ((b & 15) == 15)
+            {
+                // direct: every block issues >= 4 stores (its row-buffer segments), so all but the last
+                // 16 vector-memory operations complete covers blocks <= b - 4: row 64m columns
+                // < 16 (b - 7) (block bb stores columns <= 16 (bb - 4) + 15 of its 4 rows) and the
+                // header columns captured by block b - 4 (boundaries <= 16 (b - 7))
+                asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+                if (lane == 0)
+                    __hip_atomic_store(a.xdone + (size_t)tk * NS + w,
+                                       ((unsigned long long)a.epoch << 32) | (unsigned)max(0, kBlk * (b - 7)),
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        if constexpr (PT == 3 && !RAMP)
             if ((b & 15) == 15)
             {
                 // the strip's only global stores are its header columns, 4K per boundary (4 capture
@@ -639,7 +654,14 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         flag_st(L.flags + kFCap + 4u * (uint32_t)w, kBig);
     }
-    if (fx)
+    if (PT == 4)
+    {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0)
+            __hip_atomic_store(a.xdone + (size_t)tk * NS + w, ((unsigned long long)a.epoch << 32) | kXDone,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (PT == 3)
     {
         // block NB-1's segments (halo_stage stages each block at the next one's start)
         {
@@ -2262,23 +2284,25 @@ namespace {
 
 // ------------------------------------------------------------------------------------
 // The fused single-pair full fill: both passes of the two-pass fill in one launch.  A single pair's
-// pass 1 is a chain of ceil(R / 1024) tickets -- ten workgroups for the 10k pair, on ten CUs -- and
+// pass 1 is a chain of ceil(R / 1024) tickets -- ten workgroups for the 10k pair, 98 for 100k -- and
 // its pass 2 needs a 64-row tile's rows only once the strips above and beside it have passed its
-// columns.  So workgroups of 8 waves take the pass-1 tickets first (waves 0..6 run the (4, 4)
-// K-rows roles, wave 7 idles) and then the expansion tasks, in row-chunk-major order (512-row
-// chunks x kExpTW columns, nw_expand_dev.h), from the same counter: every task's producers hold
-// earlier claims, so they are resident and the waits end.  Hand-off, per the guide's
-// inter-workgroup rules: the strips store row 64m and the header columns write-through (sc1), wait
-// for those stores (vmcnt) and publish a word per strip -- epoch << 32 | n, n = boundaries captured
-// -- with a relaxed agent-scope store; a task's lane 0 polls the words of the strips it reads, then
-// an agent acquire, vmcnt(0) and a workgroup barrier precede the plain loads.
+// columns.  So the first a.xP workgroups of 8 waves take the pass-1 tickets (waves 0..6 the (4, 4)
+// K-rows roles, wave 7 the storer in the staged instance) and then expansion tasks; the others take
+// expansion tasks only, in the host's ready-time order (nw_expand_dev.h ex_stream): every task's
+// producers hold earlier claims, so they are resident and the waits end.  Hand-off, per the guide's
+// inter-workgroup rules: row 64m and the header columns are stored write-through (sc1), their
+// stores awaited (vmcnt), and a word per strip -- epoch << 32 | X -- published with a relaxed
+// agent-scope store; a task's loader polls the words of the strips it reads, then an agent acquire
+// precedes its loads.
+//   PTF 3 (staged): the strips hand their row-64m segments to the storer wave through LDS
+//     (kr_xstore), which stores them and publishes the words.  Under the expansion's store stream a
+//     strip's own write-through stores filled its 63 vector-memory slots and stalled it (100k x 100k:
+//     pass 1 6.2 -> 8.4 ms).
+//   PTF 4 (direct): the strips store the segments and publish every 16 blocks themselves, as round 5
+//     did: for small pairs, whose expansion never fills HBM, it saves the staging (10k x 10k: 110 ->
+//     105 cycles per step; gsa_capi.hip enqueue_full_twopass picks).
 // ------------------------------------------------------------------------------------
-// NS: pass-1 strips per ticket ((4, 4): 1024-row tickets; (8, 4): 2048 rows, two tile rows); W: waves
-// per workgroup, also the expansion's tile waves (a task = W x 64 rows of one tile column).  The
-// first a.xP workgroups to arrive take pass-1 tickets until none is left, then expansion tasks; the
-// others take expansion tasks only.  A task waits only for tickets, every ticket only for lower
-// ones, and tickets are taken only by workgroups that are running: every wait ends.
-template <int NS, int W, bool Q8>
+template <int NS, int W, bool Q8, int PTF>
 __global__ void __launch_bounds__(64 * W) nw_full_fused_kernel(StripArgs a)
 {
     constexpr int K = 4, LW = 1024;
@@ -2365,9 +2389,9 @@ __global__ void __launch_bounds__(64 * W) nw_full_fused_kernel(StripArgs a)
         unsigned long long* const sst = a.stamps ? a.stamps + 4 * ((size_t)d.ticketBase + tk) * NS : nullptr;
         if (threadIdx.x < 32) lds_st(L.flags + 4u * threadIdx.x, 0);
         if (threadIdx.x >= kFCap / 4 && threadIdx.x < kFCap / 4 + 8) lds_st(L.flags + 4u * threadIdx.x, 0);
-        if (threadIdx.x >= 64 && threadIdx.x < 64 + 3 * NS) lds_st(kr_xwords(L.flags) + 4u * (threadIdx.x - 64), 0);
+        if (PTF == 3 && threadIdx.x >= 64 && threadIdx.x < 64 + 3 * NS) lds_st(kr_xwords(L.flags) + 4u * (threadIdx.x - 64), 0);
         __syncthreads();
-        if (w == NS + 3)
+        if (PTF == 3 && w == NS + 3)
             kr_xstore<NS, K>(pa, L, tk, lane);
         else if (w == NS + 1)
             kr_drain<NS, K, LW, 3>(pa, L, tk, lane);
@@ -2383,7 +2407,7 @@ __global__ void __launch_bounds__(64 * W) nw_full_fused_kernel(StripArgs a)
                 sst[4 * w + 2] = __builtin_amdgcn_s_memtime();
             }
             __builtin_amdgcn_s_setprio(3);
-            kr_strip<NS, K, LW, 3, Q8>(pa, L, tk, w, lane);
+            kr_strip<NS, K, LW, PTF, Q8>(pa, L, tk, w, lane);
             __builtin_amdgcn_s_setprio(0);
             if (sst && lane == 0)
             {
@@ -2413,13 +2437,14 @@ __global__ void __launch_bounds__(64 * W) nw_full_fused_kernel(StripArgs a)
 #endif
 }
 
-template <int NS, int W, bool Q8>
+template <int NS, int W, bool Q8, int PTF>
 hipError_t launch_fused1(const StripArgs& a, int grid, hipStream_t stream, bool foot)
 {
     static_assert(W == kExpStreamWaves, "the streamed expansion's workgroup");
     static_assert(kr_waves<NS>() < W, "a storer wave beside the pass-1 roles");
-    const size_t lds = std::max(krow_lds_bytes(NS, 1024, a.substsz, Q8) + kr_xstage_bytes(NS), expand_stream_lds_bytes(a.substsz));
-    auto kern = nw_full_fused_kernel<NS, W, Q8>;
+    const size_t lds = std::max(krow_lds_bytes(NS, 1024, a.substsz, Q8) + (PTF == 3 ? kr_xstage_bytes(NS) : 0u),
+                                expand_stream_lds_bytes(a.substsz));
+    auto kern = nw_full_fused_kernel<NS, W, Q8, PTF>;
     constexpr int kThreads = 64 * W;
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
@@ -2437,23 +2462,23 @@ hipError_t launch_fused1(const StripArgs& a, int grid, hipStream_t stream, bool 
     return hipGetLastError();
 }
 
-template <int NS, int W>
+template <int NS, int W, int PTF>
 hipError_t launch_fused(const StripArgs& a, int grid, hipStream_t stream)
 {
-    if (!a.q8) return launch_fused1<NS, W, false>(a, grid, stream, true);
-    hipError_t e = launch_fused1<NS, W, true>(a, grid, stream, true);
+    if (!a.q8) return launch_fused1<NS, W, false, PTF>(a, grid, stream, true);
+    hipError_t e = launch_fused1<NS, W, true, PTF>(a, grid, stream, true);
     if (e != hipSuccess) return e;
     StripArgs b = a;
     b.q8 = 2;
-    return launch_fused1<NS, W, false>(b, grid, stream, false);
+    return launch_fused1<NS, W, false, PTF>(b, grid, stream, false);
 }
 
 }  // namespace
 
-hipError_t launch_full_fused(const StripArgs& a, int ns, int waves, int grid, hipStream_t stream)
+hipError_t launch_full_fused(const StripArgs& a, int ns, int waves, bool staged, int grid, hipStream_t stream)
 {
     if (!a.xpair || !a.xdone || !a.xrole || !a.xcounter) return hipErrorInvalidValue;
-    if (ns == 4 && waves == 8) return launch_fused<4, 8>(a, grid, stream);
+    if (ns == 4 && waves == 8) return staged ? launch_fused<4, 8, 3>(a, grid, stream) : launch_fused<4, 8, 4>(a, grid, stream);
     return hipErrorInvalidValue;
 }
 #elif defined(GSA_KROW_BATCH8)

@@ -284,16 +284,19 @@ def test_full_batch_pitched(engine, golden, ns, pair, monkeypatch, knobs):
     assert costs == [int(oracle.fill_full(Y, X, golden.blosum62, -11)[1]) for Y, X in pairs]
 
 
-@pytest.mark.parametrize("kernel", ["lane", "twopass", "fused"])
+@pytest.mark.parametrize("kernel", ["lane", "twopass", "fused", "fused_staged"])
 @pytest.mark.parametrize("R,C", [(1, 1), (1, 300), (300, 1), (63, 64), (64, 64), (65, 257), (255, 256), (256, 512),
                                  (511, 513), (513, 1024), (1023, 700), (1025, 1029), (2049, 300), (3100, 2222)])
 def test_full_fill_kernels(engine, golden, kernel, R, C, monkeypatch, knobs):
     """The full-fill kernels (GSA_FULL_KERNEL, GSA_FULL_FUSED): the one-pass lane fill, the two-pass
     fill in two launches (K-rows pass 1 keeping every 64th row and the 256-column tile header columns,
-    then every 64 x 512 tile recomputed by nw_expand.hip) and in one (the fused single-pair kernel):
-    every word, around the 64-row, 256-column and 1024-row tile edges."""
+    then every 64 x 512 tile recomputed by nw_expand.hip) and in one (the fused single-pair kernel;
+    its strips store row 64m themselves at these sizes, or hand it to the storer wave as large pairs
+    do, GSA_FUSED_STAGED=1): every word, around the 64-row, 256-column and 1024-row tile edges."""
     knobs("GSA_FULL_KERNEL", "lane" if kernel == "lane" else "twopass")
-    knobs("GSA_FULL_FUSED", "1" if kernel == "fused" else "0")
+    knobs("GSA_FULL_FUSED", "0" if kernel in ("lane", "twopass") else "1")
+    if kernel == "fused_staged":
+        knobs("GSA_FUSED_STAGED", "1")
     Y, X = random_pair(R, C, 13 * R + C)
     r = engine.align_full(Y, X, golden.blosum62, -11)
     S, cost = oracle.fill_full(Y, X, golden.blosum62, -11)
@@ -330,8 +333,9 @@ def test_twopass_tables_and_batches(engine, golden, ns, name, gapo, monkeypatch,
         assert (out[:31] == -7).all() and (out[31 + len(Y) * ld:] == -7).all()
 
 
+@pytest.mark.parametrize("staged", ["0", "1"])
 @pytest.mark.parametrize("name,gapo", [("blosum45", -5), ("blosum62", 3), ("blosum50", -70)])
-def test_fused_tables_pitched_repeated(engine, golden, name, gapo, monkeypatch, knobs):
+def test_fused_tables_pitched_repeated(engine, golden, name, gapo, staged, monkeypatch, knobs):
     """The fused single-pair fill (pass-1 tickets and expansion tasks in one launch, hand-off through
     per-strip progress words): other tables and gaps (-70: the int16 instance behind the declining
     int8 one), pitched and unpadded, launched back to back on one stream (a task that ran ahead of
@@ -339,6 +343,7 @@ def test_fused_tables_pitched_repeated(engine, golden, name, gapo, monkeypatch, 
     import torch
     knobs("GSA_FULL_KERNEL", "twopass")
     knobs("GSA_FULL_FUSED", "1")
+    knobs("GSA_FUSED_STAGED", staged)
     sub = golden.subst_data.matrix(name)
     dev = torch.device("cuda:0")
     s = torch.from_numpy(np.ascontiguousarray(sub, dtype=np.int32)).to(dev)
