@@ -85,6 +85,20 @@ __global__ void kern(int* out, long long ld, int R, int C, int TW, int W, const 
                 // L >> 3; 4 row bits at lane bits {0, 4, 5}, chunk {1, 2, 3}; 5 row {2, 3, 5}, chunk
                 // {0, 1, 4}; 6 row {2, 3, 4}, chunk {0, 1, 5}
                 int row, ch;
+                if (SHAPE == 7)
+                {
+                    // 16 rows x 64 B per instruction, each quad 64 contiguous bytes of one row; the
+                    // line's other half in the next instruction
+#pragma unroll
+                    for (int k = 0; k < 8; ++k)
+                    {
+                        const long long rr = r0 + 16 * (k >> 1) + (lane >> 2);
+                        const long long c = cb + 16 * (b + (k & 1)) + 4 * (lane & 3);
+                        *(int4a*)(out + rr * ld + c) = v;
+                        v += 1;
+                    }
+                    continue;
+                }
                 if (SHAPE == 3) { row = lane & 7; ch = lane >> 3; }
                 else if (SHAPE == 4) { row = (lane & 1) | ((lane >> 4) << 1); ch = (lane >> 1) & 7; }
                 else if (SHAPE == 5) { row = ((lane >> 2) & 3) | ((lane >> 5) << 2); ch = (lane & 3) | (((lane >> 4) & 1) << 2); }
@@ -225,12 +239,11 @@ int main(int argc, char** argv)
         printf("R %d C %d ld %lld shape %s W %2d x %d/CU TW %5d order %d grid %d: %8.3f ms %8.1f GB/s %6.2f GB/s/WG\n", R, C,
                ld, shape, W, wgPerCu, TW, order, g, best, wbytes / best / 1e6, wbytes / best / 1e6 / g);
     };
-    // per-CU store rate by the lane layout of an 8-row x 128-B instruction (64 CUs)
-    run(kern<1, 0>, "8x128 row-major", 8, 512, 2, 1, 0, 64);
-    run(kern<3, 0>, "8x128 chunk-major", 8, 512, 2, 1, 0, 64);
-    run(kern<4, 0>, "8x128 ch{1,2,3}", 8, 512, 2, 1, 0, 64);
-    run(kern<5, 0>, "8x128 ch{0,1,4}", 8, 512, 2, 1, 0, 64);
+    // quad-contiguous half lines (16 rows x 64 B, halves in consecutive instructions) against whole lines
+    run(kern<7, 0>, "16x64 quad-contig", 8, 512, 2, 1, 0, 64);
     run(kern<6, 0>, "8x128 ch{0,1,5}", 8, 512, 2, 1, 0, 64);
     run(kern<0, 0>, "16x64 pure", 8, 512, 2, 1, 0, 64);
+    run(kern<7, 0>, "16x64 quad-contig", 8, 512, 2, 1, 0, 256);
+    run(kern<6, 0>, "8x128 ch{0,1,5}", 8, 512, 2, 1, 0, 256);
     return 0;
 }
