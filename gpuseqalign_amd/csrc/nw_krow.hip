@@ -108,6 +108,11 @@ constexpr int kLedgerWords = 10;  // GSA_STAMPS words per strip of a K-rows fill
 #ifndef GSA_KR_BLOCK_LEDGER
 #define GSA_KR_BLOCK_LEDGER 0
 #endif
+// the strip ledger (GSA_STAMPS=1 in a GSA_KR_LEDGER build, tools/r06_ledger.py): its counters cost the
+// production instances SGPRs (the headline's spills 10 -> 24), so they exist in diagnostic builds only
+#ifndef GSA_KR_LEDGER
+#define GSA_KR_LEDGER GSA_KR_BLOCK_LEDGER
+#endif
 __host__ __device__ constexpr uint32_t kr_xwords(uint32_t flags) { return flags + 256u; }
 __host__ __device__ constexpr uint32_t kr_xdata(uint32_t flags) { return flags + 256u + 64u; }
 [[maybe_unused]] __host__ __device__ constexpr uint32_t kr_xstage_bytes(int ns) { return 64u + (uint32_t)ns * kXD * 256u; }
@@ -230,7 +235,7 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
     // the error word is a global load, which waits for this wave's outstanding header stores
     // (vmcnt retires in order): polled once per 32 LDS polls
     // ledger (GSA_STAMPS=1, plain fills): shader-clock cycles spent waiting here, and the waits
-    constexpr bool kLedger = PT < 3;
+    constexpr bool kLedger = PT < 3 && GSA_KR_LEDGER;
     uint64_t spinCyc = 0;
     unsigned spinN = 0;
 #if GSA_KR_BLOCK_LEDGER
@@ -1370,7 +1375,7 @@ __global__ void __launch_bounds__((64 * kr_waves<NS, PT>()), 1) nw_krow_kernel(S
         {
             // ledger (GSA_STAMPS=1): per strip [realtime start, end, shader clock start, end, cycles
             // waiting for input, waits, and in a GSA_KR_BLOCK_LEDGER build the block spans]
-            unsigned long long* const lg = a.stamps ? a.stamps + kLedgerWords * ((size_t)tkg * NS + w) : nullptr;
+            unsigned long long* const lg = (GSA_KR_LEDGER && a.stamps) ? a.stamps + kLedgerWords * ((size_t)tkg * NS + w) : nullptr;
             pa.stamps = lg ? a.stamps + kLedgerWords * (size_t)tkg * NS : nullptr;
             if (lg && lane == 0)
             {

@@ -1,4 +1,6 @@
-"""Cycle ledger of the headline K-rows sparse fill (config-3 100k x 100k pair, nw_krow_kernel<4,4,...>)
+"""(Needs a ledger build: tools/r06_variant_build.sh led -DGSA_KR_LEDGER=1 "nw_krow.hip nw_krowx.hip", run with
+GSA_LIB=gpuseqalign_amd/libgsa_led.so; -DGSA_KR_BLOCK_LEDGER=1 adds the block spans.)
+Cycle ledger of the headline K-rows sparse fill (config-3 100k x 100k pair, nw_krow_kernel<4,4,...>)
 under GSA_STAMPS=1: per strip the real-time and shader-clock span and the cycles spent waiting for
 input (the spin path); prints the ledger as JSON and saves the raw words under gpurun_out/.
 Usage: python tools/r06_ledger.py [R C] [xr] (default: the config-3 pair; R C: a prefix of it; xr: the
@@ -50,6 +52,8 @@ def main():
         eng.sync()
         ms.append(e0.elapsed_time(e1))
     st = eng.debug_stamps().astype(np.int64).reshape(-1, 10)
+    if not st[:, 1].any():
+        sys.exit("no ledger stamps: run a GSA_KR_LEDGER build (see the docstring)")
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     np.save(os.path.join(ROOT, "gpurun_out", f"r06_ledger_{R}x{C}{'_xr' if xr else ''}.npy"), st)
     st = st[st[:, 1] > 0]
