@@ -286,19 +286,22 @@ def test_score_both_ends_random_shapes(engine, golden, monkeypatch, knobs):
         assert (r["score"], r["i_end"], r["j_end"]) == oracle.score_ag(Y, X, sub, go, ge, False), (case, R, C, go, ge)
 
 
-def test_score_both_ends_100k(engine, golden):
-    """100k x 100k NW-AG and NW-LG (default switch: from both ends) against the one-direction kernel."""
-    import os
+@pytest.mark.timeout(300)
+def test_score_both_ends_100k(engine, golden, knobs):
+    """100k x 100k NW-AG and NW-LG (default switch: from both ends) against the oracle's tiled OpenMP
+    restatement (score_oracle.c, ~1e10 cells: seconds on the box's 16 threads) and against the
+    one-direction kernel (GSA_SCORE_BIDI=0)."""
+    import oracle
     from gpuseqalign_amd import formats as F
     Y, X = F.synthetic_seq(100000, 300), F.synthetic_seq(100000, 301)
     for go, ge in [(-11, -1), (-11, -11)]:
+        knobs("GSA_SCORE_BIDI", "1")
         r1 = engine.score(Y, X, golden.blosum62, go, ge, False)
-        os.environ["GSA_SCORE_BIDI"] = "0"
-        try:
-            r0 = engine.score(Y, X, golden.blosum62, go, ge, False)
-        finally:
-            del os.environ["GSA_SCORE_BIDI"]
-        assert (r1["score"], r1["i_end"], r1["j_end"]) == (r0["score"], r0["i_end"], r0["j_end"])
+        knobs("GSA_SCORE_BIDI", "0")
+        r0 = engine.score(Y, X, golden.blosum62, go, ge, False)
+        ref = oracle.score_ag(Y, X, golden.blosum62, go, ge, False, mt=True)
+        assert (r1["score"], r1["i_end"], r1["j_end"]) == ref, (go, ge)
+        assert (r0["score"], r0["i_end"], r0["j_end"]) == ref, (go, ge)
 
 
 @pytest.mark.parametrize("gran", ["0", "1"])
@@ -325,8 +328,9 @@ def test_score_both_ends_granule_tap(engine, golden, monkeypatch, gran, skew, kn
 
 def test_score_both_ends_large_random_shapes(engine, golden, monkeypatch, knobs):
     """Ten random shapes of 4k-30k rows and columns (both parities, both split forms: granule tap or
-    lane taps, transposed when only C suits), random affine / linear gaps: the default path against
-    the one-direction kernel (GSA_SCORE_BIDI=0) on the same inputs."""
+    lane taps, transposed when only C suits), random affine / linear gaps: the default path and the
+    one-direction kernel (GSA_SCORE_BIDI=0) against the oracle's tiled OpenMP restatement."""
+    import oracle
     rng = np.random.default_rng(77)
     for case in range(10):
         R, C = (int(v) for v in rng.integers(4000, 30001, 2))
@@ -337,7 +341,9 @@ def test_score_both_ends_large_random_shapes(engine, golden, monkeypatch, knobs)
         r1 = engine.score(Y, X, golden.blosum62, go, ge, False)
         knobs("GSA_SCORE_BIDI", "0")
         r0 = engine.score(Y, X, golden.blosum62, go, ge, False)
-        assert (r1["score"], r1["i_end"], r1["j_end"]) == (r0["score"], r0["i_end"], r0["j_end"]), (case, R, C, go, ge)
+        ref = oracle.score_ag(Y, X, golden.blosum62, go, ge, False, mt=True)
+        assert (r1["score"], r1["i_end"], r1["j_end"]) == ref, (case, R, C, go, ge)
+        assert (r0["score"], r0["i_end"], r0["j_end"]) == ref, (case, R, C, go, ge)
 
 
 def _planted(R, C, seed, plants):
