@@ -74,6 +74,9 @@ hipError_t launch_expand_stream(const ExpandArgs& a, hipStream_t stream, int gri
         grid = std::max(1, cus);
     }
     grid = std::min(grid, a.nTasks);
+#ifdef GSA_EXPAND_GRID_PROBE  // (diagnostic builds: the expansion on fewer CUs, its per-CU rate)
+    grid = std::min(grid, GSA_EXPAND_GRID_PROBE);
+#endif
     if ((e = record_foot((const void*)kern, lds, 64 * kExpStreamWaves, grid)) != hipSuccess) return e;
     hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * kExpStreamWaves), lds, stream, a);
     return hipGetLastError();

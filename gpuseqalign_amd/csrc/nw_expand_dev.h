@@ -14,7 +14,7 @@
 #endif
 #if GSA_EXPAND_PROBE == 8 || GSA_EXPAND_PROBE == 9
 // (8: probe 7 and a loader that loads nothing from HBM; 9: probe 7 without the per-task profile
-// build and its two barriers)
+// build and its two barriers; 10: the full tile work with a loader that loads nothing)
 #define GSA_EXPAND_PROBE_STORES_ONLY 1
 #else
 #define GSA_EXPAND_PROBE_STORES_ONLY (GSA_EXPAND_PROBE == 7)
@@ -578,15 +578,15 @@ __device__ __forceinline__ void ex_stream(const ExpandArgs& a, unsigned* counter
             for (int i = 0; i < kXIt; ++i)
             {
                 const int j = lane + 64 * i, c = cb + 1 + j;
-                xv[i] = (GSA_EXPAND_PROBE != 8 && j < kSlotX && c <= d.C) ? G(d.seqX)[c] : 0;
+                xv[i] = (GSA_EXPAND_PROBE != 8 && GSA_EXPAND_PROBE != 10 && j < kSlotX && c <= d.C) ? G(d.seqX)[c] : 0;
             }
 #pragma unroll
             for (int i = 0; i < NW; ++i)
             {
                 const int r0 = rc * NW * kExpRows + kExpRows * i + 1;
                 const int r = r0 + lane;
-                yv[i] = (GSA_EXPAND_PROBE != 8 && r <= d.R) ? G(d.seqY)[r] : 0;
-                if (cb == 0 || r0 > d.R || GSA_EXPAND_PROBE == 8)
+                yv[i] = (GSA_EXPAND_PROBE != 8 && GSA_EXPAND_PROBE != 10 && r <= d.R) ? G(d.seqY)[r] : 0;
+                if (cb == 0 || r0 > d.R || GSA_EXPAND_PROBE == 8 || GSA_EXPAND_PROBE == 10)
                     lbv[i] = r * a.g;
                 else
                 {
@@ -606,7 +606,7 @@ __device__ __forceinline__ void ex_stream(const ExpandArgs& a, unsigned* counter
                 for (int q = 0; q < kTIt; ++q)
                 {
                     const int j = 4 * lane + 256 * q;
-                    tv[i][q] = (GSA_EXPAND_PROBE == 8 || m == 0 || r0 > d.R || j > ce) ? int4v {0, 0, 0, 0} : rowp[lane + 64 * q];
+                    tv[i][q] = (GSA_EXPAND_PROBE == 8 || GSA_EXPAND_PROBE == 10 || m == 0 || r0 > d.R || j > ce) ? int4v {0, 0, 0, 0} : rowp[lane + 64 * q];
                 }
             }
 #pragma unroll

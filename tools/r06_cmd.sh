@@ -1,8 +1,14 @@
-# round check: every GPU test, smoke(), then the default bench line
 set -e
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/r06_gpu_all2.log 2>&1 || { tail -40 gpurun_out/r06_gpu_all2.log; exit 1; }
-tail -2 gpurun_out/r06_gpu_all2.log
-timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r06_smoke.log 2>&1 || { tail -20 gpurun_out/r06_smoke.log; exit 1; }
-tail -1 gpurun_out/r06_smoke.log
+L=gpurun_out/r06_px3.log
+: > $L
+for lib in g64 g64p10 g64p8; do
+  GSA_LIB=gpuseqalign_amd/libgsa_$lib.so GSA_FULL_FUSED=0 timeout -k 10 120 python -u tools/r06_full100k.py --pitched --timing --reps 2 --tag "$lib" >> $L 2>&1
+done
+grep "^{" $L | python3 -c "
+import sys, json
+for l in sys.stdin:
+    j = json.loads(l)
+    t = j.get('timing') or {}
+    print(j['tag'], 'p2', t.get('pass2_ms'), 'GB/s/CU', round(j['bytes']/ (t.get('pass2_ms', 1e9)*1e-3)/1e9/64, 2))"
