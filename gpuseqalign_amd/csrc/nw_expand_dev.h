@@ -214,7 +214,7 @@ __device__ __forceinline__ void ex_tile_core(const ExpandArgs& a, const ExpandPa
                     A[c][dd] = tE[4 * c + dd];
                     A[c + 4][dd] = t[4 * c + dd];
                 }
-#if !GSA_EXPAND_PROBE_STORES_ONLY
+#if !GSA_EXPAND_PROBE_STORES_ONLY && GSA_EXPAND_PROBE != 11  // (11: full tile work, no transposes; results wrong)
 #pragma unroll
             for (int c = 0; c < 4; ++c)
 #pragma unroll
