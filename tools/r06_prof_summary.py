@@ -54,7 +54,7 @@ def main():
                "hbm_frac_of_kernel_time": round(alg_batch / ((sum(p1) + sum(p2)) / len(p2) * 1e-3) / 8e12, 4)}}
     pmc = {}
     for tagw, key, alg in (("h", "nw_krow_kernel<4, 4, 1024, 0, true>", None),
-                           ("f", "nw_full_fused_kernel<4, 8, true>", alg_full),
+                           ("f", "nw_full_fused_kernel<4, 8, true", alg_full),
                            ("b1", "nw_krow_kernel<8, 4, 1024, 2, true>", None),
                            ("b2", "nw_expand_stream_kernel", alg_batch)):
         d = os.path.join(src, tagw[0] + "_")
