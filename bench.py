@@ -83,7 +83,9 @@ def full_kernel_name(single):
         return lane_kernel_name(single)
     fm = os.environ.get("GSA_FULL_FUSED", "1")
     if single and fm != "0":
-        return ("gsa::nw_full_fused_kernel<4,8,true> (both passes in one launch: (4, 4) K-rows pass-1 tickets "
+        return ("gsa::nw_full_fused_kernel<4,8,true,3> for R x C > 2^30 (pass-1 strips stage row 64m in LDS for a "
+                "storer wave), <4,8,true,4> below (strips store row 64m themselves) (both passes in one launch: (4, 4) "
+                "K-rows pass-1 tickets "
                 "publishing per-strip progress, then the streamed expansion: a loader wave per workgroup stages "
                 "each 448-row x 512-column task once pass 1 has passed it, 7 tile waves store parallelogram tiles)")
     ns = 4 if single else 8
@@ -387,7 +389,7 @@ def bench_full100k(dev, eng, tS, sh, stream, steps, warmup, world):
             "hbm_frac": round(b / (km * 1e-3) / 1e9 / PEAK_HBM_GBPS, 4),
             "bound": "hbm (4 B written per cell; MI355X 8 TB/s spec)",
             "pmc_write_over_algorithmic": pmc_full100k_ratio(),
-            "rocprof": "profiles/r06_full100k_kernel_stats.csv (nw_full_fused_kernel<4, 8, true>, this fill alone)",
+            "rocprof": "profiles/r06_full100k_kernel_stats.csv (nw_full_fused_kernel<4, 8, true, 3>, this fill alone)",
             "align_cost": cost,
             "golden_align_cost": None if gold is None else gold["pairs"]["related"]["align_cost"]}
 
