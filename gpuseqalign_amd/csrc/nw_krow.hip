@@ -701,7 +701,10 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
 // us, first strip's sweep 4.2 -> 4.7-6.4 ms; profiles/r06_fused100k.txt).
 // ------------------------------------------------------------------------------------
 constexpr int kFeedWin = 4;
-template <int NS, int K, int LW>
+constexpr int kFeedPolls = 3;
+// PIPE: kFeedPolls polls in flight (the plain fills: 100k sparse 5.368 -> 5.348 ms kernel, same box,
+// 3 rounds; the fused full fill measured 2.5 % slower with it, profiles/r06_fused100k.txt)
+template <int NS, int K, int LW, bool PIPE = false>
 __device__ __forceinline__ void kr_feed(const StripArgs& a, const KrLds& L, int tk, int lane)
 {
     const int Cp = a.Cp;
@@ -711,6 +714,98 @@ __device__ __forceinline__ void kr_feed(const StripArgs& a, const KrLds& L, int 
     int c0 = 0;     // ring 0's consumer word, re-read only when it blocks
     uint64_t last = __builtin_amdgcn_s_memrealtime();
     unsigned idle = 0;  // idle passes (error-word polls)
+    if (PIPE && tk > 0)
+    {
+        // kFeedPolls polls in flight, staggered: a granule is fed one load latency after it is
+        // visible, plus a fraction of one, instead of up to two (a poll issued just before the store
+        // landed, then the next).  Every poll issues all its loads (lanes past the room or Cp read
+        // column 0 and drop it), so the vector-memory count the compiler waits on is static.
+        constexpr int P = kFeedPolls;
+        unsigned long long q[P][kFeedWin];
+        int qb[P], qr[P];
+        auto issue = [&](auto sT) {
+            constexpr int s = decltype(sT)::value;
+            if (hnext + 64 * kFeedWin + 64 > c0 + kRing) c0 = flag_ld(F + kr_cons(0));
+            qb[s] = hnext;
+            qr[s] = max(0, min(kFeedWin, (c0 + kRing - 64 - hnext) / 64));
+#pragma unroll
+            for (int j = 0; j < kFeedWin; ++j)
+            {
+                const int c = hnext + 64 * j + lane;
+                const bool in = j < qr[s] && c <= Cp;
+                // (not masked after the load: a select would wait for it here)
+                q[s][j] = __hip_atomic_load(gprev + (in ? c : 0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        };
+        // the snapshot's published prefix from hnext on (columns below hnext were fed from an earlier
+        // snapshot; past the snapshot's room nothing is taken)
+        auto consume = [&](auto sT) {
+            constexpr int s = decltype(sT)::value;
+            // all of the snapshot's loads awaited here, before any branch: a load the consume skips
+            // is otherwise still pending where its register is next written, and the compiler waits
+            // there for everything in flight (vmcnt(0))
+            asm volatile("" ::"v"(q[s][0]), "v"(q[s][1]), "v"(q[s][2]), "v"(q[s][3]));
+            int n = hnext;
+            bool stop = false;
+#pragma unroll
+            for (int j = 0; j < kFeedWin; ++j)
+            {
+                if (stop || j >= qr[s]) break;
+                const int c = qb[s] + 64 * j + lane;
+                const bool good = c > Cp || c < hnext || (uint32_t)(q[s][j] >> 32) == a.epoch;
+                const uint64_t badm = __ballot(!good);
+                const int nj = badm ? __builtin_ctzll(badm) : 64;
+                if (c >= hnext && c <= Cp && lane < nj) lds_st(ring0 + 4u * (uint32_t)((c + 64) & (kRing - 1)), (int)(uint32_t)q[s][j]);
+                n = max(n, qb[s] + 64 * j + nj);
+                stop = nj < 64;
+            }
+            if (n > hnext)
+            {
+                hnext = n;
+                flag_st(F, hnext > Cp ? kBig : hnext + 64);
+                last = __builtin_amdgcn_s_memrealtime();
+            }
+            else if ((++idle & 63) == 0)
+            {
+                // the error word by a scalar load: a vector load here, on some passes only, would
+                // leave the compiler unsure which polls are in flight (it then waits for all)
+                unsigned e;
+                asm volatile("s_load_dword %0, %1, 0x0 glc\n"
+                             "s_waitcnt lgkmcnt(0)"
+                             : "=s"(e)
+                             : "s"(a.err)
+                             : "memory");
+                if (e != 0 || __builtin_amdgcn_s_memrealtime() - last > a.spin)
+                {
+                    atomicOr(a.err, 1u);
+                    return false;
+                }
+            }
+            return true;
+        };
+        using S0 = std::integral_constant<int, 0>;
+        using S1 = std::integral_constant<int, 1>;
+        using S2 = std::integral_constant<int, 2>;
+        static_assert(P == 3 && kFeedWin == 4, "three polls of four windows in flight");
+        issue(S0());
+        issue(S1());
+        issue(S2());
+        // (straight-line: every pass issues every poll, so the compiler's count of loads in flight
+        // is the same on every path)
+        bool ok = true;
+        for (;;)
+        {
+            ok &= consume(S0());
+            issue(S0());
+            ok &= consume(S1());
+            issue(S1());
+            ok &= consume(S2());
+            issue(S2());
+            if (!ok || hnext > Cp) break;
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the polls still in flight, unused)
+        return;
+    }
     while (hnext <= Cp)
     {
         // whole windows whose ring elements (c + 64) strip 0 has released (< c0 + kRing)
@@ -770,12 +865,12 @@ __device__ __forceinline__ void kr_feed(const StripArgs& a, const KrLds& L, int 
 // super-strip, or row 0)
 // ------------------------------------------------------------------------------------
 // ROLE 0: both jobs in one wave; 1: the feed only; 2: the profile only
-template <int NS, int K, int LW, int ROLE, bool Q8>
+template <int NS, int K, int LW, int ROLE, bool Q8, bool PIPE = false>
 __device__ __forceinline__ void kr_loader(const StripArgs& a, const KrLds& L, int tk, int lane)
 {
     if constexpr (ROLE == 1)
     {
-        kr_feed<NS, K, LW>(a, L, tk, lane);
+        kr_feed<NS, K, LW, PIPE>(a, L, tk, lane);
         return;
     }
     const int Cp = a.Cp, C = a.C;
@@ -1368,7 +1463,7 @@ __global__ void __launch_bounds__((64 * kr_waves<NS, PT>()), 1) nw_krow_kernel(S
         if (w == NS + 1)
             kr_drain<NS, K, LW, PT>(pa, L, tk, lane);
         else if (w == NS)
-            kr_loader<NS, K, LW, kr_split<NS, PT>() ? 1 : 0, Q8>(pa, L, tk, lane);
+            kr_loader<NS, K, LW, kr_split<NS, PT>() ? 1 : 0, Q8, true>(pa, L, tk, lane);
         else if (kr_split<NS, PT>() && w == NS + 2)
             kr_loader<NS, K, LW, 2, Q8>(pa, L, tk, lane);
         else

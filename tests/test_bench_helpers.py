@@ -91,7 +91,7 @@ def test_full_kernel_label(monkeypatch):
     fill under GSA_FULL_KERNEL=lane."""
     for k in ("GSA_FULL_KERNEL", "GSA_FULL_FUSED", "GSA_LANE_NS", "GSA_LANE_FEED", "GSA_LANE_PAIR"):
         monkeypatch.delenv(k, raising=False)
-    assert bench.full_kernel_name(True).startswith("gsa::nw_full_fused_kernel<4,8,true>")
+    assert bench.full_kernel_name(True).startswith("gsa::nw_full_fused_kernel<4,8,true,3>")
     assert bench.full_kernel_name(False).startswith("gsa::nw_krow_kernel<8,4,1024,2,true>")
     monkeypatch.setenv("GSA_FULL_FUSED", "0")
     assert bench.full_kernel_name(True).startswith("gsa::nw_krow_kernel<4,4,1024,2,true>")

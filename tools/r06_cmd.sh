@@ -1,14 +1,7 @@
 set -e
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-L=gpurun_out/r06_px3.log
-: > $L
-for lib in g64 g64p11; do
-  GSA_LIB=gpuseqalign_amd/libgsa_$lib.so GSA_FULL_FUSED=0 timeout -k 10 120 python -u tools/r06_full100k.py --pitched --timing --reps 2 --tag "$lib" >> $L 2>&1
-done
-grep "^{" $L | python3 -c "
-import sys, json
-for l in sys.stdin:
-    j = json.loads(l)
-    t = j.get('timing') or {}
-    print(j['tag'], 'p2', t.get('pass2_ms'), 'GB/s/CU', round(j['bytes']/ (t.get('pass2_ms', 1e9)*1e-3)/1e9/64, 2))"
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/r06_gpu_all3.log 2>&1
+tail -3 gpurun_out/r06_gpu_all3.log
+timeout -k 10 120 python -u bench.py --steps 10 --warmup 2 --no-cpu-baseline --config4-pairs 0 --no-10k --no-100k-full --no-rank-share --full-batch-pairs 0 --no-config5 2>/dev/null | grep '^{' > gpurun_out/r06_hl.json
+python3 -c "import json; j=json.load(open('gpurun_out/r06_hl.json')); print(j['value'], j['ms_per_step'], j['roofline']['kernel_ms'])"
