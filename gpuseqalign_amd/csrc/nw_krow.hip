@@ -701,9 +701,20 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
 // us, first strip's sweep 4.2 -> 4.7-6.4 ms; profiles/r06_fused100k.txt).
 // ------------------------------------------------------------------------------------
 constexpr int kFeedWin = 4;
-constexpr int kFeedPolls = 3;
-// PIPE: kFeedPolls polls in flight (the plain fills: 100k sparse 5.368 -> 5.348 ms kernel, same box,
-// 3 rounds; the fused full fill measured 2.5 % slower with it, profiles/r06_fused100k.txt)
+#ifndef GSA_FEED_POLLS  // (A/B builds: polls in flight and windows per poll of the PIPE feed)
+#define GSA_FEED_POLLS 2
+#endif
+#ifndef GSA_FEED_PWIN
+#define GSA_FEED_PWIN 4
+#endif
+constexpr int kFeedPolls = GSA_FEED_POLLS, kFeedPWin = GSA_FEED_PWIN;
+#ifndef GSA_FUSED_FEED_PIPE
+#define GSA_FUSED_FEED_PIPE false  // (A/B builds: the fused fill's feeder with polls in flight)
+#endif
+// PIPE: kFeedPolls polls in flight, for the plain fills: 100k sparse, same box, 3 rounds, kernel ms: one
+// poll 5.367-5.371 -> three 5.342-5.355; on another box three 5.353-5.374, four 5.402-5.413, three of two
+// windows 5.391-5.406, two 5.310-5.326 (kept).  The fused full fill measured 2.5 % slower with three
+// (profiles/r06_fused100k.txt)
 template <int NS, int K, int LW, bool PIPE = false>
 __device__ __forceinline__ void kr_feed(const StripArgs& a, const KrLds& L, int tk, int lane)
 {
@@ -720,16 +731,16 @@ __device__ __forceinline__ void kr_feed(const StripArgs& a, const KrLds& L, int 
         // visible, plus a fraction of one, instead of up to two (a poll issued just before the store
         // landed, then the next).  Every poll issues all its loads (lanes past the room or Cp read
         // column 0 and drop it), so the vector-memory count the compiler waits on is static.
-        constexpr int P = kFeedPolls;
-        unsigned long long q[P][kFeedWin];
+        constexpr int P = kFeedPolls, W = kFeedPWin;
+        unsigned long long q[P][W];
         int qb[P], qr[P];
         auto issue = [&](auto sT) {
             constexpr int s = decltype(sT)::value;
-            if (hnext + 64 * kFeedWin + 64 > c0 + kRing) c0 = flag_ld(F + kr_cons(0));
+            if (hnext + 64 * W + 64 > c0 + kRing) c0 = flag_ld(F + kr_cons(0));
             qb[s] = hnext;
-            qr[s] = max(0, min(kFeedWin, (c0 + kRing - 64 - hnext) / 64));
+            qr[s] = max(0, min(W, (c0 + kRing - 64 - hnext) / 64));
 #pragma unroll
-            for (int j = 0; j < kFeedWin; ++j)
+            for (int j = 0; j < W; ++j)
             {
                 const int c = hnext + 64 * j + lane;
                 const bool in = j < qr[s] && c <= Cp;
@@ -744,11 +755,12 @@ __device__ __forceinline__ void kr_feed(const StripArgs& a, const KrLds& L, int 
             // all of the snapshot's loads awaited here, before any branch: a load the consume skips
             // is otherwise still pending where its register is next written, and the compiler waits
             // there for everything in flight (vmcnt(0))
-            asm volatile("" ::"v"(q[s][0]), "v"(q[s][1]), "v"(q[s][2]), "v"(q[s][3]));
+#pragma unroll
+            for (int j = 0; j < W; ++j) asm volatile("" ::"v"(q[s][j]));
             int n = hnext;
             bool stop = false;
 #pragma unroll
-            for (int j = 0; j < kFeedWin; ++j)
+            for (int j = 0; j < W; ++j)
             {
                 if (stop || j >= qr[s]) break;
                 const int c = qb[s] + 64 * j + lane;
@@ -786,10 +798,12 @@ __device__ __forceinline__ void kr_feed(const StripArgs& a, const KrLds& L, int 
         using S0 = std::integral_constant<int, 0>;
         using S1 = std::integral_constant<int, 1>;
         using S2 = std::integral_constant<int, 2>;
-        static_assert(P == 3 && kFeedWin == 4, "three polls of four windows in flight");
+        using S3 = std::integral_constant<int, 3>;
+        static_assert(P >= 2 && P <= 4 && W >= 1 && W <= 4, "2-4 polls of 1-4 windows in flight");
         issue(S0());
         issue(S1());
-        issue(S2());
+        if constexpr (P > 2) issue(S2());
+        if constexpr (P > 3) issue(S3());
         // (straight-line: every pass issues every poll, so the compiler's count of loads in flight
         // is the same on every path)
         bool ok = true;
@@ -799,8 +813,16 @@ __device__ __forceinline__ void kr_feed(const StripArgs& a, const KrLds& L, int 
             issue(S0());
             ok &= consume(S1());
             issue(S1());
-            ok &= consume(S2());
-            issue(S2());
+            if constexpr (P > 2)
+            {
+                ok &= consume(S2());
+                issue(S2());
+            }
+            if constexpr (P > 3)
+            {
+                ok &= consume(S3());
+                issue(S3());
+            }
             if (!ok || hnext > Cp) break;
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the polls still in flight, unused)
@@ -2496,7 +2518,7 @@ __global__ void __launch_bounds__(64 * W) nw_full_fused_kernel(StripArgs a)
         else if (w == NS + 1)
             kr_drain<NS, K, LW, 3>(pa, L, tk, lane);
         else if (w == NS)
-            kr_loader<NS, K, LW, kr_split<NS>() ? 1 : 0, Q8>(pa, L, tk, lane);
+            kr_loader<NS, K, LW, kr_split<NS>() ? 1 : 0, Q8, GSA_FUSED_FEED_PIPE>(pa, L, tk, lane);
         else if (kr_split<NS>() && w == NS + 2)
             kr_loader<NS, K, LW, 2, Q8>(pa, L, tk, lane);
         else if (w < NS)
