@@ -1,9 +1,11 @@
 set -e
-mkdir -p gpurun_out
-export TMPDIR=/tmp
-LIBS="ffp" bash tools/r06_ab.sh
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/r06_gpu_all4.log 2>&1
-tail -2 gpurun_out/r06_gpu_all4.log
-for i in 1 2; do
-timeout -k 10 120 python -u bench.py --steps 10 --warmup 2 --no-cpu-baseline --config4-pairs 0 --no-10k --no-100k-full --no-rank-share --full-batch-pairs 0 --no-config5 2>/dev/null | grep '^{' | python3 -c "import sys,json; j=json.loads(sys.stdin.read()); print('headline', j['value'], j['ms_per_step'], j['roofline']['kernel_ms'])"
-done
+bash tools/r06_prof.sh r06prof4
+cd $GRAFT_REPO_ROOT
+timeout -k 10 600 python -u bench.py > gpurun_out/r06_bench_final2.json 2> gpurun_out/r06_bench_final2.err
+python3 -c "
+import json
+j = json.loads(open('gpurun_out/r06_bench_final2.json').read().strip().splitlines()[-1])
+print(j['value'], j['ms_per_step'], j['roofline']['kernel_ms'], j['roofline']['frac'])
+print('100k full', (j.get('fill_100k_full') or {}).get('kernel_ms'), (j.get('fill_100k_full') or {}).get('hbm_frac'))
+print('batch', (j.get('full_batch') or {}).get('hbm_frac'))
+"
