@@ -700,7 +700,10 @@ __device__ __forceinline__ void kr_strip(const StripArgs& a, const KrLds& L, int
 // sweeps, and every ticket ran at the feed's pace (100k x 100k fused: inter-ticket lag 6 -> 14-20
 // us, first strip's sweep 4.2 -> 4.7-6.4 ms; profiles/r06_fused100k.txt).
 // ------------------------------------------------------------------------------------
-constexpr int kFeedWin = 4;
+#ifndef GSA_FEED_WIN  // (A/B builds: windows per poll of the one-poll feed, the fused fill's)
+#define GSA_FEED_WIN 4
+#endif
+constexpr int kFeedWin = GSA_FEED_WIN;
 #ifndef GSA_FEED_POLLS  // (A/B builds: polls in flight and windows per poll of the PIPE feed)
 #define GSA_FEED_POLLS 2
 #endif
