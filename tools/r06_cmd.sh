@@ -1,2 +1,7 @@
 set -e
-LIBS="fw2 fw8" bash tools/r06_ab.sh
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/r06_smoke.log 2>&1
+tail -1 gpurun_out/r06_smoke.log
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/r06_gpu_all5.log 2>&1
+tail -1 gpurun_out/r06_gpu_all5.log
