@@ -1,7 +1,13 @@
 set -e
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/r06_smoke.log 2>&1
-tail -1 gpurun_out/r06_smoke.log
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/r06_gpu_all5.log 2>&1
-tail -1 gpurun_out/r06_gpu_all5.log
+L=gpurun_out/r06_hl_ab3.log
+: > $L
+for round in 1 2 3; do
+  for lib in default p2w2 p2w3; do
+    so=""; [ "$lib" != default ] && so=gpuseqalign_amd/libgsa_$lib.so
+    r=$(GSA_LIB=$so timeout -k 10 120 python -u bench.py --steps 10 --warmup 2 --no-cpu-baseline --config4-pairs 0 --no-10k --no-100k-full --no-rank-share --full-batch-pairs 0 --no-config5 2>/dev/null | grep '^{' | python3 -c "import sys,json; j=json.loads(sys.stdin.read()); print(j['ms_per_step'], j['roofline']['kernel_ms'])")
+    echo "$lib $r" >> $L
+  done
+done
+cat $L
